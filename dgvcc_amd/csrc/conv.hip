@@ -1,0 +1,619 @@
+// Implicit-GEMM convolution for gfx950 (MI355X): forward, data-grad and
+// weight-grad of the stride-1 "same" convolutions on the DGVCC hot path
+// (vgg16_bn.features convs, models/models.py:35-38; ConvBlock
+// models/models.py:8-21; cls_head models/models.py:238-243).
+//
+// GEMM view (NHWC activations, weights packed [Cout][R][S][C]):
+//   forward  D[co][px] = sum_{r,s,c} W[co][r][s][c] * X[px + (r-pad, s-pad)][c]
+//   wgrad    D[co][(r,s,c)] = sum_px dY[px][co] * X[px + (r-pad, s-pad)][c]
+//   dgrad    = forward of dY with the flipped, transposed filter.
+// Each K-tile row is 128 bytes (64 bf16 / 32 f32 channels of one (r,s) tap),
+// staged global->registers->LDS (XOR-swizzled, double buffered, one barrier per
+// K-tile) and consumed by v_mfma_f32_16x16x32_bf16 (perf mode) or the exact
+// f32 v_mfma_f32_16x16x4_f32 (parity mode).  Out-of-image taps are zero-filled
+// by the buffer-load range check (voffset past num_records returns 0).
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;  // 4 waves, 2x2 over the output tile
+
+struct FwdArgs {
+  const char* x; long long ldx; int N, H, W, C;
+  const char* w; int Cout, R, S, pad;
+  const float* bias;
+  char* y; long long ldy;
+  int accumulate;
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+__device__ __forceinline__ u4v bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return __builtin_bit_cast(u4v, v);
+}
+
+template <typename T>
+__device__ __forceinline__ void mfma_frag(f4v& acc, const u4v& a, const u4v& b) {
+  if constexpr (std::is_same<T, bf16>::value) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s8v, a), __builtin_bit_cast(s8v, b), acc, 0, 0, 0);
+  } else {
+    // 4 consecutive k of one 16-byte fragment; A and B use the same k order.
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[0]), __uint_as_float(b[0]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[1]), __uint_as_float(b[1]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[2]), __uint_as_float(b[2]), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[3]), __uint_as_float(b[3]), acc, 0, 0, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// forward (also used for dgrad with the flipped filter)
+// ---------------------------------------------------------------------------
+template <typename T, int BCO, int BPX>
+__global__ __launch_bounds__(NT, 2) void conv_fwd_kernel(FwdArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B chunk
+  constexpr int BK = 128 / (int)sizeof(T);   // elements per K-tile row
+  constexpr int TI = BCO / 32, TJ = BPX / 32;
+  constexpr int AR = BCO / 32, BR = BPX / 32;  // rows per thread (8 threads per row)
+  constexpr int TILE_BYTES = (BCO + BPX) * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BCO;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (bid % nco) * BCO;
+  const int px0 = (bid / nco) * BPX;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = tid & 7, rbase = tid >> 3;
+
+  // Rebased buffer descriptor over the block's pixel window (halo included).
+  const int halo = a.pad * (a.W + 1);
+  const int plo = max(0, px0 - halo);
+  const int phi = min(M, px0 + BPX + halo);
+  const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * sizeof(T));
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)plo * a.ldx * sizeof(T)), 0, win_bytes, 0x00020000);
+
+  int pp[BR], pq[BR], prow[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int m = px0 + rbase + 32 * i;
+    const int rem = m % HW;
+    prow[i] = m;
+    pp[i] = (m < M) ? rem / a.W : -100000;
+    pq[i] = rem % a.W;
+  }
+
+  const int CB = a.C / BK;
+  const int KT = a.R * a.S * CB;
+  const long long ldw = (long long)a.R * a.S * a.C;
+  const T* wp = (const T*)a.w + (long long)(co0 + rbase) * ldw + chunk * EPC;
+
+  u4v ra[AR], rb[BR];
+#define FWD_GLOAD(t_) \
+  do { \
+    const int rs = (t_) / CB, cb = (t_) - rs * CB; \
+    const int r = rs / a.S, s = rs - r * a.S; \
+    const int coff = cb * BK + chunk * EPC; \
+_Pragma("unroll") \
+    for (int i = 0; i < AR; ++i) ra[i] = *(const u4v*)(wp + (long long)(32 * i) * ldw + rs * a.C + cb * BK); \
+    const int dh = r - a.pad, dw = s - a.pad; \
+_Pragma("unroll") \
+    for (int i = 0; i < BR; ++i) { \
+      const int h = pp[i] + dh, ww = pq[i] + dw; \
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W; \
+      const long long pin = (long long)(prow[i] + dh * a.W + dw - plo); \
+      const unsigned off = ok ? (unsigned)((pin * a.ldx + coff) * (long long)sizeof(T)) : 0xFFFFFFF0u; \
+      rb[i] = bload(xr, off); \
+    } \
+  } while (0)
+#define FWD_SWRITE(buf_) \
+  do { \
+    char* As = smem + (buf_) * TILE_BYTES; \
+    char* Bs = As + BCO * 128; \
+_Pragma("unroll") \
+    for (int i = 0; i < AR; ++i) *(u4v*)(As + swz(rbase + 32 * i, chunk)) = ra[i]; \
+_Pragma("unroll") \
+    for (int i = 0; i < BR; ++i) *(u4v*)(Bs + swz(rbase + 32 * i, chunk)) = rb[i]; \
+  } while (0)
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int wco = (wid >> 1) * (BCO / 2), wpx = (wid & 1) * (BPX / 2);
+  const int fr = lane & 15, fc = lane >> 4;
+
+  FWD_GLOAD(0);
+  FWD_SWRITE(0);
+  __syncthreads();
+  for (int t = 0; t < KT; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < KT) FWD_GLOAD(t + 1);
+    const char* As = smem + cur * TILE_BYTES;
+    const char* Bs = As + BCO * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 4 * ks + fc;
+      u4v af[TI], bfr[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+    }
+    if (t + 1 < KT) FWD_SWRITE(cur ^ 1);
+    __syncthreads();
+  }
+#undef FWD_GLOAD
+#undef FWD_SWRITE
+
+  // Epilogue: lane holds pixel column fr, 4 consecutive output channels.
+  T* y = (T*)a.y;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    if (px >= M) continue;
+    T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco + 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const float4 b = *(const float4*)(a.bias + co);
+        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      st4(yrow + co, v);
+    }
+  }
+}
+
+template <typename T>
+int launch_fwd(const FwdArgs& a, hipStream_t st) {
+  const long long M = (long long)a.N * a.H * a.W;
+  const int npx = dg_cdiv(M, 128);
+  if (a.Cout % 128 == 0) {
+    const int nco = a.Cout / 128;
+    hipLaunchKernelGGL((conv_fwd_kernel<T, 128, 128>), dim3(npx * nco), dim3(NT), 0, st, a);
+  } else {
+    const int nco = a.Cout / 64;
+    hipLaunchKernelGGL((conv_fwd_kernel<T, 64, 128>), dim3(npx * nco), dim3(NT), 0, st, a);
+  }
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient: split-K over pixels into f32 slabs, then a deterministic
+// reduce that also transposes to torch's [Cout][C][R][S] layout.
+// ---------------------------------------------------------------------------
+struct WgArgs {
+  const char* x; long long ldx; int N, H, W, C;
+  const char* dy; long long lddy; int Cout, R, S, pad;
+  float* slab;         // [splits][Cout][R*S*C]
+  int splits, pps;     // pixels per split (multiple of BKP)
+};
+
+template <typename T> struct WgCfg;
+template <> struct WgCfg<bf16> { static constexpr int BKP = 64, PAD = 32; };
+template <> struct WgCfg<float> { static constexpr int BKP = 32, PAD = 64; };
+
+template <typename T, int BCO, int BC>
+__global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
+  constexpr int BKP = WgCfg<T>::BKP;
+  constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int ROWA = BCO * (int)sizeof(T) + WgCfg<T>::PAD;  // bytes per LDS row (dY tile)
+  constexpr int ROWB = BC * (int)sizeof(T) + WgCfg<T>::PAD;   // bytes per LDS row (X tile)
+  constexpr int CPRA = BCO / EPC, CPRB = BC / EPC;            // 16-B chunks per row
+  constexpr int AR = BKP * CPRA / NT, BR = BKP * CPRB / NT;   // chunks per thread
+  constexpr int TILE_BYTES = BKP * (ROWA + ROWB);
+  constexpr int TI = BCO / 32, TJ = BC / 32;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int RS = a.R * a.S;
+  const int nco = a.Cout / BCO, ncb = a.C / BC;
+  const int tiles = nco * ncb * RS;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  int t = bid - split * tiles;
+  const int cot = t % nco; t /= nco;
+  const int cbt = t % ncb;
+  const int rs = t / ncb;
+  const int co0 = cot * BCO, c0 = cbt * BC;
+  const int r = rs / a.S, s = rs - r * a.S;
+  const int dh = r - a.pad, dw = s - a.pad;
+  const int kbeg = split * a.pps;
+  const int kend = min(M, kbeg + a.pps);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  // descriptors: dY over [kbeg, kend), X over the shifted window
+  const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * sizeof(T));
+  __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.dy + (long long)kbeg * a.lddy * sizeof(T)), 0, dy_bytes, 0x00020000);
+  const int halo = a.pad * (a.W + 1);
+  const int xlo = max(0, kbeg - halo), xhi = min(M, kend + halo);
+  const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * sizeof(T));
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * sizeof(T)), 0, x_bytes, 0x00020000);
+
+  u4v ra[AR], rb[BR];
+  auto gload = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx / CPRA, ch = idx % CPRA;
+      const int px = k0 + row;
+      const unsigned off = (px < kend)
+          ? (unsigned)(((long long)(px - kbeg) * a.lddy + co0 + ch * EPC) * (long long)sizeof(T)) : 0xFFFFFFF0u;
+      ra[i] = bload(dyr, off);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int idx = tid + NT * i;
+      const int row = idx / CPRB, ch = idx % CPRB;
+      const int px = k0 + row;
+      const int rem = px % HW;
+      const int h = rem / a.W + dh, ww = rem % a.W + dw;
+      const bool ok = px < kend && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pin = (long long)(px + dh * a.W + dw - xlo);
+      const unsigned off = ok ? (unsigned)((pin * a.ldx + c0 + ch * EPC) * (long long)sizeof(T)) : 0xFFFFFFF0u;
+      rb[i] = bload(xr, off);
+    }
+  };
+  auto swrite = [&](int buf) __attribute__((always_inline)) {
+    char* As = smem + buf * TILE_BYTES;
+    char* Bs = As + BKP * ROWA;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int idx = tid + NT * i;
+      *(u4v*)(As + (idx / CPRA) * ROWA + (idx % CPRA) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int idx = tid + NT * i;
+      *(u4v*)(Bs + (idx / CPRB) * ROWB + (idx % CPRB) * 16) = rb[i];
+    }
+  };
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int wco = (wid >> 1) * (BCO / 2), wc = (wid & 1) * (BC / 2);
+  const int g = lane >> 4;
+
+  const int nkt = (kend - kbeg + BKP - 1) / BKP;
+  gload(kbeg);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kbeg + (kt + 1) * BKP);
+    const char* As = smem + cur * TILE_BYTES;
+    const char* Bs = As + BKP * ROWA;
+    if constexpr (std::is_same<T, bf16>::value) {
+      // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies row q,
+      // columns 4p..4p+3; lane i receives column i of the 4 rows.  The logical
+      // k = 8g + j maps to physical pixel row 4g + (j&3) + 16*(j>>2) for both
+      // operands (conflict-free: 8 consecutive rows per half-wave, row pitch
+      // = 8 dwords mod 64).
+      const int q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+      for (int ks = 0; ks < BKP / 32; ++ks) {
+        const int r1 = 32 * ks + 4 * g + q, r2 = r1 + 16;
+        s8v af[TI], bfv[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int col = (wco + 16 * i + 4 * p) * 2;
+          s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(As + r1 * ROWA + col));
+          s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(As + r2 * ROWA + col));
+          af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int col = (wc + 16 * j + 4 * p) * 2;
+          s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(Bs + r1 * ROWB + col));
+          s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(Bs + r2 * ROWB + col));
+          bfv[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      const int fcol = lane & 15;
+#pragma unroll
+      for (int ks = 0; ks < BKP / 4; ++ks) {
+        const int row = 4 * ks + g;
+        float af[TI], bfv[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) af[i] = *(const float*)(As + row * ROWA + (wco + 16 * i + fcol) * 4);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bfv[j] = *(const float*)(Bs + row * ROWB + (wc + 16 * j + fcol) * 4);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nkt) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  // slab[split][co][rs*C + c]; lane holds column c, rows co = 4g + r
+  const long long ldk = (long long)RS * a.C;
+  float* out = a.slab + (long long)split * a.Cout * ldk;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int c = c0 + wc + 16 * j + (lane & 15);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co0 + wco + 16 * i + 4 * g + rr;
+        out[co * ldk + rs * a.C + c] = acc[i][j][rr];
+      }
+    }
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int C, int RS,
+                                    float* __restrict__ dw, int accumulate) {
+  const long long total = (long long)Cout * C * RS;
+  const long long ldk = (long long)RS * C;
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    // o indexes the slab layout [co][rs][c] (coalesced reads)
+    const int c = (int)(o % C);
+    const long long t = o / C;
+    const int rs = (int)(t % RS);
+    const int co = (int)(t / RS);
+    float sum = 0.f;
+    for (int sp = 0; sp < splits; ++sp) sum += slab[(long long)sp * Cout * ldk + o];
+    float* d = dw + ((long long)co * C + c) * RS + rs;
+    *d = accumulate ? *d + sum : sum;
+  }
+}
+
+struct WgPlan { int splits, pps; };
+
+template <typename T>
+WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S) {
+  constexpr int BKP = WgCfg<T>::BKP;
+  const long long M = (long long)N * H * W;
+  const int bco = (Cout % 128 == 0) ? 128 : 64;
+  const int bc = (C % 128 == 0) ? 128 : 64;
+  const long long tiles = (long long)(Cout / bco) * (C / bc) * R * S;
+  long long splits = (1024 + tiles - 1) / tiles;
+  const long long max_split = (M + BKP * 4 - 1) / (BKP * 4);  // >= 4 K-tiles per block
+  if (splits > max_split) splits = max_split;
+  if (splits < 1) splits = 1;
+  long long pps = (M + splits - 1) / splits;
+  pps = (pps + BKP - 1) / BKP * BKP;
+  splits = (M + pps - 1) / pps;
+  return WgPlan{(int)splits, (int)pps};
+}
+
+template <typename T>
+int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
+  const int bco = (a.Cout % 128 == 0) ? 128 : 64;
+  const int bc = (a.C % 128 == 0) ? 128 : 64;
+  const int tiles = (a.Cout / bco) * (a.C / bc) * a.R * a.S;
+  const dim3 grid(tiles * a.splits);
+  if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), grid, dim3(NT), 0, st, a);
+  else if (bco == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), grid, dim3(NT), 0, st, a);
+  else if (bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), grid, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64>), grid, dim3(NT), 0, st, a);
+  DG_CHECK_LAUNCH();
+  const long long total = (long long)a.Cout * a.C * a.R * a.S;
+  const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.slab, a.splits, a.Cout, a.C,
+                     a.R * a.S, dw, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// weight layout transforms
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ w, int Cout, int C, int R, int S, int Cpad,
+                                   int row_len, T* __restrict__ out) {
+  const long long total = (long long)Cout * row_len;
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(o / row_len);
+    const int k = (int)(o % row_len);
+    float v = 0.f;
+    if (k < R * S * Cpad) {
+      const int rs = k / Cpad, c = k % Cpad;
+      if (c < C) v = w[(((long long)co * C + c) * R + rs / S) * S + rs % S];
+    }
+    out[o] = from_f<T>(v);
+  }
+}
+
+// wflip[ci][r][s][co] = w[co][R-1-r][S-1-s][ci]   (w packed [Cout][R][S][C])
+template <typename T>
+__global__ void flip_weight_kernel(const T* __restrict__ w, int Cout, int C, int R, int S, T* __restrict__ wf) {
+  const long long total = (long long)Cout * C * R * S;
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(o % Cout);
+    long long t = o / Cout;
+    const int s = (int)(t % S); t /= S;
+    const int r = (int)(t % R);
+    const int ci = (int)(t / R);
+    wf[o] = w[(((long long)co * R + (R - 1 - r)) * S + (S - 1 - s)) * C + ci];
+  }
+}
+
+// First layer im2col: img NCHW f32 [N][3][H][W] -> out [N*H*W][64], k = (r*3+s)*3+c.
+template <typename T>
+__global__ void im2col_c3_kernel(const float* __restrict__ img, int N, int H, int W, T* __restrict__ out) {
+  const long long M = (long long)N * H * W;
+  for (long long m = blockIdx.x * (long long)blockDim.x + threadIdx.x; m < M;
+       m += (long long)gridDim.x * blockDim.x) {
+    const int n = (int)(m / ((long long)H * W));
+    const int rem = (int)(m % ((long long)H * W));
+    const int h = rem / W, w = rem % W;
+    float v[64];
+#pragma unroll
+    for (int k = 0; k < 64; ++k) v[k] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int hh = h + r - 1, ww = w + s - 1;
+        if ((unsigned)hh < (unsigned)H && (unsigned)ww < (unsigned)W) {
+#pragma unroll
+          for (int c = 0; c < 3; ++c)
+            v[(r * 3 + s) * 3 + c] = img[(((long long)n * 3 + c) * H + hh) * W + ww];
+        }
+      }
+    T* o = out + m * 64;
+    constexpr int E = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int k = 0; k < 64; k += E) stv(o + k, v + k);
+  }
+}
+
+__global__ void unpack_c3_grad_kernel(const float* __restrict__ dwcol, int Cout, float* __restrict__ dw, int acc) {
+  const int total = Cout * 27;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int co = o / 27, k = o % 27;  // torch layout k = c*9 + r*3 + s
+    const int c = k / 9, r = (k / 3) % 3, s = k % 3;
+    const float v = dwcol[co * 64 + (r * 3 + s) * 3 + c];
+    dw[o] = acc ? dw[o] + v : v;
+  }
+}
+
+inline int grid_for(long long n, int bs = 256, int cap = 65536) {
+  long long g = (n + bs - 1) / bs;
+  if (g < 1) g = 1;
+  return (int)std::min<long long>(g, cap);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" int dg_version(void) { return DGVCC_ABI_VERSION; }
+
+extern "C" int dg_conv_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                           int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
+                           int accumulate, void* stream) {
+  DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1);
+  DG_SUPPORTED(Cout % 64 == 0);
+  DG_SUPPORTED(dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0));
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
+  DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
+  FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate};
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+}
+
+extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, int Cout, const void* w,
+                             int C, int R, int S, int pad, void* wflip, void* dx, int64_t lddx, int accumulate,
+                             void* stream) {
+  DG_REQUIRE(dy && w && wflip && dx);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(C % 64 == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)Cout * C * R * S;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(flip_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)w, Cout, C, R,
+                       S, (bf16*)wflip);
+  else
+    hipLaunchKernelGGL(flip_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)w, Cout, C,
+                       R, S, (float*)wflip);
+  DG_CHECK_LAUNCH();
+  return dg_conv_fwd(dtype, dy, lddy, N, H, W, Cout, wflip, C, R, S, R - 1 - pad, nullptr, dx, lddx, accumulate,
+                     stream);
+}
+
+extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
+  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : wg_plan<float>(N, H, W, C, Cout, R, S);
+  return (int64_t)p.splits * Cout * C * R * S * 4;
+}
+
+extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,
+                             int64_t lddy, int Cout, int R, int S, int pad, float* dw, void* workspace,
+                             int64_t ws_bytes, int accumulate, void* stream) {
+  DG_REQUIRE(x && dy && dw && workspace);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1);
+  DG_SUPPORTED(Cout % 64 == 0 && C % 64 == 0);
+  DG_REQUIRE(ldx % 8 == 0 && lddy % 8 == 0 && ldx >= C && lddy >= Cout);
+  const int64_t need = dg_conv_wgrad_workspace(dtype, N, H, W, C, Cout, R, S);
+  DG_REQUIRE(ws_bytes >= need);
+  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : wg_plan<float>(N, H, W, C, Cout, R, S);
+  DG_SUPPORTED((long long)(p.pps + 2 * pad * (W + 1)) * std::max(ldx, lddy) * 4 < (1ll << 31));
+  WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps};
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
+}
+
+extern "C" int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R, int S, int Cpad, int row_len,
+                              void* out, void* stream) {
+  DG_REQUIRE(w && out && Cout > 0 && C > 0 && Cpad >= C && row_len >= R * S * Cpad);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)Cout * row_len;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S, Cpad,
+                       row_len, (bf16*)out);
+  else if (dtype == DG_F32)
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S, Cpad,
+                       row_len, (float*)out);
+  else
+    return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_im2col3x3_c3(int dtype, const float* img, int N, int H, int W, void* out, void* stream) {
+  DG_REQUIRE(img && out && N > 0 && H > 0 && W > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long M = (long long)N * H * W;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(im2col_c3_kernel<bf16>, dim3(grid_for(M, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
+                       (bf16*)out);
+  else if (dtype == DG_F32)
+    hipLaunchKernelGGL(im2col_c3_kernel<float>, dim3(grid_for(M, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
+                       (float*)out);
+  else
+    return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_unpack_c3_grad(const float* dwcol, int Cout, float* dw, int accumulate, void* stream) {
+  DG_REQUIRE(dwcol && dw && Cout > 0);
+  hipLaunchKernelGGL(unpack_c3_grad_kernel, dim3(grid_for(Cout * 27)), dim3(256), 0, (hipStream_t)stream, dwcol,
+                     Cout, dw, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}

@@ -1,0 +1,96 @@
+// Shared device helpers for the DGVCC MI355X (gfx950) kernels.
+// Layout convention for every activation tensor: NHWC with an explicit pixel
+// stride `ld` (elements between consecutive pixels), so a channel slice of a
+// wider buffer (the decoder's concatenations) is addressed in place.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+#include "../../include/dgvcc.h"
+
+typedef __bf16 bf16;
+typedef short s8v __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef unsigned u4v __attribute__((ext_vector_type(4)));  // native 16-B vector (SROA-friendly, unlike HIP's uint4 struct)
+
+#define DG_LDS __attribute__((address_space(3)))
+
+#define DG_CHECK_LAUNCH()                                  \
+  do {                                                     \
+    hipError_t e_ = hipGetLastError();                     \
+    if (e_ != hipSuccess) return DG_ERR_HIP;               \
+  } while (0)
+
+#define DG_REQUIRE(cond)                                   \
+  do {                                                     \
+    if (!(cond)) return DG_ERR_INVALID;                    \
+  } while (0)
+
+#define DG_SUPPORTED(cond)                                 \
+  do {                                                     \
+    if (!(cond)) return DG_ERR_UNSUPPORTED;                \
+  } while (0)
+
+__device__ __forceinline__ float bf2f(unsigned short u) { return __uint_as_float(((unsigned)u) << 16); }
+__device__ __forceinline__ unsigned short f2bf(float x) { return __builtin_bit_cast(unsigned short, (bf16)x); }
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x);
+template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+
+typedef unsigned u2v __attribute__((ext_vector_type(2)));
+
+// 4-element vector load/store through float registers.
+__device__ __forceinline__ void ld4(const float* p, float v[4]) {
+  f4v t = *(const f4v*)p;
+  v[0] = t[0]; v[1] = t[1]; v[2] = t[2]; v[3] = t[3];
+}
+__device__ __forceinline__ void ld4(const bf16* p, float v[4]) {
+  u2v t = *(const u2v*)p;
+  v[0] = __uint_as_float(t[0] << 16); v[1] = __uint_as_float(t[0] & 0xffff0000u);
+  v[2] = __uint_as_float(t[1] << 16); v[3] = __uint_as_float(t[1] & 0xffff0000u);
+}
+__device__ __forceinline__ void st4(float* p, const float v[4]) { *(f4v*)p = f4v{v[0], v[1], v[2], v[3]}; }
+__device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
+  return (unsigned)f2bf(lo) | ((unsigned)f2bf(hi) << 16);
+}
+__device__ __forceinline__ void st4(bf16* p, const float v[4]) {
+  *(u2v*)p = u2v{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+}
+
+// 16-byte vector = VEC elements (4 f32 or 8 bf16).
+template <typename T> struct VecT { static constexpr int N = 16 / sizeof(T); };
+__device__ __forceinline__ void ldv(const float* p, float v[4]) { ld4(p, v); }
+__device__ __forceinline__ void ldv(const bf16* p, float v[8]) {
+  u4v t = *(const u4v*)p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(t[i] << 16); v[2 * i + 1] = __uint_as_float(t[i] & 0xffff0000u); }
+}
+__device__ __forceinline__ void stv(float* p, const float v[4]) { st4(p, v); }
+__device__ __forceinline__ void stv(bf16* p, const float v[8]) {
+  *(u4v*)p = u4v{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): consecutive logical tiles land on the same XCD so neighbouring
+// tiles that share operand panels hit the same L2.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline int dg_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }

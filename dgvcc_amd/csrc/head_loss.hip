@@ -1,0 +1,333 @@
+// Density head (1x1 conv C->1 + act), MSE loss, fused AdamW, flat gather and
+// the Gaussian density-map scatter.
+//   den_head            models/models.py:60-62  (ConvBlock(256,1,k=1), ReLU)
+//   cls_head tail       models/models.py:241-243 (Conv1x1 256->1 + Sigmoid)
+//   MSELoss             trainers/dgtrainer.py:57
+//   AdamW               main.py:85-86 (torch.optim.AdamW semantics)
+//   dmap scatter        utils/dmap_gen.py:53-81 (gaussian_filter_density_fixed)
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;
+
+inline int ew_grid(long long n, int cap = 8192) {
+  long long g = (n + NT - 1) / NT;
+  return (int)std::max<long long>(1, std::min<long long>(g, cap));
+}
+
+// ---------------------------------------------------------------- head -----
+// TPP threads cooperate on one pixel (V channels each), xor-shuffle reduce.
+template <typename T, int TPP>
+__global__ __launch_bounds__(NT) void head_fwd_kernel(const T* __restrict__ x, long long ldx, int M, int C,
+                                                      const float* __restrict__ w, const float* bias, int act,
+                                                      float* __restrict__ y) {
+  constexpr int V = 16 / (int)sizeof(T);
+  constexpr int PPB = NT / TPP;
+  const int lane = threadIdx.x % TPP;
+  for (long long p0 = (long long)blockIdx.x * PPB; p0 < M; p0 += (long long)gridDim.x * PPB) {
+    const long long p = p0 + threadIdx.x / TPP;
+    float s = 0.f;
+    if (p < M) {
+      for (int c = lane * V; c < C; c += TPP * V) {
+        float v[V];
+        ldv(x + p * ldx + c, v);
+#pragma unroll
+        for (int e = 0; e < V; ++e) s = fmaf(v[e], w[c + e], s);
+      }
+    }
+#pragma unroll
+    for (int o = TPP / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (p < M && lane == 0) {
+      if (bias) s += bias[0];
+      if (act == 1) s = s > 0.f ? s : 0.f;
+      else if (act == 2) s = 1.f / (1.f + expf(-s));
+      y[p] = s;
+    }
+  }
+}
+
+__device__ __forceinline__ float head_gpre(float gy, float y, int act) {
+  if (act == 1) return y > 0.f ? gy : 0.f;
+  if (act == 2) return gy * y * (1.f - y);
+  return gy;
+}
+
+// gx[p][c] = gpre[p] * w[c];  partial gw[blk][c] = sum_p gpre[p] * x[p][c]
+template <typename T>
+__global__ __launch_bounds__(NT) void head_bwd_kernel(const T* __restrict__ x, long long ldx, int M, int C,
+                                                      const float* __restrict__ w, int act, const float* __restrict__ y,
+                                                      const float* __restrict__ gy, T* gx, long long ldgx, int acc_gx,
+                                                      int ppb, float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[NT * V + NT];
+  const int tpp = C / V, rows = NT / tpp;
+  const int tid = threadIdx.x, ch = tid % tpp, pl = tid / tpp;
+  const int c0 = ch * V;
+  float s[V], sb = 0.f;
+#pragma unroll
+  for (int e = 0; e < V; ++e) s[e] = 0.f;
+  const int p0 = blockIdx.x * ppb, p1 = min(M, p0 + ppb);
+  if (pl < rows) {
+    float wv[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) wv[e] = w[c0 + e];
+    for (int p = p0 + pl; p < p1; p += rows) {
+      const float g = head_gpre(gy[p], y[p], act);
+      float v[V];
+      ldv(x + (long long)p * ldx + c0, v);
+#pragma unroll
+      for (int e = 0; e < V; ++e) s[e] = fmaf(g, v[e], s[e]);
+      if (ch == 0) sb += g;
+      if (gx) {
+        float o[V];
+        if (acc_gx) ldv(gx + (long long)p * ldgx + c0, o);
+        else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) o[e] = 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = fmaf(g, wv[e], o[e]);
+        stv(gx + (long long)p * ldgx + c0, o);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) sh[pl * C + c0 + e] = s[e];
+  }
+  sh[NT * V + tid] = sb;
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f;
+    for (int r = 0; r < rows; ++r) a += sh[r * C + c];
+    part[(long long)blockIdx.x * (C + 1) + c] = a;
+  }
+  if (tid == 0) {
+    float b = 0.f;
+    for (int r = 0; r < NT; ++r) b += sh[NT * V + r];
+    part[(long long)blockIdx.x * (C + 1) + C] = b;
+  }
+}
+
+__global__ void colsum_kernel(const float* __restrict__ part, int nblk, int ncol, float* out0, int n0, float* out1) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  double a = 0.0;
+  for (int k = 0; k < nblk; ++k) a += part[(long long)k * ncol + c];
+  if (c < n0) out0[c] = (float)a;
+  else if (out1) out1[c - n0] = (float)a;
+}
+
+inline int head_nblk(int M) { return std::max(1, std::min(1024, dg_cdiv(M, 64))); }
+
+// ---------------------------------------------------------------- MSE ------
+__global__ __launch_bounds__(NT) void mse_partial(const float* __restrict__ pred, const float* __restrict__ gt,
+                                                  float gs, long long n, float* __restrict__ dpred, float gcoef,
+                                                  float* __restrict__ part) {
+  __shared__ float sh[NT / 64];
+  float s = 0.f;
+  const float k = 2.f * gcoef / (float)n;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float d = pred[i] - gt[i] * gs;
+    s = fmaf(d, d, s);
+    if (dpred) dpred[i] = k * d;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < NT / 64; ++i) t += sh[i];
+    part[blockIdx.x] = t;
+  }
+}
+
+__global__ void mse_final(const float* __restrict__ part, int nblk, long long n, float* loss) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double a = 0.0;
+    for (int i = 0; i < nblk; ++i) a += part[i];
+    loss[0] = (float)(a / (double)n);
+  }
+}
+
+// ---------------------------------------------------------------- AdamW ----
+__global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v, long long n, float lr,
+                                                   float b1, float b2, float eps, float wd, float step_size,
+                                                   float bc2_sqrt) {
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    float pi = p[i];
+    const float gi = g[i];
+    pi *= 1.f - lr * wd;
+    float mi = m[i];
+    mi = fmaf(1.f - b1, gi - mi, mi);  // exp_avg.lerp_(grad, 1 - beta1)
+    float vi = v[i] * b2;
+    vi = fmaf((1.f - b2) * gi, gi, vi);  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+  }
+}
+
+__global__ void gather_flat_kernel(const float* const* __restrict__ ptrs, const int64_t* __restrict__ offsets,
+                                   int count, float* __restrict__ flat) {
+  // one block-row per tensor
+  for (int t = blockIdx.y; t < count; t += gridDim.y) {
+    const float* src = ptrs[t];
+    const long long beg = offsets[t], len = offsets[t + 1] - beg;
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < len;
+         i += (long long)gridDim.x * blockDim.x)
+      flat[beg + i] = src[i];
+  }
+}
+
+// ---------------------------------------------------------------- dmap -----
+// One wave per point: lane l < 225 handles stamp cell (l/15, l%15) — 4 passes.
+__global__ void dmap_fixed_kernel(const float* __restrict__ pts, const int64_t* __restrict__ offsets, int N, int H,
+                                  int W, float sigma, int radius, float* __restrict__ dmap) {
+  __shared__ float wts[64];
+  const int K = 2 * radius + 1;
+  if (threadIdx.x < K) {
+    // scipy.ndimage._gaussian_kernel1d in float64, then the per-axis float32 output
+    double s = 0.0;
+    for (int i = -radius; i <= radius; ++i) s += exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+    const int i = threadIdx.x - radius;
+    wts[threadIdx.x] = (float)(exp(-0.5 / ((double)sigma * sigma) * (double)(i * i)) / s);
+  }
+  __syncthreads();
+  __shared__ double wd[64];
+  if (threadIdx.x < K) {
+    double s = 0.0;
+    for (int i = -radius; i <= radius; ++i) s += exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+    const int i = threadIdx.x - radius;
+    wd[threadIdx.x] = exp(-0.5 / ((double)sigma * sigma) * (double)(i * i)) / s;
+  }
+  __syncthreads();
+  const long long total = offsets[N];
+  const int waves = blockDim.x / 64, lane = threadIdx.x & 63;
+  for (long long q = (long long)blockIdx.x * waves + (threadIdx.x >> 6); q < total; q += (long long)gridDim.x * waves) {
+    // image index of point q (binary search over offsets)
+    int lo = 0, hi = N;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (offsets[mid] <= q) lo = mid; else hi = mid;
+    }
+    const int n = lo;
+    const float px = pts[2 * q], py = pts[2 * q + 1];
+    // int() truncation; negative indices wrap like numpy (dmap_gen.py:74-75)
+    int r = (int)py, c = (int)px;
+    if (!(r < H && c < W)) continue;
+    if (r < 0) r += H;
+    if (c < 0) c += W;
+    if (r < 0 || c < 0) continue;
+    float* img = dmap + (long long)n * H * W;
+    for (int cell = lane; cell < K * K; cell += 64) {
+      const int di = cell / K, dj = cell % K;
+      const int rr = r + di - radius, cc = c + dj - radius;
+      if ((unsigned)rr < (unsigned)H && (unsigned)cc < (unsigned)W) {
+        const float v = (float)((double)wts[di] * wd[dj]);
+        atomicAdd(img + (long long)rr * W + cc, v);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w, const float* bias,
+                           int act, float* y, void* stream) {
+  DG_REQUIRE(x && w && y && M > 0 && C > 0 && act >= 0 && act <= 2);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ldx % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const int tpp_need = C / V;
+  const int grid = ew_grid((long long)M * 16, 16384);
+#define HF(T, TPP) hipLaunchKernelGGL((head_fwd_kernel<T, TPP>), dim3(grid), dim3(NT), 0, st, (const T*)x, ldx, M, C, w, bias, act, y)
+  if (dtype == DG_BF16) {
+    if (tpp_need >= 32) HF(bf16, 32); else if (tpp_need >= 16) HF(bf16, 16); else HF(bf16, 8);
+  } else {
+    if (tpp_need >= 32) HF(float, 32); else if (tpp_need >= 16) HF(float, 16); else HF(float, 8);
+  }
+#undef HF
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_head_workspace(int M, int C) {
+  if (M <= 0 || C <= 0) return DG_ERR_INVALID;
+  return (int64_t)head_nblk(M) * (C + 1) * 4;
+}
+
+extern "C" int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w, int act,
+                           const float* y, const float* gy, void* gx, int64_t ldgx, int accumulate_gx, float* gw,
+                           float* gbias, void* workspace, void* stream) {
+  DG_REQUIRE(x && w && y && gy && gw && workspace && M > 0 && C > 0 && act >= 0 && act <= 2);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && C / V <= NT && ldx % V == 0 && (!gx || ldgx % V == 0));
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = head_nblk(M), ppb = dg_cdiv(M, nblk);
+  float* part = (float*)workspace;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(head_bwd_kernel<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)x, ldx, M, C, w, act, y, gy,
+                       (bf16*)gx, ldgx, accumulate_gx, ppb, part);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(nblk), dim3(NT), 0, st, (const float*)x, ldx, M, C, w, act, y, gy,
+                       (float*)gx, ldgx, accumulate_gx, ppb, part);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_kernel, dim3(dg_cdiv(C + 1, 256)), dim3(256), 0, st, part, nblk, C + 1, gw, C, gbias);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_reduce_workspace(int64_t n) {
+  if (n <= 0) return DG_ERR_INVALID;
+  return (int64_t)ew_grid(n, 1024) * 4;
+}
+
+extern "C" int dg_mse_loss(const float* pred, const float* gt, float gt_scale, int64_t n, float* loss, float* dpred,
+                           float grad_coef, void* workspace, void* stream) {
+  DG_REQUIRE(pred && gt && loss && workspace && n > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = ew_grid(n, 1024);
+  hipLaunchKernelGGL(mse_partial, dim3(nblk), dim3(NT), 0, st, pred, gt, gt_scale, (long long)n, dpred, grad_coef,
+                     (float*)workspace);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mse_final, dim3(1), dim3(64), 0, st, (const float*)workspace, nblk, (long long)n, loss);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                             float beta2, float eps, float weight_decay, int step, void* stream) {
+  DG_REQUIRE(p && g && m && v && n > 0 && step >= 1);
+  const double bc1 = 1.0 - pow((double)beta1, step);
+  const double bc2 = 1.0 - pow((double)beta2, step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  hipLaunchKernelGGL(adamw_kernel, dim3(ew_grid(n, 16384)), dim3(NT), 0, (hipStream_t)stream, p, g, m, v,
+                     (long long)n, lr, beta1, beta2, eps, weight_decay, step_size, bc2_sqrt);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count, int64_t total,
+                              float* flat, void* stream) {
+  DG_REQUIRE(ptrs && offsets && flat && count > 0 && total > 0);
+  hipLaunchKernelGGL(gather_flat_kernel, dim3(64, std::min(count, 1024)), dim3(NT), 0, (hipStream_t)stream, ptrs,
+                     offsets, count, flat);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W, float sigma,
+                             int radius, float* dmap, void* stream) {
+  DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(dmap, 0, (size_t)N * H * W * 4, st) != hipSuccess) return DG_ERR_HIP;
+  if (!points) return DG_OK;
+  hipLaunchKernelGGL(dmap_fixed_kernel, dim3(1024), dim3(NT), 0, st, points, offsets, N, H, W, sigma, radius, dmap);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}

@@ -1,0 +1,313 @@
+// Batch normalisation (training statistics) + ReLU (+ Dropout2d channel mask)
+// for NHWC activations: replaces nn.BatchNorm2d/nn.ReLU of vgg16_bn.features
+// (models/models.py:35-38) and ConvBlock(bn=True) (models/models.py:8-21).
+//
+// HBM-bound passes.  Statistics use per-channel shifted sums (shift = first
+// pixel's value) reduced per block, then a double-precision finalize, so the
+// variance does not cancel when |mean| >> std.
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;
+
+inline int bn_nblk(int M) { return std::max(1, std::min(1024, dg_cdiv(M, 64))); }
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_stats_partial(const T* __restrict__ z, long long ldz, int M, int C, int ppb,
+                                                       float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[2][NT * V];
+  const int tpp = C / V;
+  const int rows = NT / tpp;
+  const int tid = threadIdx.x;
+  const int ch = tid % tpp, pl = tid / tpp;
+  float s1[V], s2[V], K[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const int p0 = blockIdx.x * ppb, p1 = min(M, p0 + ppb);
+  if (pl < rows) {
+    ldv(z + ch * V, K);
+    for (int p = p0 + pl; p < p1; p += rows) {
+      float v[V];
+      ldv(z + (long long)p * ldz + ch * V, v);
+#pragma unroll
+      for (int e = 0; e < V; ++e) { const float d = v[e] - K[e]; s1[e] += d; s2[e] = fmaf(d, d, s2[e]); }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sh[0][pl * C + ch * V + e] = s1[e]; sh[1][pl * C + ch * V + e] = s2[e]; }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; }
+    part[(long long)blockIdx.x * 2 * C + c] = a;
+    part[(long long)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
+template <typename T>
+__global__ void bn_stats_finalize(const T* __restrict__ z, const float* __restrict__ part, int nblk, int M, int C,
+                                  const float* __restrict__ gamma, const float* __restrict__ beta,
+                                  float* running_mean, float* running_var, float momentum, float eps,
+                                  float* save_mean, float* save_invstd, float* scale, float* shift) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nblk; ++k) { a += part[(long long)k * 2 * C + c]; b += part[(long long)k * 2 * C + C + c]; }
+  const double K = (double)to_f(z[c]);
+  const double ms = a / M;
+  double var = b / M - ms * ms;
+  if (var < 0) var = 0;
+  const double mean = K + ms;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  const float sc = gamma ? gamma[c] * invstd : invstd;
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - (float)mean * sc;
+  if (running_mean) {
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, long long ldz, int M, int C,
+                                                      const float* __restrict__ scale, const float* __restrict__ shift,
+                                                      int act, const float* __restrict__ drop, int HW,
+                                                      T* __restrict__ y, long long ldy) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)M * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int p = (int)(i / tpp), ch = (int)(i % tpp);
+    const int c0 = ch * V;
+    float v[V];
+    ldv(z + (long long)p * ldz + c0, v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      float t = fmaf(v[e], scale[c0 + e], shift[c0 + e]);
+      if (act == 1) t = t > 0.f ? t : 0.f;
+      v[e] = t;
+    }
+    if (drop) {
+      const float* d = drop + (long long)(p / HW) * C + c0;
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] *= d[e];
+    }
+    stv(y + (long long)p * ldy + c0, v);
+  }
+}
+
+// masked upstream gradient: g * drop, zeroed where the ReLU was inactive
+template <typename T>
+__device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* z, long long ldz, int p, int c0, int C,
+                                            const float* scale, const float* shift, int act, const float* drop, int HW,
+                                            float gv[], float zv[]) {
+  constexpr int V = 16 / (int)sizeof(T);
+  ldv(g + (long long)p * ldg + c0, gv);
+  ldv(z + (long long)p * ldz + c0, zv);
+  if (drop) {
+    const float* d = drop + (long long)(p / HW) * C + c0;
+#pragma unroll
+    for (int e = 0; e < V; ++e) gv[e] *= d[e];
+  }
+  if (act == 1) {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      if (!(fmaf(zv[e], scale[c0 + e], shift[c0 + e]) > 0.f)) gv[e] = 0.f;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_bwd_partial(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
+                                                     long long ldz, int M, int C, int ppb, const float* mean,
+                                                     const float* invstd, const float* scale, const float* shift,
+                                                     int act, const float* drop, int HW, float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[3][NT * V];
+  const int tpp = C / V;
+  const int rows = NT / tpp;
+  const int tid = threadIdx.x;
+  const int ch = tid % tpp, pl = tid / tpp;
+  const int c0 = ch * V;
+  float sg[V], sgx[V], sx[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { sg[e] = 0.f; sgx[e] = 0.f; sx[e] = 0.f; }
+  const int p0 = blockIdx.x * ppb, p1 = min(M, p0 + ppb);
+  if (pl < rows) {
+    float mu[V], is[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
+    for (int p = p0 + pl; p < p1; p += rows) {
+      float gv[V], zv[V];
+      bn_bwd_load(g, ldg, z, ldz, p, c0, C, scale, shift, act, drop, HW, gv, zv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float xh = (zv[e] - mu[e]) * is[e];
+        sg[e] += gv[e];
+        sgx[e] = fmaf(gv[e], xh, sgx[e]);
+        sx[e] += xh;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      sh[0][pl * C + c0 + e] = sg[e];
+      sh[1][pl * C + c0 + e] = sgx[e];
+      sh[2][pl * C + c0 + e] = sx[e];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f, d = 0.f;
+    for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; d += sh[2][r * C + c]; }
+    float* o = part + (long long)blockIdx.x * 3 * C;
+    o[c] = a; o[C + c] = b; o[2 * C + c] = d;
+  }
+}
+
+__global__ void bn_bwd_finalize(const float* __restrict__ part, int nblk, int M, int C, const float* gamma,
+                                const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double a = 0.0, b = 0.0, d = 0.0;
+  for (int k = 0; k < nblk; ++k) {
+    const float* o = part + (long long)k * 3 * C;
+    a += o[c]; b += o[C + c]; d += o[2 * C + c];
+  }
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float k1 = gm * invstd[c];
+  const float k2 = (float)(k1 * b / M);
+  const float k3 = (float)(k1 * a / M);
+  if (dgamma) dgamma[c] = (float)b;
+  if (dbeta) dbeta[c] = (float)a;
+  if (dbias) dbias[c] = (float)(-(double)k2 * d);
+  coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
+                                                   long long ldz, int M, int C, const float* mean, const float* invstd,
+                                                   const float* scale, const float* shift, int act, const float* drop,
+                                                   int HW, const float* __restrict__ coef, T* __restrict__ dz,
+                                                   long long lddz) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)M * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int p = (int)(i / tpp), ch = (int)(i % tpp);
+    const int c0 = ch * V;
+    float gv[V], zv[V];
+    bn_bwd_load(g, ldg, z, ldz, p, c0, C, scale, shift, act, drop, HW, gv, zv);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int c = c0 + e;
+      const float xh = (zv[e] - mean[c]) * invstd[c];
+      gv[e] = coef[c] * gv[e] - coef[C + c] * xh - coef[2 * C + c];
+    }
+    stv(dz + (long long)p * lddz + c0, gv);
+  }
+}
+
+inline int ew_grid(long long n) {
+  long long g = (n + NT - 1) / NT;
+  return (int)std::max<long long>(1, std::min<long long>(g, 8192));
+}
+
+template <typename T>
+int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, const float* beta, float* rm, float* rv,
+                float momentum, float eps, float* smean, float* sinv, float* scale, float* shift, void* ws,
+                hipStream_t st) {
+  const int nblk = bn_nblk(M);
+  const int ppb = dg_cdiv(M, nblk);
+  hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)z, ldz, M, C, ppb, (float*)ws);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_stats_finalize<T>, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, (const T*)z, (const float*)ws,
+                     nblk, M, C, gamma, beta, rm, rv, momentum, eps, smean, sinv, scale, shift);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+template <typename T>
+int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int M, int C, const float* gamma,
+                const float* mean, const float* inv, const float* scale, const float* shift, int act,
+                const float* drop, int HW, void* dz, long long lddz, float* dgamma, float* dbeta, float* dbias,
+                void* ws, hipStream_t st) {
+  const int nblk = bn_nblk(M);
+  const int ppb = dg_cdiv(M, nblk);
+  float* part = (float*)ws;
+  float* coef = part + (long long)nblk * 3 * C;
+  hipLaunchKernelGGL(bn_bwd_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C, ppb,
+                     mean, inv, scale, shift, act, drop, HW, part);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, part, nblk, M, C, gamma, inv, dgamma,
+                     dbeta, dbias, coef);
+  DG_CHECK_LAUNCH();
+  const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
+  hipLaunchKernelGGL(bn_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
+                     mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" int64_t dg_bn_workspace(int M, int C) {
+  if (M <= 0 || C <= 0) return DG_ERR_INVALID;
+  return ((int64_t)bn_nblk(M) * 3 + 3) * C * 4;
+}
+
+#define BN_SHAPE_OK(dtype, C, ld) \
+  ((C) % (dtype == DG_BF16 ? 8 : 4) == 0 && (C) / (dtype == DG_BF16 ? 8 : 4) <= NT && (ld) % (dtype == DG_BF16 ? 8 : 4) == 0)
+
+extern "C" int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C, const float* gamma,
+                               const float* beta, float* running_mean, float* running_var, float momentum, float eps,
+                               float* save_mean, float* save_invstd, float* scale, float* shift, void* workspace,
+                               void* stream) {
+  DG_REQUIRE(z && save_mean && save_invstd && scale && shift && workspace && M > 0 && C > 0 && ldz >= C);
+  DG_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz));
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? bn_fwd_impl<bf16>(z, ldz, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                                              save_mean, save_invstd, scale, shift, workspace, st)
+                          : bn_fwd_impl<float>(z, ldz, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                                               save_mean, save_invstd, scale, shift, workspace, st);
+}
+
+extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float* scale, const float* shift,
+                           int act, const float* drop, int HW, void* y, int64_t ldy, void* stream) {
+  DG_REQUIRE(z && y && scale && shift && M > 0 && C > 0 && ldz >= C && ldy >= C && (act == 0 || act == 1));
+  DG_REQUIRE(!drop || HW > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, ldy));
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)M * (C / (dtype == DG_BF16 ? 8 : 4));
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
+                       shift, act, drop, HW, (bf16*)y, ldy);
+  else
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
+                       scale, shift, act, drop, HW, (float*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                         const float* gamma, const float* save_mean, const float* save_invstd, const float* scale,
+                         const float* shift, int act, const float* drop, int HW, void* dz, int64_t lddz,
+                         float* dgamma, float* dbeta, float* dbias, void* workspace, void* stream) {
+  DG_REQUIRE(g && z && dz && save_mean && save_invstd && scale && shift && workspace && M > 0 && C > 0);
+  DG_REQUIRE(!drop || HW > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16
+             ? bn_bwd_impl<bf16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW, dz,
+                                 lddz, dgamma, dbeta, dbias, workspace, st)
+             : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+                                  dz, lddz, dgamma, dbeta, dbias, workspace, st);
+}

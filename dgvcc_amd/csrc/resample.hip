@@ -1,0 +1,324 @@
+// Max-pool 2x2/2 and bilinear / nearest upsampling on NHWC activations.
+//   nn.MaxPool2d(2, 2)       — vgg16_bn.features[6,13,23,33] (models/models.py:35-38)
+//   F.interpolate(...)        — upsample() (models/models.py:23-27), cls-map
+//                               nearest x4 (models/models.py:200-207),
+//                               nn.UpsamplingBilinear2d (align_corners=True,
+//                               models/ISW/__init__.py:46, models/SW/__init__.py:37)
+// Index/weight rules follow ATen's upsample kernels: align_corners=False uses
+// src = (dst + 0.5) / scale - 0.5 clamped at 0; nearest uses floor(dst / scale).
+// The backward is a deterministic gather (no atomics).
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;
+
+inline int ew_grid(long long n) {
+  long long g = (n + NT - 1) / NT;
+  return (int)std::max<long long>(1, std::min<long long>(g, 16384));
+}
+
+// first-max with NaN propagation, scan order (0,0),(0,1),(1,0),(1,1) as ATen
+__device__ __forceinline__ int argmax4(float a, float b, float c, float d, float& m) {
+  int k = 0; m = a;
+  if (b > m || isnan(b)) { m = b; k = 1; }
+  if (c > m || isnan(c)) { m = c; k = 2; }
+  if (d > m || isnan(d)) { m = d; k = 3; }
+  return k;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void maxpool_fwd_kernel(const T* __restrict__ x, long long ldx, int N, int H, int W,
+                                                         int C, T* __restrict__ y, long long ldy) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int Ho = H / 2, Wo = W / 2, tpp = C / V;
+  const long long total = (long long)N * Ho * Wo * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % tpp);
+    long long t = i / tpp;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const long long p00 = ((long long)n * H + 2 * ho) * W + 2 * wo;
+    float a[V], b[V], c[V], d[V], o[V];
+    ldv(x + p00 * ldx + ch * V, a);
+    ldv(x + (p00 + 1) * ldx + ch * V, b);
+    ldv(x + (p00 + W) * ldx + ch * V, c);
+    ldv(x + (p00 + W + 1) * ldx + ch * V, d);
+#pragma unroll
+    for (int e = 0; e < V; ++e) argmax4(a[e], b[e], c[e], d[e], o[e]);
+    stv(y + ((long long)(n * Ho + ho) * Wo + wo) * ldy + ch * V, o);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const T* __restrict__ x, long long ldx,
+                                                         const T* __restrict__ gy, long long ldgy, int N, int H, int W,
+                                                         int C, T* __restrict__ gx, long long ldgx, int accumulate) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int Ho = H / 2, Wo = W / 2, tpp = C / V;
+  const long long total = (long long)N * Ho * Wo * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % tpp);
+    long long t = i / tpp;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const long long p00 = ((long long)n * H + 2 * ho) * W + 2 * wo;
+    const long long pos[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+    float xv[4][V], g[V], out[4][V];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ldv(x + pos[k] * ldx + ch * V, xv[k]);
+    ldv(gy + ((long long)(n * Ho + ho) * Wo + wo) * ldgy + ch * V, g);
+    if (accumulate) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ldv(gx + pos[k] * ldgx + ch * V, out[k]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < V; ++e) out[k][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      float m;
+      const int k = argmax4(xv[0][e], xv[1][e], xv[2][e], xv[3][e], m);
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk)
+        if (kk == k) out[kk][e] += g[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) stv(gx + pos[k] * ldgx + ch * V, out[k]);
+  }
+}
+
+// Source taps of output index o along one axis.
+struct Tap { int i0, i1; float l1; };
+__device__ __forceinline__ Tap src_tap(int o, int in, int out, int scale, int mode) {
+  Tap t;
+  if (mode == 2) {  // nearest
+    int i = o / scale;
+    if (i > in - 1) i = in - 1;
+    t.i0 = t.i1 = i; t.l1 = 0.f;
+    return t;
+  }
+  float src;
+  if (mode == 1) {  // align_corners=True
+    const float r = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+    src = r * o;
+  } else {
+    const float r = 1.0f / (float)scale;
+    src = r * (o + 0.5f) - 0.5f;
+    if (src < 0.f) src = 0.f;
+  }
+  int i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  t.i0 = i0;
+  t.i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  t.l1 = src - (float)i0;
+  return t;
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(NT) void upsample_fwd_kernel(const T* __restrict__ x, long long ldx, int N, int H, int W,
+                                                          int C, int scale, int mode, T* __restrict__ y,
+                                                          long long ldy) {
+  const int Ho = H * scale, Wo = W * scale, tpp = C / V;
+  const long long total = (long long)N * Ho * Wo * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % tpp);
+    long long t = i / tpp;
+    const int wo = (int)(t % Wo); t /= Wo;
+    const int ho = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const Tap th = src_tap(ho, H, Ho, scale, mode), tw = src_tap(wo, W, Wo, scale, mode);
+    const float h1l = th.l1, h0l = 1.f - th.l1, w1l = tw.l1, w0l = 1.f - tw.l1;
+    const T* base = x + (long long)n * H * W * ldx + ch * V;
+    float a[V], b[V], c[V], d[V], o[V];
+    if constexpr (V == 1) {
+      a[0] = to_f(base[((long long)th.i0 * W + tw.i0) * ldx]);
+      b[0] = to_f(base[((long long)th.i0 * W + tw.i1) * ldx]);
+      c[0] = to_f(base[((long long)th.i1 * W + tw.i0) * ldx]);
+      d[0] = to_f(base[((long long)th.i1 * W + tw.i1) * ldx]);
+    } else {
+      ldv(base + ((long long)th.i0 * W + tw.i0) * ldx, a);
+      ldv(base + ((long long)th.i0 * W + tw.i1) * ldx, b);
+      ldv(base + ((long long)th.i1 * W + tw.i0) * ldx, c);
+      ldv(base + ((long long)th.i1 * W + tw.i1) * ldx, d);
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = h0l * (w0l * a[e] + w1l * b[e]) + h1l * (w0l * c[e] + w1l * d[e]);
+    T* dst = y + ((long long)(n * Ho + ho) * Wo + wo) * ldy + ch * V;
+    if constexpr (V == 1) dst[0] = from_f<T>(o[0]);
+    else stv(dst, o);
+  }
+}
+
+// Range of output indices whose taps may touch input index i (superset).
+__device__ __forceinline__ void out_range(int i, int in, int out, int scale, int mode, int& lo, int& hi) {
+  if (mode == 1) {
+    const float r = in > 1 ? (float)(out - 1) / (float)(in - 1) : (float)out;
+    lo = (int)floorf((i - 1) * r) - 1;
+    hi = (int)ceilf((i + 1) * r) + 2;
+  } else {
+    lo = scale * (i - 1) - 1;
+    hi = scale * (i + 2) + 1;
+  }
+  lo = max(lo, 0);
+  hi = min(hi, out);
+}
+
+__device__ __forceinline__ float tap_weight(const Tap& t, int i) {
+  float w = 0.f;
+  if (t.i0 == i) w += 1.f - t.l1;
+  if (t.i1 == i) w += t.l1;
+  return w;
+}
+
+template <typename T, int V>
+__global__ __launch_bounds__(NT) void upsample_bwd_kernel(const T* __restrict__ gy, long long ldgy,
+                                                          const T* __restrict__ gy2, long long ldgy2, int N, int H,
+                                                          int W, int C, int scale, int mode, T* __restrict__ gx,
+                                                          long long ldgx, int accumulate) {
+  const int Ho = H * scale, Wo = W * scale, tpp = C / V;
+  const long long total = (long long)N * H * W * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % tpp);
+    long long t = i / tpp;
+    const int iw = (int)(t % W); t /= W;
+    const int ih = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    int hlo, hhi, wlo, whi;
+    out_range(ih, H, Ho, scale, mode, hlo, hhi);
+    out_range(iw, W, Wo, scale, mode, wlo, whi);
+    for (int oh = hlo; oh < hhi; ++oh) {
+      const float wh = tap_weight(src_tap(oh, H, Ho, scale, mode), ih);
+      if (wh == 0.f) continue;
+      for (int ow = wlo; ow < whi; ++ow) {
+        const Tap tw = src_tap(ow, W, Wo, scale, mode);
+        const float ww = tap_weight(tw, iw);
+        if (ww == 0.f) continue;
+        // ATen's backward applies h-lambda * w-lambda to each grad element
+        const float wgt = wh * ww;
+        const long long op = (long long)(n * Ho + oh) * Wo + ow;
+        float g[V];
+        if constexpr (V == 1) g[0] = to_f(gy[op * ldgy + ch]);
+        else ldv(gy + op * ldgy + ch * V, g);
+        if (gy2) {
+          float g2[V];
+          if constexpr (V == 1) g2[0] = to_f(gy2[op * ldgy2 + ch]);
+          else ldv(gy2 + op * ldgy2 + ch * V, g2);
+#pragma unroll
+          for (int e = 0; e < V; ++e) g[e] += g2[e];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = fmaf(wgt, g[e], acc[e]);
+      }
+    }
+    T* dst = gx + ((long long)(n * H + ih) * W + iw) * ldgx + ch * V;
+    if (accumulate) {
+      if constexpr (V == 1) acc[0] += to_f(dst[0]);
+      else {
+        float o[V];
+        ldv(dst, o);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] += o[e];
+      }
+    }
+    if constexpr (V == 1) dst[0] = from_f<T>(acc[0]);
+    else stv(dst, acc);
+  }
+}
+
+template <typename T>
+int up_fwd(const void* x, long long ldx, int N, int H, int W, int C, int scale, int mode, void* y, long long ldy,
+           hipStream_t st) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const bool vec = (C % V == 0) && (ldx % V == 0) && (ldy % V == 0);
+  const long long total = (long long)N * H * scale * W * scale * (vec ? C / V : C);
+  if (vec)
+    hipLaunchKernelGGL((upsample_fwd_kernel<T, V>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)x, ldx, N, H, W,
+                       C, scale, mode, (T*)y, ldy);
+  else
+    hipLaunchKernelGGL((upsample_fwd_kernel<T, 1>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)x, ldx, N, H, W,
+                       C, scale, mode, (T*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+template <typename T>
+int up_bwd(const void* gy, long long ldgy, const void* gy2, long long ldgy2, int N, int H, int W, int C, int scale,
+           int mode, void* gx, long long ldgx, int acc, hipStream_t st) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const bool vec = (C % V == 0) && (ldgy % V == 0) && (ldgx % V == 0) && (!gy2 || ldgy2 % V == 0);
+  const long long total = (long long)N * H * W * (vec ? C / V : C);
+  if (vec)
+    hipLaunchKernelGGL((upsample_bwd_kernel<T, V>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gy, ldgy,
+                       (const T*)gy2, ldgy2, N, H, W, C, scale, mode, (T*)gx, ldgx, acc);
+  else
+    hipLaunchKernelGGL((upsample_bwd_kernel<T, 1>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gy, ldgy,
+                       (const T*)gy2, ldgy2, N, H, W, C, scale, mode, (T*)gx, ldgx, acc);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+}  // namespace
+
+extern "C" int dg_maxpool2_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, void* y,
+                               int64_t ldy, void* stream) {
+  DG_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && C % V == 0 && ldx % V == 0 && ldy % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * (H / 2) * (W / 2) * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, H, W,
+                       C, (bf16*)y, ldy);
+  else
+    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, H,
+                       W, C, (float*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_maxpool2_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy, int N, int H,
+                               int W, int C, void* gx, int64_t ldgx, int accumulate, void* stream) {
+  DG_REQUIRE(x && gy && gx && N > 0 && H > 0 && W > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && C % V == 0 && ldx % V == 0 && ldgy % V == 0 && ldgx % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * (H / 2) * (W / 2) * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx,
+                       (const bf16*)gy, ldgy, N, H, W, C, (bf16*)gx, ldgx, accumulate);
+  else
+    hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx,
+                       (const float*)gy, ldgy, N, H, W, C, (float*)gx, ldgx, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_upsample_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int scale, int mode,
+                               void* y, int64_t ldy, void* stream) {
+  DG_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0 && scale >= 1 && mode >= 0 && mode <= 2);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? up_fwd<bf16>(x, ldx, N, H, W, C, scale, mode, y, ldy, st)
+                          : up_fwd<float>(x, ldx, N, H, W, C, scale, mode, y, ldy, st);
+}
+
+extern "C" int dg_upsample_bwd(int dtype, const void* gy, int64_t ldgy, const void* gy2, int64_t ldgy2, int N, int H,
+                               int W, int C, int scale, int mode, void* gx, int64_t ldgx, int accumulate,
+                               void* stream) {
+  DG_REQUIRE(gy && gx && N > 0 && H > 0 && W > 0 && C > 0 && scale >= 1 && mode >= 0 && mode <= 2);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? up_bwd<bf16>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st)
+                          : up_bwd<float>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st);
+}

@@ -1,0 +1,148 @@
+/*
+ * dgvcc.h — C-ABI of libdgvcc_hip.so, the MI355X (gfx950) kernels behind the
+ * DGVCC crowd-density training hot path.
+ *
+ * Conventions (SURVEY.md §8b "C-ABI exports"):
+ *   - every entry point returns int: DG_OK (0) or a negative DG_ERR_* code;
+ *   - the library never allocates or owns tensors: callers pass device pointers
+ *     (PyTorch caching allocator), sizes and a hipStream_t (as void*);
+ *     workspaces are queried (`*_workspace`) then caller-allocated;
+ *   - all launches are stream-ordered on the caller's stream; no implicit sync;
+ *   - activations are NHWC with an explicit pixel stride `ld` (elements between
+ *     consecutive pixels) so channel slices of concatenation buffers are
+ *     addressed in place (replaces torch.cat, models/models.py:72,76,84);
+ *   - dtype: DG_F32 (parity mode, exact-f32 MFMA) or DG_BF16 (perf mode, bf16
+ *     storage + bf16 MFMA, f32 accumulation/statistics).
+ *   - the library is stateless: no globals, safe to call from any thread.
+ */
+#ifndef DGVCC_H
+#define DGVCC_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DG_OK 0
+#define DG_ERR_INVALID (-1)     /* bad argument (null pointer, negative size, ...) */
+#define DG_ERR_UNSUPPORTED (-2) /* shape/dtype combination not implemented */
+#define DG_ERR_HIP (-3)         /* HIP launch/runtime error */
+
+#define DG_F32 0
+#define DG_BF16 1
+
+/* ---- library ----------------------------------------------------------- */
+int dg_version(void); /* returns DGVCC_ABI_VERSION */
+#define DGVCC_ABI_VERSION 1
+
+/* ---- convolution (implicit GEMM on MFMA) --------------------------------
+ * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
+ * (models/models.py:35-38), ConvBlock (models/models.py:8-21) and the cls head
+ * (models/models.py:238-243).  Stride 1, "same" padding (2*pad == R-1).
+ * x: [N,H,W,C] (pixel stride ldx), w: [Cout][R][S][C] packed (dg_pack_weight),
+ * y: [N,H,W,Cout] (pixel stride ldy).  C % 64 == 0 (bf16) / C % 32 == 0 (f32),
+ * Cout % 64 == 0.  bias (f32 [Cout]) may be NULL.  accumulate != 0 adds into y. */
+int dg_conv_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                const void* w, int Cout, int R, int S, int pad, const float* bias,
+                void* y, int64_t ldy, int accumulate, void* stream);
+
+/* dX = conv_transpose(dY, W): dy [N,H,W,Cout] (lddy), wflip workspace of
+ * R*S*C*Cout elements of dtype (caller-allocated), dx [N,H,W,C] (lddx). */
+int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, int Cout,
+                  const void* w, int C, int R, int S, int pad, void* wflip,
+                  void* dx, int64_t lddx, int accumulate, void* stream);
+
+/* dW[Cout][C][R][S] (f32, torch layout) = sum_pixels dY (x) X (split-K over
+ * pixels, deterministic slab reduce).  `accumulate` adds into dw. */
+int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S);
+int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                  const void* dy, int64_t lddy, int Cout, int R, int S, int pad,
+                  float* dw, void* workspace, int64_t ws_bytes, int accumulate, void* stream);
+
+/* torch [Cout][C][R][S] f32 -> packed rows out[Cout][row_len] of dtype holding
+ * [R][S][Cpad] (zero-padded C, zero tail up to row_len). Cpad=3,row_len=64 gives
+ * the im2col filter of the first layer. */
+int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R, int S, int Cpad,
+                   int row_len, void* out, void* stream);
+
+/* First VGG layer (Cin=3): NCHW f32 image -> im2col rows [N*H*W][64] (27 taps,
+ * zero padded to 64) so conv1_1 runs on the same MFMA GEMM (models/models.py:36). */
+int dg_im2col3x3_c3(int dtype, const float* img, int N, int H, int W, void* out, void* stream);
+/* dW for the im2col'd first layer: col-layout grad [Cout][64] -> torch [Cout][3][3][3]. */
+int dg_unpack_c3_grad(const float* dwcol, int Cout, float* dw, int accumulate, void* stream);
+
+/* ---- batch norm (training statistics) + activation -------------------------
+ * Replaces nn.BatchNorm2d(train) + nn.ReLU (vgg16_bn, ConvBlock bn=True).
+ * Stats are per channel over N*H*W pixels; running stats use momentum and the
+ * unbiased variance exactly as torch.nn.BatchNorm2d. */
+int64_t dg_bn_workspace(int M, int C);
+int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C,
+                    const float* gamma, const float* beta, float* running_mean,
+                    float* running_var, float momentum, float eps,
+                    float* save_mean, float* save_invstd, float* scale, float* shift,
+                    void* workspace, void* stream);
+/* y = act(z*scale + shift) * drop[n][c]; act: 0 none, 1 relu. drop may be NULL
+ * (Dropout2d mask already scaled by 1/(1-p), models/models.py:55-58). HW = pixels per image. */
+int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float* scale,
+                const float* shift, int act, const float* drop, int HW, void* y, int64_t ldy,
+                void* stream);
+/* Backward: g = dL/dy (pixel stride ldg).  Produces dz (lddz), dgamma, dbeta
+ * (written, not accumulated) and dbias_conv (sum dz, may be NULL). */
+int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+              const float* gamma, const float* save_mean, const float* save_invstd,
+              const float* scale, const float* shift, int act, const float* drop, int HW,
+              void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
+              void* workspace, void* stream);
+
+/* ---- pooling / resampling ---------------------------------------------------
+ * nn.MaxPool2d(2,2) (vgg16_bn features 6,13,23,33) and F.interpolate
+ * (models/models.py:23-27).  Bilinear supports align_corners 0/1, nearest. */
+int dg_maxpool2_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                    void* y, int64_t ldy, void* stream);
+int dg_maxpool2_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy,
+                    int N, int H, int W, int C, void* gx, int64_t ldgx, int accumulate,
+                    void* stream);
+/* mode: 0 bilinear(align_corners=False), 1 bilinear(align_corners=True), 2 nearest */
+int dg_upsample_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int scale,
+                    int mode, void* y, int64_t ldy, void* stream);
+/* gx (+)= U^T (gy + gy2); gy2 may be NULL (two consumers of one upsample). */
+int dg_upsample_bwd(int dtype, const void* gy, int64_t ldgy, const void* gy2, int64_t ldgy2,
+                    int N, int H, int W, int C, int scale, int mode, void* gx, int64_t ldgx,
+                    int accumulate, void* stream);
+
+/* ---- density head: 1x1 conv C->1 (+ReLU) --------------------------------------
+ * den_head (models/models.py:60-62) / cls_head tail (models/models.py:241-242). */
+int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w,
+                const float* bias, int act, float* y, void* stream);
+/* act: 0 none, 1 relu, 2 sigmoid (y is the saved output) */
+int64_t dg_head_workspace(int M, int C);
+int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w, int act,
+                const float* y, const float* gy, void* gx, int64_t ldgx, int accumulate_gx,
+                float* gw, float* gbias, void* workspace, void* stream);
+
+/* ---- losses ------------------------------------------------------------------
+ * nn.MSELoss()(pred, gt*log_para) (trainers/dgtrainer.py:57): loss (f32 scalar
+ * on device) and optionally dpred = coef*2*(pred-gt*scale)/n. */
+int dg_mse_loss(const float* pred, const float* gt, float gt_scale, int64_t n, float* loss,
+                float* dpred, float grad_coef, void* workspace, void* stream);
+int64_t dg_reduce_workspace(int64_t n);
+
+/* ---- optimizer -----------------------------------------------------------------
+ * torch.optim.AdamW step over one flat f32 buffer (main.py:85-86). */
+int dg_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                  float beta1, float beta2, float eps, float weight_decay, int step,
+                  void* stream);
+/* Gather `count` tensors (ptrs[i], sizes[i]; device arrays) into a flat buffer. */
+int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
+                   int64_t total, float* flat, void* stream);
+
+/* ---- Gaussian density-map scatter (utils/dmap_gen.py:53-81) --------------------
+ * points: [npts][2] f32 (x=col, y=row) per image, concatenated; offsets[N+1]
+ * (device int64) delimit images.  dmap: [N][H][W] f32, overwritten.  sigma=4,
+ * radius 7 (15x15 normalized separable Gaussian, constant-0 borders). */
+int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
+                  float sigma, int radius, float* dmap, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DGVCC_H */

@@ -1,0 +1,263 @@
+"""Per-kernel numerics on the GPU against plain PyTorch fp32 on the CPU.
+
+f32 (parity mode) must agree to ~1e-5 relative (exact-f32 MFMA, different
+summation order); bf16 (perf mode) is compared against the CPU op applied to
+the same bf16-rounded inputs with a bf16-output tolerance.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _k():
+    from dgvcc_amd import kernels as K
+    return K
+
+
+def to_nhwc(x):
+    return x.permute(0, 2, 3, 1).contiguous()
+
+
+def to_nchw(x):
+    return x.permute(0, 3, 1, 2).contiguous()
+
+
+def relerr(a, b):
+    a = a.double().cpu()
+    b = b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+CONV_CASES = [
+    # N, H, W, C, Cout, R
+    (2, 20, 24, 64, 128, 3),
+    (1, 16, 16, 128, 64, 3),
+    (2, 9, 13, 64, 64, 3),
+    (1, 12, 8, 256, 128, 1),
+    (1, 8, 8, 896, 256, 1),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd_dgrad_wgrad(dev, dtype, case):
+    K = _k()
+    N, H, W, C, Cout, R = case
+    pad = R // 2
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    if dtype == torch.bfloat16:  # reference on the rounded operands
+        x = x.bfloat16().float()
+        w = w.bfloat16().float()
+        gy = gy.bfloat16().float()
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, b, padding=pad)
+    yr.backward(gy)
+
+    xd = K.Act(to_nhwc(x).to(dev, dtype))
+    wp = K.pack_weight(w.to(dev), dtype)
+    y = K.Act(K.nhwc(N, H, W, Cout, dtype, dev))
+    K.conv_fwd(xd, wp, Cout, R, pad, y, bias=b.to(dev))
+    gyd = K.Act(to_nhwc(gy).to(dev, dtype))
+    dx = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    K.conv_dgrad(gyd, wp, C, R, pad, dx)
+    dw = torch.empty(Cout, C, R, R, device=dev)
+    K.conv_wgrad(xd, gyd, R, pad, dw)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dtype == torch.float32 else 1.5e-2
+    assert relerr(to_nchw(y.buf.float()), yr.detach()) < tol
+    assert relerr(to_nchw(dx.buf.float()), xr.grad) < tol
+    wtol = 2e-5 if dtype == torch.float32 else 2e-3  # f32 accumulation of bf16 products
+    assert relerr(dw, wr.grad) < wtol
+
+
+def test_conv_slices_and_accumulate(dev):
+    """Input/output as channel slices of wider NHWC buffers (the decoder concat)."""
+    K = _k()
+    N, H, W = 1, 10, 12
+    g = torch.Generator().manual_seed(1)
+    big = torch.randn(N, H, W, 192, generator=g)
+    w = torch.randn(64, 64, 3, 3, generator=g) * 0.1
+    x = big[..., 64:128]
+    ref = F.conv2d(to_nchw(x), w, padding=1)
+    out = torch.randn(N, H, W, 128, generator=g)
+    base = out.clone()
+    xd = K.Act(big.to(dev), 64, 64)
+    od = K.Act(out.to(dev), 32, 64)
+    K.conv_fwd(xd, K.pack_weight(w.to(dev), torch.float32), 64, 3, 1, od, accumulate=True)
+    torch.cuda.synchronize()
+    res = od.buf.cpu()
+    assert relerr(to_nchw(res[..., 32:96] - base[..., 32:96]), ref) < 2e-5
+    assert torch.equal(res[..., :32], base[..., :32]) and torch.equal(res[..., 96:], base[..., 96:])
+
+
+def test_first_layer_im2col(dev):
+    K = _k()
+    N, H, W = 2, 16, 20
+    g = torch.Generator().manual_seed(2)
+    img = torch.randn(N, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 3, 3, generator=g) * 0.2
+    b = torch.randn(64, generator=g)
+    gy = torch.randn(N, 64, H, W, generator=g)
+    wr = w.clone().requires_grad_(True)
+    yr = F.conv2d(img, wr, b, padding=1)
+    yr.backward(gy)
+    col = K.Act(K.im2col_c3(img.to(dev), torch.float32))
+    wp = K.pack_weight(w.to(dev), torch.float32, cpad=3, row_len=64)
+    y = K.Act(K.nhwc(N, H, W, 64, torch.float32, dev))
+    K.conv_fwd(col, wp, 64, 1, 0, y, bias=b.to(dev))
+    dwcol = torch.empty(64, 64, 1, 1, device=dev)
+    K.conv_wgrad(col, K.Act(to_nhwc(gy).to(dev)), 1, 0, dwcol)
+    dw = torch.empty(64, 3, 3, 3, device=dev)
+    K.unpack_c3_grad(dwcol, dw)
+    torch.cuda.synchronize()
+    assert relerr(to_nchw(y.buf), yr.detach()) < 2e-5
+    assert relerr(dw, wr.grad) < 2e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", [0, 1])
+def test_bn_train_fwd_bwd(dev, dtype, act):
+    K = _k()
+    N, H, W, C = 2, 12, 10, 64
+    g = torch.Generator().manual_seed(3)
+    z = (torch.randn(N, C, H, W, generator=g) * 3 + 5)
+    if dtype == torch.bfloat16:
+        z = z.bfloat16().float()
+    gam = torch.rand(C, generator=g) + 0.5
+    bet = torch.randn(C, generator=g)
+    gy = torch.randn(N, C, H, W, generator=g)
+    if dtype == torch.bfloat16:
+        gy = gy.bfloat16().float()
+    bn = torch.nn.BatchNorm2d(C)
+    bn.weight.data.copy_(gam)
+    bn.bias.data.copy_(bet)
+    zr = z.clone().requires_grad_(True)
+    yr = bn(zr)
+    if act:
+        yr = F.relu(yr)
+    yr.backward(gy)
+
+    rm = torch.zeros(C, device=dev)
+    rv = torch.ones(C, device=dev)
+    zd = K.Act(to_nhwc(z).to(dev, dtype))
+    stats = K.bn_fwd_train(zd, gam.to(dev), bet.to(dev), rm, rv, 0.1, 1e-5)
+    y = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    K.bn_apply(zd, stats, act, y)
+    dz = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    dgam = torch.empty(C, device=dev)
+    dbet = torch.empty(C, device=dev)
+    K.bn_bwd(K.Act(to_nhwc(gy).to(dev, dtype)), zd, gam.to(dev), stats, act, dz, dgam, dbet)
+    torch.cuda.synchronize()
+    tol = 2e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(to_nchw(y.buf.float()), yr.detach()) < tol
+    assert relerr(rm, bn.running_mean) < 1e-5 and relerr(rv, bn.running_var) < 1e-5
+    assert relerr(to_nchw(dz.buf.float()), zr.grad) < (1e-4 if dtype == torch.float32 else 2e-2)
+    assert relerr(dgam, bn.weight.grad) < 1e-4 and relerr(dbet, bn.bias.grad) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_maxpool(dev, dtype):
+    K = _k()
+    N, H, W, C = 2, 8, 12, 64
+    g = torch.Generator().manual_seed(4)
+    x = F.relu(torch.randn(N, C, H, W, generator=g)).to(dtype).float()  # many ties at 0
+    gy = torch.randn(N, C, H // 2, W // 2, generator=g).to(dtype).float()
+    xr = x.clone().requires_grad_(True)
+    yr = F.max_pool2d(xr, 2, 2)
+    yr.backward(gy)
+    xd = K.Act(to_nhwc(x).to(dev, dtype))
+    y = K.Act(K.nhwc(N, H // 2, W // 2, C, dtype, dev))
+    K.maxpool_fwd(xd, y)
+    gx = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    K.maxpool_bwd(xd, K.Act(to_nhwc(gy).to(dev, dtype)), gx)
+    torch.cuda.synchronize()
+    assert torch.equal(to_nchw(y.buf.float()).cpu(), yr.detach())
+    assert torch.equal(to_nchw(gx.buf.float()).cpu(), xr.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("scale,mode,C", [(2, 0, 64), (4, 0, 512), (4, 2, 1), (16, 1, 1), (4, 0, 1), (2, 1, 16)])
+def test_upsample(dev, dtype, scale, mode, C):
+    K = _k()
+    N, H, W = 2, 6, 5
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, C, H, W, generator=g).to(dtype).float()
+    gy = torch.randn(N, C, H * scale, W * scale, generator=g).to(dtype).float()
+    xr = x.clone().requires_grad_(True)
+    if mode == 2:
+        yr = F.interpolate(xr, scale_factor=scale, mode="nearest")
+    else:
+        yr = F.interpolate(xr, scale_factor=scale, mode="bilinear", align_corners=(mode == 1))
+    yr.backward(gy)
+    xd = K.Act(to_nhwc(x).to(dev, dtype))
+    y = K.Act(K.nhwc(N, H * scale, W * scale, C, dtype, dev))
+    K.upsample_fwd(xd, scale, mode, y)
+    gx = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    K.upsample_bwd(K.Act(to_nhwc(gy).to(dev, dtype)), scale, mode, gx)
+    torch.cuda.synchronize()
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(to_nchw(y.buf.float()), yr.detach()) < tol
+    assert relerr(to_nchw(gx.buf.float()), xr.grad) < tol
+
+
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_head(dev, act):
+    K = _k()
+    N, H, W, C = 2, 7, 9, 256
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(1, C, 1, 1, generator=g) * 0.1
+    b = torch.randn(1, generator=g) if act == 2 else None
+    gy = torch.randn(N, 1, H, W, generator=g)
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True) if b is not None else None
+    yr = F.conv2d(xr, wr, br)
+    yr = [yr, F.relu(yr), torch.sigmoid(yr)][act]
+    yr.backward(gy)
+    xd = K.Act(to_nhwc(x).to(dev))
+    y = K.head_fwd(xd, w.view(-1).to(dev), b.to(dev) if b is not None else None, act)
+    gx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+    gw = torch.empty(C, device=dev)
+    gb = torch.empty(1, device=dev)
+    K.head_bwd(xd, w.view(-1).to(dev), act, y, gy.view(N, H, W).to(dev), gx, gw, gb)
+    torch.cuda.synchronize()
+    assert relerr(y.view(N, 1, H, W), yr.detach()) < 1e-5
+    assert relerr(to_nchw(gx.buf), xr.grad) < 1e-5
+    assert relerr(gw, wr.grad.view(-1)) < 1e-5
+    if b is not None:
+        assert relerr(gb, br.grad) < 1e-5
+
+
+def test_mse_and_adamw(dev):
+    K = _k()
+    g = torch.Generator().manual_seed(7)
+    pred = torch.randn(3, 1, 17, 19, generator=g)
+    gt = torch.rand(3, 1, 17, 19, generator=g) * 1e-3
+    pr = pred.clone().requires_grad_(True)
+    lr_ = F.mse_loss(pr, gt * 1000)
+    lr_.backward()
+    loss, dpred = K.mse_loss(pred.to(dev), gt.to(dev), 1000.0)
+    torch.cuda.synchronize()
+    assert abs(loss.item() - lr_.item()) / lr_.item() < 1e-6
+    assert relerr(dpred, pr.grad) < 1e-6
+
+    n = 1000
+    p = torch.randn(n, generator=g)
+    p_ref = torch.nn.Parameter(p.clone())
+    opt = torch.optim.AdamW([p_ref], lr=1e-3, weight_decay=1e-4)
+    pd, md, vd = p.to(dev), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+    for step in range(1, 4):
+        grad = torch.randn(n, generator=g)
+        p_ref.grad = grad.clone()
+        opt.step()
+        K.adamw_step(pd, grad.to(dev), md, vd, 1e-3, 0.9, 0.999, 1e-8, 1e-4, step)
+    torch.cuda.synchronize()
+    assert relerr(pd, p_ref.detach()) < 1e-6
