@@ -535,6 +535,22 @@ extern "C" int dg_conv_fwd(int dtype, const void* x, int64_t ldx, int N, int H, 
   return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
 }
 
+extern "C" int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream) {
+  DG_REQUIRE(w && wflip && Cout > 0 && C > 0 && R > 0 && S > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)Cout * C * R * S;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(flip_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)w, Cout, C, R,
+                       S, (bf16*)wflip);
+  else if (dtype == DG_F32)
+    hipLaunchKernelGGL(flip_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)w, Cout, C,
+                       R, S, (float*)wflip);
+  else
+    return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
 extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, int Cout, const void* w,
                              int C, int R, int S, int pad, void* wflip, void* dx, int64_t lddx, int accumulate,
                              void* stream) {

@@ -150,6 +150,30 @@ __global__ void mse_final(const float* __restrict__ part, int nblk, long long n,
   }
 }
 
+// ---------------------------------------------------------------- BCE ------
+// F.binary_cross_entropy (mean): -(t*max(log p,-100) + (1-t)*max(log(1-p),-100));
+// grad = (p - t) / max((1-p)*p, 1e-12) / n   (ATen binary_cross_entropy_backward)
+__global__ __launch_bounds__(NT) void bce_partial(const float* __restrict__ p, const float* __restrict__ t,
+                                                  long long n, float* __restrict__ dp, float gcoef,
+                                                  float* __restrict__ part) {
+  __shared__ float sh[NT / 64];
+  float s = 0.f;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < n; i += (long long)gridDim.x * NT) {
+    const float pi = p[i], ti = t[i];
+    const float lp = fmaxf(logf(pi), -100.f), l1p = fmaxf(logf(1.f - pi), -100.f);
+    s -= ti * lp + (1.f - ti) * l1p;
+    if (dp) dp[i] = gcoef * (pi - ti) / fmaxf((1.f - pi) * pi, 1e-12f) / (float)n;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float a = 0.f;
+    for (int i = 0; i < NT / 64; ++i) a += sh[i];
+    part[blockIdx.x] = a;
+  }
+}
+
 // ---------------------------------------------------------------- AdamW ----
 __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v, long long n, float lr,
@@ -292,6 +316,19 @@ extern "C" int dg_mse_loss(const float* pred, const float* gt, float gt_scale, i
   hipStream_t st = (hipStream_t)stream;
   const int nblk = ew_grid(n, 1024);
   hipLaunchKernelGGL(mse_partial, dim3(nblk), dim3(NT), 0, st, pred, gt, gt_scale, (long long)n, dpred, grad_coef,
+                     (float*)workspace);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mse_final, dim3(1), dim3(64), 0, st, (const float*)workspace, nblk, (long long)n, loss);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bce_loss(const float* pred, const float* target, int64_t n, float* loss, float* dpred,
+                           float grad_coef, void* workspace, void* stream) {
+  DG_REQUIRE(pred && target && loss && workspace && n > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = ew_grid(n, 1024);
+  hipLaunchKernelGGL(bce_partial, dim3(nblk), dim3(NT), 0, st, pred, target, (long long)n, dpred, grad_coef,
                      (float*)workspace);
   DG_CHECK_LAUNCH();
   hipLaunchKernelGGL(mse_final, dim3(1), dim3(64), 0, st, (const float*)workspace, nblk, (long long)n, loss);

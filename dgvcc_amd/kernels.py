@@ -66,6 +66,22 @@ def nhwc(N, H, W, C, dtype, device="cuda", zero=False) -> torch.Tensor:
 
 
 # ---------------------------------------------------------------- conv -----
+_CONV_TIMER = None
+
+
+def set_conv_timer(timer):
+    """Install a callable timer(kind, flops, launch_fn) around conv GEMM launches
+    (bench.py roofline measurement); None disables."""
+    global _CONV_TIMER
+    _CONV_TIMER = timer
+
+
+def _timed(kind, flops, fn):
+    if _CONV_TIMER is None:
+        fn()
+    else:
+        _CONV_TIMER(kind, flops, fn)
+
 def pack_weight(w: torch.Tensor, dtype: torch.dtype, cpad: int | None = None,
                 row_len: int | None = None) -> torch.Tensor:
     Cout, C, R, S = w.shape
@@ -78,22 +94,33 @@ def pack_weight(w: torch.Tensor, dtype: torch.dtype, cpad: int | None = None,
 
 
 def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
-             bias: torch.Tensor | None = None, accumulate=False):
-    call("dg_conv_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout, R, R, pad,
-         ptr(bias), y.ptr, y.ld, int(accumulate), stream())
+             bias: torch.Tensor | None = None, accumulate=False, kind="fwd", k_alg=None):
+    """k_alg: algorithmic reduction length when the GEMM K is padded (im2col layer)."""
+    flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * Cout
+    _timed(kind, flops, lambda: call("dg_conv_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
+                                     Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate),
+                                     stream()))
+
+
+def flip_weight(wp: torch.Tensor, Cout: int, C: int, R: int) -> torch.Tensor:
+    wflip = torch.empty_like(wp)
+    call("dg_flip_weight", dtype_code(wp.dtype), ptr(wp), Cout, C, R, R, ptr(wflip), stream())
+    return wflip
 
 
 def conv_dgrad(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, accumulate=False):
-    wflip = torch.empty_like(wp)
-    call("dg_conv_dgrad", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W, dy.C, ptr(wp), C, R, R, pad,
-         ptr(wflip), dx.ptr, dx.ld, int(accumulate), stream())
+    """dX = conv(dY, flipped W^T): the forward GEMM kernel on the flipped filter."""
+    wflip = flip_weight(wp, dy.C, C, R)
+    conv_fwd(dy, wflip, C, R, R - 1 - pad, dx, accumulate=accumulate, kind="dgrad")
 
 
-def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=False):
+def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=False, k_alg=None):
     ws = query("dg_conv_wgrad_workspace", x.dt, x.N, x.H, x.W, x.C, dy.C, R, R)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
-    call("dg_conv_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, dy.ptr, dy.ld, dy.C, R, R, pad,
-         ptr(dw), ptr(work), ws, int(accumulate), stream())
+    flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * dy.C
+    _timed("wgrad", flops, lambda: call("dg_conv_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
+                                        dy.ptr, dy.ld, dy.C, R, R, pad, ptr(dw), ptr(work), ws,
+                                        int(accumulate), stream()))
 
 
 def im2col_c3(img: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

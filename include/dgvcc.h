@@ -51,6 +51,9 @@ int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, 
                   const void* w, int C, int R, int S, int pad, void* wflip,
                   void* dx, int64_t lddx, int accumulate, void* stream);
 
+/* wflip[C][R][S][Cout] = w[Cout][R-1-r][S-1-s][C] (packed filters of dtype). */
+int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream);
+
 /* dW[Cout][C][R][S] (f32, torch layout) = sum_pixels dY (x) X (split-K over
  * pixels, deterministic slab reduce).  `accumulate` adds into dw. */
 int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S);
@@ -125,6 +128,10 @@ int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, const float
 int dg_mse_loss(const float* pred, const float* gt, float gt_scale, int64_t n, float* loss,
                 float* dpred, float grad_coef, void* workspace, void* stream);
 int64_t dg_reduce_workspace(int64_t n);
+/* F.binary_cross_entropy(pred, target) mean (trainers/dgtrainer.py:178,188) and
+ * dpred = coef * dBCE/dpred (ATen clamps: log >= -100, denominator >= 1e-12). */
+int dg_bce_loss(const float* pred, const float* target, int64_t n, float* loss, float* dpred,
+                float grad_coef, void* workspace, void* stream);
 
 /* ---- optimizer -----------------------------------------------------------------
  * torch.optim.AdamW step over one flat f32 buffer (main.py:85-86). */

@@ -1,0 +1,79 @@
+"""TEST INFRASTRUCTURE ONLY — imports the read-only reference at /root/reference
+(Python) so fixture scripts can run it as the parity oracle.  Never imported by
+the product package.
+
+The reference imports packages absent from this image; they are replaced by
+*import placeholders* that provide only what the hot path touches:
+  * torchvision.models.vgg16_bn(weights=None) — the standard cfg-D + BN
+    `features` layout (the reference only slices `.features`), plus empty
+    torchvision.transforms(.functional) modules (imported, never used by the step);
+  * cv2 — imported by utils/dmap_gen.py, used only by its file driver `run`;
+  * kmeans1d — imported by models/ISW/cov_settings.py, called only when
+    relax_denom == 0 (never with the shipped defaults).
+No reference source is copied; nothing here is shipped to the GPU box.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+REF = os.environ.get("DGVCC_REFERENCE", "/root/reference")
+
+
+def available() -> bool:
+    return os.path.isdir(os.path.join(REF, "models"))
+
+
+def _install_placeholders():
+    import torch.nn as nn
+
+    if "torchvision" not in sys.modules:
+        tv = types.ModuleType("torchvision")
+        tvm = types.ModuleType("torchvision.models")
+        tvt = types.ModuleType("torchvision.transforms")
+        tvtf = types.ModuleType("torchvision.transforms.functional")
+
+        class _VGG(nn.Module):
+            def __init__(self, features):
+                super().__init__()
+                self.features = features
+
+        def vgg16_bn(weights=None, **kw):
+            if weights is not None:
+                raise RuntimeError("no pretrained weights offline")
+            from dgvcc_amd.models.models import vgg16_bn_features  # same cfg-D layout/init
+            return _VGG(vgg16_bn_features())
+
+        class VGG16_BN_Weights:
+            DEFAULT = "DEFAULT"
+
+        tvm.vgg16_bn = vgg16_bn
+        tvm.VGG16_BN_Weights = VGG16_BN_Weights
+        tv.models = tvm
+        tv.transforms = tvt
+        tvt.functional = tvtf
+        sys.modules.update({"torchvision": tv, "torchvision.models": tvm,
+                            "torchvision.transforms": tvt,
+                            "torchvision.transforms.functional": tvtf})
+    if "cv2" not in sys.modules:
+        sys.modules["cv2"] = types.ModuleType("cv2")
+    if "kmeans1d" not in sys.modules:
+        km = types.ModuleType("kmeans1d")
+
+        def cluster(*a, **k):
+            raise RuntimeError("kmeans1d placeholder: relax_denom=0 path is parity-unpinned")
+
+        km.cluster = cluster
+        sys.modules["kmeans1d"] = km
+
+
+def import_ref(modname: str):
+    """Import `modname` (e.g. 'models.models') from the reference tree."""
+    if not available():
+        raise RuntimeError(f"reference not found at {REF}")
+    _install_placeholders()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    import importlib
+    return importlib.import_module(modname)

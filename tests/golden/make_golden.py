@@ -1,0 +1,119 @@
+"""Generate the golden fixtures by RUNNING THE REFERENCE (/root/reference) on
+seeded synthetic inputs.  Run in the build container (the reference does not
+exist on the GPU box):
+
+    python tests/golden/make_golden.py
+
+Outputs tests/golden/*.npz (small: inputs + expected outputs only).  The
+reference is imported with the import placeholders of oracle/ref_import.py;
+its `.cuda()` calls (models/ISW/cov_settings.py:21,24,66) are made
+device-agnostic by patching torch.Tensor.cuda to a no-op for this process.
+"""
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle.ref_import import import_ref  # noqa: E402
+from oracle import dg_oracle as O  # noqa: E402
+
+N_SAMPLE = 16
+
+
+def summarize(prefix, d, out):
+    """Full tensors when small; else sampled entries + sums (index seed fixed)."""
+    g = torch.Generator().manual_seed(7)
+    for k, v in d.items():
+        v = v.detach().float().reshape(-1)
+        key = prefix + k.replace(".", "__")
+        if v.numel() <= 1024:
+            out[key] = v.numpy()
+        else:
+            idx = torch.randint(0, v.numel(), (N_SAMPLE,), generator=g)
+            out[key + "@idx"] = idx.numpy()
+            out[key + "@val"] = v[idx].numpy()
+            out[key + "@sum"] = np.array([v.double().sum().item(), v.double().abs().sum().item()])
+
+
+def gen_dmap():
+    dg = import_ref("utils.dmap_gen")
+    rng = np.random.default_rng(0)
+    out = {}
+    cases = []
+    H, W = 96, 128
+    edge = np.array([[0, 0], [W - 0.5, H - 0.5], [3.2, H - 0.1], [-0.5, 10], [-3.7, 20.2],
+                     [W, 5], [5, H], [W - 1, 0.2], [64.9, 48.1], [64.9, 48.1]], np.float32)
+    cases.append(("edge", H, W, np.concatenate([rng.uniform(0, [W, H], (40, 2)), edge]).astype(np.float32)))
+    cases.append(("empty", H, W, np.zeros((0, 2), np.float32)))
+    cases.append(("full", 768, 1024, rng.uniform(0, [1024, 768], (500, 2)).astype(np.float32)))
+    for name, H, W, pts in cases:
+        ref = dg.gaussian_filter_density_fixed(np.zeros((H, W)), pts)
+        out[f"{name}__points"] = pts
+        out[f"{name}__shape"] = np.array([H, W])
+        out[f"{name}__dmap"] = ref.astype(np.float32)
+    np.savez_compressed(os.path.join(HERE, "dmap_fixed.npz"), **out)
+
+
+def run_ref_step(model_cls, kwargs, mode, B, H, W):
+    rm = import_ref("models.models")
+    dgt = import_ref("trainers.dgtrainer")
+    model = getattr(rm, model_cls)(pretrained=False, **kwargs)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    batch = O.synthetic_batch(B, H, W, seed=2112)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as td:
+        os.chdir(td)
+        try:
+            tr = dgt.DGTrainer(seed=2112, version="golden", device="cpu", log_para=1000,
+                               patch_size=10000, mode=mode)
+            opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+            model.train()
+            # capture outputs with a forward hook on the top-level module
+            loss = tr.train_step(model, torch.nn.MSELoss(), opt, batch, 0)
+        finally:
+            os.chdir(cwd)
+    grads = {k: p.grad if p.grad is not None else torch.zeros_like(p) for k, p in model.named_parameters()}
+    return sd0, batch, loss, grads, model.state_dict()
+
+
+def gen_train(name, model_cls, kwargs, mode, B=2, H=64, W=64):
+    sd0, batch, loss, grads, sd1 = run_ref_step(model_cls, kwargs, mode, B, H, W)
+    out = {"loss": np.array([loss], np.float64), "shape": np.array([B, H, W])}
+    summarize("grad__", grads, out)
+    summarize("post__", {k: v for k, v in sd1.items() if not k.endswith("num_batches_tracked")}, out)
+    # forward outputs of a second, separate forward from the same initial weights (no step)
+    rm = import_ref("models.models")
+    model = getattr(rm, model_cls)(pretrained=False, **kwargs)
+    model.load_state_dict(sd0)
+    model.train()
+    imgs1, imgs2, (pts, dmaps, bmaps) = batch
+    with torch.no_grad():
+        if mode in ("simple", "base"):
+            out["out_d1"] = model(imgs1).numpy()
+        else:
+            dc1, dc2, c1, c2, c_err, loss_con, _ = model.forward_train(imgs1, imgs2, bmaps)
+            out["out_dc1"] = dc1.numpy()
+            out["out_dc2"] = dc2.numpy()
+            out["out_c1"] = c1.numpy()
+            out["out_c2"] = c2.numpy()
+            out["out_loss_con"] = np.array([loss_con.item()])
+    np.savez_compressed(os.path.join(HERE, f"train_{name}.npz"), **out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["dmap", "base", "final"]
+    if "dmap" in which:
+        gen_dmap()
+    if "base" in which:
+        gen_train("simple_base", "DGModel_base", {"den_dropout": 0.0}, "simple")
+    if "final" in which:
+        gen_train("final", "DGModel_final", {"den_dropout": 0.0, "cls_dropout": 0.0}, "final")
+    print("fixtures written to", HERE)
