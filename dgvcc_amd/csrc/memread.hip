@@ -1,0 +1,458 @@
+// Two-view consistency + memory read of DGModel_memadd / DGModel_final
+// (models/models.py:116-125 forward_mem, :147-184 and :298-335 forward_train):
+//   instance-norm statistics of y_den (F.instance_norm, eps 1e-5, biased var),
+//   e_mask = |IN(y1) - IN(y2)| < err_thrs, masked + Dropout2d'd features,
+//   row softmax over the 1024 memory slots for both views + JSD-MSE loss,
+//   and the matching backward, plus the class-map combination of the cls head
+//   (models/models.py:196-207, 323-327).
+// The two GEMMs of the memory read run on the implicit-GEMM conv kernel (1x1).
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;
+
+inline int ew_grid(long long n, int cap = 16384) {
+  long long g = (n + NT - 1) / NT;
+  return (int)std::max<long long>(1, std::min<long long>(g, cap));
+}
+
+// ------------------------------------------------------------ instance norm --
+// grid (nb, N): block b of sample n reduces pixels [b*ppb, (b+1)*ppb) of that sample
+template <typename T>
+__global__ __launch_bounds__(NT) void in_stats_partial(const T* __restrict__ x, long long ldx, int HW, int C, int ppb,
+                                                       float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[2][NT * V];
+  const int n = blockIdx.y, nb = gridDim.x;
+  const int tpp = C / V, rows = NT / tpp;
+  const int tid = threadIdx.x, ch = tid % tpp, pl = tid / tpp;
+  const T* xs = x + (long long)n * HW * ldx;
+  float s1[V], s2[V], K[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  if (pl < rows) {
+    ldv(xs + ch * V, K);
+    for (int p = p0 + pl; p < p1; p += rows) {
+      float v[V];
+      ldv(xs + (long long)p * ldx + ch * V, v);
+#pragma unroll
+      for (int e = 0; e < V; ++e) { const float d = v[e] - K[e]; s1[e] += d; s2[e] = fmaf(d, d, s2[e]); }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sh[0][pl * C + ch * V + e] = s1[e]; sh[1][pl * C + ch * V + e] = s2[e]; }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; }
+    float* o = part + ((long long)n * nb + blockIdx.x) * 2 * C;
+    o[c] = a; o[C + c] = b;
+  }
+}
+
+template <typename T>
+__global__ void in_stats_finalize(const T* __restrict__ x, long long ldx, int N, int HW, int C, int nb,
+                                  const float* __restrict__ part, float eps, float* mean, float* invstd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * C) return;
+  const int n = i / C, c = i % C;
+  double a = 0.0, b = 0.0;
+  for (int k = 0; k < nb; ++k) {
+    const float* o = part + ((long long)n * nb + k) * 2 * C;
+    a += o[c]; b += o[C + c];
+  }
+  const double K = (double)to_f(x[(long long)n * HW * ldx + c]);
+  const double ms = a / HW;
+  double var = b / HW - ms * ms;
+  if (var < 0) var = 0;
+  mean[i] = (float)(K + ms);
+  invstd[i] = (float)(1.0 / sqrt(var + (double)eps));
+}
+
+// m_v = y_v * e * drop_v ; e = |(y1-mu1)*is1 - (y2-mu2)*is2| < thr  (stored as 0/1 bytes)
+template <typename T>
+__global__ __launch_bounds__(NT) void emask_fwd_kernel(const T* __restrict__ y1, const T* __restrict__ y2, long long ld,
+                                                       int N, int HW, int C, const float* mu1, const float* is1,
+                                                       const float* mu2, const float* is2, float thr,
+                                                       const float* drop1, const float* drop2, T* __restrict__ m1,
+                                                       T* __restrict__ m2, unsigned char* __restrict__ mask) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * HW * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    const int n = (int)(p / HW);
+    float a[V], b[V];
+    ldv(y1 + p * ld + c0, a);
+    ldv(y2 + p * ld + c0, b);
+    unsigned char mk[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int nc = n * C + c0 + e;
+      const float ia = (a[e] - mu1[nc]) * is1[nc];
+      const float ib = (b[e] - mu2[nc]) * is2[nc];
+      const bool keep = fabsf(ia - ib) < thr;
+      mk[e] = keep ? 1 : 0;
+      a[e] = keep ? a[e] * (drop1 ? drop1[nc] : 1.f) : 0.f;
+      b[e] = keep ? b[e] * (drop2 ? drop2[nc] : 1.f) : 0.f;
+    }
+    stv(m1 + p * C + c0, a);
+    stv(m2 + p * C + c0, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) mask[p * C + c0 + e] = mk[e];
+  }
+}
+
+// g_y_v = g_m_v * e * drop_v  (gy written with pixel stride ldgy; g_m dense)
+template <typename T>
+__global__ __launch_bounds__(NT) void emask_bwd_kernel(const T* __restrict__ gm1, const T* __restrict__ gm2, int N,
+                                                       int HW, int C, const unsigned char* __restrict__ mask,
+                                                       const float* drop1, const float* drop2, T* __restrict__ gy1,
+                                                       T* __restrict__ gy2, long long ldgy) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * HW * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    const int n = (int)(p / HW);
+    float a[V], b[V];
+    ldv(gm1 + p * C + c0, a);
+    ldv(gm2 + p * C + c0, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int nc = n * C + c0 + e;
+      const float k = mask[p * C + c0 + e] ? 1.f : 0.f;
+      a[e] *= k * (drop1 ? drop1[nc] : 1.f);
+      b[e] *= k * (drop2 ? drop2[nc] : 1.f);
+    }
+    stv(gy1 + p * ldgy + c0, a);
+    stv(gy2 + p * ldgy + c0, b);
+  }
+}
+
+// ------------------------------------------------------------ slot softmax ---
+// One wave per pixel row of C (= 1024) logits; EPL elements per lane.
+template <typename T>
+__device__ __forceinline__ void load_row(const T* row, int lane, int C, float* v, int EPL) {
+  constexpr int V = 16 / (int)sizeof(T);
+  for (int j = 0; j < EPL; j += V) ldv(row + (long long)(j / V) * 64 * V + lane * V, v + j);
+}
+template <typename T>
+__device__ __forceinline__ void store_row(T* row, int lane, float* v, int EPL) {
+  constexpr int V = 16 / (int)sizeof(T);
+  for (int j = 0; j < EPL; j += V) stv(row + (long long)(j / V) * 64 * V + lane * V, v + j);
+}
+
+template <typename T, int EPL>
+__global__ __launch_bounds__(NT) void softmax_pair_fwd(const T* __restrict__ L1, const T* __restrict__ L2, int M, int C,
+                                                       T* __restrict__ P1, T* __restrict__ P2,
+                                                       float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float a[EPL], b[EPL];
+    load_row(L1 + r * C, lane, C, a, EPL);
+    load_row(L2 + r * C, lane, C, b, EPL);
+    float ma = -INFINITY, mb = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) { ma = fmaxf(ma, a[j]); mb = fmaxf(mb, b[j]); }
+    ma = wave_max(ma); mb = wave_max(mb);
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) { a[j] = expf(a[j] - ma); sa += a[j]; b[j] = expf(b[j] - mb); sb += b[j]; }
+    sa = wave_sum(sa); sb = wave_sum(sb);
+    const float ra = 1.f / sa, rb = 1.f / sb;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      a[j] = to_f(from_f<T>(a[j] * ra));  // the loss sees the stored probabilities
+      b[j] = to_f(from_f<T>(b[j] * rb));
+      const float d = a[j] - b[j];
+      acc = fmaf(d, d, acc);
+    }
+    store_row(P1 + r * C, lane, a, EPL);
+    store_row(P2 + r * C, lane, b, EPL);
+  }
+  acc = wave_sum(acc);
+  __shared__ float sh[4];
+  if (lane == 0) sh[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+__global__ void sum_final(const float* __restrict__ part, int nblk, double denom, float* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double a = 0.0;
+    for (int i = 0; i < nblk; ++i) a += part[i];
+    out[0] = (float)(a / denom);
+  }
+}
+
+// gL_v = P_v * (gP_v' - sum(P_v * gP_v')),  gP1' = gP1 + k (P1 - P2), gP2' = gP2 - k (P1 - P2),
+// k = 2 * coef[0] / (M*C)  (d/dP of mean((P1-P2)^2) times the upstream grad of loss_con)
+template <typename T, int EPL>
+__global__ __launch_bounds__(NT) void softmax_pair_bwd(const T* __restrict__ P1, const T* __restrict__ P2,
+                                                       const T* __restrict__ G1, const T* __restrict__ G2, int M,
+                                                       int C, const float* __restrict__ coef, T* __restrict__ GL1,
+                                                       T* __restrict__ GL2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float k = coef ? 2.f * coef[0] / ((float)M * (float)C) : 0.f;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float p1[EPL], p2[EPL], g1[EPL], g2[EPL];
+    load_row(P1 + r * C, lane, C, p1, EPL);
+    load_row(P2 + r * C, lane, C, p2, EPL);
+    if (G1) load_row(G1 + r * C, lane, C, g1, EPL);
+    else for (int j = 0; j < EPL; ++j) g1[j] = 0.f;
+    if (G2) load_row(G2 + r * C, lane, C, g2, EPL);
+    else for (int j = 0; j < EPL; ++j) g2[j] = 0.f;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      const float d = k * (p1[j] - p2[j]);
+      g1[j] += d; g2[j] -= d;
+      s1 = fmaf(p1[j], g1[j], s1);
+      s2 = fmaf(p2[j], g2[j], s2);
+    }
+    s1 = wave_sum(s1); s2 = wave_sum(s2);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) { g1[j] = p1[j] * (g1[j] - s1); g2[j] = p2[j] * (g2[j] - s2); }
+    store_row(GL1 + r * C, lane, g1, EPL);
+    store_row(GL2 + r * C, lane, g2, EPL);
+  }
+}
+
+// single-view softmax (DGModel_mem.forward / memcls.forward)
+template <typename T, int EPL>
+__global__ __launch_bounds__(NT) void softmax_fwd(const T* __restrict__ L, int M, int C, T* __restrict__ P) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float a[EPL];
+    load_row(L + r * C, lane, C, a, EPL);
+    float m = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) m = fmaxf(m, a[j]);
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) { a[j] = expf(a[j] - m); s += a[j]; }
+    s = wave_sum(s);
+    const float rs = 1.f / s;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) a[j] *= rs;
+    store_row(P + r * C, lane, a, EPL);
+  }
+}
+
+template <typename T, int EPL>
+__global__ __launch_bounds__(NT) void softmax_bwd(const T* __restrict__ P, const T* __restrict__ G, int M, int C,
+                                                  T* __restrict__ GL) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float p[EPL], g[EPL];
+    load_row(P + r * C, lane, C, p, EPL);
+    load_row(G + r * C, lane, C, g, EPL);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) s = fmaf(p[j], g[j], s);
+    s = wave_sum(s);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) g[j] = p[j] * (g[j] - s);
+    store_row(GL + r * C, lane, g, EPL);
+  }
+}
+
+// ------------------------------------------------------------ class maps -----
+// c_v: [N][h][w] sigmoid outputs; cgt: [N][h][w] or NULL; outputs at (s*h, s*w):
+// c_resized = clamp(up_nearest(cgt) + |up(c1>=thr) - up(c2>=thr)|, 0, 1), c_err.
+// With c2 == NULL (single view): c_resized = cgt ? up(cgt) : up(c1>=thr).
+__global__ void cls_combine_kernel(const float* __restrict__ c1, const float* __restrict__ c2,
+                                   const float* __restrict__ cgt, int N, int h, int w, int s, float thr,
+                                   float* __restrict__ cres, float* __restrict__ cerr) {
+  const long long total = (long long)N * h * s * w * s;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int ow = (int)(i % (w * s));
+    const long long t = i / (w * s);
+    const int oh = (int)(t % (h * s));
+    const int n = (int)(t / (h * s));
+    const long long src = ((long long)n * h + oh / s) * w + ow / s;
+    auto bin = [&](float v) { return v < thr ? 0.f : (v >= thr ? 1.f : v); };
+    if (c2) {
+      const float e = fabsf(bin(c1[src]) - bin(c2[src]));
+      const float g = cgt ? cgt[src] : 0.f;
+      cres[i] = fminf(fmaxf(g + e, 0.f), 1.f);
+      if (cerr) cerr[i] = e;
+    } else {
+      cres[i] = cgt ? cgt[src] : bin(c1[src]);
+    }
+  }
+}
+
+__global__ void mul_kernel(const float* __restrict__ a, const float* __restrict__ b, long long n,
+                           float* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = a[i] * b[i];
+}
+
+#define SOFTMAX_DISPATCH(KERNEL, T, C, ...)                                                           \
+  do {                                                                                                 \
+    if ((C) == 1024) hipLaunchKernelGGL((KERNEL<T, 16>), dim3(grid), dim3(NT), 0, st, __VA_ARGS__);   \
+    else if ((C) == 512) hipLaunchKernelGGL((KERNEL<T, 8>), dim3(grid), dim3(NT), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<T, 32>), dim3(grid), dim3(NT), 0, st, __VA_ARGS__);                \
+  } while (0)
+
+}  // namespace
+
+extern "C" int64_t dg_instnorm_workspace(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0) return DG_ERR_INVALID;
+  const int nb = std::max(1, std::min(64, dg_cdiv(HW, 256)));
+  return (int64_t)N * nb * 2 * C * 4;
+}
+
+extern "C" int dg_instnorm_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float eps, float* mean,
+                                 float* invstd, void* workspace, void* stream) {
+  DG_REQUIRE(x && mean && invstd && workspace && N > 0 && HW > 0 && C > 0);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && C / V <= NT && ldx % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = std::max(1, std::min(64, dg_cdiv(HW, 256)));
+  const int ppb = dg_cdiv(HW, nb);
+  if (dtype == DG_BF16) {
+    hipLaunchKernelGGL(in_stats_partial<bf16>, dim3(nb, N), dim3(NT), 0, st, (const bf16*)x, ldx, HW, C, ppb,
+                       (float*)workspace);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_stats_finalize<bf16>, dim3(dg_cdiv(N * C, 256)), dim3(256), 0, st, (const bf16*)x, ldx, N,
+                       HW, C, nb, (const float*)workspace, eps, mean, invstd);
+  } else {
+    hipLaunchKernelGGL(in_stats_partial<float>, dim3(nb, N), dim3(NT), 0, st, (const float*)x, ldx, HW, C, ppb,
+                       (float*)workspace);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_stats_finalize<float>, dim3(dg_cdiv(N * C, 256)), dim3(256), 0, st, (const float*)x, ldx,
+                       N, HW, C, nb, (const float*)workspace, eps, mean, invstd);
+  }
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_emask_fwd(int dtype, const void* y1, const void* y2, int64_t ld, int N, int HW, int C,
+                            const float* mu1, const float* is1, const float* mu2, const float* is2, float thr,
+                            const float* drop1, const float* drop2, void* m1, void* m2, unsigned char* mask,
+                            void* stream) {
+  DG_REQUIRE(y1 && y2 && mu1 && is1 && mu2 && is2 && m1 && m2 && mask && N > 0 && HW > 0 && C > 0);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ld % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * HW * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(emask_fwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)y1,
+                       (const bf16*)y2, ld, N, HW, C, mu1, is1, mu2, is2, thr, drop1, drop2, (bf16*)m1, (bf16*)m2,
+                       mask);
+  else
+    hipLaunchKernelGGL(emask_fwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)y1,
+                       (const float*)y2, ld, N, HW, C, mu1, is1, mu2, is2, thr, drop1, drop2, (float*)m1, (float*)m2,
+                       mask);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_emask_bwd(int dtype, const void* gm1, const void* gm2, int N, int HW, int C,
+                            const unsigned char* mask, const float* drop1, const float* drop2, void* gy1, void* gy2,
+                            int64_t ldgy, void* stream) {
+  DG_REQUIRE(gm1 && gm2 && mask && gy1 && gy2 && N > 0 && HW > 0 && C > 0);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ldgy % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * HW * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(emask_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)gm1,
+                       (const bf16*)gm2, N, HW, C, mask, drop1, drop2, (bf16*)gy1, (bf16*)gy2, ldgy);
+  else
+    hipLaunchKernelGGL(emask_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)gm1,
+                       (const float*)gm2, N, HW, C, mask, drop1, drop2, (float*)gy1, (float*)gy2, ldgy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_softmax_workspace(int M) {
+  if (M <= 0) return DG_ERR_INVALID;
+  return (int64_t)std::min(4096, dg_cdiv(M, 4)) * 4;
+}
+
+#define SOFTMAX_C_OK(C) ((C) == 1024 || (C) == 512 || (C) == 2048)
+
+extern "C" int dg_softmax_pair_fwd(int dtype, const void* L1, const void* L2, int M, int C, void* P1, void* P2,
+                                   float* loss_con, void* workspace, void* stream) {
+  DG_REQUIRE(L1 && L2 && P1 && P2 && loss_con && workspace && M > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = std::min(4096, dg_cdiv(M, 4));
+  if (dtype == DG_BF16)
+    SOFTMAX_DISPATCH(softmax_pair_fwd, bf16, C, (const bf16*)L1, (const bf16*)L2, M, C, (bf16*)P1, (bf16*)P2,
+                     (float*)workspace);
+  else
+    SOFTMAX_DISPATCH(softmax_pair_fwd, float, C, (const float*)L1, (const float*)L2, M, C, (float*)P1, (float*)P2,
+                     (float*)workspace);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_final, dim3(1), dim3(64), 0, st, (const float*)workspace, grid, (double)M * C, loss_con);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_pair_bwd(int dtype, const void* P1, const void* P2, const void* G1, const void* G2, int M,
+                                   int C, const float* coef, void* GL1, void* GL2, void* stream) {
+  DG_REQUIRE(P1 && P2 && GL1 && GL2 && M > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = std::min(4096, dg_cdiv(M, 4));
+  if (dtype == DG_BF16)
+    SOFTMAX_DISPATCH(softmax_pair_bwd, bf16, C, (const bf16*)P1, (const bf16*)P2, (const bf16*)G1, (const bf16*)G2,
+                     M, C, coef, (bf16*)GL1, (bf16*)GL2);
+  else
+    SOFTMAX_DISPATCH(softmax_pair_bwd, float, C, (const float*)P1, (const float*)P2, (const float*)G1,
+                     (const float*)G2, M, C, coef, (float*)GL1, (float*)GL2);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_fwd(int dtype, const void* L, int M, int C, void* P, void* stream) {
+  DG_REQUIRE(L && P && M > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = std::min(4096, dg_cdiv(M, 4));
+  if (dtype == DG_BF16) SOFTMAX_DISPATCH(softmax_fwd, bf16, C, (const bf16*)L, M, C, (bf16*)P);
+  else SOFTMAX_DISPATCH(softmax_fwd, float, C, (const float*)L, M, C, (float*)P);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_bwd(int dtype, const void* P, const void* G, int M, int C, void* GL, void* stream) {
+  DG_REQUIRE(P && G && GL && M > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = std::min(4096, dg_cdiv(M, 4));
+  if (dtype == DG_BF16) SOFTMAX_DISPATCH(softmax_bwd, bf16, C, (const bf16*)P, (const bf16*)G, M, C, (bf16*)GL);
+  else SOFTMAX_DISPATCH(softmax_bwd, float, C, (const float*)P, (const float*)G, M, C, (float*)GL);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_cls_combine(const float* c1, const float* c2, const float* cgt, int N, int h, int w, int scale,
+                              float thr, float* c_resized, float* c_err, void* stream) {
+  DG_REQUIRE(c1 && c_resized && N > 0 && h > 0 && w > 0 && scale >= 1);
+  const long long total = (long long)N * h * w * scale * scale;
+  hipLaunchKernelGGL(cls_combine_kernel, dim3(ew_grid(total)), dim3(NT), 0, (hipStream_t)stream, c1, c2, cgt, N, h,
+                     w, scale, thr, c_resized, c_err);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_mul_f32(const float* a, const float* b, int64_t n, float* out, void* stream) {
+  DG_REQUIRE(a && b && out && n > 0);
+  hipLaunchKernelGGL(mul_kernel, dim3(ew_grid(n)), dim3(NT), 0, (hipStream_t)stream, a, b, (long long)n, out);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}

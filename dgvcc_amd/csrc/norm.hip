@@ -47,15 +47,26 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const T* __restrict__ z, 
   }
 }
 
+// 64 channels per block, 4 lanes per channel striding over the block partials.
 template <typename T>
-__global__ void bn_stats_finalize(const T* __restrict__ z, const float* __restrict__ part, int nblk, int M, int C,
-                                  const float* __restrict__ gamma, const float* __restrict__ beta,
-                                  float* running_mean, float* running_var, float momentum, float eps,
-                                  float* save_mean, float* save_invstd, float* scale, float* shift) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(NT) void bn_stats_finalize(const T* __restrict__ z, const float* __restrict__ part,
+                                                        int nblk, int M, int C, const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float* running_mean,
+                                                        float* running_var, float momentum, float eps,
+                                                        float* save_mean, float* save_invstd, float* scale,
+                                                        float* shift) {
+  __shared__ double sh[2][4][64];
+  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   double a = 0.0, b = 0.0;
-  for (int k = 0; k < nblk; ++k) { a += part[(long long)k * 2 * C + c]; b += part[(long long)k * 2 * C + C + c]; }
+  if (c < C)
+    for (int k = r; k < nblk; k += 4) { a += part[(long long)k * 2 * C + c]; b += part[(long long)k * 2 * C + C + c]; }
+  sh[0][r][cl] = a;
+  sh[1][r][cl] = b;
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   const double K = (double)to_f(z[c]);
   const double ms = a / M;
   double var = b / M - ms * ms;
@@ -74,6 +85,8 @@ __global__ void bn_stats_finalize(const T* __restrict__ z, const float* __restri
   }
 }
 
+// The grid stride (gridDim*NT) is a multiple of tpp = C/V (a power of two <= NT),
+// so each thread keeps one channel chunk: per-channel parameters live in registers.
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, long long ldz, int M, int C,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
@@ -81,44 +94,58 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
                                                       T* __restrict__ y, long long ldy) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const long long total = (long long)M * tpp;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int p = (int)(i / tpp), ch = (int)(i % tpp);
-    const int c0 = ch * V;
+  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const int c0 = (int)(gt % tpp) * V;
+  const long long pstride = (long long)gridDim.x * NT / tpp;
+  float sc[V], sf[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
+  for (long long p = gt / tpp; p < M; p += pstride) {
     float v[V];
-    ldv(z + (long long)p * ldz + c0, v);
+    ldv(z + p * ldz + c0, v);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      float t = fmaf(v[e], scale[c0 + e], shift[c0 + e]);
+      float t = fmaf(v[e], sc[e], sf[e]);
       if (act == 1) t = t > 0.f ? t : 0.f;
       v[e] = t;
     }
     if (drop) {
-      const float* d = drop + (long long)(p / HW) * C + c0;
+      const float* d = drop + (p / HW) * C + c0;
 #pragma unroll
       for (int e = 0; e < V; ++e) v[e] *= d[e];
     }
-    stv(y + (long long)p * ldy + c0, v);
+    stv(y + p * ldy + c0, v);
   }
 }
 
+// Per-thread channel-chunk parameters (registers).
+template <int V>
+struct ChanParams {
+  float sc[V], sf[V], mu[V], is[V];
+  __device__ __forceinline__ void load(int c0, const float* scale, const float* shift, const float* mean,
+                                       const float* invstd) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
+  }
+};
+
 // masked upstream gradient: g * drop, zeroed where the ReLU was inactive
-template <typename T>
-__device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* z, long long ldz, int p, int c0, int C,
-                                            const float* scale, const float* shift, int act, const float* drop, int HW,
+// (relu mask recomputed from z exactly as the forward: fmaf(z, scale, shift) > 0)
+template <typename T, int V>
+__device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* z, long long ldz, long long p, int c0,
+                                            int C, const ChanParams<V>& cp, int act, const float* drop, int HW,
                                             float gv[], float zv[]) {
-  constexpr int V = 16 / (int)sizeof(T);
-  ldv(g + (long long)p * ldg + c0, gv);
-  ldv(z + (long long)p * ldz + c0, zv);
+  ldv(g + p * ldg + c0, gv);
+  ldv(z + p * ldz + c0, zv);
   if (drop) {
-    const float* d = drop + (long long)(p / HW) * C + c0;
+    const float* d = drop + (p / HW) * C + c0;
 #pragma unroll
     for (int e = 0; e < V; ++e) gv[e] *= d[e];
   }
   if (act == 1) {
 #pragma unroll
     for (int e = 0; e < V; ++e)
-      if (!(fmaf(zv[e], scale[c0 + e], shift[c0 + e]) > 0.f)) gv[e] = 0.f;
+      if (!(fmaf(zv[e], cp.sc[e], cp.sf[e]) > 0.f)) gv[e] = 0.f;
   }
 }
 
@@ -139,15 +166,14 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const T* __restrict__ g, lo
   for (int e = 0; e < V; ++e) { sg[e] = 0.f; sgx[e] = 0.f; sx[e] = 0.f; }
   const int p0 = blockIdx.x * ppb, p1 = min(M, p0 + ppb);
   if (pl < rows) {
-    float mu[V], is[V];
-#pragma unroll
-    for (int e = 0; e < V; ++e) { mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
+    ChanParams<V> cp;
+    cp.load(c0, scale, shift, mean, invstd);
     for (int p = p0 + pl; p < p1; p += rows) {
       float gv[V], zv[V];
-      bn_bwd_load(g, ldg, z, ldz, p, c0, C, scale, shift, act, drop, HW, gv, zv);
+      bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const float xh = (zv[e] - mu[e]) * is[e];
+        const float xh = (zv[e] - cp.mu[e]) * cp.is[e];
         sg[e] += gv[e];
         sgx[e] = fmaf(gv[e], xh, sgx[e]);
         sx[e] += xh;
@@ -169,15 +195,24 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const T* __restrict__ g, lo
   }
 }
 
-__global__ void bn_bwd_finalize(const float* __restrict__ part, int nblk, int M, int C, const float* gamma,
-                                const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+__global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ part, int nblk, int M, int C,
+                                                      const float* gamma, const float* invstd, float* dgamma,
+                                                      float* dbeta, float* dbias, float* coef) {
+  __shared__ double sh[3][4][64];
+  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   double a = 0.0, b = 0.0, d = 0.0;
-  for (int k = 0; k < nblk; ++k) {
-    const float* o = part + (long long)k * 3 * C;
-    a += o[c]; b += o[C + c]; d += o[2 * C + c];
-  }
+  if (c < C)
+    for (int k = r; k < nblk; k += 4) {
+      const float* o = part + (long long)k * 3 * C;
+      a += o[c]; b += o[C + c]; d += o[2 * C + c];
+    }
+  sh[0][r][cl] = a; sh[1][r][cl] = b; sh[2][r][cl] = d;
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
+  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+  d = sh[2][0][cl] + sh[2][1][cl] + sh[2][2][cl] + sh[2][3][cl];
   const float gm = gamma ? gamma[c] : 1.f;
   const float k1 = gm * invstd[c];
   const float k2 = (float)(k1 * b / M);
@@ -196,19 +231,23 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const T* __restrict__ g, long
                                                    long long lddz) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const long long total = (long long)M * tpp;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int p = (int)(i / tpp), ch = (int)(i % tpp);
-    const int c0 = ch * V;
+  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const int c0 = (int)(gt % tpp) * V;
+  const long long pstride = (long long)gridDim.x * NT / tpp;
+  ChanParams<V> cp;
+  cp.load(c0, scale, shift, mean, invstd);
+  float k1[V], k2[V], k3[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { k1[e] = coef[c0 + e]; k2[e] = coef[C + c0 + e]; k3[e] = coef[2 * C + c0 + e]; }
+  for (long long p = gt / tpp; p < M; p += pstride) {
     float gv[V], zv[V];
-    bn_bwd_load(g, ldg, z, ldz, p, c0, C, scale, shift, act, drop, HW, gv, zv);
+    bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int c = c0 + e;
-      const float xh = (zv[e] - mean[c]) * invstd[c];
-      gv[e] = coef[c] * gv[e] - coef[C + c] * xh - coef[2 * C + c];
+      const float xh = (zv[e] - cp.mu[e]) * cp.is[e];
+      gv[e] = k1[e] * gv[e] - k2[e] * xh - k3[e];
     }
-    stv(dz + (long long)p * lddz + c0, gv);
+    stv(dz + p * lddz + c0, gv);
   }
 }
 
@@ -225,7 +264,7 @@ int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, 
   const int ppb = dg_cdiv(M, nblk);
   hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)z, ldz, M, C, ppb, (float*)ws);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_finalize<T>, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, (const T*)z, (const float*)ws,
+  hipLaunchKernelGGL(bn_stats_finalize<T>, dim3(dg_cdiv(C, 64)), dim3(NT), 0, st, (const T*)z, (const float*)ws,
                      nblk, M, C, gamma, beta, rm, rv, momentum, eps, smean, sinv, scale, shift);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -243,7 +282,7 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
   hipLaunchKernelGGL(bn_bwd_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C, ppb,
                      mean, inv, scale, shift, act, drop, HW, part);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, part, nblk, M, C, gamma, inv, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 64)), dim3(NT), 0, st, part, nblk, M, C, gamma, inv, dgamma,
                      dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
@@ -260,8 +299,10 @@ extern "C" int64_t dg_bn_workspace(int M, int C) {
   return ((int64_t)bn_nblk(M) * 3 + 3) * C * 4;
 }
 
-#define BN_SHAPE_OK(dtype, C, ld) \
-  ((C) % (dtype == DG_BF16 ? 8 : 4) == 0 && (C) / (dtype == DG_BF16 ? 8 : 4) <= NT && (ld) % (dtype == DG_BF16 ? 8 : 4) == 0)
+// C/V must divide NT (power of two <= 256): every thread then owns one channel chunk.
+#define BN_SHAPE_OK(dtype, C, ld)                                                        \
+  ((C) % (dtype == DG_BF16 ? 8 : 4) == 0 && NT % ((C) / (dtype == DG_BF16 ? 8 : 4)) == 0 && \
+   (ld) % (dtype == DG_BF16 ? 8 : 4) == 0)
 
 extern "C" int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C, const float* gamma,
                                const float* beta, float* running_mean, float* running_var, float momentum, float eps,

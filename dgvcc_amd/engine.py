@@ -241,11 +241,15 @@ class _PlanFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, plan, fwd, n_in, *tensors):
+        ctx.set_materialize_grads(False)  # unused outputs -> None, not zero tensors
         ctx.plan = plan
         ctx.n_in = n_in
         ctx.params = tensors[n_in:]
         ctx.tape = {}
         outs = fwd(*tensors[:n_in], tape=ctx.tape)
+        nd = getattr(plan, "nondiff", ())
+        if nd:
+            ctx.mark_non_differentiable(*[outs[i] for i in nd])
         return outs
 
     @staticmethod
@@ -330,3 +334,349 @@ class DensityPlan:
         if gb is not None:
             grads[self.head_b] = gb
         return (g_ycat,), grads
+
+
+# ---------------------------------------------------------------------------
+# Memory read (DGModel_mem.forward_mem, models/models.py:116-125) on NHWC:
+#   logits[px][slot] = y[px] . mem[:, slot] / sqrt(k)   (1x1 conv, Cout = 1024)
+#   P = softmax over slots ; y_new[px][k] = sum_slot P[px][slot] mem[k][slot]
+# ---------------------------------------------------------------------------
+class MemRead:
+    def __init__(self, mem: nn.Parameter):
+        self.mem = mem  # [1, k, slots]
+
+    def packs(self, dt):
+        m = self.mem.detach()[0]  # [k, slots]
+        k, S = m.shape
+        scale = 1.0 / float(k) ** 0.5
+        memT_s = K.pack_weight((m.t() * scale).contiguous().view(S, k, 1, 1), dt)  # logits GEMM
+        mem_p = K.pack_weight(m.contiguous().view(k, S, 1, 1), dt)                 # y_new GEMM
+        return memT_s, mem_p, scale
+
+    def logits(self, y: Act, memT_s, dt):
+        S = self.mem.shape[2]
+        L = Act(K.nhwc(y.N, y.H, y.W, S, dt, y.buf.device))
+        K.conv_fwd(y, memT_s, S, 1, 0, L)
+        return L
+
+    def readout(self, P: Act, mem_p, dt):
+        k = self.mem.shape[1]
+        yn = Act(K.nhwc(P.N, P.H, P.W, k, dt, P.buf.device))
+        K.conv_fwd(P, mem_p, k, 1, 0, yn)
+        return yn
+
+    def bwd_readout(self, g_yn: Act, P: Act, dt):
+        """g_P = g_yn . mem ; dmem_a[k][slot] = sum_px g_yn[px][k] P[px][slot]."""
+        m = self.mem.detach()[0]
+        k, S = m.shape
+        memT = K.pack_weight(m.t().contiguous().view(S, k, 1, 1), dt)
+        gP = Act(K.nhwc(P.N, P.H, P.W, S, dt, P.buf.device))
+        K.conv_fwd(g_yn, memT, S, 1, 0, gP)
+        dmem = torch.empty((k, S, 1, 1), dtype=torch.float32, device=P.buf.device)
+        K.conv_wgrad(P, g_yn, 1, 0, dmem)
+        return gP, dmem.view(k, S)
+
+    def bwd_logits(self, gL: Act, y: Act, mem_p, scale, dt):
+        """g_y = gL . mem^T * scale ; dmem_b[k][slot] = scale * sum_px y[px][k] gL[px][slot]."""
+        k, S = self.mem.shape[1], self.mem.shape[2]
+        gy = Act(K.nhwc(y.N, y.H, y.W, k, dt, y.buf.device))
+        m_s = K.pack_weight((self.mem.detach()[0] * scale).contiguous().view(k, S, 1, 1), dt)
+        K.conv_fwd(gL, m_s, k, 1, 0, gy)
+        dmem = torch.empty((k, S, 1, 1), dtype=torch.float32, device=y.buf.device)
+        K.conv_wgrad(gL, y, 1, 0, dmem)
+        return gy, dmem.view(k, S) * scale
+
+
+class _Heads:
+    """Shared pieces after forward_fe for the DGModel_* family (models/models.py:98-335)."""
+
+    def __init__(self, model, mem: bool, cls: bool):
+        dd = model.den_dec[0]
+        self.den = ConvLayer(dd.conv, dd.bn, ACT_RELU)
+        self.den_drop_module = next((m for m in model.den_dec if isinstance(m, nn.Dropout2d)), None)
+        hc = model.den_head[0].conv
+        self.head_w, self.head_b = hc.weight, hc.bias
+        self.head_act = K.ACT_RELU if model.den_head[0].relu is not None else K.ACT_NONE
+        self.memr = MemRead(model.mem) if mem else None
+        self.cls = None
+        if cls:
+            c0 = model.cls_head[0]
+            self.cls = ConvLayer(c0.conv, c0.bn, ACT_RELU)
+            self.cls_drop_module = model.cls_head[1]
+            self.cls_w = model.cls_head[2].conv.weight
+            self.cls_b = model.cls_head[2].conv.bias
+        self.model = model
+
+    def params(self):
+        ps = self.den.params() + [self.head_w] + ([self.head_b] if self.head_b is not None else [])
+        if self.memr is not None:
+            ps.append(self.memr.mem)
+        if self.cls is not None:
+            ps += self.cls.params() + [self.cls_w] + ([self.cls_b] if self.cls_b is not None else [])
+        return ps
+
+    # --- pieces ---------------------------------------------------------------
+    def head(self, y: Act):
+        hb = self.head_b.detach() if self.head_b is not None else None
+        return K.head_fwd(y, self.head_w.detach().reshape(-1), hb, self.head_act)
+
+    def head_bwd(self, y: Act, yh, g_h, grads):
+        g_y = Act(torch.empty_like(y.buf))
+        gw = torch.empty(y.C, dtype=torch.float32, device=y.buf.device)
+        gb = torch.empty(1, dtype=torch.float32, device=y.buf.device) if self.head_b is not None else None
+        K.head_bwd(y, self.head_w.detach().reshape(-1), self.head_act, yh, g_h, g_y, gw, gb)
+        _acc(grads, self.head_w, gw.view_as(self.head_w))
+        if gb is not None:
+            _acc(grads, self.head_b, gb)
+        return g_y
+
+    def cls_fwd(self, x3: torch.Tensor, training, tape, key):
+        N, h, w, _ = x3.shape
+        drop = dropout2d_mask(N, self.cls.Cout, self.cls_drop_module.p, x3.device) \
+            if training and self.cls_drop_module.p > 0 else None
+        a = Act(K.nhwc(N, h, w, self.cls.Cout, x3.dtype, x3.device))
+        sub = {} if tape is not None else None
+        self.cls.forward(Act(x3), a, training, sub, drop=drop)
+        cb = self.cls_b.detach() if self.cls_b is not None else None
+        c = K.head_fwd(a, self.cls_w.detach().reshape(-1), cb, K.ACT_SIGMOID)
+        if tape is not None:
+            tape[key] = (sub, a, c, x3.shape, x3.dtype)
+        return c  # [N, h, w] f32
+
+    def cls_bwd(self, tape, key, g_c, grads):
+        sub, a, c, shape, dt = tape.pop(key)
+        g_a = Act(torch.empty_like(a.buf))
+        gw = torch.empty(a.C, dtype=torch.float32, device=a.buf.device)
+        gb = torch.empty(1, dtype=torch.float32, device=a.buf.device) if self.cls_b is not None else None
+        K.head_bwd(a, self.cls_w.detach().reshape(-1), K.ACT_SIGMOID, c,
+                   g_c.contiguous().view(c.shape).float(), g_a, gw, gb)
+        _acc(grads, self.cls_w, gw.view_as(self.cls_w))
+        if gb is not None:
+            _acc(grads, self.cls_b, gb)
+        g_x3 = torch.empty(shape, dtype=dt, device=a.buf.device)
+        for p, g in self.cls.backward(sub, g_a, Act(g_x3)).items():
+            _acc(grads, p, g)
+        return g_x3
+
+
+def _acc(grads, p, g):
+    if p in grads:
+        grads[p] = grads[p] + g
+    else:
+        grads[p] = g
+
+
+def _up4(x_small: torch.Tensor, N, h, w):
+    d = torch.empty((N, 4 * h, 4 * w, 1), dtype=torch.float32, device=x_small.device)
+    K.upsample_fwd(Act(x_small.reshape(N, h, w, 1)), 4, K.UP_BILINEAR, Act(d))
+    return d.view(N, 1, 4 * h, 4 * w)
+
+
+def _up4_bwd(g: torch.Tensor, N, h, w):
+    gs = torch.empty((N, h, w, 1), dtype=torch.float32, device=g.device)
+    K.upsample_bwd(Act(g.contiguous().view(N, 4 * h, 4 * w, 1)), 4, K.UP_BILINEAR, Act(gs))
+    return gs.view(N, h, w)
+
+
+class SinglePlan(_Heads):
+    """`.forward` of DGModel_mem / cls / memcls / final (and base via mem=cls=False):
+    ycat, x3 (NHWC) [, c_gt] -> d  or  (dc, c)."""
+
+    def forward(self, ycat, x3, c_gt, training, tape=None):
+        N, h, w, _ = ycat.shape
+        dt, dev = ycat.dtype, ycat.device
+        p = self.den_drop_module.p if (self.den_drop_module is not None and training) else 0.0
+        drop = dropout2d_mask(N, self.den.Cout, p, dev)
+        sub = {} if tape is not None else None
+        yden = Act(K.nhwc(N, h, w, self.den.Cout, dt, dev))
+        self.den.forward(Act(ycat), yden, training, sub, drop=drop)
+        st = {"sub": sub, "yden": yden, "shape": ycat.shape}
+        y = yden
+        if self.memr is not None:
+            memT_s, mem_p, scale = self.memr.packs(dt)
+            L = self.memr.logits(yden, memT_s, dt)
+            P = Act(torch.empty_like(L.buf))
+            K.call("dg_softmax_fwd", L.dt, L.ptr, L.M, L.C, P.ptr, K.stream())
+            y = self.memr.readout(P, mem_p, dt)
+            st.update(P=P, ynew=y, mem_p=mem_p, scale=scale)
+        yh = self.head(y)
+        st["yh"] = yh
+        if self.cls is None:
+            out = _up4(yh, N, h, w)
+            outs = out
+        else:
+            c = self.cls_fwd(x3, training, sub, "cls")
+            cres = torch.empty((N, h, w), dtype=torch.float32, device=dev)
+            cg = c_gt.float().contiguous() if c_gt is not None else None
+            K.call("dg_cls_combine", K.ptr(c), None, K.ptr(cg), N, h // 4, w // 4, 4,
+                   float(self.model.cls_thrs), K.ptr(cres), None, K.stream())
+            prod = torch.empty_like(yh)
+            K.call("dg_mul_f32", K.ptr(yh), K.ptr(cres), yh.numel(), K.ptr(prod), K.stream())
+            st["cres"] = cres
+            outs = (_up4(prod, N, h, w), c.view(N, 1, h // 4, w // 4))
+        if tape is not None:
+            tape[self] = st
+        return outs
+
+    def backward(self, tape, *gouts):
+        st = tape.pop(self)
+        sub = st["sub"]
+        N, h, w, Cy = st["shape"]
+        grads = {}
+        g_d = gouts[0]
+        g_x3 = None
+        if g_d is not None:
+            g_h = _up4_bwd(g_d, N, h, w)
+            if self.cls is not None:
+                K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
+            y = st.get("ynew", st["yden"])
+            g_y = self.head_bwd(y, st["yh"], g_h, grads)
+            if self.memr is not None:
+                dt = y.buf.dtype
+                gP, dmem_a = self.memr.bwd_readout(g_y, st["P"], dt)
+                gL = Act(torch.empty_like(gP.buf))
+                K.call("dg_softmax_bwd", gP.dt, st["P"].ptr, gP.ptr, gP.M, gP.C, gL.ptr, K.stream())
+                g_y, dmem_b = self.memr.bwd_logits(gL, st["yden"], st["mem_p"], st["scale"], dt)
+                _acc(grads, self.memr.mem, (dmem_a + dmem_b).view_as(self.memr.mem))
+            g_ycat = torch.empty(st["shape"], dtype=y.buf.dtype, device=y.buf.device)
+            for p, g in self.den.backward(sub, g_y, Act(g_ycat)).items():
+                _acc(grads, p, g)
+        else:
+            g_ycat = None
+        if self.cls is not None and len(gouts) > 1 and gouts[1] is not None:
+            g_x3 = self.cls_bwd(sub, "cls", gouts[1], grads)
+        return (g_ycat, g_x3), grads
+
+
+class PairPlan(_Heads):
+    """forward_train of DGModel_memadd (cls=False) and DGModel_final (cls=True)
+    (models/models.py:147-184, 298-335): two views, e_mask from instance norms,
+    functional Dropout2d (always on), memory read, JSD-MSE consistency loss."""
+
+    def __init__(self, model, cls: bool):
+        super().__init__(model, mem=True, cls=cls)
+        # final: (dc1, dc2, c1, c2, c_err, loss_con); memadd: (d1, d2, loss_con)
+        self.nondiff = (4,) if cls else ()
+
+    def forward(self, ycat1, ycat2, x3_1, x3_2, c_gt, p_drop, err_thrs, tape=None):
+        N, h, w, _ = ycat1.shape
+        HW = h * w
+        dt, dev = ycat1.dtype, ycat1.device
+        training = True
+        sub = {} if tape is not None else None
+        C = self.den.Cout
+        y1 = Act(K.nhwc(N, h, w, C, dt, dev))
+        y2 = Act(K.nhwc(N, h, w, C, dt, dev))
+        s1 = {} if tape is not None else None
+        s2 = {} if tape is not None else None
+        self.den.forward(Act(ycat1), y1, training, s1)
+        self.den.forward(Act(ycat2), y2, training, s2)
+        # instance-norm statistics -> e_mask (detached) -> masked, dropped features
+        stats = torch.empty((4, N * C), dtype=torch.float32, device=dev)
+        ws = K.query("dg_instnorm_workspace", N, HW, C)
+        work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
+        K.call("dg_instnorm_stats", y1.dt, y1.ptr, y1.ld, N, HW, C, 1e-5, K.ptr(stats[0]),
+               K.ptr(stats[1]), K.ptr(work), K.stream())
+        K.call("dg_instnorm_stats", y2.dt, y2.ptr, y2.ld, N, HW, C, 1e-5, K.ptr(stats[2]),
+               K.ptr(stats[3]), K.ptr(work), K.stream())
+        d1 = dropout2d_mask(N, C, p_drop, dev)
+        d2 = dropout2d_mask(N, C, p_drop, dev)
+        m1 = Act(K.nhwc(N, h, w, C, dt, dev))
+        m2 = Act(K.nhwc(N, h, w, C, dt, dev))
+        mask = torch.empty((N * HW * C,), dtype=torch.uint8, device=dev)
+        K.call("dg_emask_fwd", y1.dt, y1.ptr, y2.ptr, y1.ld, N, HW, C, K.ptr(stats[0]), K.ptr(stats[1]),
+               K.ptr(stats[2]), K.ptr(stats[3]), float(err_thrs), K.ptr(d1), K.ptr(d2), m1.ptr, m2.ptr,
+               K.ptr(mask), K.stream())
+        # memory read, both views, + consistency loss
+        memT_s, mem_p, scale = self.memr.packs(dt)
+        L1 = self.memr.logits(m1, memT_s, dt)
+        L2 = self.memr.logits(m2, memT_s, dt)
+        P1, P2 = Act(torch.empty_like(L1.buf)), Act(torch.empty_like(L2.buf))
+        loss_con = torch.empty((), dtype=torch.float32, device=dev)
+        ws = K.query("dg_softmax_workspace", L1.M)
+        work2 = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
+        K.call("dg_softmax_pair_fwd", L1.dt, L1.ptr, L2.ptr, L1.M, L1.C, P1.ptr, P2.ptr, K.ptr(loss_con),
+               K.ptr(work2), K.stream())
+        yn1 = self.memr.readout(P1, mem_p, dt)
+        yn2 = self.memr.readout(P2, mem_p, dt)
+        yh1, yh2 = self.head(yn1), self.head(yn2)
+        st = dict(s1=s1, s2=s2, shape=ycat1.shape, mask=mask, d1=d1, d2=d2, m1=m1, m2=m2, P1=P1,
+                  P2=P2, yn1=yn1, yn2=yn2, yh1=yh1, yh2=yh2, mem_p=mem_p, scale=scale)
+        if self.cls is None:
+            outs = (_up4(yh1, N, h, w), _up4(yh2, N, h, w), loss_con)
+        else:
+            c1 = self.cls_fwd(x3_1, training, sub, "c1")
+            c2 = self.cls_fwd(x3_2, training, sub, "c2")
+            cres = torch.empty((N, h, w), dtype=torch.float32, device=dev)
+            cerr = torch.empty((N, h, w), dtype=torch.float32, device=dev)
+            cg = c_gt.float().contiguous() if c_gt is not None else None
+            K.call("dg_cls_combine", K.ptr(c1), K.ptr(c2), K.ptr(cg), N, h // 4, w // 4, 4,
+                   float(self.model.cls_thrs), K.ptr(cres), K.ptr(cerr), K.stream())
+            p1, p2 = torch.empty_like(yh1), torch.empty_like(yh2)
+            K.call("dg_mul_f32", K.ptr(yh1), K.ptr(cres), yh1.numel(), K.ptr(p1), K.stream())
+            K.call("dg_mul_f32", K.ptr(yh2), K.ptr(cres), yh2.numel(), K.ptr(p2), K.stream())
+            st.update(cres=cres, sub=sub)
+            outs = (_up4(p1, N, h, w), _up4(p2, N, h, w), c1.view(N, 1, h // 4, w // 4),
+                    c2.view(N, 1, h // 4, w // 4), _up4(cerr, N, h, w), loss_con)
+        if tape is not None:
+            tape[self] = st
+        return outs
+
+    def backward(self, tape, *gouts):
+        st = tape.pop(self)
+        N, h, w, Cy = st["shape"]
+        HW = h * w
+        grads = {}
+        if self.cls is None:
+            g_d1, g_d2, g_con = gouts
+            g_c1 = g_c2 = None
+        else:
+            g_d1, g_d2, g_c1, g_c2, _g_cerr, g_con = gouts
+        dt = st["m1"].buf.dtype
+        dev = st["m1"].buf.device
+        C = self.den.Cout
+
+        def head_path(g_d, yh, yn):
+            if g_d is None:
+                return None
+            g_h = _up4_bwd(g_d, N, h, w)
+            if self.cls is not None:
+                K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
+            return self.head_bwd(yn, yh, g_h, grads)
+
+        g_yn1 = head_path(g_d1, st["yh1"], st["yn1"])
+        g_yn2 = head_path(g_d2, st["yh2"], st["yn2"])
+        gP1 = gP2 = None
+        dmem = torch.zeros((C, self.memr.mem.shape[2]), dtype=torch.float32, device=dev)
+        if g_yn1 is not None:
+            gP1, da = self.memr.bwd_readout(g_yn1, st["P1"], dt)
+            dmem += da
+        if g_yn2 is not None:
+            gP2, da = self.memr.bwd_readout(g_yn2, st["P2"], dt)
+            dmem += da
+        P1, P2 = st["P1"], st["P2"]
+        gL1, gL2 = Act(torch.empty_like(P1.buf)), Act(torch.empty_like(P2.buf))
+        coef = g_con.float().reshape(1).contiguous() if g_con is not None else None
+        K.call("dg_softmax_pair_bwd", P1.dt, P1.ptr, P2.ptr, gP1.ptr if gP1 is not None else None,
+               gP2.ptr if gP2 is not None else None, P1.M, P1.C, K.ptr(coef), gL1.ptr, gL2.ptr, K.stream())
+        g_m1, db1 = self.memr.bwd_logits(gL1, st["m1"], st["mem_p"], st["scale"], dt)
+        g_m2, db2 = self.memr.bwd_logits(gL2, st["m2"], st["mem_p"], st["scale"], dt)
+        dmem += db1 + db2
+        _acc(grads, self.memr.mem, dmem.view_as(self.memr.mem))
+        g_y1 = Act(K.nhwc(N, h, w, C, dt, dev))
+        g_y2 = Act(K.nhwc(N, h, w, C, dt, dev))
+        K.call("dg_emask_bwd", g_m1.dt, g_m1.ptr, g_m2.ptr, N, HW, C, K.ptr(st["mask"]), K.ptr(st["d1"]),
+               K.ptr(st["d2"]), g_y1.ptr, g_y2.ptr, g_y1.ld, K.stream())
+        g_ycat1 = torch.empty(st["shape"], dtype=dt, device=dev)
+        g_ycat2 = torch.empty(st["shape"], dtype=dt, device=dev)
+        for p, g in self.den.backward(st["s1"], g_y1, Act(g_ycat1)).items():
+            _acc(grads, p, g)
+        for p, g in self.den.backward(st["s2"], g_y2, Act(g_ycat2)).items():
+            _acc(grads, p, g)
+        g_x3_1 = g_x3_2 = None
+        if self.cls is not None:
+            if g_c1 is not None:
+                g_x3_1 = self.cls_bwd(st["sub"], "c1", g_c1, grads)
+            if g_c2 is not None:
+                g_x3_2 = self.cls_bwd(st["sub"], "c2", g_c2, grads)
+        return (g_ycat1, g_ycat2, g_x3_1, g_x3_2), grads

@@ -190,3 +190,160 @@ class DGModel_base(_DGBase):
     def forward(self, x):
         ycat, _ = self._forward_fe_nhwc(x)
         return self._density(ycat)
+
+
+class DGModel_mem(DGModel_base):
+    """reference models/models.py:98-136 (memory read after den_dec)."""
+
+    def __init__(self, pretrained=True, mem_size=1024, mem_dim=256, den_dropout=0.5):
+        super().__init__(pretrained, den_dropout)
+        self.mem_size = mem_size
+        self.mem_dim = mem_dim
+        self.mem = nn.Parameter(torch.FloatTensor(1, self.mem_dim, self.mem_size).normal_(0.0, 1.0))
+        self.den_dec = nn.Sequential(
+            ConvBlock(512 + 256 + 128, self.mem_dim, kernel_size=1, padding=0, bn=True),
+            nn.Dropout2d(p=den_dropout))
+        self.den_head = nn.Sequential(ConvBlock(self.mem_dim, 1, kernel_size=1, padding=0))
+
+    _USE_MEM, _USE_CLS = True, False
+
+    def _build_head_plans(self, plans):
+        plans["single"] = E.SinglePlan(self, mem=self._USE_MEM, cls=self._USE_CLS)
+        if hasattr(self, "forward_train"):
+            plans["pair"] = E.PairPlan(self, cls=self._USE_CLS)
+
+    def forward_mem(self, y):
+        """NCHW y -> (y_new NCHW, logits [b, mem_size, h*w]) (models/models.py:116-125)."""
+        from .. import kernels as K
+        b, k, h, w = y.shape
+        plan = self._get_plans()["single"]
+        dt = self.compute_dtype
+        ya = K.Act(y.detach().permute(0, 2, 3, 1).contiguous().to(dt))
+        memT_s, mem_p, _ = plan.memr.packs(dt)
+        L = plan.memr.logits(ya, memT_s, dt)
+        P = K.Act(torch.empty_like(L.buf))
+        K.call("dg_softmax_fwd", L.dt, L.ptr, L.M, L.C, P.ptr, K.stream())
+        yn = plan.memr.readout(P, mem_p, dt)
+        return yn.buf.permute(0, 3, 1, 2), L.buf.view(b, h * w, -1).transpose(1, 2)
+
+    def _single(self, ycat, x3, c_gt=None):
+        plan = self._get_plans()["single"]
+
+        def fwd(yc, x, tape):
+            return plan.forward(yc, x, c_gt, self.training, tape)
+
+        return E.run_plan(plan, fwd, (ycat, x3), plan.params())
+
+    def forward(self, x):
+        ycat, x3 = self._forward_fe_nhwc(x)
+        return self._single(ycat, x3)
+
+
+class _PairMixin:
+    def jsd(self, logits1, logits2):
+        """mean((softmax(l1) - softmax(l2))^2) over the slot axis (models/models.py:147-157)."""
+        import torch.nn.functional as F
+        return F.mse_loss(F.softmax(logits1, dim=1), F.softmax(logits2, dim=1))
+
+    def _pair(self, img1, img2, c_gt):
+        ycat1, x3_1 = self._forward_fe_nhwc(img1)
+        ycat2, x3_2 = self._forward_fe_nhwc(img2)
+        plan = self._get_plans()["pair"]
+        p = float(self.den_dropout)
+        thr = float(self.err_thrs)
+
+        def fwd(y1, y2, a, b, tape):
+            return plan.forward(y1, y2, a, b, c_gt, p, thr, tape)
+
+        return E.run_plan(plan, fwd, (ycat1, ycat2, x3_1, x3_2), plan.params())
+
+
+class DGModel_memadd(_PairMixin, DGModel_mem):
+    """reference models/models.py:138-184."""
+
+    def __init__(self, pretrained=True, mem_size=1024, mem_dim=256, den_dropout=0.5, err_thrs=0.5):
+        super().__init__(pretrained, mem_size, mem_dim, den_dropout)
+        self.err_thrs = err_thrs
+        self.den_dec = nn.Sequential(ConvBlock(512 + 256 + 128, 256, kernel_size=1, padding=0, bn=True))
+
+    def forward_train(self, img1, img2):
+        d1, d2, loss_con = self._pair(img1, img2, None)
+        return d1, d2, loss_con
+
+
+def _cls_head(cls_dropout):
+    return nn.Sequential(
+        ConvBlock(512, 256, bn=True),
+        nn.Dropout2d(p=cls_dropout),
+        ConvBlock(256, 1, kernel_size=1, padding=0, relu=False),
+        nn.Sigmoid())
+
+
+class DGModel_cls(DGModel_base):
+    """reference models/models.py:186-228."""
+
+    def __init__(self, pretrained=True, den_dropout=0.5, cls_dropout=0.5, cls_thrs=0.5):
+        super().__init__(pretrained, den_dropout)
+        self.cls_dropout = cls_dropout
+        self.cls_thrs = cls_thrs
+        self.cls_head = _cls_head(self.cls_dropout)
+
+    def _build_head_plans(self, plans):
+        plans["single"] = E.SinglePlan(self, mem=False, cls=True)
+
+    def transform_cls_map_gt(self, c_gt):
+        return upsample(c_gt, scale_factor=4, mode="nearest")
+
+    def transform_cls_map_pred(self, c):
+        c_new = (c.detach() >= self.cls_thrs).to(c.dtype)
+        return upsample(c_new, scale_factor=4, mode="nearest")
+
+    def transform_cls_map(self, c, c_gt=None):
+        return self.transform_cls_map_gt(c_gt) if c_gt is not None else self.transform_cls_map_pred(c)
+
+    _single = DGModel_mem._single
+
+    def forward(self, x, c_gt=None):
+        ycat, x3 = self._forward_fe_nhwc(x)
+        return self._single(ycat, x3, c_gt)
+
+
+class DGModel_memcls(DGModel_mem):
+    """reference models/models.py:230-273."""
+
+    _USE_MEM, _USE_CLS = True, True
+
+    def __init__(self, pretrained=True, mem_size=1024, mem_dim=256, den_dropout=0.5, cls_dropout=0.5,
+                 cls_thrs=0.5):
+        super().__init__(pretrained, mem_size, mem_dim, den_dropout)
+        self.cls_dropout = cls_dropout
+        self.cls_thrs = cls_thrs
+        self.cls_head = _cls_head(self.cls_dropout)
+
+    transform_cls_map_gt = DGModel_cls.transform_cls_map_gt
+    transform_cls_map_pred = DGModel_cls.transform_cls_map_pred
+    transform_cls_map = DGModel_cls.transform_cls_map
+
+    def forward(self, x, c_gt=None):
+        ycat, x3 = self._forward_fe_nhwc(x)
+        return self._single(ycat, x3, c_gt)
+
+
+class DGModel_final(_PairMixin, DGModel_memcls):
+    """reference models/models.py:275-335."""
+
+    def __init__(self, pretrained=True, mem_size=1024, mem_dim=256, cls_thrs=0.5, err_thrs=0.5, den_dropout=0.5,
+                 cls_dropout=0.5, has_err_loss=False):
+        super().__init__(pretrained, mem_size, mem_dim, den_dropout, cls_dropout, cls_thrs)
+        self.err_thrs = err_thrs
+        self.has_err_loss = has_err_loss
+        self.den_dec = nn.Sequential(
+            ConvBlock(512 + 256 + 128, self.mem_dim, kernel_size=1, padding=0, bn=True))
+
+    def forward_train(self, img1, img2, c_gt=None):
+        if self.has_err_loss:
+            raise NotImplementedError("has_err_loss=True (L1 between instance norms) is not on the HIP path")
+        if c_gt is None:
+            raise ValueError("DGModel_final.forward_train needs c_gt (the block map)")
+        dc1, dc2, c1, c2, c_err, loss_con = self._pair(img1, img2, c_gt)
+        return dc1, dc2, c1, c2, c_err, loss_con, 0

@@ -11,9 +11,9 @@ update — the only collective on the hot path.
 from __future__ import annotations
 
 import torch
-import torch.distributed as dist
 
 from . import kernels as K
+from .dist import average_flat_
 from ._capi import call, ptr, stream
 
 
@@ -77,10 +77,8 @@ class AdamW(torch.optim.Optimizer):
                 continue
             self._gather(group)
             g = group["_g"]
-            if self.allreduce and dist.is_available() and dist.is_initialized() \
-                    and dist.get_world_size() > 1:
-                dist.all_reduce(g)
-                g.div_(dist.get_world_size())
+            if self.allreduce:
+                average_flat_(g)
             group["_step"] += 1
             b1, b2 = group["betas"]
             K.adamw_step(group["_flat"], g, group["_m"], group["_v"], group["lr"], b1, b2,

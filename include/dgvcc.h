@@ -122,6 +122,40 @@ int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, const float
                 const float* y, const float* gy, void* gx, int64_t ldgx, int accumulate_gx,
                 float* gw, float* gbias, void* workspace, void* stream);
 
+/* ---- two-view consistency + memory read ----------------------------------------
+ * DGModel_memadd/final.forward_train (models/models.py:147-184, 298-335) and
+ * forward_mem (models/models.py:116-125).  The memory GEMMs run on dg_conv_fwd /
+ * dg_conv_wgrad as 1x1 convolutions; these are the non-GEMM pieces. */
+int64_t dg_instnorm_workspace(int N, int HW, int C);
+/* F.instance_norm statistics (biased variance) per (n, c) over HW pixels. */
+int dg_instnorm_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float eps,
+                      float* mean, float* invstd, void* workspace, void* stream);
+/* e = |IN(y1) - IN(y2)| < thr (bytes, [N*HW][C]); m_v = y_v * e * drop_v[n][c] (dense). */
+int dg_emask_fwd(int dtype, const void* y1, const void* y2, int64_t ld, int N, int HW, int C,
+                 const float* mu1, const float* is1, const float* mu2, const float* is2, float thr,
+                 const float* drop1, const float* drop2, void* m1, void* m2, unsigned char* mask,
+                 void* stream);
+int dg_emask_bwd(int dtype, const void* gm1, const void* gm2, int N, int HW, int C,
+                 const unsigned char* mask, const float* drop1, const float* drop2, void* gy1,
+                 void* gy2, int64_t ldgy, void* stream);
+/* softmax over the C (1024) memory slots of each pixel row, both views, plus
+ * loss_con = mean((P1-P2)^2) (the `jsd`, models/models.py:286-296). */
+int64_t dg_softmax_workspace(int M);
+int dg_softmax_pair_fwd(int dtype, const void* L1, const void* L2, int M, int C, void* P1, void* P2,
+                        float* loss_con, void* workspace, void* stream);
+/* dL_v = P_v (g_v' - <P_v, g_v'>), g_1' = g_1 + k(P1-P2), g_2' = g_2 - k(P1-P2),
+ * k = 2*coef[0]/(M*C) with coef a device scalar (upstream grad of loss_con; may be NULL). */
+int dg_softmax_pair_bwd(int dtype, const void* P1, const void* P2, const void* G1, const void* G2,
+                        int M, int C, const float* coef, void* GL1, void* GL2, void* stream);
+int dg_softmax_fwd(int dtype, const void* L, int M, int C, void* P, void* stream);
+int dg_softmax_bwd(int dtype, const void* P, const void* G, int M, int C, void* GL, void* stream);
+/* class maps (models/models.py:196-207, 323-327): nearest x`scale` of thresholded
+ * c1/c2 and of c_gt; two-view: c_resized = clamp(gt + |c1b - c2b|, 0, 1), c_err;
+ * single view (c2 NULL): c_resized = cgt ? up(cgt) : up(c1 >= thr). */
+int dg_cls_combine(const float* c1, const float* c2, const float* cgt, int N, int h, int w, int scale,
+                   float thr, float* c_resized, float* c_err, void* stream);
+int dg_mul_f32(const float* a, const float* b, int64_t n, float* out, void* stream);
+
 /* ---- losses ------------------------------------------------------------------
  * nn.MSELoss()(pred, gt*log_para) (trainers/dgtrainer.py:57): loss (f32 scalar
  * on device) and optionally dpred = coef*2*(pred-gt*scale)/n. */

@@ -117,3 +117,15 @@ if __name__ == "__main__":
     if "final" in which:
         gen_train("final", "DGModel_final", {"den_dropout": 0.0, "cls_dropout": 0.0}, "final")
     print("fixtures written to", HERE)
+
+
+def gen_state_dict_keys():
+    """Key order + shapes of every DGModel_* state_dict (checkpoint interchange)."""
+    import json
+    rm = import_ref("models.models")
+    out = {}
+    for name in ("DGModel_base", "DGModel_mem", "DGModel_memadd", "DGModel_cls", "DGModel_memcls",
+                 "DGModel_final"):
+        m = getattr(rm, name)(pretrained=False)
+        out[name] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
+    json.dump(out, open(os.path.join(HERE, "state_dict_keys.json"), "w"))

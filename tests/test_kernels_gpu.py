@@ -123,9 +123,10 @@ def test_first_layer_im2col(dev):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("act", [0, 1])
-def test_bn_train_fwd_bwd(dev, dtype, act):
+@pytest.mark.parametrize("C,H,W", [(64, 12, 10), (256, 16, 16), (512, 8, 8), (1024, 6, 4), (128, 40, 33)])
+def test_bn_train_fwd_bwd(dev, dtype, act, C, H, W):
     K = _k()
-    N, H, W, C = 2, 12, 10, 64
+    N = 2
     g = torch.Generator().manual_seed(3)
     z = (torch.randn(N, C, H, W, generator=g) * 3 + 5)
     if dtype == torch.bfloat16:

@@ -1,0 +1,47 @@
+import os, sys, tempfile
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from oracle import dg_oracle as O
+from dgvcc_amd.models.models import DGModel_final
+from dgvcc_amd.losses import mse_loss
+from dgvcc_amd.losses.bce import binary_cross_entropy
+dev = torch.device("cuda")
+m = DGModel_final(pretrained=False, den_dropout=0.0, cls_dropout=0.0)
+sd0 = O.seeded_state_dict(m.state_dict()); m.load_state_dict(sd0)
+m = m.to(dev).set_precision("fp32").train()
+batch = O.synthetic_batch(2, 64, 64, seed=2112)
+i1, i2, (pts, dm, bm) = batch
+sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd0.items()}
+b64 = (i1.double(), i2.double(), (pts, dm.double(), bm.double()))
+which = sys.argv[1] if len(sys.argv) > 1 else "all"
+def loss_fn_ref(outs, gt, bmap):
+    dc1, dc2, c1, c2, c_err, lc, _ = outs
+    import torch.nn.functional as F
+    terms = {"den": F.mse_loss(dc1, gt) + F.mse_loss(dc2, gt), "cls": 10 * (F.binary_cross_entropy(c1, bmap) + F.binary_cross_entropy(c2, bmap)), "con": 10 * lc}
+    return terms
+for term in ["den", "cls", "con"]:
+    keys = O.trainable_keys(sd64)
+    sdr = {k: v.clone() for k, v in sd64.items()}
+    for k in keys: sdr[k].requires_grad_(True)
+    outs = O.final_forward(sdr, b64[0], b64[1], b64[2][2])
+    L = loss_fn_ref(outs, b64[2][1] * 1000, b64[2][2])[term]
+    ref = dict(zip(keys, torch.autograd.grad(L, [sdr[k] for k in keys], allow_unused=True)))
+    m.zero_grad()
+    m.load_state_dict(sd0)
+    dc1, dc2, c1, c2, ce, lc, _ = m.forward_train(i1.to(dev), i2.to(dev), bm.to(dev))
+    gt = dm.to(dev)
+    if term == "den": Lm = mse_loss(dc1, gt, 1000.0) + mse_loss(dc2, gt, 1000.0)
+    elif term == "cls": Lm = 10 * (binary_cross_entropy(c1, bm.to(dev)) + binary_cross_entropy(c2, bm.to(dev)))
+    else: Lm = 10 * lc
+    Lm.backward()
+    print(f"== term {term}: loss mine {Lm.item():.6g} ref {L.item():.6g}")
+    errs = []
+    for k, p in m.named_parameters():
+        r = ref.get(k)
+        if r is None or r.norm() == 0:
+            if p.grad is not None and p.grad.norm() > 0 and r is None: print("  extra grad", k)
+            continue
+        if p.grad is None: errs.append((9.9, k)); continue
+        errs.append((((p.grad.double().cpu() - r).norm() / r.norm()).item(), k))
+    errs.sort(reverse=True)
+    for e, k in errs[:10]: print(f"  {e:.2e} {k}")
