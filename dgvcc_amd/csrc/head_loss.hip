@@ -256,7 +256,97 @@ __global__ void dmap_fixed_kernel(const float* __restrict__ pts, const int64_t* 
   }
 }
 
+// ---------------------------------------------------------------- adaptive dmap
+// utils/dmap_gen.py:14-51: sigma_i = 0.1 * (d1 + d2 + d3) over the 4 nearest
+// points (KDTree query k=4 includes the point itself; duplicates count as 0),
+// sigma = 15 when the image has <= 3 points; truncate 4 -> radius int(4 sigma + 0.5).
+__global__ void knn_sigma_kernel(const float* __restrict__ pts, const int64_t* __restrict__ offsets, int N,
+                                 double* __restrict__ sigma) {
+  const long long total = offsets[N];
+  for (long long q = blockIdx.x * (long long)blockDim.x + threadIdx.x; q < total;
+       q += (long long)gridDim.x * blockDim.x) {
+    int lo = 0, hi = N;
+    while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (offsets[mid] <= q) lo = mid; else hi = mid; }
+    const long long p0 = offsets[lo], p1 = offsets[lo + 1];
+    if (p1 - p0 <= 3) { sigma[q] = 15.0; continue; }
+    const double x = pts[2 * q], y = pts[2 * q + 1];
+    double d[4] = {INFINITY, INFINITY, INFINITY, INFINITY};
+    for (long long j = p0; j < p1; ++j) {
+      const double dx = (double)pts[2 * j] - x, dy = (double)pts[2 * j + 1] - y;
+      double v = sqrt(dx * dx + dy * dy);
+      if (v < d[3]) {  // insertion into the sorted 4 smallest
+        int k = 3;
+        while (k > 0 && d[k - 1] > v) { d[k] = d[k - 1]; --k; }
+        d[k] = v;
+      }
+    }
+    sigma[q] = (d[1] + d[2] + d[3]) * 0.1;
+  }
+}
+
+// one block per point: separable stamp of radius int(4 sigma + 0.5), clipped
+__global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restrict__ pts,
+                                                           const int64_t* __restrict__ offsets, int N, int H, int W,
+                                                           const double* __restrict__ sigma, float* __restrict__ dmap) {
+  __shared__ double wd[2048];
+  __shared__ float wf[2048];
+  __shared__ double ssum;
+  const long long total = offsets[N];
+  for (long long q = blockIdx.x; q < total; q += gridDim.x) {
+    int lo = 0, hi = N;
+    while (hi - lo > 1) { const int mid = (lo + hi) >> 1; if (offsets[mid] <= q) lo = mid; else hi = mid; }
+    const float px = pts[2 * q], py = pts[2 * q + 1];
+    int r = (int)py, c = (int)px;
+    if (!(r < H && c < W)) continue;  // uniform per block
+    if (r < 0) r += H;
+    if (c < 0) c += W;
+    if (r < 0 || c < 0) continue;
+    const double sg = sigma[q];
+    int rad = (int)(4.0 * sg + 0.5);
+    if (rad > 1023) rad = 1023;
+    const int K = 2 * rad + 1;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double s = 0.0;
+      for (int i = -rad; i <= rad; ++i) s += exp(-0.5 / (sg * sg) * (double)i * i);
+      ssum = s;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < K; i += blockDim.x) {
+      const double v = exp(-0.5 / (sg * sg) * (double)(i - rad) * (i - rad)) / ssum;
+      wd[i] = v;
+      wf[i] = (float)v;
+    }
+    __syncthreads();
+    // only the in-frame part of the stamp
+    const int r0 = max(0, r - rad), r1 = min(H, r + rad + 1);
+    const int c0 = max(0, c - rad), c1 = min(W, c + rad + 1);
+    const int cw = c1 - c0;
+    float* img = dmap + (long long)lo * H * W;
+    const long long cells = (long long)(r1 - r0) * cw;
+    for (long long t = threadIdx.x; t < cells; t += blockDim.x) {
+      const int rr = r0 + (int)(t / cw), cc = c0 + (int)(t % cw);
+      const float v = (float)((double)wf[rr - r + rad] * wd[cc - c + rad]);
+      atomicAdd(img + (long long)rr * W + cc, v);
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" int dg_dmap_adaptive(const float* points, const int64_t* offsets, int N, int H, int W, double* sigma_ws,
+                                float* dmap, void* stream) {
+  DG_REQUIRE(offsets && dmap && sigma_ws && N > 0 && H > 0 && W > 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(dmap, 0, (size_t)N * H * W * 4, st) != hipSuccess) return DG_ERR_HIP;
+  if (!points) return DG_OK;
+  hipLaunchKernelGGL(knn_sigma_kernel, dim3(256), dim3(NT), 0, st, points, offsets, N, sigma_ws);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dmap_adaptive_kernel, dim3(2048), dim3(NT), 0, st, points, offsets, N, H, W,
+                     (const double*)sigma_ws, dmap);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
 
 extern "C" int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w, const float* bias,
                            int act, float* y, void* stream) {

@@ -40,6 +40,28 @@ def gaussian_filter_density_fixed_batch(points_list, H: int, W: int, sigma: floa
     return K.dmap_fixed(pts, offs, len(points_list), H, W, sigma, radius)
 
 
+def gaussian_filter_density_batch(points_list, H: int, W: int) -> torch.Tensor:
+    """Adaptive-sigma maps (k-NN sigma, truncate 4) for N images -> [N, H, W] on device."""
+    dev = points_list[0].device if len(points_list) and points_list[0].is_cuda else _device()
+    counts = [int(p.shape[0]) for p in points_list]
+    offs = torch.tensor(np.concatenate([[0], np.cumsum(counts)]), dtype=torch.int64, device=dev)
+    total = int(sum(counts))
+    pts = torch.cat([p.to(dev, torch.float32).reshape(-1, 2) for p in points_list]).contiguous() \
+        if total else torch.empty((0, 2), dtype=torch.float32, device=dev)
+    sig = torch.empty(max(total, 1), dtype=torch.float64, device=dev)
+    out = torch.empty((len(points_list), H, W), dtype=torch.float32, device=dev)
+    K.call("dg_dmap_adaptive", K.ptr(pts) if total else None, K.ptr(offs), len(points_list), H, W,
+           K.ptr(sig), K.ptr(out), K.stream())
+    return out
+
+
+def gaussian_filter_density(img, points):
+    """reference dmap_gen.py:14-51 (k-nearest-neighbour adaptive sigma)."""
+    H, W = int(img.shape[0]), int(img.shape[1])
+    pts = torch.as_tensor(np.asarray(points, dtype=np.float32).reshape(-1, 2))
+    return gaussian_filter_density_batch([pts.to(_device())], H, W)[0].cpu().numpy()
+
+
 def gaussian_filter_density_fixed(img, points):
     """reference dmap_gen.py:53-81: `img` only supplies the shape (rows, cols)."""
     H, W = int(img.shape[0]), int(img.shape[1])

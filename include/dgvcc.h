@@ -167,6 +167,21 @@ int64_t dg_reduce_workspace(int64_t n);
 int dg_bce_loss(const float* pred, const float* target, int64_t n, float* loss, float* dpred,
                 float grad_coef, void* workspace, void* stream);
 
+/* ---- Bayesian loss (losses/bl.py:5-91) ------------------------------------------
+ * points [total][2] (x, y) concatenated over images with offsets[B+1] (device
+ * int64); st_sizes[B]; targets [total]; density [B][G][G] (G = c_size/stride).
+ * loss (device scalar) = BL(points, st_sizes, targets, density); ddensity (may be
+ * NULL) = grad_coef[0] (device scalar, NULL = 1) * dloss/ddensity. */
+int64_t dg_bl_workspace(int B, int G, int64_t total_points);
+int dg_bl_loss(const float* points, const int64_t* offsets, int64_t total_points,
+               const float* st_sizes, const float* targets, const float* density, int B, int G,
+               float stride, float sigma, float bg_ratio, int use_bg, float* loss, float* ddensity,
+               const float* grad_coef, void* workspace, void* stream);
+/* Post_Prob posterior rows (n_b [+1 background]) x G^2 per image at prob + row_offsets[b]*G^2. */
+int dg_bl_prob(const float* points, const int64_t* offsets, int64_t total_points,
+               const float* st_sizes, int B, int G, float stride, float sigma, float bg_ratio,
+               int use_bg, const int64_t* row_offsets, float* prob, void* workspace, void* stream);
+
 /* ---- optimizer -----------------------------------------------------------------
  * torch.optim.AdamW step over one flat f32 buffer (main.py:85-86). */
 int dg_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
@@ -182,6 +197,12 @@ int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
  * radius 7 (15x15 normalized separable Gaussian, constant-0 borders). */
 int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
                   float sigma, int radius, float* dmap, void* stream);
+
+/* gaussian_filter_density (utils/dmap_gen.py:14-51): per-point sigma from the
+ * 3 nearest neighbours (0.1 * sum; 15 when <= 3 points), truncate 4.
+ * sigma_ws: caller workspace of total-points doubles (receives the sigmas). */
+int dg_dmap_adaptive(const float* points, const int64_t* offsets, int N, int H, int W,
+                     double* sigma_ws, float* dmap, void* stream);
 
 #ifdef __cplusplus
 }

@@ -44,3 +44,35 @@ def dmap_fixed(points, H: int, W: int, sigma: float = 4.0, radius: int | None = 
         c0, c1 = max(0, c - radius), min(W, c + radius + 1)
         den[r0:r1, c0:c1] += st[r0 - r + radius:r1 - r + radius, c0 - c + radius:c1 - c + radius]
     return den
+
+
+def dmap_adaptive(points, H: int, W: int) -> np.ndarray:
+    """utils/dmap_gen.py:14-51: sigma = 0.1 * (sum of the 3 nearest-neighbour
+    distances; brute force = the KDTree k=4 query incl. self), 15 for <= 3
+    points; truncate 4 -> radius int(4 sigma + 0.5); same per-axis float32 rounding."""
+    pts = np.asarray(points, dtype=np.float32).reshape(-1, 2)
+    den = np.zeros((H, W), dtype=np.float32)
+    n = len(pts)
+    if n == 0:
+        return den
+    p64 = pts.astype(np.float64)
+    for i in range(n):
+        r, c = int(pts[i, 1]), int(pts[i, 0])
+        if not (r < H and c < W):
+            continue
+        if n > 3:
+            d = np.sort(np.sqrt(((p64 - p64[i]) ** 2).sum(1)))[:4]
+            sigma = (d[1] + d[2] + d[3]) * 0.1
+        else:
+            sigma = 15.0
+        rad = int(4.0 * sigma + 0.5)
+        w = gauss1d(sigma, rad)
+        st = (w.astype(np.float32).astype(np.float64)[:, None] * w[None, :]).astype(np.float32)
+        if r < 0:
+            r += H
+        if c < 0:
+            c += W
+        r0, r1 = max(0, r - rad), min(H, r + rad + 1)
+        c0, c1 = max(0, c - rad), min(W, c + rad + 1)
+        den[r0:r1, c0:c1] += st[r0 - r + rad:r1 - r + rad, c0 - c + rad:c1 - c + rad]
+    return den

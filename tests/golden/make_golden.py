@@ -107,16 +107,6 @@ def gen_train(name, model_cls, kwargs, mode, B=2, H=64, W=64):
     np.savez_compressed(os.path.join(HERE, f"train_{name}.npz"), **out)
 
 
-if __name__ == "__main__":
-    torch.set_num_threads(8)
-    which = sys.argv[1:] or ["dmap", "base", "final"]
-    if "dmap" in which:
-        gen_dmap()
-    if "base" in which:
-        gen_train("simple_base", "DGModel_base", {"den_dropout": 0.0}, "simple")
-    if "final" in which:
-        gen_train("final", "DGModel_final", {"den_dropout": 0.0, "cls_dropout": 0.0}, "final")
-    print("fixtures written to", HERE)
 
 
 def gen_state_dict_keys():
@@ -129,3 +119,65 @@ def gen_state_dict_keys():
         m = getattr(rm, name)(pretrained=False)
         out[name] = [[k, list(v.shape)] for k, v in m.state_dict().items()]
     json.dump(out, open(os.path.join(HERE, "state_dict_keys.json"), "w"))
+
+
+def gen_bl():
+    """losses/bl.py BL on synthetic inputs: loss and d loss / d pre_density."""
+    blm = import_ref("losses.bl")
+    rng = np.random.default_rng(3)
+    out = {}
+    cases = [("g96_bg", 768, 8, 8.0, 1.0, True, [37, 0, 5]),
+             ("g96_nobg", 768, 8, 8.0, 1.0, False, [20, 1, 9]),
+             ("g32_bg", 32, 1, 4.0, 0.5, True, [12, 3])]
+    for name, c_size, stride, sigma, bgr, use_bg, ns in cases:
+        G = c_size // stride
+        pts = [torch.from_numpy(rng.uniform(0, c_size, (n, 2)).astype(np.float32)) for n in ns]
+        st = torch.from_numpy(rng.uniform(c_size * 0.8, c_size * 1.2, len(ns)).astype(np.float32))
+        tg = [torch.ones(n) for n in ns]
+        dens = torch.from_numpy(rng.uniform(0, 0.02, (len(ns), 1, G, G)).astype(np.float32)).requires_grad_(True)
+        loss = blm.BL(sigma, c_size, stride, bgr, use_bg, "cpu")(pts, st, tg, dens)
+        loss.backward()
+        pre = f"{name}__"
+        out[pre + "cfg"] = np.array([c_size, stride, sigma, bgr, float(use_bg)])
+        out[pre + "counts"] = np.array(ns)
+        out[pre + "points"] = np.concatenate([p.numpy().reshape(-1, 2) for p in pts]) if sum(ns) else np.zeros((0, 2), np.float32)
+        out[pre + "st"] = st.numpy()
+        out[pre + "dens"] = dens.detach().numpy()
+        out[pre + "loss"] = np.array([loss.item()])
+        out[pre + "grad"] = dens.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "bl.npz"), **out)
+
+
+
+
+def gen_dmap_adaptive():
+    dg = import_ref("utils.dmap_gen")
+    rng = np.random.default_rng(11)
+    out = {}
+    H, W = 64, 80
+    for name, pts in [("many", rng.uniform(0, [W, H], (25, 2))),
+                      ("dup", np.array([[10.5, 10.5], [10.5, 10.5], [30, 40], [31, 40], [60.2, 5.5]])),
+                      ("few", np.array([[5.0, 5.0], [70.0, 60.0]]))]:
+        pts = pts.astype(np.float32)
+        out[name + "__points"] = pts
+        out[name + "__dmap"] = dg.gaussian_filter_density(np.zeros((H, W)), pts).astype(np.float32)
+    out["shape"] = np.array([H, W])
+    np.savez_compressed(os.path.join(HERE, "dmap_adaptive.npz"), **out)
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["dmap", "base", "final", "bl", "keys", "dmap_adaptive"]
+    if "dmap" in which:
+        gen_dmap()
+    if "base" in which:
+        gen_train("simple_base", "DGModel_base", {"den_dropout": 0.0}, "simple")
+    if "final" in which:
+        gen_train("final", "DGModel_final", {"den_dropout": 0.0, "cls_dropout": 0.0}, "final")
+    if "bl" in which:
+        gen_bl()
+    if "keys" in which:
+        gen_state_dict_keys()
+    if "dmap_adaptive" in which:
+        gen_dmap_adaptive()
+    print("fixtures written to", HERE)

@@ -36,7 +36,9 @@ for term in ["den", "cls", "con"]:
     Lm.backward()
     print(f"== term {term}: loss mine {Lm.item():.6g} ref {L.item():.6g}")
     errs = []
+    P = dict(m.named_parameters())
     for k, p in m.named_parameters():
+        if k.endswith(".bias") and P[k[:-5] + ".weight"].dim() == 4: continue
         r = ref.get(k)
         if r is None or r.norm() == 0:
             if p.grad is not None and p.grad.norm() > 0 and r is None: print("  extra grad", k)
