@@ -96,23 +96,25 @@ class ConvTimer:
     def __init__(self):
         self.ev = {}
 
-    def __call__(self, kind, flops, launch):
+    def __call__(self, kind, flops, launch, nbytes=0.0):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
-        self.ev.setdefault(kind, []).append((s, e, flops))
+        self.ev.setdefault(kind, []).append((s, e, flops, nbytes))
 
     def summary(self, kinds):
         torch.cuda.synchronize()
-        ms = fl = 0.0
+        ms = fl = nb = 0.0
         n = 0
         for k in kinds:
-            for s, e, f in self.ev.get(k, []):
+            for s, e, f, b in self.ev.get(k, []):
                 ms += s.elapsed_time(e)
                 fl += f
+                nb += b
                 n += 1
+        self.nbytes = nb
         return ms, fl, n
 
 
@@ -196,6 +198,7 @@ def main():
     elapsed = time.perf_counter() - t0
     K.set_conv_timer(None)
     conv_ms, conv_flops, conv_launches = timer.summary(("fwd", "dgrad"))
+    conv_alg_bytes = timer.nbytes / max(conv_launches, 1)
     wg_ms, wg_flops, wg_launches = timer.summary(("wgrad",))
     if world > 1:
         import torch.distributed as dist
@@ -236,6 +239,8 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "conv_fwd_kernel (implicit-GEMM conv: forward + dgrad launches)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
+                     "algorithmic_bytes_per_launch": round(conv_alg_bytes),
+                     "algorithmic_flop_per_launch": round(conv_flops / max(conv_launches, 1)),
                      "launches_per_step": conv_launches // args.steps,
                      "avg_launch_us": round(conv_ms * 1e3 / max(conv_launches, 1), 2),
                      "kernel_ms_per_step": round(conv_ms / args.steps, 3),

@@ -76,11 +76,11 @@ def set_conv_timer(timer):
     _CONV_TIMER = timer
 
 
-def _timed(kind, flops, fn):
+def _timed(kind, flops, fn, nbytes=0.0):
     if _CONV_TIMER is None:
         fn()
     else:
-        _CONV_TIMER(kind, flops, fn)
+        _CONV_TIMER(kind, flops, fn, nbytes)
 
 def pack_weight(w: torch.Tensor, dtype: torch.dtype, cpad: int | None = None,
                 row_len: int | None = None) -> torch.Tensor:
@@ -97,9 +97,11 @@ def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
              bias: torch.Tensor | None = None, accumulate=False, kind="fwd", k_alg=None):
     """k_alg: algorithmic reduction length when the GEMM K is padded (im2col layer)."""
     flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * Cout
+    es = x.buf.element_size()
+    nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout * (2 if accumulate else 1))  # x, w, y (+y read)
     _timed(kind, flops, lambda: call("dg_conv_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
                                      Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate),
-                                     stream()))
+                                     stream()), nbytes)
 
 
 def flip_weight(wp: torch.Tensor, Cout: int, C: int, R: int) -> torch.Tensor:
@@ -118,9 +120,10 @@ def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=F
     ws = query("dg_conv_wgrad_workspace", x.dt, x.N, x.H, x.W, x.C, dy.C, R, R)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
     flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * dy.C
+    nbytes = x.buf.element_size() * (x.M * x.C + dy.M * dy.C) + 4 * dw.numel()
     _timed("wgrad", flops, lambda: call("dg_conv_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
                                         dy.ptr, dy.ld, dy.C, R, R, pad, ptr(dw), ptr(work), ws,
-                                        int(accumulate), stream()))
+                                        int(accumulate), stream()), nbytes)
 
 
 def im2col_c3(img: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:

@@ -1,0 +1,44 @@
+"""Data-parallel plumbing on CPU with gloo, world_size 2: the
+flat-gradient average the fused optimizer performs and the initial-weight
+broadcast.  The GPU path uses the same calls over RCCL."""
+import os
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from dgvcc_amd import dist as D
+    D.init_from_env("gloo")
+    try:
+        flat = torch.arange(10, dtype=torch.float32) * (rank + 1)
+        D.average_flat_(flat)
+        lin = torch.nn.Linear(4, 3)
+        with torch.no_grad():
+            lin.weight.fill_(float(rank))
+        D.broadcast_module_(lin)
+        q.put((rank, flat.tolist(), float(lin.weight.sum()), D.world(), D.rank()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_average_and_broadcast_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + (os.getpid() % 1000)
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    expect = [i * 1.5 for i in range(10)]
+    for rank, flat, wsum, world, rk in res:
+        assert flat == pytest.approx(expect)
+        assert wsum == 0.0  # rank 0's weights everywhere
+        assert world == 2 and rk == rank
