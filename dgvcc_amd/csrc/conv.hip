@@ -180,6 +180,181 @@ _Pragma("unroll") \
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// general implicit GEMM: any R x S, stride, pad (ResNet-50 trunks: 7x7/2 stem via
+// im2col, 3x3/2 and 1x1/2 convs), mode 0 = convolution (rows = output pixels
+// [N,P,Q] gathering x [N,H,W] at (p*st - pad + r, q*st - pad + s)), mode 1 =
+// transposed convolution for dgrad (rows = dX pixels [N,P,Q] gathering dY
+// [N,H,W] at ((p + pad - r)/st, (q + pad - s)/st) when divisible).
+// The gathered tensor is addressed through one whole-tensor buffer descriptor.
+// ---------------------------------------------------------------------------
+struct GenArgs {
+  const char* x; long long ldx; int N, H, W, C;   // gathered tensor
+  int P, Q;                                        // GEMM row grid
+  const char* w; int Cout, R, S, stride, pad, mode;
+  const float* bias;
+  char* y; long long ldy;
+  int accumulate;
+};
+
+__device__ __forceinline__ bool gen_src(const GenArgs& a, int n, int p, int q, int r, int s, long long& src) {
+  int ih, iw;
+  if (a.mode == 0) {
+    ih = p * a.stride - a.pad + r;
+    iw = q * a.stride - a.pad + s;
+  } else {
+    const int th = p + a.pad - r, tw = q + a.pad - s;
+    if (th < 0 || tw < 0) return false;
+    ih = th / a.stride; iw = tw / a.stride;
+    if (ih * a.stride != th || iw * a.stride != tw) return false;
+  }
+  if ((unsigned)ih >= (unsigned)a.H || (unsigned)iw >= (unsigned)a.W) return false;
+  src = ((long long)n * a.H + ih) * a.W + iw;
+  return true;
+}
+
+template <typename T, int BCO, int BPX>
+__global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
+  constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int BK = 128 / (int)sizeof(T);
+  constexpr int TI = BCO / 32, TJ = BPX / 32;
+  constexpr int AR = BCO / 32, BR = BPX / 32;
+  constexpr int TILE_BYTES = (BCO + BPX) * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+
+  const int PQ = a.P * a.Q;
+  const int M = a.N * PQ;
+  const int nco = a.Cout / BCO;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (bid % nco) * BCO;
+  const int px0 = (bid / nco) * BPX;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = tid & 7, rbase = tid >> 3;
+
+  const unsigned xbytes = (unsigned)((((long long)a.N * a.H * a.W - 1) * a.ldx + a.C) * sizeof(T));
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, xbytes, 0x00020000);
+
+  int rn[BR], rp[BR], rq[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int m = px0 + rbase + 32 * i;
+    const int rem = m % PQ;
+    rn[i] = (m < M) ? m / PQ : -1;
+    rp[i] = rem / a.Q;
+    rq[i] = rem % a.Q;
+  }
+  const int CB = a.C / BK;
+  const int KT = a.R * a.S * CB;
+  const long long ldw = (long long)a.R * a.S * a.C;
+  const T* wp = (const T*)a.w + (long long)(co0 + rbase) * ldw + chunk * EPC;
+
+  u4v ra[AR], rb[BR];
+#define GEN_GLOAD(t_) \
+  do { \
+    const int rs = (t_) / CB, cb = (t_) - rs * CB; \
+    const int r = rs / a.S, s = rs - r * a.S; \
+    const int coff = cb * BK + chunk * EPC; \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) ra[i] = *(const u4v*)(wp + (long long)(32 * i) * ldw + rs * a.C + cb * BK); \
+    _Pragma("unroll") for (int i = 0; i < BR; ++i) { \
+      long long src = 0; \
+      const bool ok = rn[i] >= 0 && gen_src(a, rn[i], rp[i], rq[i], r, s, src); \
+      const unsigned off = ok ? (unsigned)((src * a.ldx + coff) * (long long)sizeof(T)) : 0xFFFFFFF0u; \
+      rb[i] = bload(xr, off); \
+    } \
+  } while (0)
+#define GEN_SWRITE(buf_) \
+  do { \
+    char* As = smem + (buf_) * TILE_BYTES; \
+    char* Bs = As + BCO * 128; \
+    _Pragma("unroll") for (int i = 0; i < AR; ++i) *(u4v*)(As + swz(rbase + 32 * i, chunk)) = ra[i]; \
+    _Pragma("unroll") for (int i = 0; i < BR; ++i) *(u4v*)(Bs + swz(rbase + 32 * i, chunk)) = rb[i]; \
+  } while (0)
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wco = (wid >> 1) * (BCO / 2), wpx = (wid & 1) * (BPX / 2);
+  const int fr = lane & 15, fc = lane >> 4;
+
+  GEN_GLOAD(0);
+  GEN_SWRITE(0);
+  __syncthreads();
+  for (int t = 0; t < KT; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < KT) GEN_GLOAD(t + 1);
+    const char* As = smem + cur * TILE_BYTES;
+    const char* Bs = As + BCO * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 4 * ks + fc;
+      u4v af[TI], bfr[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+    }
+    if (t + 1 < KT) GEN_SWRITE(cur ^ 1);
+    __syncthreads();
+  }
+#undef GEN_GLOAD
+#undef GEN_SWRITE
+  T* y = (T*)a.y;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    if (px >= M) continue;
+    T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco + 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      st4(yrow + co, v);
+    }
+  }
+}
+
+template <typename T>
+int launch_gen(const GenArgs& a, hipStream_t st) {
+  const long long M = (long long)a.N * a.P * a.Q;
+  const int npx = dg_cdiv(M, 128);
+  if (a.Cout % 128 == 0)
+    hipLaunchKernelGGL((conv_gen_kernel<T, 128, 128>), dim3(npx * (a.Cout / 128)), dim3(NT), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_gen_kernel<T, 64, 128>), dim3(npx * (a.Cout / 64)), dim3(NT), 0, st, a);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// transpose (no flip): wt[c][r][s][co] = w[co][r][s][c]
+template <typename T>
+__global__ void transpose_weight_kernel(const T* __restrict__ w, int Cout, int C, int R, int S, T* __restrict__ wt) {
+  const long long total = (long long)Cout * C * R * S;
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    const int co = (int)(o % Cout);
+    long long t = o / Cout;
+    const int rs = (int)(t % (R * S));
+    const int c = (int)(t / (R * S));
+    wt[o] = w[((long long)co * R * S + rs) * C + c];
+  }
+}
+
 template <typename T>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
@@ -204,6 +379,8 @@ struct WgArgs {
   const char* dy; long long lddy; int Cout, R, S, pad;
   float* slab;         // [splits][Cout][R*S*C]
   int splits, pps;     // pixels per split (multiple of BKP)
+  int stride, P, Q;    // output grid of dy (stride 1: P = H, Q = W)
+  int whole_x;         // 1: descriptor over the whole x (strided convs)
 };
 
 template <typename T> struct WgCfg;
@@ -223,7 +400,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
 
   const int HW = a.H * a.W;
-  const int M = a.N * HW;
+  const int PQ = a.P * a.Q;
+  const int M = a.N * PQ;
   const int RS = a.R * a.S;
   const int nco = a.Cout / BCO, ncb = a.C / BC;
   const int tiles = nco * ncb * RS;
@@ -246,7 +424,8 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
   __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.dy + (long long)kbeg * a.lddy * sizeof(T)), 0, dy_bytes, 0x00020000);
   const int halo = a.pad * (a.W + 1);
-  const int xlo = max(0, kbeg - halo), xhi = min(M, kend + halo);
+  const int xlo = a.whole_x ? 0 : max(0, kbeg - halo);
+  const int xhi = a.whole_x ? a.N * HW : min(M, kend + halo);
   const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * sizeof(T));
   __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.x + (long long)xlo * a.ldx * sizeof(T)), 0, x_bytes, 0x00020000);
@@ -267,10 +446,10 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
       const int idx = tid + NT * i;
       const int row = idx / CPRB, ch = idx % CPRB;
       const int px = k0 + row;
-      const int rem = px % HW;
-      const int h = rem / a.W + dh, ww = rem % a.W + dw;
+      const int rem = px % PQ;
+      const int h = (rem / a.Q) * a.stride + dh, ww = (rem % a.Q) * a.stride + dw;
       const bool ok = px < kend && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-      const long long pin = (long long)(px + dh * a.W + dw - xlo);
+      const long long pin = (long long)(px / PQ) * HW + (long long)h * a.W + ww - xlo;
       const unsigned off = ok ? (unsigned)((pin * a.ldx + c0 + ch * EPC) * (long long)sizeof(T)) : 0xFFFFFFF0u;
       rb[i] = bload(xr, off);
     }
@@ -397,7 +576,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
 struct WgPlan { int splits, pps; };
 
 template <typename T>
-WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S) {
+WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S) {  // H, W: output grid
   constexpr int BKP = WgCfg<T>::BKP;
   const long long M = (long long)N * H * W;
   const int bco = (Cout % 128 == 0) ? 128 : 64;
@@ -497,6 +676,38 @@ __global__ void im2col_c3_kernel(const float* __restrict__ img, int N, int H, in
   }
 }
 
+// general im2col for Cin = 3 stems: out[(n,p,q)][k], k = (r*S + s)*3 + c, zero tail to Kpad
+template <typename T>
+__global__ void im2col_c3_ex_kernel(const float* __restrict__ img, int N, int H, int W, int R, int S, int stride,
+                                    int pad, int P, int Q, int Kpad, T* __restrict__ out) {
+  const long long total = (long long)N * P * Q * Kpad;
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
+       o += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(o % Kpad);
+    const long long m = o / Kpad;
+    float v = 0.f;
+    if (k < R * S * 3) {
+      const int c = k % 3, rs = k / 3, r = rs / S, s = rs % S;
+      const int n = (int)(m / ((long long)P * Q));
+      const int rem = (int)(m % ((long long)P * Q));
+      const int h = (rem / Q) * stride - pad + r, w = (rem % Q) * stride - pad + s;
+      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = img[(((long long)n * 3 + c) * H + h) * W + w];
+    }
+    out[o] = from_f<T>(v);
+  }
+}
+
+__global__ void unpack_c3_ex_kernel(const float* __restrict__ dwcol, int Cout, int R, int S, int Kpad,
+                                    float* __restrict__ dw, int acc) {
+  const int total = Cout * 3 * R * S;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int co = o / (3 * R * S), k = o % (3 * R * S);  // torch layout k = (c*R + r)*S + s
+    const int c = k / (R * S), r = (k / S) % R, s = k % S;
+    const float v = dwcol[(long long)co * Kpad + (r * S + s) * 3 + c];
+    dw[o] = acc ? dw[o] + v : v;
+  }
+}
+
 __global__ void unpack_c3_grad_kernel(const float* __restrict__ dwcol, int Cout, float* __restrict__ dw, int acc) {
   const int total = Cout * 27;
   for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
@@ -588,7 +799,8 @@ extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H
   DG_REQUIRE(ws_bytes >= need);
   WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : wg_plan<float>(N, H, W, C, Cout, R, S);
   DG_SUPPORTED((long long)(p.pps + 2 * pad * (W + 1)) * std::max(ldx, lddy) * 4 < (1ll << 31));
-  WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps};
+  WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
+           1, H, W, 0};
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
 }
@@ -630,6 +842,114 @@ extern "C" int dg_unpack_c3_grad(const float* dwcol, int Cout, float* dw, int ac
   DG_REQUIRE(dwcol && dw && Cout > 0);
   hipLaunchKernelGGL(unpack_c3_grad_kernel, dim3(grid_for(Cout * 27)), dim3(256), 0, (hipStream_t)stream, dwcol,
                      Cout, dw, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+
+// ---------------------------------------------------------------------------
+// general (strided) convolution C-ABI
+// ---------------------------------------------------------------------------
+static inline int conv_out(int in, int R, int stride, int pad) { return (in + 2 * pad - R) / stride + 1; }
+
+extern "C" int dg_conv2d_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                             int Cout, int R, int S, int stride, int pad, const float* bias, void* y, int64_t ldy,
+                             int accumulate, void* stream) {
+  DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0 && stride >= 1 && pad >= 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(Cout % 64 == 0 && (dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0)));
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
+  DG_SUPPORTED((((long long)N * H * W - 1) * ldx + C) * (dtype == DG_BF16 ? 2 : 4) < (1ll << 31));
+  const int P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
+  DG_REQUIRE(P > 0 && Q > 0);
+  GenArgs a{(const char*)x, ldx, N, H, W, C, P, Q, (const char*)w, Cout, R, S, stride, pad, 0, bias, (char*)y, ldy,
+            accumulate};
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_gen<bf16>(a, st) : launch_gen<float>(a, st);
+}
+
+extern "C" int dg_transpose_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wt, void* stream) {
+  DG_REQUIRE(w && wt && Cout > 0 && C > 0 && R > 0 && S > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)Cout * C * R * S;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(transpose_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)w, Cout, C,
+                       R, S, (bf16*)wt);
+  else if (dtype == DG_F32)
+    hipLaunchKernelGGL(transpose_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)w, Cout,
+                       C, R, S, (float*)wt);
+  else
+    return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// dX [N,H,W,C] of a conv x[N,H,W,C] -> y[N,P,Q,Cout]: transposed gather of dY with
+// wt = dg_transpose_weight(w) ([C][R][S][Cout]).
+extern "C" int dg_conv2d_dgrad(int dtype, const void* dy, int64_t lddy, int N, int P, int Q, int Cout, const void* wt,
+                               int C, int H, int W, int R, int S, int stride, int pad, void* dx, int64_t lddx,
+                               int accumulate, void* stream) {
+  DG_REQUIRE(dy && wt && dx && N > 0 && P > 0 && Q > 0 && H > 0 && W > 0 && stride >= 1 && pad >= 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(C % 64 == 0 && (dtype == DG_BF16 ? (Cout % 64 == 0) : (Cout % 32 == 0)));
+  DG_REQUIRE(conv_out(H, R, stride, pad) == P && conv_out(W, S, stride, pad) == Q);
+  DG_REQUIRE(lddy % 8 == 0 && lddx % 4 == 0);
+  DG_SUPPORTED((((long long)N * P * Q - 1) * lddy + Cout) * (dtype == DG_BF16 ? 2 : 4) < (1ll << 31));
+  GenArgs a{(const char*)dy, lddy, N, P, Q, Cout, H, W, (const char*)wt, C, R, S, stride, pad, 1, nullptr, (char*)dx,
+            lddx, accumulate};
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_gen<bf16>(a, st) : launch_gen<float>(a, st);
+}
+
+extern "C" int64_t dg_conv2d_wgrad_workspace(int dtype, int N, int P, int Q, int C, int Cout, int R, int S) {
+  return dg_conv_wgrad_workspace(dtype, N, P, Q, C, Cout, R, S);
+}
+
+extern "C" int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,
+                               int64_t lddy, int Cout, int R, int S, int stride, int pad, float* dw, void* workspace,
+                               int64_t ws_bytes, int accumulate, void* stream) {
+  DG_REQUIRE(x && dy && dw && workspace && stride >= 1 && pad >= 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(Cout % 64 == 0 && C % 64 == 0);
+  DG_REQUIRE(ldx % 8 == 0 && lddy % 8 == 0 && ldx >= C && lddy >= Cout);
+  const int P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
+  DG_REQUIRE(P > 0 && Q > 0);
+  const int64_t need = dg_conv_wgrad_workspace(dtype, N, P, Q, C, Cout, R, S);
+  DG_REQUIRE(ws_bytes >= need);
+  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, P, Q, C, Cout, R, S) : wg_plan<float>(N, P, Q, C, Cout, R, S);
+  DG_SUPPORTED((((long long)N * H * W - 1) * ldx + C) * (dtype == DG_BF16 ? 2 : 4) < (1ll << 31));
+  DG_SUPPORTED((long long)p.pps * lddy * 4 < (1ll << 31));
+  WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
+           stride, P, Q, 1};
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
+}
+
+
+extern "C" int dg_im2col_c3(int dtype, const float* img, int N, int H, int W, int R, int S, int stride, int pad,
+                            int Kpad, void* out, void* stream) {
+  DG_REQUIRE(img && out && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride >= 1 && Kpad >= R * S * 3);
+  const int P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
+  DG_REQUIRE(P > 0 && Q > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * P * Q * Kpad;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(im2col_c3_ex_kernel<bf16>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
+                       R, S, stride, pad, P, Q, Kpad, (bf16*)out);
+  else if (dtype == DG_F32)
+    hipLaunchKernelGGL(im2col_c3_ex_kernel<float>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H,
+                       W, R, S, stride, pad, P, Q, Kpad, (float*)out);
+  else
+    return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_unpack_c3(const float* dwcol, int Cout, int R, int S, int Kpad, float* dw, int accumulate,
+                            void* stream) {
+  DG_REQUIRE(dwcol && dw && Cout > 0 && Kpad >= R * S * 3);
+  hipLaunchKernelGGL(unpack_c3_ex_kernel, dim3(grid_for((long long)Cout * 3 * R * S)), dim3(256), 0,
+                     (hipStream_t)stream, dwcol, Cout, R, S, Kpad, dw, accumulate);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -93,6 +93,95 @@ __global__ __launch_bounds__(NT) void maxpool_bwd_kernel(const T* __restrict__ x
   }
 }
 
+// General max-pool (ResNet stem: 3x3, stride 2, pad 1; -inf padding, first max
+// in (kh, kw) scan order, NaN propagates — ATen max_pool2d).
+template <typename T>
+__global__ __launch_bounds__(NT) void maxpool_gen_fwd(const T* __restrict__ x, long long ldx, int N, int H, int W, int C,
+                                                      int k, int st, int pad, int P, int Q, T* __restrict__ y,
+                                                      long long ldy) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * P * Q * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % tpp);
+    long long t = i / tpp;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float m[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) m[e] = -INFINITY;
+    for (int r = 0; r < k; ++r) {
+      const int h = p * st - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < k; ++s) {
+        const int w = q * st - pad + s;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float v[V];
+        ldv(x + (((long long)n * H + h) * W + w) * ldx + ch * V, v);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (v[e] > m[e] || isnan(v[e])) m[e] = v[e];
+      }
+    }
+    stv(y + (((long long)n * P + p) * Q + q) * ldy + ch * V, m);
+  }
+}
+
+// gather backward: input (h,w) collects gy of every window whose argmax it is
+template <typename T>
+__global__ __launch_bounds__(NT) void maxpool_gen_bwd(const T* __restrict__ x, long long ldx, const T* __restrict__ gy,
+                                                      long long ldgy, int N, int H, int W, int C, int k, int st,
+                                                      int pad, int P, int Q, T* __restrict__ gx, long long ldgx,
+                                                      int accumulate) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * H * W * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const int ch = (int)(i % tpp);
+    long long t = i / tpp;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[V];
+    if (accumulate) ldv(gx + (((long long)n * H + h) * W + w) * ldgx + ch * V, acc);
+    else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    }
+    // windows p with p*st - pad <= h <= p*st - pad + k - 1
+    const int plo = max(0, (h + pad - k + st) / st), phi = min(P - 1, (h + pad) / st);
+    const int qlo = max(0, (w + pad - k + st) / st), qhi = min(Q - 1, (w + pad) / st);
+    for (int p = plo; p <= phi; ++p)
+      for (int q = qlo; q <= qhi; ++q) {
+        // argmax of window (p, q), per channel, in scan order
+        float m[V];
+        int am[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) { m[e] = -INFINITY; am[e] = -1; }
+        for (int r = 0; r < k; ++r) {
+          const int hh = p * st - pad + r;
+          if ((unsigned)hh >= (unsigned)H) continue;
+          for (int s = 0; s < k; ++s) {
+            const int ww = q * st - pad + s;
+            if ((unsigned)ww >= (unsigned)W) continue;
+            float v[V];
+            ldv(x + (((long long)n * H + hh) * W + ww) * ldx + ch * V, v);
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              if (v[e] > m[e] || isnan(v[e]) || am[e] < 0) { m[e] = v[e]; am[e] = hh * W + ww; }
+          }
+        }
+        float g[V];
+        ldv(gy + (((long long)n * P + p) * Q + q) * ldgy + ch * V, g);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (am[e] == h * W + w) acc[e] += g[e];
+      }
+    stv(gx + (((long long)n * H + h) * W + w) * ldgx + ch * V, acc);
+  }
+}
+
 // Source taps of output index o along one axis.
 struct Tap { int i0, i1; float l1; };
 __device__ __forceinline__ Tap src_tap(int o, int in, int out, int scale, int mode) {
@@ -321,4 +410,43 @@ extern "C" int dg_upsample_bwd(int dtype, const void* gy, int64_t ldgy, const vo
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? up_bwd<bf16>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st)
                           : up_bwd<float>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st);
+}
+
+
+extern "C" int dg_maxpool_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int k, int stride,
+                              int pad, void* y, int64_t ldy, void* stream) {
+  DG_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && stride > 0 && pad >= 0 && 2 * pad <= k);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ldx % V == 0 && ldy % V == 0);
+  const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * P * Q * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(maxpool_gen_fwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, H, W, C, k,
+                       stride, pad, P, Q, (bf16*)y, ldy);
+  else
+    hipLaunchKernelGGL(maxpool_gen_fwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, H, W,
+                       C, k, stride, pad, P, Q, (float*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy, int N, int H, int W,
+                              int C, int k, int stride, int pad, void* gx, int64_t ldgx, int accumulate, void* stream) {
+  DG_REQUIRE(x && gy && gx && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && stride > 0 && pad >= 0 && 2 * pad <= k);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ldx % V == 0 && ldgy % V == 0 && ldgx % V == 0);
+  const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * H * W * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(maxpool_gen_bwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx,
+                       (const bf16*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (bf16*)gx, ldgx, accumulate);
+  else
+    hipLaunchKernelGGL(maxpool_gen_bwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx,
+                       (const float*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (float*)gx, ldgx, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
 }

@@ -1,0 +1,296 @@
+// Elementwise/normalisation kernels of the ResNet-50 trunks (IBN-Net b, ISW, SW):
+//   residual join  out = act(bn3(z) + residual)   models/ibnnet/resnet_ibn.py:96-107,
+//                  models/ISW/Resnet.py:187-216, models/SW/backbones/resnet.py:100-118
+//   InstanceNorm2d (affine or not) forward/backward: the IBN-b IN layers
+//                  (resnet_ibn.py:77,115) and ISW's InstanceWhitening
+//                  (models/ISW/instance_whitening.py:5-16)
+//   ReLU backward from the saved output (torch threshold_backward semantics).
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int NT = 256;
+
+inline int ew_grid(long long n) {
+  long long g = (n + NT - 1) / NT;
+  return (int)std::max<long long>(1, std::min<long long>(g, 16384));
+}
+
+// y = act(z1*s1 + b1 + (s2 ? z2*s2 + b2 : z2))
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, long long ld1, int M, int C,
+                                                    const float* __restrict__ s1, const float* __restrict__ b1,
+                                                    const T* __restrict__ z2, long long ld2,
+                                                    const float* __restrict__ s2, const float* __restrict__ b2, int act,
+                                                    T* __restrict__ y, long long ldy) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const int c0 = (int)(gt % tpp) * V;
+  const long long pstride = (long long)gridDim.x * NT / tpp;
+  float a1[V], c1[V], a2[V], c2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    a1[e] = s1[c0 + e]; c1[e] = b1[c0 + e];
+    a2[e] = s2 ? s2[c0 + e] : 1.f; c2[e] = s2 ? b2[c0 + e] : 0.f;
+  }
+  for (long long p = gt / tpp; p < M; p += pstride) {
+    float u[V], v[V];
+    ldv(z1 + p * ld1 + c0, u);
+    ldv(z2 + p * ld2 + c0, v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      float t = fmaf(u[e], a1[e], c1[e]) + (s2 ? fmaf(v[e], a2[e], c2[e]) : v[e]);
+      if (act == 1) t = t > 0.f ? t : 0.f;
+      u[e] = t;
+    }
+    stv(y + p * ldy + c0, u);
+  }
+}
+
+// out = g * (y > 0)
+template <typename T>
+__global__ __launch_bounds__(NT) void relu_bwd_kernel(const T* __restrict__ g, long long ldg, const T* __restrict__ y,
+                                                      long long ldy, int M, int C, T* __restrict__ out, long long ldo) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)M * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    float a[V], b[V];
+    ldv(g + p * ldg + c0, a);
+    ldv(y + p * ldy + c0, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) a[e] = b[e] > 0.f ? a[e] : 0.f;
+    stv(out + p * ldo + c0, a);
+  }
+}
+
+// ---------------------------------------------------------------- IN apply --
+// y = act((x - mu[n,c]) * is[n,c] * gamma[c] + beta[c])
+template <typename T>
+__global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, long long ldx, int N, int HW, int C,
+                                                      const float* __restrict__ mu, const float* __restrict__ is,
+                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                      int act, T* __restrict__ y, long long ldy) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * HW * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    const int n = (int)(p / HW);
+    float v[V];
+    ldv(x + p * ldx + c0, v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int nc = n * C + c0 + e;
+      float t = (v[e] - mu[nc]) * is[nc];
+      if (gamma) t = fmaf(t, gamma[c0 + e], beta[c0 + e]);
+      if (act == 1) t = t > 0.f ? t : 0.f;
+      v[e] = t;
+    }
+    stv(y + p * ldy + c0, v);
+  }
+}
+
+// ---------------------------------------------------------------- IN bwd ----
+// grid (nb, N): per (n, block) partial sums of g and g*xhat over HW
+template <typename T>
+__global__ __launch_bounds__(NT) void in_bwd_partial(const T* __restrict__ g, long long ldg, const T* __restrict__ x,
+                                                     long long ldx, int HW, int C, int ppb, const float* __restrict__ mu,
+                                                     const float* __restrict__ is, float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[2][NT * V];
+  const int n = blockIdx.y, nb = gridDim.x;
+  const int tpp = C / V, rows = NT / tpp;
+  const int tid = threadIdx.x, ch = tid % tpp, pl = tid / tpp;
+  const int c0 = ch * V;
+  float sg[V], sx[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { sg[e] = 0.f; sx[e] = 0.f; }
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  if (pl < rows) {
+    float m[V], s[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { m[e] = mu[n * C + c0 + e]; s[e] = is[n * C + c0 + e]; }
+    for (int p = p0 + pl; p < p1; p += rows) {
+      const long long pp = (long long)n * HW + p;
+      float gv[V], xv[V];
+      ldv(g + pp * ldg + c0, gv);
+      ldv(x + pp * ldx + c0, xv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        sg[e] += gv[e];
+        sx[e] = fmaf(gv[e], (xv[e] - m[e]) * s[e], sx[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sh[0][pl * C + c0 + e] = sg[e]; sh[1][pl * C + c0 + e] = sx[e]; }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; }
+    float* o = part + ((long long)n * nb + blockIdx.x) * 2 * C;
+    o[c] = a; o[C + c] = b;
+  }
+}
+
+// coef[n][c] = (k1, k2, k3): dx = k1*g - k2*xhat - k3 ; dgamma/dbeta summed over n
+__global__ void in_bwd_finalize(const float* __restrict__ part, int N, int nb, int HW, int C,
+                                const float* __restrict__ is, const float* __restrict__ gamma, float* dgamma,
+                                float* dbeta, float* __restrict__ coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double tg = 0.0, tx = 0.0;
+  for (int n = 0; n < N; ++n) {
+    double a = 0.0, b = 0.0;
+    for (int k = 0; k < nb; ++k) {
+      const float* o = part + ((long long)n * nb + k) * 2 * C;
+      a += o[c]; b += o[C + c];
+    }
+    tg += a; tx += b;
+    const float gm = gamma ? gamma[c] : 1.f;
+    const float k1 = gm * is[n * C + c];
+    float* cf = coef + ((long long)n * C + c) * 3;
+    cf[0] = k1;
+    cf[1] = (float)(k1 * b / HW);
+    cf[2] = (float)(k1 * a / HW);
+  }
+  if (dgamma) dgamma[c] = (float)tx;
+  if (dbeta) dbeta[c] = (float)tg;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ x,
+                                                   long long ldx, int N, int HW, int C, const float* __restrict__ mu,
+                                                   const float* __restrict__ is, const float* __restrict__ coef,
+                                                   T* __restrict__ dx, long long lddx, int accumulate) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * HW * tpp;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    const int n = (int)(p / HW);
+    float gv[V], xv[V], o[V];
+    ldv(g + p * ldg + c0, gv);
+    ldv(x + p * ldx + c0, xv);
+    if (accumulate) ldv(dx + p * lddx + c0, o);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int nc = n * C + c0 + e;
+      const float* cf = coef + (long long)nc * 3;
+      const float xh = (xv[e] - mu[nc]) * is[nc];
+      const float d = cf[0] * gv[e] - cf[1] * xh - cf[2];
+      o[e] = accumulate ? o[e] + d : d;
+    }
+    stv(dx + p * lddx + c0, o);
+  }
+}
+
+}  // namespace
+
+#define VOK(dtype, C, ld) ((C) % ((dtype) == DG_BF16 ? 8 : 4) == 0 && (ld) % ((dtype) == DG_BF16 ? 8 : 4) == 0)
+
+extern "C" int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, int C, const float* scale1,
+                               const float* shift1, const void* z2, int64_t ld2, const float* scale2,
+                               const float* shift2, int act, void* y, int64_t ldy, void* stream) {
+  DG_REQUIRE(z1 && z2 && y && scale1 && shift1 && M > 0 && C > 0 && (!scale2 || shift2));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(VOK(dtype, C, ld1) && VOK(dtype, C, ld2) && VOK(dtype, C, ldy) && NT % (C / V) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)M * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_add_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z1, ld1, M, C, scale1,
+                       shift1, (const bf16*)z2, ld2, scale2, shift2, act, (bf16*)y, ldy);
+  else
+    hipLaunchKernelGGL(bn_add_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z1, ld1, M, C,
+                       scale1, shift1, (const float*)z2, ld2, scale2, shift2, act, (float*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_relu_bwd(int dtype, const void* g, int64_t ldg, const void* y, int64_t ldy, int M, int C, void* out,
+                           int64_t ldo, void* stream) {
+  DG_REQUIRE(g && y && out && M > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(VOK(dtype, C, ldg) && VOK(dtype, C, ldy) && VOK(dtype, C, ldo));
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)M * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(relu_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg,
+                       (const bf16*)y, ldy, M, C, (bf16*)out, ldo);
+  else
+    hipLaunchKernelGGL(relu_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+                       (const float*)y, ldy, M, C, (float*)out, ldo);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, int HW, int C, const float* mean,
+                                 const float* invstd, const float* gamma, const float* beta, int act, void* y,
+                                 int64_t ldy, void* stream) {
+  DG_REQUIRE(x && y && mean && invstd && N > 0 && HW > 0 && C > 0 && (!gamma || beta));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(VOK(dtype, C, ldx) && VOK(dtype, C, ldy));
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * HW * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(in_apply_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, HW, C,
+                       mean, invstd, gamma, beta, act, (bf16*)y, ldy);
+  else
+    hipLaunchKernelGGL(in_apply_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, HW, C,
+                       mean, invstd, gamma, beta, act, (float*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+static inline int in_nb(int HW) { return std::max(1, std::min(64, dg_cdiv(HW, 256))); }
+
+extern "C" int64_t dg_instnorm_bwd_workspace(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0) return DG_ERR_INVALID;
+  return ((int64_t)N * in_nb(HW) * 2 * C + (int64_t)N * C * 3) * 4;
+}
+
+// g: upstream gradient already masked by any following ReLU; dgamma/dbeta may be NULL
+extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void* x, int64_t ldx, int N, int HW, int C,
+                               const float* mean, const float* invstd, const float* gamma, void* dx, int64_t lddx,
+                               int accumulate, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  DG_REQUIRE(g && x && dx && mean && invstd && workspace && N > 0 && HW > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(VOK(dtype, C, ldg) && VOK(dtype, C, ldx) && VOK(dtype, C, lddx) && C / V <= NT);
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = in_nb(HW), ppb = dg_cdiv(HW, nb);
+  float* part = (float*)workspace;
+  float* coef = part + (long long)N * nb * 2 * C;
+  const long long total = (long long)N * HW * (C / V);
+  if (dtype == DG_BF16) {
+    hipLaunchKernelGGL(in_bwd_partial<bf16>, dim3(nb, N), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x, ldx,
+                       HW, C, ppb, mean, invstd, part);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, part, N, nb, HW, C, invstd, gamma,
+                       dgamma, dbeta, coef);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x,
+                       ldx, N, HW, C, mean, invstd, coef, (bf16*)dx, lddx, accumulate);
+  } else {
+    hipLaunchKernelGGL(in_bwd_partial<float>, dim3(nb, N), dim3(NT), 0, st, (const float*)g, ldg, (const float*)x,
+                       ldx, HW, C, ppb, mean, invstd, part);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_bwd_finalize, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, part, N, nb, HW, C, invstd, gamma,
+                       dgamma, dbeta, coef);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+                       (const float*)x, ldx, N, HW, C, mean, invstd, coef, (float*)dx, lddx, accumulate);
+  }
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}

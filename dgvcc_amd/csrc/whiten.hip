@@ -1,0 +1,754 @@
+// Whitening kernels of the domain-generalisation trunks.
+//
+// ISW (models/ISW/instance_whitening.py:19-39, models/ISW/__init__.py:93-120):
+//   the per-instance Gram matrices f_cor = w w^T/(HW-1) + eps I are produced by
+//   dg_conv2d_wgrad (a 1x1 "weight gradient" of w against itself, one launch per
+//   instance); here live the masked-L1 loss + its gradient and the
+//   variance-of-covariance statistic of cal_covstat.
+//
+// SW (models/SW/ops/switchwhiten.py:84-183), sw_type 2 (BW + IW), groups of 16
+// channels: statistics with f32 MFMA (16x16x4: one group's 16x16 covariance per
+// wave), Newton-Schulz whitening matrices in one 256-thread block per group
+// (thread = matrix element), and a fused whiten+affine+ReLU apply.  Backward is
+// the exact adjoint (Newton iterations recomputed in LDS, no autograd tape).
+#include "dg_common.h"
+#include <algorithm>
+
+extern "C" int64_t dg_instnorm_workspace(int N, int HW, int C);
+extern "C" int dg_instnorm_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float eps, float* mean,
+                                 float* invstd, void* workspace, void* stream);
+
+namespace {
+
+// ============================================================== ISW ========
+// grid (chunks, B): partial sums of |f_ij| * mask_ij
+__global__ __launch_bounds__(256) void iw_loss_partial(const float* __restrict__ fraw, int C, float inv_hw1, float eps,
+                                                       const float* __restrict__ mask, float* __restrict__ part) {
+  const int b = blockIdx.y;
+  const long long CC = (long long)C * C;
+  const float* f = fraw + b * CC;
+  float s = 0.f;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < CC; e += (long long)gridDim.x * 256) {
+    const int i = (int)(e / C), j = (int)(e % C);
+    const float v = fmaf(f[e], inv_hw1, i == j ? eps : 0.f);
+    s = fmaf(fabsf(v), mask[e], s);
+  }
+  __shared__ float sh[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[b * gridDim.x + blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// loss (+)= out_scale * sum_b max(0, sum_e / ns) / B
+__global__ void iw_loss_finalize(const float* __restrict__ part, int B, int nch, const float* __restrict__ ns,
+                                 float out_scale, int accumulate, float* __restrict__ loss) {
+  if (threadIdx.x != 0) return;
+  double tot = 0.0;
+  for (int b = 0; b < B; ++b) {
+    double s = 0.0;
+    for (int k = 0; k < nch; ++k) s += part[b * nch + k];
+    s /= (double)ns[0];
+    tot += s > 0.0 ? s : 0.0;
+  }
+  const float v = (float)(tot / B) * out_scale;
+  loss[0] = accumulate ? loss[0] + v : v;
+}
+
+// gsym[b] = k * (M∘sgn(f) + (M∘sgn(f))^T),  k = coef*out_scale*inv_hw1/(ns*B)
+// (the clamp(min=0) of instance_whitening_loss is inactive: its argument is a sum
+// of absolute values with margin 0, models/ISW/cov_settings.py:47)
+__global__ __launch_bounds__(256) void iw_loss_grad(const float* __restrict__ fraw, int B, int C, float inv_hw1,
+                                                    float eps, const float* __restrict__ mask,
+                                                    const float* __restrict__ ns, const float* __restrict__ coef,
+                                                    float out_scale, float* __restrict__ gsym) {
+  const long long CC = (long long)C * C, total = CC * B;
+  const float k = (coef ? coef[0] : 1.f) * out_scale * inv_hw1 / (ns[0] * (float)B);
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const long long b = e / CC, r = e % CC;
+    const int i = (int)(r / C), j = (int)(r % C);
+    const float* f = fraw + b * CC;
+    const float vij = fmaf(f[r], inv_hw1, i == j ? eps : 0.f);
+    const float vji = fmaf(f[(long long)j * C + i], inv_hw1, i == j ? eps : 0.f);
+    const float sij = vij > 0.f ? 1.f : (vij < 0.f ? -1.f : 0.f);
+    const float sji = vji > 0.f ? 1.f : (vji < 0.f ? -1.f : 0.f);
+    gsym[e] = k * (mask[r] * sij + mask[(long long)j * C + i] * sji);
+  }
+}
+
+// var over instances (unbiased) of f_ij * [j > i]  (cal_covstat, __init__.py:96-103)
+__global__ __launch_bounds__(256) void iw_cov_var(const float* __restrict__ fraw, int B, int C, float inv_hw1,
+                                                  float* __restrict__ var, int accumulate) {
+  const long long CC = (long long)C * C;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < CC; e += (long long)gridDim.x * 256) {
+    const int i = (int)(e / C), j = (int)(e % C);
+    float v = 0.f;
+    if (j > i) {
+      double m = 0.0;
+      for (int b = 0; b < B; ++b) m += (double)(fraw[b * CC + e] * inv_hw1);
+      m /= B;
+      double s = 0.0;
+      for (int b = 0; b < B; ++b) {
+        const double d = (double)(fraw[b * CC + e] * inv_hw1) - m;
+        s += d * d;
+      }
+      v = (float)(s / (B - 1));  // B == 1 -> NaN, as torch.var
+    }
+    var[e] = accumulate ? var[e] + v : v;
+  }
+}
+
+// ============================================================== SW =========
+constexpr int SWC = 16;  // channels per whitening group (sw_cfg num_pergroup)
+constexpr int SW_MAXT = 8;
+
+// Per-(n, block) partial 16x16 covariance of every group, centred on the
+// instance mean: part[n][blk][g][16*16].  A wave owns groups w, w+4, ...; one
+// f32 MFMA 16x16x4 consumes 4 pixels x 16 channels with a == b (lane l holds
+// xc[p + l/16][g*16 + l%16]), so D = sum_p xc xc^T.
+template <typename T, int MAXG>
+__global__ __launch_bounds__(256) void sw_cov_partial(const T* __restrict__ x, long long ldx, int HW, int C, int ppb,
+                                                      const float* __restrict__ mu, float* __restrict__ part) {
+  const int n = blockIdx.y, nb = gridDim.x, G = C / SWC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kq = lane >> 4, ch = lane & 15;
+  f4v acc[MAXG];
+  float m[MAXG];
+#pragma unroll
+  for (int q = 0; q < MAXG; ++q) {
+    acc[q] = f4v{0.f, 0.f, 0.f, 0.f};
+    const int g = wave + 4 * q;
+    m[q] = g < G ? mu[(long long)n * C + g * SWC + ch] : 0.f;
+  }
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  const T* xn = x + (long long)n * HW * ldx;
+  for (int p = p0; p < p1; p += 4) {
+    const int pp = p + kq;
+    const bool ok = pp < p1;
+#pragma unroll
+    for (int q = 0; q < MAXG; ++q) {
+      const int g = wave + 4 * q;
+      if (g < G) {
+        const float v = ok ? to_f(xn[(long long)pp * ldx + g * SWC + ch]) - m[q] : 0.f;
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, acc[q], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXG; ++q) {
+    const int g = wave + 4 * q;
+    if (g < G) {
+      float* o = part + (((long long)n * nb + blockIdx.x) * G + g) * 256;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(kq * 4 + r) * 16 + ch] = acc[q][r];
+    }
+  }
+}
+
+// 16x16 product for thread t = (i, j):  sum_k A(i,k) B(k,j), optional transposes.
+template <bool TA, bool TB>
+__device__ __forceinline__ float mm16(const float* A, const float* B, int i, int j) {
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float a = TA ? A[k * 16 + i] : A[i * 16 + k];
+    const float b = TB ? B[j * 16 + k] : B[k * 16 + j];
+    s = fmaf(a, b, s);
+  }
+  return s;
+}
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float r = red[0] + red[1] + red[2] + red[3];
+  __syncthreads();
+  return r;
+}
+
+__device__ __forceinline__ void softmax2(const float* w, float& a0, float& a1) {
+  const float m = fmaxf(w[0], w[1]);
+  const float e0 = expf(w[0] - m), e1 = expf(w[1] - m);
+  a0 = e0 / (e0 + e1);
+  a1 = e1 / (e0 + e1);
+}
+
+// Newton-Schulz whitening matrix of S (LDS, 256): P_{k+1} = 1.5 P_k - 0.5 P_k^3 (S/tr S),
+// W = P_T sqrt(1/tr S).  Ps[k] (k = 0..T) kept in LDS when Ps != nullptr.
+struct SwLds {
+  float S[256], A[256], P[256], P2[256], P3[256], X[256], Y[256], G[256];
+  float red[4];
+  float vec[4][16];
+};
+
+__device__ float sw_newton(SwLds& L, float* Ps, int T, int t) {
+  const int i = t >> 4, j = t & 15;
+  // trace
+  __shared__ float tr_s;
+  if (t == 0) {
+    float tr = 0.f;
+    for (int d = 0; d < 16; ++d) tr += L.S[d * 17];
+    tr_s = tr;
+  }
+  __syncthreads();
+  const float r = 1.f / tr_s;
+  L.A[t] = L.S[t] * r;
+  L.P[t] = i == j ? 1.f : 0.f;
+  if (Ps) Ps[t] = L.P[t];
+  __syncthreads();
+  for (int k = 0; k < T; ++k) {
+    const float p2 = mm16<false, false>(L.P, L.P, i, j);
+    L.P2[t] = p2;
+    __syncthreads();
+    const float p3 = mm16<false, false>(L.P2, L.P, i, j);
+    L.P3[t] = p3;
+    __syncthreads();
+    const float q = mm16<false, false>(L.P3, L.A, i, j);
+    const float pn = 1.5f * L.P[t] - 0.5f * q;
+    __syncthreads();
+    L.P[t] = pn;
+    if (Ps) Ps[(k + 1) * 256 + t] = pn;
+    __syncthreads();
+  }
+  return r;
+}
+
+// Statistics + whitening matrices, one block per group g.
+//   save layout (floats): mu_in[N][C] | cov_in[N][G][256] | mu_bn[C] | cov_bn[G][256]
+//                         | aff[N][G][256] | bias[N][C]
+__global__ __launch_bounds__(256) void sw_stats_finalize(const float* __restrict__ part, int N, int nb, int HW, int C,
+                                                         int T, float eps, float momentum, const float* mean_w,
+                                                         const float* var_w, const float* gamma, const float* beta,
+                                                         float* running_mean, float* running_cov, int training,
+                                                         float* __restrict__ save) {
+  __shared__ SwLds L;
+  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  float* mu_in = save;
+  float* cov_in = mu_in + (long long)N * C;
+  float* mu_bn = cov_in + (long long)N * G * 256;
+  float* cov_bn = mu_bn + C;
+  float* aff = cov_bn + (long long)G * 256;
+  float* bias = aff + (long long)N * G * 256;
+  // instance covariances and batch statistics
+  float mb = 0.f;  // thread t < 16: batch mean of channel t
+  if (t < 16) {
+    for (int n = 0; n < N; ++n) mb += mu_in[(long long)n * C + g * 16 + t];
+    mb /= N;
+    L.vec[0][t] = mb;
+  }
+  __syncthreads();
+  double cb = 0.0;
+  for (int n = 0; n < N; ++n) {
+    double s = 0.0;
+    for (int k = 0; k < nb; ++k) s += part[(((long long)n * nb + k) * G + g) * 256 + t];
+    const float ci = (float)(s / HW);
+    cov_in[((long long)n * G + g) * 256 + t] = ci;
+    const float di = mu_in[(long long)n * C + g * 16 + i] - L.vec[0][i];
+    const float dj = mu_in[(long long)n * C + g * 16 + j] - L.vec[0][j];
+    cb += (double)ci + (double)di * dj;
+  }
+  float cbn = (float)(cb / N);
+  __syncthreads();
+  if (training) {
+    if (t < 16) {
+      mu_bn[g * 16 + t] = mb;
+      float* rm = running_mean + g * 16 + t;
+      *rm = *rm * momentum + (1.f - momentum) * mb;
+    }
+    cov_bn[g * 256 + t] = cbn;
+    float* rc = running_cov + g * 256 + t;
+    *rc = *rc * momentum + (1.f - momentum) * cbn;
+  } else {
+    if (t < 16) {
+      mb = running_mean[g * 16 + t];
+      mu_bn[g * 16 + t] = mb;
+      L.vec[0][t] = mb;
+    }
+    cbn = running_cov[g * 256 + t];
+    cov_bn[g * 256 + t] = cbn;
+  }
+  __syncthreads();
+  float a0, a1, b0, b1;
+  softmax2(mean_w, a0, a1);
+  softmax2(var_w, b0, b1);
+  for (int n = 0; n < N; ++n) {
+    const float ci = cov_in[((long long)n * G + g) * 256 + t];
+    L.S[t] = b0 * cbn + b1 * ci + (i == j ? eps : 0.f);
+    if (t < 16) L.vec[1][t] = a0 * L.vec[0][t] + a1 * mu_in[(long long)n * C + g * 16 + t];  // mixed mean
+    __syncthreads();
+    const float r = sw_newton(L, nullptr, T, t);
+    const float w = L.P[t] * sqrtf(r);
+    const float gi = gamma ? gamma[g * 16 + i] : 1.f;
+    L.X[t] = gi * w;
+    __syncthreads();
+    aff[((long long)n * G + g) * 256 + t] = L.X[t];
+    if (t < 16) {
+      float s = 0.f;
+      for (int k = 0; k < 16; ++k) s = fmaf(L.X[t * 16 + k], L.vec[1][k], s);
+      bias[(long long)n * C + g * 16 + t] = (beta ? beta[g * 16 + t] : 0.f) - s;
+    }
+    __syncthreads();
+  }
+}
+
+// y[p][g*16+i] = act(sum_j aff[n][g][i][j] x[p][g*16+j] + bias[n][g*16+i]);  thread = (pixel, group)
+template <typename T>
+__global__ __launch_bounds__(256) void sw_apply(const T* __restrict__ x, long long ldx, int HW, int C, int ppb,
+                                                const float* __restrict__ aff, const float* __restrict__ bias, int act,
+                                                T* __restrict__ y, long long ldy) {
+  extern __shared__ float sm[];  // [G][273]
+  const int n = blockIdx.y, G = C / SWC;
+  for (int e = threadIdx.x; e < G * 256; e += 256) sm[(e >> 8) * 273 + (e & 255)] = aff[(long long)n * G * 256 + e];
+  for (int e = threadIdx.x; e < C; e += 256) sm[(e >> 4) * 273 + 256 + (e & 15)] = bias[(long long)n * C + e];
+  __syncthreads();
+  const int g = threadIdx.x % G, pl = threadIdx.x / G, rows = 256 / G;
+  if (pl >= rows) return;
+  const float* A = sm + g * 273;
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  for (int p = p0 + pl; p < p1; p += rows) {
+    const long long pp = (long long)n * HW + p;
+    float v[16], o[16];
+    constexpr int V = 16 / (int)sizeof(T);
+#pragma unroll
+    for (int q = 0; q < 16; q += V) ldv(x + pp * ldx + g * 16 + q, v + q);
+#pragma unroll
+    for (int a = 0; a < 16; ++a) {
+      float s = A[256 + a];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) s = fmaf(A[a * 16 + b], v[b], s);
+      o[a] = (act == 1 && s < 0.f) ? 0.f : s;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q += V) stv(y + pp * ldy + g * 16 + q, o + q);
+  }
+}
+
+// ---------------------------------------------------------------- SW bwd --
+// Per-(n, block) partials: GXc[g] = sum_p ge_p (x_p - mu_n)^T (MFMA, a = ge, b = xc)
+// and sgy[g] = sum_p ge_p, where ge = gy * (y > 0) when act == 1.
+// part layout: [n][blk][g][256 + 16]
+template <typename T, int MAXG>
+__global__ __launch_bounds__(256) void sw_bwd_partial(const T* __restrict__ gy, long long ldg, const T* __restrict__ y,
+                                                      long long ldy, const T* __restrict__ x, long long ldx, int HW,
+                                                      int C, int ppb, int act, const float* __restrict__ mu,
+                                                      float* __restrict__ part) {
+  const int n = blockIdx.y, nb = gridDim.x, G = C / SWC;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int kq = lane >> 4, ch = lane & 15;
+  f4v acc[MAXG];
+  float m[MAXG], sg[MAXG];
+#pragma unroll
+  for (int q = 0; q < MAXG; ++q) {
+    acc[q] = f4v{0.f, 0.f, 0.f, 0.f};
+    sg[q] = 0.f;
+    const int g = wave + 4 * q;
+    m[q] = g < G ? mu[(long long)n * C + g * SWC + ch] : 0.f;
+  }
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  const long long base = (long long)n * HW;
+  for (int p = p0; p < p1; p += 4) {
+    const int pp = p + kq;
+    const bool ok = pp < p1;
+#pragma unroll
+    for (int q = 0; q < MAXG; ++q) {
+      const int g = wave + 4 * q;
+      if (g < G) {
+        const int c = g * SWC + ch;
+        float ge = 0.f, xc = 0.f;
+        if (ok) {
+          ge = to_f(gy[(base + pp) * ldg + c]);
+          if (act == 1 && !(to_f(y[(base + pp) * ldy + c]) > 0.f)) ge = 0.f;
+          xc = to_f(x[(base + pp) * ldx + c]) - m[q];
+        }
+        sg[q] += ge;
+        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ge, xc, acc[q], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < MAXG; ++q) {
+    const int g = wave + 4 * q;
+    float s = sg[q];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (g < G) {
+      float* o = part + (((long long)n * nb + blockIdx.x) * G + g) * 272;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[(kq * 4 + r) * 16 + ch] = acc[q][r];
+      if (kq == 0) o[256 + ch] = s;
+    }
+  }
+}
+
+// One block per group: exact adjoint of sw_stats_finalize for every instance.
+// coef layout: [n][g][ K(256) | L(256) | c(16) ]  so that
+//   dx_p = K ge_p + L (x_p - mu_n) + c.
+// wpart[g][4] = (da0, da1, db0, db1) partial over n; dgamma/dbeta written.
+__global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ part, int N, int nb, int HW, int C, int T,
+                                                    float eps, const float* mean_w, const float* var_w,
+                                                    const float* gamma, const float* __restrict__ save,
+                                                    float* __restrict__ coef, float* __restrict__ wpart,
+                                                    float* dgamma, float* dbeta) {
+  __shared__ SwLds L;
+  __shared__ float Ps[(SW_MAXT + 1) * 256];
+  __shared__ float mv[4][16];  // mu_bn, mixed mean, mu_n, sgy
+  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  const float* mu_in = save;
+  const float* cov_in = mu_in + (long long)N * C;
+  const float* mu_bn = cov_in + (long long)N * G * 256;
+  const float* cov_bn = mu_bn + C;
+  float a0, a1, b0, b1;
+  softmax2(mean_w, a0, a1);
+  softmax2(var_w, b0, b1);
+  const float cbn = cov_bn[g * 256 + t];
+  const float gam_i = gamma ? gamma[g * 16 + i] : 1.f;
+  const float gam_j = gamma ? gamma[g * 16 + j] : 1.f;
+  if (t < 16) mv[0][t] = mu_bn[g * 16 + t];
+  float dcov_bn = 0.f, dmu_bn = 0.f, dgam = 0.f, dbet = 0.f;
+  float da0 = 0.f, da1 = 0.f, db0 = 0.f, db1 = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float ci = cov_in[((long long)n * G + g) * 256 + t];
+    // reduce partials of this (n, g)
+    float gx = 0.f, sg = 0.f;
+    for (int k = 0; k < nb; ++k) {
+      const float* o = part + (((long long)n * nb + k) * G + g) * 272;
+      gx += o[t];
+      if (t < 16) sg += o[256 + t];
+    }
+    if (t < 16) {
+      mv[2][t] = mu_in[(long long)n * C + g * 16 + t];
+      mv[1][t] = a0 * mv[0][t] + a1 * mv[2][t];
+      mv[3][t] = sg;
+    }
+    L.S[t] = b0 * cbn + b1 * ci + (i == j ? eps : 0.f);
+    __syncthreads();
+    const float r = sw_newton(L, Ps, T, t);
+    const float sr = sqrtf(r);
+    const float PT = L.P[t];
+    const float W = PT * sr;
+    // H = GXc - sgy (m - mu_n)^T ; dW = diag(gamma) H
+    const float H = gx - mv[3][i] * (mv[1][j] - mv[2][j]);
+    const float dW = gam_i * H;
+    // dgamma_i += sum_j W_ij H_ij ; dbeta_i += sgy_i
+    float wh = W * H;
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) wh += __shfl_xor(wh, o, 16);
+    if (j == 0) { dgam += wh; dbet += mv[3][i]; }
+    // K = W^T diag(gamma): K_ij = W_ji gamma_j  (store W into X for the transpose)
+    L.X[t] = W;
+    __syncthreads();
+    float* cf = coef + ((long long)n * G + g) * 528;
+    cf[t] = L.X[j * 16 + i] * gam_j;
+    // dm_t = -sum_k W_kt gamma_k sgy_k  (t < 16)
+    float dm = 0.f;
+    if (t < 16) {
+      for (int k = 0; k < 16; ++k) dm -= L.X[k * 16 + t] * (gamma ? gamma[g * 16 + k] : 1.f) * mv[3][k];
+    }
+    // Newton adjoint: G = dP_T
+    L.G[t] = dW * sr;
+    const float dr_w = block_sum256(dW * PT, L.red) * 0.5f / sr;
+    float dA = 0.f;
+    __syncthreads();
+    for (int k = T - 1; k >= 0; --k) {
+      const float* P = Ps + k * 256;
+      L.P2[t] = mm16<false, false>(P, P, i, j);           // P^2
+      L.X[t] = mm16<false, false>(P, L.A, i, j);          // P A
+      __syncthreads();
+      L.P3[t] = mm16<false, false>(L.P2, P, i, j);        // P^3
+      L.Y[t] = mm16<false, false>(L.P2, L.A, i, j);       // P^2 A
+      __syncthreads();
+      dA -= 0.5f * mm16<true, false>(L.P3, L.G, i, j);    // (P^3)^T G
+      const float t1 = mm16<false, true>(L.G, L.Y, i, j);  // G (P^2 A)^T
+      const float u = mm16<false, true>(L.G, L.X, i, j);   // G (P A)^T
+      const float v = mm16<false, true>(L.G, L.A, i, j);   // G A^T
+      __syncthreads();
+      L.Y[t] = u;
+      L.X[t] = v;
+      __syncthreads();
+      const float t2 = mm16<true, false>(P, L.Y, i, j);      // P^T G (P A)^T
+      const float t3 = mm16<true, false>(L.P2, L.X, i, j);   // (P^2)^T G A^T
+      const float gn = 1.5f * L.G[t] - 0.5f * (t1 + t2 + t3);
+      __syncthreads();
+      L.G[t] = gn;
+      __syncthreads();
+    }
+    // A = S r ; r = 1/tr(S)
+    const float dr = dr_w + block_sum256(dA * L.S[t], L.red);
+    const float dS = r * dA + (i == j ? -r * r * dr : 0.f);
+    db0 += block_sum256(dS * cbn, L.red);
+    db1 += block_sum256(dS * ci, L.red);
+    dcov_bn += b0 * dS;
+    // D_n = b1 (dS + dS^T) / HW  (stored in the L slot; E added below)
+    L.X[t] = dS;
+    __syncthreads();
+    cf[256 + t] = b1 * (dS + L.X[j * 16 + i]) / (float)HW;
+    if (t < 16) {
+      da0 += dm * mv[0][t];
+      da1 += dm * mv[2][t];
+      dmu_bn += a0 * dm;
+      cf[512 + t] = a1 * dm / (float)HW;  // dmu_n / HW (completed below)
+    }
+    __syncthreads();
+  }
+  // Esym = (dcov_bn + dcov_bn^T) / (N HW)
+  L.X[t] = dcov_bn;
+  if (t < 16) mv[3][t] = dmu_bn / ((float)N * HW);
+  __syncthreads();
+  const float E = (dcov_bn + L.X[j * 16 + i]) / ((float)N * HW);
+  L.Y[t] = E;
+  __syncthreads();
+  for (int n = 0; n < N; ++n) {
+    float* cf = coef + ((long long)n * G + g) * 528;
+    cf[256 + t] += E;
+    if (t < 16) {
+      // c = E (mu_n - mu_bn) + dmu_n/HW + dmu_bn/(N HW)
+      float s = 0.f;
+      for (int k = 0; k < 16; ++k) s = fmaf(L.Y[t * 16 + k], mu_in[(long long)n * C + g * 16 + k] - mv[0][k], s);
+      cf[512 + t] += s + mv[3][t];
+    }
+  }
+  if (j == 0) {
+    if (dgamma) dgamma[g * 16 + i] = dgam;
+    if (dbeta) dbeta[g * 16 + i] = dbet;
+  }
+  const float s0 = block_sum256(t < 16 ? da0 : 0.f, L.red);
+  const float s1 = block_sum256(t < 16 ? da1 : 0.f, L.red);
+  if (t == 0) {
+    wpart[g * 4 + 0] = s0;
+    wpart[g * 4 + 1] = s1;
+    wpart[g * 4 + 2] = db0;
+    wpart[g * 4 + 3] = db1;
+  }
+}
+
+// softmax backward of the two mixing weights: dtheta = a (da - <a, da>)
+__global__ void sw_bwd_weights(const float* __restrict__ wpart, int G, const float* mean_w, const float* var_w,
+                               float* dmean_w, float* dvar_w) {
+  if (threadIdx.x != 0) return;
+  double s[4] = {0, 0, 0, 0};
+  for (int g = 0; g < G; ++g)
+    for (int k = 0; k < 4; ++k) s[k] += wpart[g * 4 + k];
+  float a0, a1, b0, b1;
+  softmax2(mean_w, a0, a1);
+  softmax2(var_w, b0, b1);
+  const double ma = a0 * s[0] + a1 * s[1], mb = b0 * s[2] + b1 * s[3];
+  if (dmean_w) { dmean_w[0] = (float)(a0 * (s[0] - ma)); dmean_w[1] = (float)(a1 * (s[1] - ma)); }
+  if (dvar_w) { dvar_w[0] = (float)(b0 * (s[2] - mb)); dvar_w[1] = (float)(b1 * (s[3] - mb)); }
+}
+
+// dx_p = K ge_p + L (x_p - mu_n) + c ; thread = (pixel, group)
+template <typename T>
+__global__ __launch_bounds__(256) void sw_bwd_apply(const T* __restrict__ gy, long long ldg, const T* __restrict__ y,
+                                                    long long ldy, const T* __restrict__ x, long long ldx, int HW,
+                                                    int C, int ppb, int act, const float* __restrict__ mu,
+                                                    const float* __restrict__ coef, T* __restrict__ dx,
+                                                    long long lddx, int accumulate) {
+  extern __shared__ float sm[];  // [G][545]: K | L | c | mu
+  const int n = blockIdx.y, G = C / SWC;
+  for (int e = threadIdx.x; e < G * 528; e += 256)
+    sm[(e / 528) * 545 + (e % 528)] = coef[(long long)n * G * 528 + e];
+  for (int e = threadIdx.x; e < C; e += 256) sm[(e >> 4) * 545 + 528 + (e & 15)] = mu[(long long)n * C + e];
+  __syncthreads();
+  const int g = threadIdx.x % G, pl = threadIdx.x / G, rows = 256 / G;
+  if (pl >= rows) return;
+  const float* Km = sm + g * 545;
+  const float* Lm = Km + 256;
+  const float* cv = Km + 512;
+  const float* mv = Km + 528;
+  constexpr int V = 16 / (int)sizeof(T);
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  for (int p = p0 + pl; p < p1; p += rows) {
+    const long long pp = (long long)n * HW + p;
+    float ge[16], xc[16], o[16];
+#pragma unroll
+    for (int q = 0; q < 16; q += V) {
+      ldv(gy + pp * ldg + g * 16 + q, ge + q);
+      ldv(x + pp * ldx + g * 16 + q, xc + q);
+    }
+    if (act == 1) {
+      float yv[16];
+#pragma unroll
+      for (int q = 0; q < 16; q += V) ldv(y + pp * ldy + g * 16 + q, yv + q);
+#pragma unroll
+      for (int a = 0; a < 16; ++a) ge[a] = yv[a] > 0.f ? ge[a] : 0.f;
+    }
+#pragma unroll
+    for (int a = 0; a < 16; ++a) xc[a] -= mv[a];
+    if (accumulate) {
+#pragma unroll
+      for (int q = 0; q < 16; q += V) ldv(dx + pp * lddx + g * 16 + q, o + q);
+    }
+#pragma unroll
+    for (int a = 0; a < 16; ++a) {
+      float s = cv[a];
+#pragma unroll
+      for (int b = 0; b < 16; ++b) s = fmaf(Km[a * 16 + b], ge[b], fmaf(Lm[a * 16 + b], xc[b], s));
+      o[a] = accumulate ? o[a] + s : s;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; q += V) stv(dx + pp * lddx + g * 16 + q, o + q);
+  }
+}
+
+inline int sw_nb(int HW) { return std::max(1, std::min(64, dg_cdiv(HW, 1024))); }
+
+}  // namespace
+
+// ================================================================ C-ABI ====
+extern "C" int64_t dg_iw_loss_workspace(int B, int C) {
+  if (B <= 0 || C <= 0) return DG_ERR_INVALID;
+  return (int64_t)B * 64 * 4;
+}
+
+extern "C" int dg_iw_loss(const float* fraw, int B, int C, float inv_hw1, float eps, const float* mask,
+                          const float* num_sensitive, const float* grad_coef, float out_scale, int accumulate,
+                          float* loss, float* gsym, void* workspace, void* stream) {
+  DG_REQUIRE(fraw && mask && num_sensitive && B > 0 && C > 0 && (loss || gsym));
+  hipStream_t st = (hipStream_t)stream;
+  if (loss) {
+    DG_REQUIRE(workspace);
+    const int nch = std::max(1, std::min(64, dg_cdiv((long long)C * C, 4096)));
+    hipLaunchKernelGGL(iw_loss_partial, dim3(nch, B), dim3(256), 0, st, fraw, C, inv_hw1, eps, mask,
+                       (float*)workspace);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(iw_loss_finalize, dim3(1), dim3(64), 0, st, (const float*)workspace, B, nch, num_sensitive,
+                       out_scale, accumulate, loss);
+    DG_CHECK_LAUNCH();
+  }
+  if (gsym) {
+    const long long total = (long long)B * C * C;
+    const int grid = (int)std::min<long long>(16384, (total + 255) / 256);
+    hipLaunchKernelGGL(iw_loss_grad, dim3(grid), dim3(256), 0, st, fraw, B, C, inv_hw1, eps, mask, num_sensitive,
+                       grad_coef, out_scale, gsym);
+    DG_CHECK_LAUNCH();
+  }
+  return DG_OK;
+}
+
+extern "C" int dg_iw_cov_var(const float* fraw, int B, int C, float inv_hw1, float* var, int accumulate,
+                             void* stream) {
+  DG_REQUIRE(fraw && var && B > 0 && C > 0);
+  const long long CC = (long long)C * C;
+  const int grid = (int)std::min<long long>(16384, (CC + 255) / 256);
+  hipLaunchKernelGGL(iw_cov_var, dim3(grid), dim3(256), 0, (hipStream_t)stream, fraw, B, C, inv_hw1, var, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_sw_save_size(int N, int C) {
+  if (N <= 0 || C <= 0 || C % SWC) return DG_ERR_INVALID;
+  const int64_t G = C / SWC;
+  return (2 * (int64_t)N * C + 2 * (int64_t)N * G * 256 + C + G * 256) * 4;
+}
+
+extern "C" int64_t dg_sw_workspace(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % SWC) return DG_ERR_INVALID;
+  const int64_t G = C / SWC, nb = sw_nb(HW);
+  const int64_t fwd = std::max<int64_t>(dg_instnorm_workspace(N, HW, C), 0) + (int64_t)N * C * 4 +
+                      (int64_t)N * nb * G * 256 * 4;
+  const int64_t bwd = (int64_t)N * nb * G * 272 * 4 + (int64_t)N * G * 528 * 4 + G * 4 * 4;
+  return std::max(fwd, bwd);
+}
+
+#define SW_DISPATCH_G(KERNEL, T, ...)                                                                \
+  do {                                                                                              \
+    if (G <= 4)                                                                                     \
+      hipLaunchKernelGGL((KERNEL<T, 1>), __VA_ARGS__);                                              \
+    else if (G <= 8)                                                                                \
+      hipLaunchKernelGGL((KERNEL<T, 2>), __VA_ARGS__);                                              \
+    else                                                                                            \
+      hipLaunchKernelGGL((KERNEL<T, 4>), __VA_ARGS__);                                              \
+  } while (0)
+
+// SwitchWhiten2d forward (sw_type 2).  mean_w/var_w: the raw sw_mean_weight /
+// sw_var_weight parameters (softmax taken here).  save: dg_sw_save_size bytes,
+// consumed by dg_sw_bwd.  training: batch statistics + running-stat update;
+// otherwise running_mean/running_cov replace the batch statistics.
+extern "C" int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T, float eps,
+                         float momentum, const float* mean_w, const float* var_w, const float* gamma,
+                         const float* beta, float* running_mean, float* running_cov, int training, int act,
+                         float* save, void* y, int64_t ldy, void* workspace, void* stream) {
+  DG_REQUIRE(x && y && save && workspace && mean_w && var_w && running_mean && running_cov);
+  DG_REQUIRE(N > 0 && HW > 0 && C > 0 && T >= 0 && (!gamma || beta));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % SWC == 0 && C <= 256 && T <= SW_MAXT && ldx % V == 0 && ldy % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const int G = C / SWC, nb = sw_nb(HW), ppb = dg_cdiv(HW, nb);
+  float* mu = save;  // mu_in is the first save slot
+  char* w = (char*)workspace;
+  const int64_t in_ws = dg_instnorm_workspace(N, HW, C);
+  float* invstd_scratch = (float*)(w + in_ws);
+  float* part = invstd_scratch + (int64_t)N * C;
+  int rc = dg_instnorm_stats(dtype, x, ldx, N, HW, C, 1e-5f, mu, invstd_scratch, w, stream);
+  if (rc) return rc;
+  if (dtype == DG_BF16)
+    SW_DISPATCH_G(sw_cov_partial, bf16, dim3(nb, N), dim3(256), 0, st, (const bf16*)x, ldx, HW, C, ppb, mu, part);
+  else
+    SW_DISPATCH_G(sw_cov_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)x, ldx, HW, C, ppb, mu, part);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sw_stats_finalize, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, T, eps, momentum, mean_w,
+                     var_w, gamma, beta, running_mean, running_cov, training, save);
+  DG_CHECK_LAUNCH();
+  const float* aff = save + (int64_t)N * C + (int64_t)N * G * 256 + C + (int64_t)G * 256;
+  const float* bias = aff + (int64_t)N * G * 256;
+  const int anb = std::max(1, std::min(256, dg_cdiv(HW, 256)));
+  const int appb = dg_cdiv(HW, anb);
+  const size_t lds = (size_t)G * 273 * 4;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(sw_apply<bf16>, dim3(anb, N), dim3(256), lds, st, (const bf16*)x, ldx, HW, C, appb, aff, bias,
+                       act, (bf16*)y, ldy);
+  else
+    hipLaunchKernelGGL(sw_apply<float>, dim3(anb, N), dim3(256), lds, st, (const float*)x, ldx, HW, C, appb, aff,
+                       bias, act, (float*)y, ldy);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// Backward of dg_sw_fwd (training mode).  gy: upstream gradient of y; y: the
+// forward output (ReLU mask when act == 1); x: forward input.  Writes dx (+=
+// when accumulate), dgamma/dbeta, d(sw_mean_weight), d(sw_var_weight) (each
+// may be NULL).
+extern "C" int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+                         int64_t ldx, int N, int HW, int C, int T, float eps, const float* mean_w,
+                         const float* var_w, const float* gamma, int act, const float* save, void* dx, int64_t lddx,
+                         int accumulate, float* dgamma, float* dbeta, float* dmean_w, float* dvar_w,
+                         void* workspace, void* stream) {
+  DG_REQUIRE(gy && x && dx && save && workspace && mean_w && var_w && (act == 0 || y));
+  DG_REQUIRE(N > 0 && HW > 0 && C > 0 && T >= 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % SWC == 0 && C <= 256 && T <= SW_MAXT && ldx % V == 0 && ldg % V == 0 && lddx % V == 0 &&
+               (act == 0 || ldy % V == 0));
+  hipStream_t st = (hipStream_t)stream;
+  const int G = C / SWC, nb = sw_nb(HW), ppb = dg_cdiv(HW, nb);
+  const float* mu = save;
+  float* part = (float*)workspace;
+  float* coef = part + (int64_t)N * nb * G * 272;
+  float* wpart = coef + (int64_t)N * G * 528;
+  if (dtype == DG_BF16)
+    SW_DISPATCH_G(sw_bwd_partial, bf16, dim3(nb, N), dim3(256), 0, st, (const bf16*)gy, ldg, (const bf16*)y, ldy,
+                  (const bf16*)x, ldx, HW, C, ppb, act, mu, part);
+  else
+    SW_DISPATCH_G(sw_bwd_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)gy, ldg, (const float*)y, ldy,
+                  (const float*)x, ldx, HW, C, ppb, act, mu, part);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sw_bwd_small, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, T, eps, mean_w, var_w, gamma, save,
+                     coef, wpart, dgamma, dbeta);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sw_bwd_weights, dim3(1), dim3(64), 0, st, wpart, G, mean_w, var_w, dmean_w, dvar_w);
+  DG_CHECK_LAUNCH();
+  const int anb = std::max(1, std::min(256, dg_cdiv(HW, 256)));
+  const int appb = dg_cdiv(HW, anb);
+  const size_t lds = (size_t)G * 545 * 4;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(sw_bwd_apply<bf16>, dim3(anb, N), dim3(256), lds, st, (const bf16*)gy, ldg, (const bf16*)y, ldy,
+                       (const bf16*)x, ldx, HW, C, appb, act, mu, coef, (bf16*)dx, lddx, accumulate);
+  else
+    hipLaunchKernelGGL(sw_bwd_apply<float>, dim3(anb, N), dim3(256), lds, st, (const float*)gy, ldg, (const float*)y,
+                       ldy, (const float*)x, ldx, HW, C, appb, act, mu, coef, (float*)dx, lddx, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}

@@ -236,3 +236,157 @@ def dmap_fixed(points: torch.Tensor, offsets: torch.Tensor, N: int, H: int, W: i
     call("dg_dmap_fixed", ptr(points) if points.numel() else None, ptr(offsets), N, H, W,
          float(sigma), int(radius), ptr(out), stream())
     return out
+
+
+# ---------------------------------------------------------------- ResNet trunks -
+def conv_out(H: int, R: int, stride: int, pad: int) -> int:
+    return (H + 2 * pad - R) // stride + 1
+
+
+def pack_weight_t(wp: torch.Tensor, Cout: int, C: int, R: int, S: int) -> torch.Tensor:
+    """packed [Cout][R][S][C] -> [C][R][S][Cout] (dgrad operand of strided convs)."""
+    wt = torch.empty((C, R * S * Cout), dtype=wp.dtype, device=wp.device)
+    call("dg_transpose_weight", dtype_code(wp.dtype), ptr(wp), Cout, C, R, S, ptr(wt), stream())
+    return wt
+
+
+def conv2d_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, stride: int, pad: int, y: Act,
+               bias: torch.Tensor | None = None, accumulate=False, kind="fwd", k_alg=None):
+    """General conv (any R, stride, pad): y [N,P,Q,Cout]."""
+    P, Q = conv_out(x.H, R, stride, pad), conv_out(x.W, R, stride, pad)
+    if (y.H, y.W, y.N, y.C) != (P, Q, x.N, Cout):
+        raise DGError(f"conv2d_fwd: output {tuple(y.view().shape)} != {(x.N, P, Q, Cout)}")
+    M = x.N * P * Q
+    flops = 2.0 * M * (k_alg if k_alg else x.C * R * R) * Cout
+    es = x.buf.element_size()
+    nbytes = es * (x.M * x.C + wp.numel() + M * Cout * (2 if accumulate else 1))
+    _timed(kind, flops, lambda: call("dg_conv2d_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
+                                     Cout, R, R, stride, pad, ptr(bias), y.ptr, y.ld,
+                                     int(accumulate), stream()), nbytes)
+
+
+def conv2d_dgrad(dy: Act, wt: torch.Tensor, R: int, stride: int, pad: int, dx: Act, accumulate=False):
+    """dX [N,H,W,C] of a general conv from dY [N,P,Q,Cout] and the transposed filter wt."""
+    if conv_out(dx.H, R, stride, pad) != dy.H or conv_out(dx.W, R, stride, pad) != dy.W:
+        raise DGError("conv2d_dgrad: dx/dy spatial sizes disagree with R/stride/pad")
+    flops = 2.0 * dy.M * dx.C * R * R * dy.C
+    es = dy.buf.element_size()
+    nbytes = es * (dy.M * dy.C + wt.numel() + dx.M * dx.C * (2 if accumulate else 1))
+    _timed("dgrad", flops, lambda: call("dg_conv2d_dgrad", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W,
+                                        dy.C, ptr(wt), dx.C, dx.H, dx.W, R, R, stride, pad, dx.ptr,
+                                        dx.ld, int(accumulate), stream()), nbytes)
+
+
+def conv2d_wgrad(x: Act, dy: Act, R: int, stride: int, pad: int, dw: torch.Tensor,
+                 accumulate=False, k_alg=None):
+    ws = query("dg_conv2d_wgrad_workspace", x.dt, dy.N, dy.H, dy.W, x.C, dy.C, R, R)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
+    flops = 2.0 * dy.M * (k_alg if k_alg else x.C * R * R) * dy.C
+    nbytes = x.buf.element_size() * (x.M * x.C + dy.M * dy.C) + 4 * dw.numel()
+    _timed("wgrad", flops, lambda: call("dg_conv2d_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
+                                        dy.ptr, dy.ld, dy.C, R, R, stride, pad, ptr(dw), ptr(work),
+                                        ws, int(accumulate), stream()), nbytes)
+
+
+def im2col_c3_general(img: torch.Tensor, dtype: torch.dtype, R: int, stride: int, pad: int,
+                      kpad: int) -> torch.Tensor:
+    N, _, H, W = img.shape
+    P, Q = conv_out(H, R, stride, pad), conv_out(W, R, stride, pad)
+    out = torch.empty((N, P, Q, kpad), dtype=dtype, device=img.device)
+    call("dg_im2col_c3", dtype_code(dtype), ptr(img.contiguous()), N, H, W, R, R, stride, pad, kpad,
+         ptr(out), stream())
+    return out
+
+
+def unpack_c3(dwcol: torch.Tensor, dw: torch.Tensor, accumulate=False):
+    Cout, _, R, S = dw.shape
+    call("dg_unpack_c3", ptr(dwcol), Cout, R, S, dwcol.shape[1], ptr(dw), int(accumulate), stream())
+
+
+def maxpool_k_fwd(x: Act, k: int, stride: int, pad: int, y: Act):
+    call("dg_maxpool_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, k, stride, pad, y.ptr, y.ld,
+         stream())
+
+
+def maxpool_k_bwd(x: Act, gy: Act, k: int, stride: int, pad: int, gx: Act, accumulate=False):
+    call("dg_maxpool_bwd", x.dt, x.ptr, x.ld, gy.ptr, gy.ld, x.N, x.H, x.W, x.C, k, stride, pad,
+         gx.ptr, gx.ld, int(accumulate), stream())
+
+
+def bn_add_apply(z1: Act, st1, z2: Act, st2, act: int, y: Act):
+    """y = act(bn1(z1) + (bn2(z2) if st2 is not None else z2)) — Bottleneck join."""
+    call("dg_bn_add_apply", z1.dt, z1.ptr, z1.ld, z1.M, z1.C, ptr(st1[2]), ptr(st1[3]), z2.ptr,
+         z2.ld, ptr(st2[2]) if st2 is not None else None, ptr(st2[3]) if st2 is not None else None,
+         act, y.ptr, y.ld, stream())
+
+
+def relu_bwd(g: Act, y: Act, out: Act):
+    call("dg_relu_bwd", g.dt, g.ptr, g.ld, y.ptr, y.ld, y.M, y.C, out.ptr, out.ld, stream())
+
+
+def instnorm_stats(x: Act, eps: float = 1e-5) -> torch.Tensor:
+    """[2, N, C] f32: mean, invstd (biased variance) per (n, c)."""
+    st = torch.empty((2, x.N, x.C), dtype=torch.float32, device=x.buf.device)
+    ws = query("dg_instnorm_workspace", x.N, x.H * x.W, x.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
+    call("dg_instnorm_stats", x.dt, x.ptr, x.ld, x.N, x.H * x.W, x.C, float(eps), ptr(st[0]),
+         ptr(st[1]), ptr(work), stream())
+    return st
+
+
+def instnorm_apply(x: Act, st, gamma, beta, act: int, y: Act):
+    call("dg_instnorm_apply", x.dt, x.ptr, x.ld, x.N, x.H * x.W, x.C, ptr(st[0]), ptr(st[1]),
+         ptr(gamma), ptr(beta), act, y.ptr, y.ld, stream())
+
+
+def instnorm_bwd(g: Act, x: Act, st, gamma, dx: Act, dgamma=None, dbeta=None, accumulate=False):
+    ws = query("dg_instnorm_bwd_workspace", x.N, x.H * x.W, x.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
+    call("dg_instnorm_bwd", x.dt, g.ptr, g.ld, x.ptr, x.ld, x.N, x.H * x.W, x.C, ptr(st[0]),
+         ptr(st[1]), ptr(gamma), dx.ptr, dx.ld, int(accumulate), ptr(dgamma), ptr(dbeta),
+         ptr(work), stream())
+
+
+# ---------------------------------------------------------------- whitening -
+def iw_loss(fraw: torch.Tensor, hw: int, mask: torch.Tensor, num_sensitive: torch.Tensor,
+            out_scale: float, loss: torch.Tensor | None, accumulate: bool,
+            want_grad: bool, grad_coef: torch.Tensor | None = None, eps: float = 1e-5):
+    """instance_whitening_loss over a batch of raw Gram matrices fraw [B,C,C]."""
+    B, C, _ = fraw.shape
+    ws = query("dg_iw_loss_workspace", B, C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=fraw.device)
+    gsym = torch.empty_like(fraw) if want_grad else None
+    call("dg_iw_loss", ptr(fraw), B, C, 1.0 / (hw - 1), float(eps), ptr(mask), ptr(num_sensitive),
+         ptr(grad_coef), float(out_scale), int(accumulate), ptr(loss), ptr(gsym), ptr(work), stream())
+    return gsym
+
+
+def iw_cov_var(fraw: torch.Tensor, hw: int, var: torch.Tensor, accumulate=False):
+    B, C, _ = fraw.shape
+    call("dg_iw_cov_var", ptr(fraw), B, C, 1.0 / (hw - 1), ptr(var), int(accumulate), stream())
+
+
+def sw_fwd(x: Act, mean_w, var_w, gamma, beta, running_mean, running_cov, training: bool,
+           act: int, y: Act, T: int = 5, eps: float = 1e-5, momentum: float = 0.9) -> torch.Tensor:
+    """SwitchWhiten2d (sw_type 2) forward; returns the `save` statistics buffer."""
+    HW = x.H * x.W
+    save = torch.empty(query("dg_sw_save_size", x.N, x.C) // 4, dtype=torch.float32,
+                       device=x.buf.device)
+    ws = query("dg_sw_workspace", x.N, HW, x.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
+    call("dg_sw_fwd", x.dt, x.ptr, x.ld, x.N, HW, x.C, int(T), float(eps), float(momentum),
+         ptr(mean_w), ptr(var_w), ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_cov),
+         int(training), act, ptr(save), y.ptr, y.ld, ptr(work), stream())
+    return save
+
+
+def sw_bwd(gy: Act, y: Act | None, x: Act, save, mean_w, var_w, gamma, act: int, dx: Act,
+           dgamma=None, dbeta=None, dmean_w=None, dvar_w=None, accumulate=False, T: int = 5,
+           eps: float = 1e-5):
+    HW = x.H * x.W
+    ws = query("dg_sw_workspace", x.N, HW, x.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
+    call("dg_sw_bwd", x.dt, gy.ptr, gy.ld, y.ptr if y is not None else None,
+         y.ld if y is not None else 0, x.ptr, x.ld, x.N, HW, x.C, int(T), float(eps), ptr(mean_w),
+         ptr(var_w), ptr(gamma), act, ptr(save), dx.ptr, dx.ld, int(accumulate), ptr(dgamma),
+         ptr(dbeta), ptr(dmean_w), ptr(dvar_w), ptr(work), stream())

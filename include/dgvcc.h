@@ -73,6 +73,32 @@ int dg_im2col3x3_c3(int dtype, const float* img, int N, int H, int W, void* out,
 /* dW for the im2col'd first layer: col-layout grad [Cout][64] -> torch [Cout][3][3][3]. */
 int dg_unpack_c3_grad(const float* dwcol, int Cout, float* dw, int accumulate, void* stream);
 
+/* ---- general convolution (ResNet-50 trunks of IBN-Net / ISW / SW) ------------
+ * Replaces the strided nn.Conv2d of models/ibnnet/resnet_ibn.py:65-107,
+ * models/ISW/Resnet.py:137-216,395-495 and models/SW/backbones/resnet.py:75-212.
+ * Any R x S, stride, pad; output P = (H+2pad-R)/stride+1.  Whole-tensor buffer
+ * addressing: the gathered tensor must be < 2 GiB. */
+int dg_conv2d_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                  const void* w, int Cout, int R, int S, int stride, int pad, const float* bias,
+                  void* y, int64_t ldy, int accumulate, void* stream);
+/* wt[C][R][S][Cout] = w[Cout][R][S][C] (packed filters, no flip) */
+int dg_transpose_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wt, void* stream);
+/* dX [N,H,W,C] from dY [N,P,Q,Cout] and wt (transposed gather: taps whose
+ * (p + pad - r) is a multiple of stride). */
+int dg_conv2d_dgrad(int dtype, const void* dy, int64_t lddy, int N, int P, int Q, int Cout,
+                    const void* wt, int C, int H, int W, int R, int S, int stride, int pad,
+                    void* dx, int64_t lddx, int accumulate, void* stream);
+int64_t dg_conv2d_wgrad_workspace(int dtype, int N, int P, int Q, int C, int Cout, int R, int S);
+int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                    const void* dy, int64_t lddy, int Cout, int R, int S, int stride, int pad,
+                    float* dw, void* workspace, int64_t ws_bytes, int accumulate, void* stream);
+/* Cin=3 stems (7x7/2 of the ResNets): NCHW f32 -> im2col [N*P*Q][Kpad], k=(r*S+s)*3+c */
+int dg_im2col_c3(int dtype, const float* img, int N, int H, int W, int R, int S, int stride,
+                 int pad, int Kpad, void* out, void* stream);
+/* col-layout filter grad [Cout][Kpad] -> torch [Cout][3][R][S] */
+int dg_unpack_c3(const float* dwcol, int Cout, int R, int S, int Kpad, float* dw, int accumulate,
+                 void* stream);
+
 /* ---- batch norm (training statistics) + activation -------------------------
  * Replaces nn.BatchNorm2d(train) + nn.ReLU (vgg16_bn, ConvBlock bn=True).
  * Stats are per channel over N*H*W pixels; running stats use momentum and the
@@ -96,6 +122,62 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
               void* workspace, void* stream);
 
+/* ---- ResNet bottleneck joins and InstanceNorm (IBN-b / ISW / SW trunks) --------
+ * Residual join out = act(bn3(z1) + bn_ds(z2) | z2) of Bottleneck.forward
+ * (models/ibnnet/resnet_ibn.py:96-107, models/ISW/Resnet.py:187-216,
+ * models/SW/backbones/resnet.py:100-118). scale2/shift2 NULL = identity shortcut. */
+int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, int C, const float* scale1,
+                    const float* shift1, const void* z2, int64_t ld2, const float* scale2,
+                    const float* shift2, int act, void* y, int64_t ldy, void* stream);
+/* nn.ReLU backward from the saved output: out = g * (y > 0) (out may alias g). */
+int dg_relu_bwd(int dtype, const void* g, int64_t ldg, const void* y, int64_t ldy, int M, int C,
+                void* out, int64_t ldo, void* stream);
+/* nn.InstanceNorm2d(affine) with statistics from dg_instnorm_stats:
+ * y = act((x-mean[n,c])*invstd[n,c]*gamma[c]+beta[c]); gamma/beta NULL = affine=False
+ * (IBN-b IN, resnet_ibn.py:77,115,159; ISW InstanceWhitening, instance_whitening.py:5-16). */
+int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, int HW, int C,
+                      const float* mean, const float* invstd, const float* gamma,
+                      const float* beta, int act, void* y, int64_t ldy, void* stream);
+/* Backward of the above (g already masked by any following ReLU): dx (+)=, dgamma/dbeta
+ * written (sum over n), either may be NULL. */
+int64_t dg_instnorm_bwd_workspace(int N, int HW, int C);
+int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void* x, int64_t ldx, int N,
+                    int HW, int C, const float* mean, const float* invstd, const float* gamma,
+                    void* dx, int64_t lddx, int accumulate, float* dgamma, float* dbeta,
+                    void* workspace, void* stream);
+
+/* ---- instance / switchable whitening ------------------------------------------
+ * ISW (models/ISW/instance_whitening.py:19-39, models/ISW/__init__.py:93-120):
+ * fraw [B][C][C] = per-instance sum_p w_p w_p^T (dg_conv2d_wgrad of w with itself);
+ * f = fraw*inv_hw1 + eps*I.  loss (+)= out_scale * mean_b sum|f o mask|/ns (ns = device
+ * scalar); gsym[b] (may be NULL) = d loss/d fraw symmetrised and scaled by inv_hw1, so
+ * dL/dw_b = w_b gsym[b] (a 1x1 conv).  grad_coef: device scalar upstream grad (NULL = 1). */
+int64_t dg_iw_loss_workspace(int B, int C);
+int dg_iw_loss(const float* fraw, int B, int C, float inv_hw1, float eps, const float* mask,
+               const float* num_sensitive, const float* grad_coef, float out_scale, int accumulate,
+               float* loss, float* gsym, void* workspace, void* stream);
+/* cal_covstat: var[C][C] (+)= unbiased variance over B of f_ij*[j>i]. */
+int dg_iw_cov_var(const float* fraw, int B, int C, float inv_hw1, float* var, int accumulate,
+                  void* stream);
+/* SwitchWhiten2d sw_type 2 (BW+IW), 16 channels per group, C <= 256
+ * (models/SW/ops/switchwhiten.py:84-183).  mean_w/var_w: raw sw_mean_weight /
+ * sw_var_weight (softmax inside).  running_mean [G][16], running_cov [G][16][16] updated
+ * with `momentum` when training.  y = act(gamma*W(x-mean)+beta); `save`
+ * (dg_sw_save_size bytes) holds the statistics for dg_sw_bwd. */
+int64_t dg_sw_save_size(int N, int C);
+int64_t dg_sw_workspace(int N, int HW, int C);
+int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T, float eps,
+              float momentum, const float* mean_w, const float* var_w, const float* gamma,
+              const float* beta, float* running_mean, float* running_cov, int training, int act,
+              float* save, void* y, int64_t ldy, void* workspace, void* stream);
+/* Exact adjoint (batch statistics, Newton-Schulz iterations recomputed). y = forward
+ * output (ReLU mask when act == 1). Any of dgamma/dbeta/dmean_w/dvar_w may be NULL. */
+int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+              int64_t ldx, int N, int HW, int C, int T, float eps, const float* mean_w,
+              const float* var_w, const float* gamma, int act, const float* save, void* dx,
+              int64_t lddx, int accumulate, float* dgamma, float* dbeta, float* dmean_w,
+              float* dvar_w, void* workspace, void* stream);
+
 /* ---- pooling / resampling ---------------------------------------------------
  * nn.MaxPool2d(2,2) (vgg16_bn features 6,13,23,33) and F.interpolate
  * (models/models.py:23-27).  Bilinear supports align_corners 0/1, nearest. */
@@ -104,6 +186,14 @@ int dg_maxpool2_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, 
 int dg_maxpool2_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy,
                     int N, int H, int W, int C, void* gx, int64_t ldgx, int accumulate,
                     void* stream);
+/* nn.MaxPool2d(k, stride, pad) of the ResNet stems (models/ibnnet/resnet_ibn.py:161,
+ * models/ISW/Resnet.py:288, models/SW/backbones/resnet.py:153): -inf padding, first
+ * maximum wins, NaN propagates (ATen). Output P = (H+2pad-k)/stride+1. */
+int dg_maxpool_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int k,
+                   int stride, int pad, void* y, int64_t ldy, void* stream);
+int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy, int N,
+                   int H, int W, int C, int k, int stride, int pad, void* gx, int64_t ldgx,
+                   int accumulate, void* stream);
 /* mode: 0 bilinear(align_corners=False), 1 bilinear(align_corners=True), 2 nearest */
 int dg_upsample_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int scale,
                     int mode, void* y, int64_t ldy, void* stream);

@@ -165,6 +165,152 @@ def gen_dmap_adaptive():
     np.savez_compressed(os.path.join(HERE, "dmap_adaptive.npz"), **out)
 
 
+# ---------------------------------------------------------------------------
+# ResNet-50 DG trunks (IBN-b / SW / ISW), SwitchWhiten2d and the ISW loss
+# ---------------------------------------------------------------------------
+def _patch_offline():
+    """The counters hard-code pretrained=True (remote weights) and call .cuda();
+    build them with pretrained=False and make .cuda() a no-op for this process."""
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    torch.cuda.current_device = lambda: 0  # only gates a log print (cov_settings.py:79)
+    ibn = import_ref("models.ibnnet")
+    if not getattr(ibn, "_dg_patched", False):
+        f = ibn.resnet50_ibn_b
+        ibn.resnet50_ibn_b = lambda pretrained=True, **k: f(pretrained=False, **k)
+        ibn._dg_patched = True
+    sw = import_ref("models.SW")
+    if not getattr(sw, "_dg_patched", False):
+        f2 = sw.resnet50
+        sw.resnet50 = lambda pretrained=True, **k: f2(pretrained=False, **k)
+        sw._dg_patched = True
+    R = import_ref("models.ISW.Resnet")
+    if not getattr(R, "_dg_patched", False):
+        f3 = R.resnet50
+        R.resnet50 = lambda pretrained=True, **k: f3(pretrained=False, **k)
+        R._dg_patched = True
+    isw = import_ref("models.ISW")
+    return {"ibn": ibn.IBNCounter_ResNet, "sw": sw.SWCounter_ResNet, "isw": isw.ISWCounter_ResNet}
+
+
+def gen_sw_op():
+    _patch_offline()
+    swm = import_ref("models.SW.ops.switchwhiten")
+    g = torch.Generator().manual_seed(5)
+    out = {}
+    m = swm.SwitchWhiten2d(32, num_pergroup=16, sw_type=2, T=5, tie_weight=False, eps=1e-5,
+                           momentum=0.9, affine=True)
+    with torch.no_grad():
+        m.sw_mean_weight.copy_(torch.randn(2, generator=g))
+        m.sw_var_weight.copy_(torch.randn(2, generator=g))
+        m.weight.copy_(torch.rand(32, generator=g) + 0.5)
+        m.bias.copy_(torch.randn(32, generator=g) * 0.1)
+        m.running_mean.copy_(torch.randn(2, 16, 1, generator=g) * 0.1)
+        a = torch.randn(2, 16, 16, generator=g) * 0.3
+        m.running_cov.copy_(a @ a.transpose(1, 2) + torch.eye(16))
+    for k, v in m.state_dict().items():
+        out["init__" + k] = v.numpy().copy()
+    x = (torch.randn(3, 32, 5, 7, generator=g) * 2 + 0.5).requires_grad_(True)
+    gy = torch.randn(3, 32, 5, 7, generator=g)
+    m.train()
+    y = m(x)
+    y.backward(gy)
+    out["x"] = x.detach().numpy()
+    out["gy"] = gy.numpy()
+    out["y"] = y.detach().numpy()
+    out["gx"] = x.grad.numpy()
+    for k, p in m.named_parameters():
+        out["grad__" + k] = p.grad.numpy()
+    for k in ("running_mean", "running_cov"):
+        out["post__" + k] = getattr(m, k).numpy()
+    m.eval()
+    with torch.no_grad():
+        out["y_eval"] = m(x.detach()).numpy()
+    np.savez_compressed(os.path.join(HERE, "sw_op.npz"), **out)
+
+
+def gen_iw_loss():
+    _patch_offline()
+    iwm = import_ref("models.ISW.instance_whitening")
+    cs = import_ref("models.ISW.cov_settings")
+    g = torch.Generator().manual_seed(6)
+    out = {}
+    C = 16
+    cm = cs.CovMatrix_ISW(dim=C, relax_denom=2.0, clusters=3)
+    eye, rev = cm.get_eye_matrix()
+    for r in range(2):  # cal_covstat accumulations (ISW/__init__.py:93-104)
+        f = torch.randn(4, C, 6, 5, generator=g)
+        f = f + 0.5 * f[:, :1]  # correlated channels
+        out[f"cov_in{r}"] = f.numpy()
+        fc = torch.bmm(f.view(4, C, -1), f.view(4, C, -1).transpose(1, 2)).div(30 - 1) + 1e-5 * eye
+        cm.set_variance_of_covariance(torch.var(fc * rev, dim=0))
+    eye, mask, margin, ns = cm.get_mask_matrix()
+    out["mask"] = mask.numpy()
+    out["num_sensitive"] = np.array([float(ns)])
+    f_map = torch.randn(3, C, 7, 4, generator=g)
+    f_map = (f_map + 0.3 * f_map[:, 1:2]).requires_grad_(True)
+    loss = iwm.instance_whitening_loss(f_map, eye, mask, margin, ns)
+    loss.backward()
+    out["f_map"] = f_map.detach().numpy()
+    out["loss"] = np.array([loss.item()])
+    out["grad"] = f_map.grad.numpy()
+    np.savez_compressed(os.path.join(HERE, "iw_loss.npz"), **out)
+
+
+def gen_trunk(kind, B=2, H=64, W=64, dtype=torch.float32):
+    """dtype float64 for SW: the fp32 reference's Newton-Schulz backward amplifies
+    rounding noise to ~1e-2 in early-layer grads; the float64 run is the exact math."""
+    ctors = _patch_offline()
+    model = ctors[kind]()
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    model.to(dtype)
+    img1, img2, (pts, dmaps, bmaps) = O.synthetic_batch(B, H, W, seed=2112)
+    img1, img2, dmaps = img1.to(dtype), img2.to(dtype), dmaps.to(dtype)
+    out = {"shape": np.array([B, H, W]), "dtype64": np.array([dtype == torch.float64])}
+    if kind == "isw":
+        model.eval()  # cal_covstat runs from predict2 during validation (dgtrainer.py:94-100)
+        with torch.no_grad():
+            model([img1, img2], cal_covstat=True)
+        masks = []
+        for li, cm in enumerate(model.cov_matrix_layer):
+            summarize(f"var{li}", {"": cm.var_matrix / cm.count_var_cov}, out)
+            _, mk, _, ns = cm.get_mask_matrix()
+            out[f"mask{li}"] = np.packbits(mk.numpy().astype(np.uint8).reshape(-1))
+            out[f"ns{li}"] = np.array([float(ns)])
+            masks.append(mk)
+        model.train()
+        cap = {}
+        h = model.head.register_forward_hook(lambda mod, inp, o: cap.update(out=o.detach()))  # returns None
+        loss1, wt = model(img1, gts=dmaps, apply_wtloss=True)
+        h.remove()
+        out["out"] = cap["out"].numpy()
+        total = loss1 + 0.6 * wt  # dgtrainer.py:196-203 (epoch > 5)
+        out["loss1"] = np.array([loss1.item()])
+        out["wt_loss"] = np.array([float(wt)])
+        total.sum().backward()
+    else:
+        model.train()
+        pred = model(img1)
+        out["out"] = pred.detach().float().numpy()
+        loss = torch.nn.functional.mse_loss(pred, dmaps * 1000)
+        out["loss"] = np.array([loss.item()])
+        loss.backward()
+    grads = {k: p.grad if p.grad is not None else torch.zeros_like(p)
+             for k, p in model.named_parameters()}
+    summarize("grad__", grads, out)
+    summarize("post__", {k: v for k, v in model.state_dict().items()
+                         if not k.endswith("num_batches_tracked")}, out)
+    np.savez_compressed(os.path.join(HERE, f"trunk_{kind}.npz"), **out)
+
+
+def gen_trunk_keys():
+    import json
+    ctors = _patch_offline()
+    out = {k: [[n, list(v.shape)] for n, v in c().state_dict().items()] for k, c in ctors.items()}
+    json.dump(out, open(os.path.join(HERE, "trunk_state_dict_keys.json"), "w"))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
     which = sys.argv[1:] or ["dmap", "base", "final", "bl", "keys", "dmap_adaptive"]
@@ -180,4 +326,13 @@ if __name__ == "__main__":
         gen_state_dict_keys()
     if "dmap_adaptive" in which:
         gen_dmap_adaptive()
+    if "sw_op" in which:
+        gen_sw_op()
+    if "iw_loss" in which:
+        gen_iw_loss()
+    for kind in ("ibn", "sw", "isw"):
+        if "trunk_" + kind in which:
+            gen_trunk(kind, dtype=torch.float64 if kind == "sw" else torch.float32)
+    if "trunk_keys" in which:
+        gen_trunk_keys()
     print("fixtures written to", HERE)

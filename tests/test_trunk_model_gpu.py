@@ -1,0 +1,187 @@
+"""ResNet-50 DG counters (IBN-b / SW / ISW) on the HIP trunk plans against the
+CPU oracle (oracle/trunk_oracle.py, pinned to the reference by
+tests/test_trunk_oracle.py) on the same seeded weights and synthetic frames.
+
+Criteria: outputs/losses vs the float64 oracle within max(3 x the fp32 oracle's
+own error, 1e-4) relative; gradients normwise per parameter within
+max(2 x the fp32 oracle's error, 5e-3) (BN over a handful of pixels and
+ReLU-mask flips make fp32 gradients differ at that level in any implementation,
+see tests/test_model_gpu.py::_check_grads).
+"""
+import os
+import tempfile
+
+import pytest
+import torch
+
+from oracle import dg_oracle as O
+from oracle import trunk_oracle as TO
+
+pytestmark = pytest.mark.gpu
+
+GRAD_TOL = 5e-3
+
+
+def rel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
+
+
+def _cls(kind):
+    from dgvcc_amd.models import trunks
+    return {"ibn": trunks.IBNCounter_ResNet, "sw": trunks.SWCounter_ResNet,
+            "isw": trunks.ISWCounter_ResNet}[kind]
+
+
+def _setup(kind, dev, B=2, H=64, W=64, precision="fp32"):
+    model = _cls(kind)(pretrained=False)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    model = model.to(dev).set_precision(precision)
+    return model, sd0, O.synthetic_batch(B, H, W, seed=2112)
+
+
+def _oracle(kind, sd0, img, dmaps, dtype, masks=None):
+    sd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd0.items()}
+    sd = {k: v.requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
+    if kind == "isw":
+        l1, wt, out = TO.isw_train_forward(img.to(dtype), dmaps.to(dtype), sd,
+                                           [(m.to(dtype), ns) for m, ns in masks])
+        (l1 + 0.6 * wt).backward()
+        loss = (l1.detach(), wt.detach())
+    else:
+        out, _ = TO.counter_forward(kind, img.to(dtype), sd, True)
+        l1 = torch.nn.functional.mse_loss(out, dmaps.to(dtype) * 1000)
+        l1.backward()
+        loss = (l1.detach(),)
+    grads = {k: (v.grad if v.grad is not None else torch.zeros_like(v)).double()
+             for k, v in sd.items() if v.requires_grad}
+    return out.detach().double(), loss, grads
+
+
+def _check_grads(model, g64, g32, tol=GRAD_TOL):
+    bad = {}
+    for k, p in model.named_parameters():
+        if k not in g64 or g64[k].norm() == 0:
+            continue
+        g = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().cpu()
+        mine = ((g - g64[k]).norm() / g64[k].norm()).item()
+        ref = ((g32[k] - g64[k]).norm() / g64[k].norm()).item()
+        if mine > max(2 * ref, tol):
+            bad[k] = (mine, ref)
+    assert not bad, bad
+
+
+def _masks_from_model(model):
+    return [(cm.mask_matrix.float().cpu(), float(cm.num_sensitive)) for cm in model.cov_matrix_layer]
+
+
+@pytest.mark.parametrize("kind", ["ibn", "sw"])
+def test_counter_train_fp32(dev, kind):
+    from dgvcc_amd.losses import mse_loss
+    model, sd0, batch = _setup(kind, dev)
+    img, _, (_, dmaps, _) = batch
+    out64, (l64,), g64 = _oracle(kind, sd0, img, dmaps, torch.float64)
+    out32, (l32,), g32 = _oracle(kind, sd0, img, dmaps, torch.float32)
+    model.train()
+    out = model(img.to(dev))
+    loss = mse_loss(out, dmaps.to(dev), 1000.0)
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel(out, out64) < max(3 * rel(out32, out64), 1e-4)
+    assert abs(loss.item() - l64.item()) <= max(3 * abs(l32.item() - l64.item()), 1e-4 * l64.item())
+    _check_grads(model, g64, {k: v.double() for k, v in g32.items()})
+
+
+def test_sw_running_stats(dev):
+    """SwitchWhiten2d running_mean/running_cov updates (momentum 0.9) and the eval
+    forward on the updated statistics (running stats start at zero, as the
+    reference's reset_parameters, switchwhiten.py:64-67)."""
+    model, sd0, batch = _setup("sw", dev)
+    sd0 = {k: (torch.zeros_like(v) if k.endswith(("running_mean", "running_cov")) else v)
+           for k, v in sd0.items()}
+    model.load_state_dict(sd0)
+    img = batch[0]
+    sd = {k: v.double().clone() if v.is_floating_point() else v.clone() for k, v in sd0.items()}
+    with torch.no_grad():
+        TO.counter_forward("sw", img.double(), sd, True)
+        model.train()
+        model(img.to(dev))
+    msd = model.state_dict()
+    for k in sd:
+        if k.endswith(("running_mean", "running_cov", "running_var")):
+            assert rel(msd[k], sd[k]) < 1e-3, k
+    with torch.no_grad():
+        model.eval()
+        out = model(img.to(dev))
+        ref, _ = TO.counter_forward("sw", img.double(), sd, False)
+    assert rel(out, ref) < 1e-3
+
+
+def test_isw_covstat_and_train_fp32(dev):
+    model, sd0, batch = _setup("isw", dev)
+    img1, img2, (_, dmaps, _) = batch
+    # cal_covstat in eval mode (dgtrainer.py:94-100) -> sensitive-covariance masks
+    model.eval()
+    with torch.no_grad():
+        assert model([img1.to(dev), img2.to(dev)], cal_covstat=True) == 0
+    model.set_mask_matrix()
+    masks = _masks_from_model(model)
+    with torch.no_grad():
+        _, w = TO.counter_forward("isw", torch.cat([img1, img2]).double(),
+                                  {k: v.double() if v.is_floating_point() else v for k, v in sd0.items()},
+                                  False)
+    for (m, ns), f in zip(masks, w):
+        mref, kref = TO.sensitive_mask(TO.cov_variance(f), 1)
+        assert ns == kref
+        # top-k boundary ties can swap a few entries between fp32 and f64 variances
+        assert (m != mref.float()).float().mean().item() < 1e-3
+    model.train()
+    losses = model(img1.to(dev), gts=dmaps.to(dev), apply_wtloss=True)
+    (losses[0] + 0.6 * losses[1]).sum().backward()
+    torch.cuda.synchronize()
+    out64, (l64, wt64), g64 = _oracle("isw", sd0, img1, dmaps, torch.float64, masks)
+    _, (l32, wt32), g32 = _oracle("isw", sd0, img1, dmaps, torch.float32, masks)
+    assert abs(losses[0].item() - l64.item()) <= max(3 * abs(l32.item() - l64.item()), 1e-4 * l64.item())
+    assert abs(losses[1].item() - wt64.item()) <= max(3 * abs(wt32.item() - wt64.item()), 1e-4 * wt64.item())
+    _check_grads(model, g64, {k: v.double() for k, v in g32.items()})
+
+
+def test_isw_trainer_step(dev):
+    """DGTrainer mode 'isw' (dgtrainer.py:194-204): epoch > 5 adds 0.6 x the whitening loss."""
+    from dgvcc_amd.trainers.dgtrainer import DGTrainer
+    model, sd0, batch = _setup("isw", dev)
+    img1, img2, _ = batch
+    model.eval()
+    with torch.no_grad():
+        model([img1.to(dev), img2.to(dev)], cal_covstat=True)
+    with tempfile.TemporaryDirectory() as td:
+        cwd = os.getcwd()
+        os.chdir(td)
+        try:
+            tr = DGTrainer(2112, "t", dev, 1000, 10000, "isw")
+            opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+            model.train()
+            l0 = tr.train_step(model, torch.nn.MSELoss(), opt, batch, 0)
+            l6 = tr.train_step(model, torch.nn.MSELoss(), opt, batch, 6)
+        finally:
+            os.chdir(cwd)
+    assert l0 > 0 and l6 > 0 and torch.isfinite(torch.tensor([l0, l6])).all()
+
+
+@pytest.mark.parametrize("kind", ["ibn", "sw", "isw"])
+def test_counter_bf16_close(dev, kind):
+    """bf16 storage + bf16 MFMA (f32 statistics): the count and map stay close to the
+    float64 oracle (training-mode statistics; ISW in eval mode)."""
+    model, sd0, batch = _setup(kind, dev, precision="bf16")
+    img = batch[0]
+    training = kind != "isw"
+    with torch.no_grad():
+        model.train(training)
+        out = model(img.to(dev))
+        sd = {k: v.double().clone() if v.is_floating_point() else v.clone() for k, v in sd0.items()}
+        ref, _ = TO.counter_forward(kind, img.double(), sd, training)
+    c, cr = out.sum().item(), ref.sum().item()
+    assert abs(c - cr) <= 5e-2 * abs(cr) + 1e-2 * ref.abs().sum().item()
+    assert rel(out, ref) < 0.15
