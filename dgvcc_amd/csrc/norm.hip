@@ -125,7 +125,12 @@ struct ChanParams {
   __device__ __forceinline__ void load(int c0, const float* scale, const float* shift, const float* mean,
                                        const float* invstd) {
 #pragma unroll
-    for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e]; }
+    for (int e = 0; e < V; ++e) {  // NULL = identity (conv + activation without normalisation)
+      sc[e] = scale ? scale[c0 + e] : 1.f;
+      sf[e] = shift ? shift[c0 + e] : 0.f;
+      mu[e] = mean ? mean[c0 + e] : 0.f;
+      is[e] = invstd ? invstd[c0 + e] : 1.f;
+    }
   }
 };
 
@@ -213,6 +218,13 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ 
   a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
   b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
   d = sh[2][0][cl] + sh[2][1][cl] + sh[2][2][cl] + sh[2][3][cl];
+  if (!invstd) {  // no normalisation: dz = act'(z) g ; dbeta = dbias = sum dz
+    if (dgamma) dgamma[c] = 0.f;
+    if (dbeta) dbeta[c] = (float)a;
+    if (dbias) dbias[c] = (float)a;
+    coef[c] = 1.f; coef[C + c] = 0.f; coef[2 * C + c] = 0.f;
+    return;
+  }
   const float gm = gamma ? gamma[c] : 1.f;
   const float k1 = gm * invstd[c];
   const float k2 = (float)(k1 * b / M);
@@ -341,7 +353,8 @@ extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, i
                          const float* gamma, const float* save_mean, const float* save_invstd, const float* scale,
                          const float* shift, int act, const float* drop, int HW, void* dz, int64_t lddz,
                          float* dgamma, float* dbeta, float* dbias, void* workspace, void* stream) {
-  DG_REQUIRE(g && z && dz && save_mean && save_invstd && scale && shift && workspace && M > 0 && C > 0);
+  DG_REQUIRE(g && z && dz && workspace && M > 0 && C > 0);
+  DG_REQUIRE((save_mean && save_invstd && scale && shift) || (!save_mean && !save_invstd));
   DG_REQUIRE(!drop || HW > 0);
   DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));

@@ -95,7 +95,8 @@ class ConvLayer:
         dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) \
             if self.conv.bias is not None else None
         gamma = self.bn.weight.detach() if self.bn is not None else None
-        K.bn_bwd(g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
+        K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta,
+                 dbias, drop)
         dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
         if self.first:
             dwcol = torch.empty((self.Cout, 64, 1, 1), dtype=torch.float32, device=dev)

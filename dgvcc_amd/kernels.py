@@ -167,8 +167,9 @@ def bn_bwd(g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias
            drop: torch.Tensor | None = None):
     ws = query("dg_bn_workspace", z.M, z.C)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
-    call("dg_bn_bwd", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma), ptr(stats[0]),
-         ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, dz.ptr, dz.ld,
+    st = stats if stats is not None else (None, None, None, None)  # None: no normalisation
+    call("dg_bn_bwd", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma), ptr(st[0]),
+         ptr(st[1]), ptr(st[2]), ptr(st[3]), act, ptr(drop), z.H * z.W, dz.ptr, dz.ld,
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), stream())
 
 

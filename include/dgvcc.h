@@ -115,7 +115,11 @@ int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float
                 const float* shift, int act, const float* drop, int HW, void* y, int64_t ldy,
                 void* stream);
 /* Backward: g = dL/dy (pixel stride ldg).  Produces dz (lddz), dgamma, dbeta
- * (written, not accumulated) and dbias_conv (sum dz, may be NULL). */
+ * (written, not accumulated) and dbias_conv (sum dz, may be NULL).
+ * save_mean = save_invstd = NULL: no normalisation (a biased conv + activation, e.g. the
+ * counter heads' Conv+ReLU, models/ibnnet/__init__.py:17-23): dz = act'(z)*g, where z is
+ * the pre-activation and scale/shift (NULL = identity) map it as in the forward;
+ * dbeta = dbias = sum dz. */
 int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
               const float* gamma, const float* save_mean, const float* save_invstd,
               const float* scale, const float* shift, int act, const float* drop, int HW,

@@ -299,3 +299,25 @@ def test_iw_loss_and_grad(dev, dtype, C):
     assert relerr(vd, var) < (1e-4 if dtype == torch.float32 else 3e-2)
     assert abs(loss.item() - loss_ref.item()) <= tol * abs(loss_ref.item())
     assert relerr(to_nchw(gt.buf.float()), fr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_bias_relu_bwd_no_norm(dev, dtype):
+    """dg_bn_bwd without normalisation (counter-head Conv+bias+ReLU): dz = g*(z>0),
+    dbias = sum dz."""
+    K = _k()
+    N, H, W, C = 2, 5, 7, 128
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(N, H, W, C, generator=g)
+    gy = torch.randn(N, H, W, C, generator=g)
+    if dtype == torch.bfloat16:
+        z, gy = z.bfloat16().float(), gy.bfloat16().float()
+    dz = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    db = torch.empty(C, device=dev)
+    dbias = torch.empty(C, device=dev)
+    K.bn_bwd(K.Act(gy.to(dev, dtype)), K.Act(z.to(dev, dtype)), None, None, 1, dz, None, db, dbias)
+    torch.cuda.synchronize()
+    ref = gy * (z > 0)
+    assert torch.equal(dz.buf.float().cpu(), ref.to(dtype).float())
+    assert relerr(db, ref.sum(dim=(0, 1, 2))) < 1e-5
+    assert relerr(dbias, ref.sum(dim=(0, 1, 2))) < 1e-5

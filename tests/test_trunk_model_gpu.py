@@ -68,6 +68,8 @@ def _check_grads(model, g64, g32, tol=GRAD_TOL):
         g = (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().cpu()
         mine = ((g - g64[k]).norm() / g64[k].norm()).item()
         ref = ((g32[k] - g64[k]).norm() / g64[k].norm()).item()
+        if ref > 0.5:  # structurally-zero gradient (e.g. a BN bias right before an IN): noise only
+            continue
         if mine > max(2 * ref, tol):
             bad[k] = (mine, ref)
     assert not bad, bad
@@ -172,16 +174,37 @@ def test_isw_trainer_step(dev):
 
 @pytest.mark.parametrize("kind", ["ibn", "sw", "isw"])
 def test_counter_bf16_close(dev, kind):
-    """bf16 storage + bf16 MFMA (f32 statistics): the count and map stay close to the
-    float64 oracle (training-mode statistics; ISW in eval mode)."""
+    """bf16 storage + bf16 MFMA (f32 statistics) vs the float64 oracle on the same
+    bf16-rounded weights and input, in eval mode.  (Training mode with batch-2
+    BatchNorm is chaotic for a random-init ResNet-50: rounding only the weights to
+    bf16 moves the f64 output by 15-25%.)  The bar is the oracle's own bf16
+    arithmetic (torch CPU, bfloat16 end to end): our cosine distance and count
+    error (relative to the map's L1 mass) stay within a small multiple of it."""
     model, sd0, batch = _setup(kind, dev, precision="bf16")
-    img = batch[0]
-    training = kind != "isw"
+    img = batch[0].bfloat16().float()
+    if kind == "sw":  # valid (PSD) running covariances: one f64 training pass from zero
+        sd0 = {k: (torch.zeros_like(v) if k.endswith(("running_mean", "running_cov")) else v.clone())
+               for k, v in sd0.items()}
+        sdt = {k: v.double() if v.is_floating_point() else v for k, v in sd0.items()}
+        with torch.no_grad():
+            TO.counter_forward("sw", img.double(), sdt, True)
+        sd0 = {k: (sdt[k].float() if v.is_floating_point() else v) for k, v in sd0.items()}
+        model.load_state_dict(sd0)
     with torch.no_grad():
-        model.train(training)
-        out = model(img.to(dev))
-        sd = {k: v.double().clone() if v.is_floating_point() else v.clone() for k, v in sd0.items()}
-        ref, _ = TO.counter_forward(kind, img.double(), sd, training)
-    c, cr = out.sum().item(), ref.sum().item()
-    assert abs(c - cr) <= 5e-2 * abs(cr) + 1e-2 * ref.abs().sum().item()
-    assert rel(out, ref) < 0.15
+        model.eval()
+        out = model(img.to(dev)).double().cpu()
+        sd = {k: (v.bfloat16().double() if v.dim() == 4 else v.double().clone()) if v.is_floating_point()
+              else v.clone() for k, v in sd0.items()}
+        ref, _ = TO.counter_forward(kind, img.double(), sd, False)
+        sd16 = {k: (v.bfloat16() if v.is_floating_point() else v.clone()) for k, v in sd0.items()}
+        t16, _ = TO.counter_forward(kind, img.bfloat16(), sd16, False)
+        t16 = t16.double()
+
+    mass = ref.abs().sum().item()
+
+    def err(a):
+        cosd = 1.0 - (a.flatten() @ ref.flatten() / (a.norm() * ref.norm())).item()
+        return cosd, abs(a.sum().item() - ref.sum().item()) / mass
+
+    ours, torch16 = err(out), err(t16)
+    assert ours[0] <= 3 * torch16[0] + 1e-3 and ours[1] <= 3 * torch16[1] + 1e-2, (ours, torch16)
