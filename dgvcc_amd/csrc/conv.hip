@@ -14,6 +14,7 @@
 // by the buffer-load range check (voffset past num_records returns 0).
 #include "dg_common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -355,9 +356,199 @@ __global__ void transpose_weight_kernel(const T* __restrict__ w, int Cout, int C
   }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 forward, pipelined: 256-pixel x BN-channel tile, 8 waves (4 px x 2 co),
+// operands staged global->LDS by LDS-DMA (buffer_load ... lds, 16 B per lane,
+// out-of-window taps zero-filled by the descriptor range check) into a 3-stage
+// ring with ONE raw barrier per K-step and a counted vmcnt that keeps the next
+// K-step's DMA in flight across it (cdna_hip_programming.md §5 "Pipelining across
+// barriers").  The XOR swizzle of the 128-B rows is applied on the SOURCE side
+// (LDS-DMA destinations are lane-linear): LDS slot p of row r holds global 16-B
+// chunk p ^ (r & 7), exactly the image swz() reads.
+// ---------------------------------------------------------------------------
+constexpr int PBM = 256;   // pixels per tile
+
+// 16-B LDS-DMA: lane l's 16 bytes at voff land at lds + 16*l (wave-uniform base).
+// Kept in a __device__ helper: the builtin is not valid in the host pass, which
+// would otherwise silently drop the kernel's launch stub.
+__device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, const char* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (DG_LDS void*)lds, 16, voff, 0, 0, 0);
+}
+constexpr int PSTAGES = 3;
+
+template <int BN, int STG>
+__global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
+  using T = bf16;
+  constexpr int BK = 64;                    // bf16 channels per K-step (128-B rows)
+  constexpr int AI = BN / 64;               // A (weight) DMA instructions per wave per K-step
+  constexpr int BI = PBM / 64;              // B (pixel) DMA instructions per wave per K-step
+  constexpr int TI = BN / 32, TJ = 4;       // wave tile: 64 px x BN/2 co
+  constexpr int STAGE = (BN + PBM) * 128;
+  constexpr int PF = STG - 1;               // K-steps issued ahead
+  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (bid % nco) * BN;
+  const int px0 = (bid / nco) * PBM;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lrow = lane >> 3;                          // row within an 8-row DMA group
+  const int gchunk = (lane & 7) ^ lrow;                // source chunk landing in slot lane&7
+
+  const int halo = a.pad * (a.W + 1);
+  const int plo = max(0, px0 - halo);
+  const int phi = min(M, px0 + PBM + halo);
+  const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 2);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)plo * a.ldx * 2), 0, win_bytes, 0x00020000);
+  const long long ldw = (long long)a.R * a.S * a.C;
+  __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.w + (long long)co0 * ldw * 2), 0, (unsigned)(BN * ldw * 2), 0x00020000);
+
+  // this lane's B rows: pixel (wid*BI + i)*8 + lrow of the tile
+  int pp[BI], pq[BI], prow[BI];
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int m = px0 + (wid * BI + i) * 8 + lrow;
+    const int rem = m % HW;
+    prow[i] = m - plo;
+    pp[i] = (m < M) ? rem / a.W : -100000;
+    pq[i] = rem % a.W;
+  }
+  unsigned aoff[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) aoff[i] = (unsigned)((((wid * AI + i) * 8 + lrow) * ldw + gchunk * 8) * 2);
+
+  const int CB = a.C / BK;
+  const int KT = a.R * a.S * CB;
+  const unsigned cbytes = (unsigned)(gchunk * 16);
+
+#define PIPE_ISSUE(t_, stage_) \
+  do { \
+    const int rs = (t_) / CB, cb = (t_) - rs * CB; \
+    const int r = rs / a.S, s = rs - r * a.S; \
+    char* As = smem + (stage_) * STAGE; \
+    char* Bs = As + BN * 128; \
+    const unsigned kofs = (unsigned)((rs * a.C + cb * BK) * 2); \
+    _Pragma("unroll") for (int i = 0; i < AI; ++i) \
+      lds_dma16(wr, As + (wid * AI + i) * 1024, aoff[i] + kofs); \
+    const int dh = r - a.pad, dw = s - a.pad; \
+    _Pragma("unroll") for (int i = 0; i < BI; ++i) { \
+      const int h = pp[i] + dh, ww = pq[i] + dw; \
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W; \
+      const unsigned off = ok ? (unsigned)(((long long)(prow[i] + dh * a.W + dw) * a.ldx + cb * BK) * 2) + cbytes \
+                              : 0xFFFFFFF0u; \
+      lds_dma16(xr, Bs + (wid * BI + i) * 1024, off); \
+    } \
+  } while (0)
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wpx = (wid & 3) * 64, wco = (wid >> 2) * (BN / 2);
+  const int fr = lane & 15, fc = lane >> 4;
+
+  PIPE_ISSUE(0, 0);
+  if (PF > 1 && KT > 1) PIPE_ISSUE(1, 1);
+  for (int t = 0; t < KT; ++t) {
+    if (PF > 1 && t + 1 < KT) {  // leave step t+1's DMA in flight across the barrier
+      if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (AI + BI == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + PF < KT) PIPE_ISSUE(t + PF, (t + PF) % STG);
+    const char* As = smem + (t % STG) * STAGE;
+    const char* Bs = As + BN * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int ch = 4 * ks + fc;
+      u4v af[TI], bfr[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+    }
+  }
+#undef PIPE_ISSUE
+
+  T* y = (T*)a.y;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    if (px >= M) continue;
+    T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco + 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      st4(yrow + co, v);
+    }
+  }
+}
+
+static bool pipe_wide() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_CONV_WIDE");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
+static bool use_wgrad_pipe() {
+  const char* e = getenv("DGVCC_WGRAD_PIPE");
+  return e && e[0] == '1';
+}
+
+static bool use_pipe() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_CONV_PIPE");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
+}
+
 template <typename T>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
+        (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31)) {
+      const int np = dg_cdiv(M, PBM);
+      if (a.Cout % 256 == 0 && pipe_wide())
+        hipLaunchKernelGGL((conv_fwd_pipe_kernel<256, 2>), dim3(np * (a.Cout / 256)), dim3(512), 0, st, a);
+      else if (a.Cout % 128 == 0)
+        hipLaunchKernelGGL((conv_fwd_pipe_kernel<128, 3>), dim3(np * (a.Cout / 128)), dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_fwd_pipe_kernel<64, 3>), dim3(np * (a.Cout / 64)), dim3(512), 0, st, a);
+      DG_CHECK_LAUNCH();
+      return DG_OK;
+    }
+  }
   const int npx = dg_cdiv(M, 128);
   if (a.Cout % 128 == 0) {
     const int nco = a.Cout / 128;
@@ -573,6 +764,177 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
   }
 }
 
+// bf16 weight gradient, pipelined: 8 waves (2 co x 4 c) over a BCO x BC tile of
+// one (r,s) tap, K = 64 pixels per step.  dY and X pixel rows are staged by
+// LDS-DMA into a 3-stage ring (one raw barrier per step, counted vmcnt) and read
+// transposed with ds_read_b64_tr_b16.  Rows are unpadded (DMA images are
+// lane-linear); bank conflicts of the transposed reads are removed by an XOR
+// swizzle of the 16-B chunk index with the row (applied on the DMA source side).
+template <int CPR>
+__device__ __forceinline__ int wg_swz(int r) { return CPR >= 16 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }
+
+template <int BCO, int BC>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(WgArgs a) {
+  constexpr int BKP = 64;
+  constexpr int RA = BCO * 2, RB = BC * 2;                 // bytes per LDS row
+  constexpr int CPRA = RA / 16, CPRB = RB / 16;            // 16-B chunks per row
+  constexpr int RPIA = 1024 / RA, RPIB = 1024 / RB;        // rows per DMA instruction
+  constexpr int AIw = BKP * RA / 1024 / 8, BIw = BKP * RB / 1024 / 8;   // DMA instr. per wave per step
+  constexpr int STAGE = BKP * (RA + RB);
+  constexpr int TI = BCO / 32, TJ = BC / 64;
+  static_assert(AIw >= 1 && BIw >= 1, "tile too small for 8 loader waves");
+  __shared__ __attribute__((aligned(1024))) char smem[PSTAGES * STAGE];
+
+  const int HW = a.H * a.W;
+  const int PQ = a.P * a.Q;
+  const int M = a.N * PQ;
+  const int RS = a.R * a.S;
+  const int nco = a.Cout / BCO, ncb = a.C / BC;
+  const int tiles = nco * ncb * RS;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  int t = bid - split * tiles;
+  const int cot = t % nco; t /= nco;
+  const int cbt = t % ncb;
+  const int rs = t / ncb;
+  const int co0 = cot * BCO, c0 = cbt * BC;
+  const int r = rs / a.S, s = rs - r * a.S;
+  const int dh = r - a.pad, dw = s - a.pad;
+  const int kbeg = split * a.pps;
+  const int kend = min(M, kbeg + a.pps);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 2);
+  __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.dy + (long long)kbeg * a.lddy * 2), 0, dy_bytes, 0x00020000);
+  const int halo = a.pad * (a.W + 1);
+  const int xlo = a.whole_x ? 0 : max(0, kbeg - halo);
+  const int xhi = a.whole_x ? a.N * HW : min(M, kend + halo);
+  const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 2);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * 2), 0, x_bytes, 0x00020000);
+
+  // DMA geometry of this lane: row within the instruction and the source chunk
+  const int arow = lane / CPRA, achunk = (lane % CPRA) ^ wg_swz<CPRA>(arow);
+  const int brow = lane / CPRB, bchunk = (lane % CPRB) ^ wg_swz<CPRB>(brow);
+  // (rows of instruction ii start at ii*RPI: RPI is a multiple of 8 or divides 8,
+  //  so wg_swz(ii*RPI + row) == wg_swz(row) whenever RPI >= 8 ... handled below)
+  const int nkt = (kend - kbeg + BKP - 1) / BKP;
+  int bn[BIw], bp[BIw], bq[BIw];  // output-grid coordinates of this lane's X rows at the next issue
+#pragma unroll
+  for (int i = 0; i < BIw; ++i) {
+    const int px = kbeg + (wid * BIw + i) * RPIB + brow;
+    bn[i] = px / PQ;
+    const int rem = px - bn[i] * PQ;
+    bp[i] = rem / a.Q;
+    bq[i] = rem - bp[i] * a.Q;
+  }
+
+#define WG_ISSUE(kt_, stage_) \
+  do { \
+    const int k0 = kbeg + (kt_) * BKP; \
+    char* As = smem + (stage_) * STAGE; \
+    char* Bs = As + BKP * RA; \
+    _Pragma("unroll") for (int i = 0; i < AIw; ++i) { \
+      const int ii = wid * AIw + i; \
+      const int row = ii * RPIA + arow; \
+      const int ch = (lane % CPRA) ^ wg_swz<CPRA>(row); \
+      const int px = k0 + row; \
+      const unsigned off = px < kend ? (unsigned)(((long long)(px - kbeg) * a.lddy + co0 + ch * 8) * 2) : 0xFFFFFFF0u; \
+      lds_dma16(dyr, As + ii * 1024, off); \
+    } \
+    _Pragma("unroll") for (int i = 0; i < BIw; ++i) { \
+      const int ii = wid * BIw + i; \
+      const int row = ii * RPIB + brow; \
+      const int ch = (lane % CPRB) ^ wg_swz<CPRB>(row); \
+      const int px = k0 + row; \
+      const int h = bp[i] * a.stride + dh, ww = bq[i] * a.stride + dw; \
+      const bool ok = px < kend && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W; \
+      const long long pin = (long long)bn[i] * HW + (long long)h * a.W + ww - xlo; \
+      const unsigned off = ok ? (unsigned)((pin * a.ldx + c0 + ch * 8) * 2) : 0xFFFFFFF0u; \
+      lds_dma16(xr, Bs + ii * 1024, off); \
+      /* advance this row's (n, p, q) by one K-step (64 pixels): no divisions in the loop */ \
+      bq[i] += BKP; \
+      while (bq[i] >= a.Q) { bq[i] -= a.Q; if (++bp[i] >= a.P) { bp[i] = 0; ++bn[i]; } } \
+    } \
+  } while (0)
+  (void)achunk; (void)bchunk;
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wco = (wid >> 2) * (BCO / 2), wc = (wid & 3) * (BC / 4);
+  const int g = lane >> 4, q = (lane & 15) >> 2, p4 = lane & 3;
+
+  WG_ISSUE(0, 0);
+  if (nkt > 1) WG_ISSUE(1, 1);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) {
+      if constexpr (AIw + BIw == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if constexpr (AIw + BIw == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if constexpr (AIw + BIw == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (AIw + BIw == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nkt) WG_ISSUE(kt + 2, (kt + 2) % PSTAGES);
+    const char* As = smem + (kt % PSTAGES) * STAGE;
+    const char* Bs = As + BKP * RA;
+#pragma unroll
+    for (int ks = 0; ks < BKP / 32; ++ks) {
+      const int r1 = 32 * ks + 4 * g + q, r2 = r1 + 16;
+      s8v af[TI], bfv[TJ];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int cc = (wco + 16 * i) / 8 + (p4 >> 1);
+        const int hb = (p4 & 1) * 8;
+        s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DG_LDS s4v*)(As + r1 * RA + ((cc ^ wg_swz<CPRA>(r1)) << 4) + hb));
+        s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DG_LDS s4v*)(As + r2 * RA + ((cc ^ wg_swz<CPRA>(r2)) << 4) + hb));
+        af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int cc = (wc + 16 * j) / 8 + (p4 >> 1);
+        const int hb = (p4 & 1) * 8;
+        s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DG_LDS s4v*)(Bs + r1 * RB + ((cc ^ wg_swz<CPRB>(r1)) << 4) + hb));
+        s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DG_LDS s4v*)(Bs + r2 * RB + ((cc ^ wg_swz<CPRB>(r2)) << 4) + hb));
+        bfv[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#undef WG_ISSUE
+
+  const long long ldk = (long long)RS * a.C;
+  float* out = a.slab + (long long)split * a.Cout * ldk;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int c = c0 + wc + 16 * j + (lane & 15);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co0 + wco + 16 * i + 4 * g + rr;
+        out[co * ldk + rs * a.C + c] = acc[i][j][rr];
+      }
+    }
+}
+
 struct WgPlan { int splits, pps; };
 
 template <typename T>
@@ -598,7 +960,27 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   const int bc = (a.C % 128 == 0) ? 128 : 64;
   const int tiles = (a.Cout / bco) * (a.C / bc) * a.R * a.S;
   const dim3 grid(tiles * a.splits);
-  if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), grid, dim3(NT), 0, st, a);
+  bool done = false;
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (use_wgrad_pipe()) {  // opt-in: measured slower than the register-staged kernel (round 1)
+      const int RS = a.R * a.S;
+      if (bco == 128 && a.C % 256 == 0) {
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 256>), dim3((a.Cout / 128) * (a.C / 256) * RS * a.splits),
+                           dim3(512), 0, st, a);
+      } else if (bco == 128 && bc == 128) {
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128>), grid, dim3(512), 0, st, a);
+      } else if (bco == 128) {
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 64>), grid, dim3(512), 0, st, a);
+      } else if (bc == 128) {
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128>), grid, dim3(512), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 64>), grid, dim3(512), 0, st, a);
+      }
+      done = true;
+    }
+  }
+  if (done) {
+  } else if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), grid, dim3(NT), 0, st, a);
   else if (bco == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), grid, dim3(NT), 0, st, a);
   else if (bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), grid, dim3(NT), 0, st, a);
   else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64>), grid, dim3(NT), 0, st, a);

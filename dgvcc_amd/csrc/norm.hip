@@ -47,7 +47,8 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const T* __restrict__ z, 
   }
 }
 
-// 64 channels per block, 4 lanes per channel striding over the block partials.
+// 16 channels per block, 16 lanes per channel striding over the block partials
+// (independent loads, 4 in flight per lane), then an LDS combine in double.
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_stats_finalize(const T* __restrict__ z, const float* __restrict__ part,
                                                         int nblk, int M, int C, const float* __restrict__ gamma,
@@ -55,18 +56,30 @@ __global__ __launch_bounds__(NT) void bn_stats_finalize(const T* __restrict__ z,
                                                         float* running_var, float momentum, float eps,
                                                         float* save_mean, float* save_invstd, float* scale,
                                                         float* shift) {
-  __shared__ double sh[2][4][64];
-  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double sh[2][16][17];
+  const int cl = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double a = 0.0, b = 0.0;
-  if (c < C)
-    for (int k = r; k < nblk; k += 4) { a += part[(long long)k * 2 * C + c]; b += part[(long long)k * 2 * C + C + c]; }
+  if (c < C) {
+    int k = r;
+    for (; k + 48 < nblk; k += 64) {
+      float a4[4], b4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a4[u] = part[(long long)(k + 16 * u) * 2 * C + c];
+        b4[u] = part[(long long)(k + 16 * u) * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a += a4[u]; b += b4[u]; }
+    }
+    for (; k < nblk; k += 16) { a += part[(long long)k * 2 * C + c]; b += part[(long long)k * 2 * C + C + c]; }
+  }
   sh[0][r][cl] = a;
   sh[1][r][cl] = b;
   __syncthreads();
   if (r != 0 || c >= C) return;
-  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
+  a = 0.0; b = 0.0;
+  for (int q = 0; q < 16; ++q) { a += sh[0][q][cl]; b += sh[1][q][cl]; }
   const double K = (double)to_f(z[c]);
   const double ms = a / M;
   double var = b / M - ms * ms;
@@ -203,21 +216,32 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const T* __restrict__ g, lo
 __global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ part, int nblk, int M, int C,
                                                       const float* gamma, const float* invstd, float* dgamma,
                                                       float* dbeta, float* dbias, float* coef) {
-  __shared__ double sh[3][4][64];
-  const int cl = threadIdx.x & 63, r = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  __shared__ double sh[3][16][17];
+  const int cl = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
   double a = 0.0, b = 0.0, d = 0.0;
-  if (c < C)
-    for (int k = r; k < nblk; k += 4) {
+  if (c < C) {
+    int k = r;
+    for (; k + 48 < nblk; k += 64) {
+      float a4[4], b4[4], d4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float* o = part + (long long)(k + 16 * u) * 3 * C;
+        a4[u] = o[c]; b4[u] = o[C + c]; d4[u] = o[2 * C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { a += a4[u]; b += b4[u]; d += d4[u]; }
+    }
+    for (; k < nblk; k += 16) {
       const float* o = part + (long long)k * 3 * C;
       a += o[c]; b += o[C + c]; d += o[2 * C + c];
     }
+  }
   sh[0][r][cl] = a; sh[1][r][cl] = b; sh[2][r][cl] = d;
   __syncthreads();
   if (r != 0 || c >= C) return;
-  a = sh[0][0][cl] + sh[0][1][cl] + sh[0][2][cl] + sh[0][3][cl];
-  b = sh[1][0][cl] + sh[1][1][cl] + sh[1][2][cl] + sh[1][3][cl];
-  d = sh[2][0][cl] + sh[2][1][cl] + sh[2][2][cl] + sh[2][3][cl];
+  a = 0.0; b = 0.0; d = 0.0;
+  for (int q = 0; q < 16; ++q) { a += sh[0][q][cl]; b += sh[1][q][cl]; d += sh[2][q][cl]; }
   if (!invstd) {  // no normalisation: dz = act'(z) g ; dbeta = dbias = sum dz
     if (dgamma) dgamma[c] = 0.f;
     if (dbeta) dbeta[c] = (float)a;
@@ -276,7 +300,7 @@ int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, 
   const int ppb = dg_cdiv(M, nblk);
   hipLaunchKernelGGL(bn_stats_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)z, ldz, M, C, ppb, (float*)ws);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_stats_finalize<T>, dim3(dg_cdiv(C, 64)), dim3(NT), 0, st, (const T*)z, (const float*)ws,
+  hipLaunchKernelGGL(bn_stats_finalize<T>, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, (const T*)z, (const float*)ws,
                      nblk, M, C, gamma, beta, rm, rv, momentum, eps, smean, sinv, scale, shift);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -294,7 +318,7 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
   hipLaunchKernelGGL(bn_bwd_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C, ppb,
                      mean, inv, scale, shift, act, drop, HW, part);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 64)), dim3(NT), 0, st, part, nblk, M, C, gamma, inv, dgamma,
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, inv, dgamma,
                      dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
