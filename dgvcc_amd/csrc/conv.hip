@@ -935,11 +935,199 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(WgArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// bf16 weight gradient of a 3x3 / stride 1 / pad 1 conv with all 9 taps fused in
+// one block (W % 64 == 0).  A K-step is 64 output pixels of ONE image row; the
+// block stages dY[64 px][BCO] once and, per kernel row dh, the 72-pixel X strip
+// [q0-4, q0+68) of image row p+dh-1 (64 channels), so every tap reads shifted
+// rows of the same LDS image: 9 GEMM taps per dY tile, ~4x fewer L2->LDS bytes
+// per FLOP than one-tap-per-block.  LDS-DMA 3-stage ring as conv_fwd_pipe_kernel;
+// transposed fragment reads (ds_read_b64_tr_b16) on XOR-swizzled rows.
+// ---------------------------------------------------------------------------
+constexpr int W9_XROWS = 72;
+
+template <int BCO>
+__global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
+  constexpr int BKP = 64, BC = 64;
+  constexpr int RA = BCO * 2, RX = BC * 2;                    // bytes per LDS row
+  constexpr int CPRA = RA / 16, CPRX = RX / 16;
+  constexpr int RPIA = 1024 / RA;                             // A rows per DMA instruction
+  constexpr int A_INST = BKP * RA / 1024;                     // 16 (BCO 128) / 8 (BCO 64)
+  constexpr int X_INST = 3 * W9_XROWS * RX / 1024;            // 27
+  constexpr int N_INST = A_INST + X_INST;
+  constexpr int A_BYTES = BKP * RA, X_BYTES = W9_XROWS * RX;
+  constexpr int STAGE = A_BYTES + 3 * X_BYTES;
+  constexpr int TI = 2, TJ = BCO == 128 ? 2 : 1;             // wave tile: 32 co x 16*TJ c, 9 taps
+  __shared__ __attribute__((aligned(1024))) char smem[PSTAGES * STAGE];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BCO, ncb = a.C / BC;
+  const int tiles = nco * ncb;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  const int t0 = bid - split * tiles;
+  const int co0 = (t0 % nco) * BCO, c0 = (t0 / nco) * BC;
+  const int kbeg = split * a.pps;
+  const int kend = min(M, kbeg + a.pps);
+  const int nkt = (kend - kbeg) / BKP;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+  const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 2);
+  __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.dy + (long long)kbeg * a.lddy * 2), 0, dy_bytes, 0x00020000);
+  const int halo = a.W + 8;
+  const int xlo = max(0, kbeg - halo), xhi = min(M, kend + halo);
+  const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 2);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * 2), 0, x_bytes, 0x00020000);
+  const int my_inst = (N_INST - wid + 7) / 8;                 // wave-uniform DMA count per step
+
+#define W9_ISSUE(kt_, stage_) \
+  do { \
+    const int px0 = kbeg + (kt_) * BKP; \
+    const int n = px0 / HW, rem = px0 - n * HW; \
+    const int pr = rem / a.W, q0 = rem - pr * a.W; \
+    char* As = smem + (stage_) * STAGE; \
+    char* Xs = As + A_BYTES; \
+    for (int ii = wid; ii < N_INST; ii += 8) { \
+      if (ii < A_INST) { \
+        const int row = ii * RPIA + lane / CPRA; \
+        const int ch = (lane % CPRA) ^ wg_swz<CPRA>(row); \
+        lds_dma16(dyr, As + ii * 1024, (unsigned)(((long long)(px0 + row - kbeg) * a.lddy + co0 + ch * 8) * 2)); \
+      } else { \
+        const int jj = ii - A_INST; \
+        const int dhi = jj / 9, sub = jj - dhi * 9; \
+        const int row = sub * 8 + (lane >> 3); \
+        const int ch = (lane & 7) ^ wg_swz<CPRX>(row); \
+        const int h = pr + dhi - 1, w = q0 - 4 + row; \
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W; \
+        const long long pin = (long long)n * HW + (long long)h * a.W + w - xlo; \
+        lds_dma16(xr, Xs + dhi * X_BYTES + sub * 1024, ok ? (unsigned)((pin * a.ldx + c0 + ch * 8) * 2) : 0xFFFFFFF0u); \
+      } \
+    } \
+  } while (0)
+
+  f4v acc[9][TI][TJ];
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[tp][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wco = BCO == 128 ? (wid & 3) * 32 : (wid & 1) * 32;
+  const int wc = BCO == 128 ? (wid >> 2) * 32 : (wid >> 1) * 16;
+  const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
+  const int hb = (p4 & 1) * 8;
+
+  if (nkt > 0) W9_ISSUE(0, 0);
+  if (nkt > 1) W9_ISSUE(1, 1);
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 1 < nkt) {
+      if (my_inst == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (my_inst == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else if (my_inst == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nkt) W9_ISSUE(kt + 2, (kt + 2) % PSTAGES);
+    const char* As = smem + (kt % PSTAGES) * STAGE;
+    const char* Xs = As + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < BKP / 32; ++ks) {
+      const int r1 = 32 * ks + 4 * g + qq, r2 = r1 + 16;
+      s8v af[TI];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int cc = (wco + 16 * i) / 8 + (p4 >> 1);
+        s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DG_LDS s4v*)(As + r1 * RA + ((cc ^ wg_swz<CPRA>(r1)) << 4) + hb));
+        s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (DG_LDS s4v*)(As + r2 * RA + ((cc ^ wg_swz<CPRA>(r2)) << 4) + hb));
+        af[i] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int dhi = 0; dhi < 3; ++dhi) {
+#pragma unroll
+        for (int sw = 0; sw < 3; ++sw) {
+          const int x1 = r1 + sw + 3, x2 = r2 + sw + 3;
+          s8v bfv[TJ];
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            const int cc = (wc + 16 * j) / 8 + (p4 >> 1);
+            const char* X = Xs + dhi * X_BYTES;
+            s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (DG_LDS s4v*)(X + x1 * RX + ((cc ^ wg_swz<CPRX>(x1)) << 4) + hb));
+            s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (DG_LDS s4v*)(X + x2 * RX + ((cc ^ wg_swz<CPRX>(x2)) << 4) + hb));
+            bfv[j] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          }
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[dhi * 3 + sw][i][j] =
+                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[dhi * 3 + sw][i][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+#undef W9_ISSUE
+
+  const long long ldk = 9ll * a.C;
+  float* out = a.slab + (long long)split * a.Cout * ldk;
+#pragma unroll
+  for (int tp = 0; tp < 9; ++tp)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int c = c0 + wc + 16 * j + (lane & 15);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int co = co0 + wco + 16 * i + 4 * g + rr;
+          out[co * ldk + tp * a.C + c] = acc[tp][i][j][rr];
+        }
+      }
+}
+
+static bool wg9_ok(int C, int Cout, int R, int S, int W, int pad) {
+  return use_pipe() && R == 3 && S == 3 && pad == 1 && W % 64 == 0 && C % 64 == 0 && Cout % 64 == 0;
+}
+
 struct WgPlan { int splits, pps; };
+
+// splits for the fused-tap kernel: >= 8 K-steps per block, block count chosen for
+// whole rounds of one block per CU (tail efficiency >= 90% where possible).
+static WgPlan wg9_plan(int N, int H, int W, int C, int Cout) {
+  const long long M = (long long)N * H * W;
+  const long long steps = M / 64;
+  const int bco = Cout % 128 == 0 ? 128 : 64;
+  const long long tiles = (long long)(Cout / bco) * (C / 64);
+  long long best = 1;
+  double best_eff = -1.0;
+  for (int rounds = 2; rounds <= 12; ++rounds) {
+    long long sp = (256ll * rounds + tiles - 1) / tiles;
+    sp = std::max(1ll, std::min(sp, std::max(1ll, steps / 8)));
+    const long long blocks = tiles * sp;
+    const double eff = (double)blocks / (256.0 * ((blocks + 255) / 256));
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = sp; }
+    if (eff >= 0.9) break;
+  }
+  long long sps = (steps + best - 1) / best;  // K-steps per split
+  const long long splits = (steps + sps - 1) / sps;
+  return WgPlan{(int)splits, (int)(sps * 64)};
+}
 
 template <typename T>
 WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S) {  // H, W: output grid
   constexpr int BKP = WgCfg<T>::BKP;
+  if (std::is_same<T, bf16>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2)) return wg9_plan(N, H, W, C, Cout);
   const long long M = (long long)N * H * W;
   const int bco = (Cout % 128 == 0) ? 128 : 64;
   const int bc = (C % 128 == 0) ? 128 : 64;
@@ -962,7 +1150,13 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   const dim3 grid(tiles * a.splits);
   bool done = false;
   if constexpr (std::is_same<T, bf16>::value) {
-    if (use_wgrad_pipe()) {  // opt-in: measured slower than the register-staged kernel (round 1)
+    if (a.stride == 1 && !a.whole_x && wg9_ok(a.C, a.Cout, a.R, a.S, a.W, a.pad)) {
+      const int b9 = a.Cout % 128 == 0 ? 128 : 64;
+      const dim3 g9((a.Cout / b9) * (a.C / 64) * a.splits);
+      if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad9_kernel<64>), g9, dim3(512), 0, st, a);
+      done = true;
+    } else if (use_wgrad_pipe()) {  // opt-in: measured slower than the register-staged kernel (round 1)
       const int RS = a.R * a.S;
       if (bco == 128 && a.C % 256 == 0) {
         hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 256>), dim3((a.Cout / 128) * (a.C / 256) * RS * a.splits),
