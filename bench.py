@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=16, help="frames per GPU")
     ap.add_argument("--mode", default="simple", choices=["simple", "final"])
+    ap.add_argument("--trunk", default=None, choices=["ibn", "sw", "isw"],
+                    help="secondary workload: ResNet-50 DG counter (IBN-b / SW / ISW) train step")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--height", type=int, default=H0)
     ap.add_argument("--width", type=int, default=W0)
@@ -162,7 +164,13 @@ def main():
 
     B, H, W = args.batch, args.height, args.width
     torch.manual_seed(2112)
-    if args.mode == "simple":
+    mode = args.mode
+    if args.trunk:
+        from dgvcc_amd.models import trunks as TM
+        cls = {"ibn": TM.IBNCounter_ResNet, "sw": TM.SWCounter_ResNet, "isw": TM.ISWCounter_ResNet}
+        model = cls[args.trunk](pretrained=False)
+        mode = "isw" if args.trunk == "isw" else "simple"
+    elif args.mode == "simple":
         model = MM.DGModel_base(pretrained=False, den_dropout=0.5)
     else:
         model = MM.DGModel_final(pretrained=False)
@@ -175,14 +183,20 @@ def main():
     cwd = os.getcwd()
     os.makedirs("/tmp/dgvcc_bench", exist_ok=True)
     os.chdir("/tmp/dgvcc_bench")
-    trainer = DGTrainer(2112 + rank, f"bench_r{rank}", dev, 1000, 10000, args.mode)
+    trainer = DGTrainer(2112 + rank, f"bench_r{rank}", dev, 1000, 10000, mode)
     os.chdir(cwd)
     batch = synthetic(B, H, W, dev, seed=1000 + rank)
     loss_fn = MSELoss()
+    epoch = 0
+    if args.trunk == "isw":  # cal_covstat pass (validation-time in the reference) -> masks; epoch > 5 -> wt loss on
+        model.eval()
+        with torch.no_grad():
+            model([batch[0], batch[1]], cal_covstat=True)
+        epoch = 6
     model.train()
 
     for _ in range(args.warmup):
-        trainer.train_step(model, loss_fn, opt, batch, 0)
+        trainer.train_step(model, loss_fn, opt, batch, epoch)
 
     timer = ConvTimer()
     K.set_conv_timer(timer)
@@ -191,7 +205,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        last = trainer.train_step(model, loss_fn, opt, batch, 0)
+        last = trainer.train_step(model, loss_fn, opt, batch, epoch)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -206,7 +220,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
 
-    views = 2 if args.mode == "final" else 1
+    views = 2 if (args.mode == "final" and not args.trunk) else 1
     frames = B * views * world * args.steps
     value = frames / elapsed
     peak = BF16_DENSE_PEAK_TFLOPS if args.precision == "bf16" else F32_MFMA_PEAK_TFLOPS
@@ -218,7 +232,8 @@ def main():
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    step_flops = conv_flops_per_step(B, H, W, args.mode)
+    step_flops = conv_flops_per_step(B, H, W, args.mode) if not args.trunk else \
+        (conv_flops + wg_flops) / args.steps
     out = {
         "metric": "train-step frames/sec at 768×1024, ShanghaiTech-A; MAE vs reference",
         "value": round(value, 3),
@@ -232,11 +247,13 @@ def main():
         "vs_baseline": None,
         "dtype": args.precision,
         "data": "synthetic 3x768x1024 frames + Poisson(500) point sets (dmap via HIP scatter), HBM-resident",
-        "config": {"workload": f"DGModel_base {args.mode}-mode DGTrainer.train_step (configs/stb_reg_base.yml)"
-                   if args.mode == "simple" else "DGModel_final final-mode DGTrainer.train_step (configs/sta_final.yml)",
+        "config": {"workload": (f"{type(model).__name__} {mode}-mode DGTrainer.train_step "
+                                f"(configs/baselines/sta_{args.trunk}.yml)") if args.trunk else
+                   (f"DGModel_base {args.mode}-mode DGTrainer.train_step (configs/stb_reg_base.yml)"
+                    if args.mode == "simple" else "DGModel_final final-mode DGTrainer.train_step (configs/sta_final.yml)"),
                    "global_batch": B * world, "frames_per_gpu_step": B * views,
                    "resolution": f"{H}x{W}", "parallelism": f"dp{world}", "last_loss": last},
-        "roofline": {"bound": "mfma", "kernel": "conv_fwd_kernel (implicit-GEMM conv: forward + dgrad launches)",
+        "roofline": {"bound": "mfma", "kernel": "conv_fwd_pipe_kernel (implicit-GEMM conv: forward + dgrad launches)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": round(conv_alg_bytes),

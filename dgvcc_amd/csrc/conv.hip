@@ -376,7 +376,7 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, const char* 
 }
 constexpr int PSTAGES = 3;
 
-template <int BN, int STG>
+template <int BN, int STG, int VAR = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   using T = bf16;
   constexpr int BK = 64;                    // bf16 channels per K-step (128-B rows)
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + PF < KT) PIPE_ISSUE(t + PF, (t + PF) % STG);
+    if (VAR != 2 && t + PF < KT) PIPE_ISSUE(t + PF, (t + PF) % STG);
     const char* As = smem + (t % STG) * STAGE;
     const char* Bs = As + BN * 128;
 #pragma unroll
@@ -477,10 +477,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
       for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
 #pragma unroll
       for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+      if constexpr (VAR >= 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+      if constexpr (VAR >= 1) __builtin_amdgcn_s_setprio(0);
+      if constexpr (VAR == 2) {
+        if (ks == 0 && t + PF < KT) PIPE_ISSUE(t + PF, (t + PF) % STG);
+      }
     }
   }
 #undef PIPE_ISSUE
@@ -507,6 +512,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
       st4(yrow + co, v);
     }
   }
+}
+
+static int pipe_var() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_PIPE_VAR");
+    v = e ? atoi(e) : 2;
+  }
+  return v;
 }
 
 static bool pipe_wide() {
@@ -539,12 +553,17 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
     if (use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
         (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31)) {
       const int np = dg_cdiv(M, PBM);
-      if (a.Cout % 256 == 0 && pipe_wide())
-        hipLaunchKernelGGL((conv_fwd_pipe_kernel<256, 2>), dim3(np * (a.Cout / 256)), dim3(512), 0, st, a);
-      else if (a.Cout % 128 == 0)
-        hipLaunchKernelGGL((conv_fwd_pipe_kernel<128, 3>), dim3(np * (a.Cout / 128)), dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv_fwd_pipe_kernel<64, 3>), dim3(np * (a.Cout / 64)), dim3(512), 0, st, a);
+      const int var = pipe_var();
+#define PIPE_LAUNCH(BN_, STG_, G_) \
+      do { \
+        if (var == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 1>), dim3(G_), dim3(512), 0, st, a); \
+        else if (var == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2>), dim3(G_), dim3(512), 0, st, a); \
+        else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 0>), dim3(G_), dim3(512), 0, st, a); \
+      } while (0)
+      if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
+      else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
+      else PIPE_LAUNCH(64, 3, np * (a.Cout / 64));
+#undef PIPE_LAUNCH
       DG_CHECK_LAUNCH();
       return DG_OK;
     }

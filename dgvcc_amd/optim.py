@@ -48,23 +48,40 @@ class AdamW(torch.optim.Optimizer):
             group["_offs_dev"] = torch.tensor(offs, dtype=torch.int64, device=dev)
 
     def _gather(self, group):
+        """Gather live gradients into the flat buffer; returns the [start, end) runs of
+        parameters that have a gradient (torch.optim.AdamW skips params whose .grad
+        is None: no decay, no moment update — e.g. the ISW counter's unused layer4)."""
         ps = group["params"]
         g = group["_g"]
-        if all(p.grad is not None for p in ps):
-            for p in ps:
-                if not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
-                    p.grad = p.grad.contiguous().float()
-            table = torch.tensor([p.grad.data_ptr() for p in ps], dtype=torch.int64).to(g.device)
-            call("dg_gather_flat", ptr(table), ptr(group["_offs_dev"]), len(ps), g.numel(), ptr(g),
-                 stream())
-            group["_table"] = table  # keep alive until the launch retires
-            return True
-        for p, o in zip(ps, group["_offs"]):
-            if p.grad is None:
-                g[o:o + p.numel()].zero_()
-            else:
-                g[o:o + p.numel()].copy_(p.grad.reshape(-1))
-        return True
+        live = tuple(p.grad is not None for p in ps)
+        for p in ps:
+            if p.grad is not None and (not p.grad.is_contiguous() or p.grad.dtype != torch.float32):
+                p.grad = p.grad.contiguous().float()
+        cache = group.get("_live_cache")
+        if cache is None or cache[0] != live:
+            runs, start = [], None  # maximal runs [i0, i1) of consecutive live params
+            for i, l in enumerate(live + (False,)):
+                if l and start is None:
+                    start = i
+                elif not l and start is not None:
+                    runs.append((start, i))
+                    start = None
+            offs = group["_offs"]
+            dev_offs = [torch.tensor(offs[i0:i1] + [offs[i1 - 1] + ps[i1 - 1].numel()], dtype=torch.int64,
+                                     device=g.device) for i0, i1 in runs]
+            cache = (live, runs, dev_offs)
+            group["_live_cache"] = cache
+            if not all(live):
+                g.zero_()  # dead regions stay zero (the all-reduce sums them harmlessly)
+        _, runs, dev_offs = cache
+        tables = []
+        for (i0, i1), o in zip(runs, dev_offs):
+            table = torch.tensor([ps[i].grad.data_ptr() for i in range(i0, i1)], dtype=torch.int64).to(g.device)
+            call("dg_gather_flat", ptr(table), ptr(o), i1 - i0, g.numel(), ptr(g), stream())
+            tables.append(table)
+        group["_table"] = tables  # keep alive until the launches retire
+        offs = group["_offs"]
+        return [(offs[i0], offs[i1 - 1] + ps[i1 - 1].numel()) for i0, i1 in runs]
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -75,14 +92,16 @@ class AdamW(torch.optim.Optimizer):
         for group in self.param_groups:
             if all(p.grad is None for p in group["params"]):
                 continue
-            self._gather(group)
+            runs = self._gather(group)
             g = group["_g"]
             if self.allreduce:
                 average_flat_(g)
             group["_step"] += 1
             b1, b2 = group["betas"]
-            K.adamw_step(group["_flat"], g, group["_m"], group["_v"], group["lr"], b1, b2,
-                         group["eps"], group["weight_decay"], group["_step"])
+            flat, m, v = group["_flat"], group["_m"], group["_v"]
+            for a, b in runs:
+                K.adamw_step(flat[a:b], g[a:b], m[a:b], v[a:b], group["lr"], b1, b2,
+                             group["eps"], group["weight_decay"], group["_step"])
         return loss
 
     def zero_grad(self, set_to_none: bool = True):

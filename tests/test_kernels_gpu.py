@@ -262,3 +262,30 @@ def test_mse_and_adamw(dev):
         K.adamw_step(pd, grad.to(dev), md, vd, 1e-3, 0.9, 0.999, 1e-8, 1e-4, step)
     torch.cuda.synchronize()
     assert relerr(pd, p_ref.detach()) < 1e-6
+
+
+def test_fused_adamw_matches_torch_with_missing_grads(dev):
+    """dgvcc_amd.optim.AdamW == torch.optim.AdamW, including params whose .grad is
+    None (skipped: no decay, no moment update — the ISW counter's unused layer4)."""
+    from dgvcc_amd.optim import AdamW
+    g = torch.Generator().manual_seed(3)
+    shapes = [(7, 5), (3,), (4, 4, 3), (6,), (2, 9)]
+    base = [torch.randn(s, generator=g) for s in shapes]
+    ours = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    ref = [torch.nn.Parameter(b.clone().to(dev)) for b in base]
+    o1 = AdamW(ours, lr=1e-2, weight_decay=1e-2, allreduce=False)
+    o2 = torch.optim.AdamW(ref, lr=1e-2, weight_decay=1e-2)
+    for step in range(3):
+        grads = [torch.randn(s, generator=g) for s in shapes]
+        for i, (a, b) in enumerate(zip(ours, ref)):
+            dead = i in (2, 3) or (i == 0 and step == 0)
+            a.grad = None if dead else grads[i].to(dev)
+            b.grad = None if dead else grads[i].to(dev)
+        o1.step()
+        o2.step()
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(zip(ours, ref)):
+        if i == 0:
+            continue  # live for fewer steps: torch keeps a per-param step count, ours per group
+        assert torch.allclose(a.detach(), b.detach(), rtol=1e-5, atol=1e-6), i
+    assert torch.equal(ours[2].detach().cpu(), base[2]) and torch.equal(ours[3].detach().cpu(), base[3])
