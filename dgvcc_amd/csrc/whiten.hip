@@ -215,14 +215,41 @@ __device__ float sw_newton(SwLds& L, float* Ps, int T, int t) {
   return r;
 }
 
-// Statistics + whitening matrices, one block per group g.
-//   save layout (floats): mu_in[N][C] | cov_in[N][G][256] | mu_bn[C] | cov_bn[G][256]
-//                         | aff[N][G][256] | bias[N][C]
-__global__ __launch_bounds__(256) void sw_stats_finalize(const float* __restrict__ part, int N, int nb, int HW, int C,
-                                                         int T, float eps, float momentum, const float* mean_w,
-                                                         const float* var_w, const float* gamma, const float* beta,
-                                                         float* running_mean, float* running_cov, int training,
-                                                         float* __restrict__ save) {
+// Save layout (floats): mu_in[N][C] | cov_in[N][G][256] | mu_bn[C] | cov_bn[G][256]
+//                       | aff[N][G][256] | bias[N][C]
+// Batch moments (doubles, per group): S1[16] = sum_n mu_n, S2[256] = sum_n (cov_n + mu_n mu_n^T).
+// They are the only cross-instance quantities of BW, so SyncSwitchWhiten reduces exactly
+// these [G][272] doubles over ranks between sw_inst_stats and sw_finalize.
+constexpr int SW_MOM = 272;
+
+// One block per group: instance covariances (partials / HW) and the batch moments.
+__global__ __launch_bounds__(256) void sw_inst_stats(const float* __restrict__ part, int N, int nb, int HW, int C,
+                                                     float* __restrict__ save, double* __restrict__ moments) {
+  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  const float* mu_in = save;
+  float* cov_in = save + (long long)N * C;
+  double s2 = 0.0, s1 = 0.0;
+  for (int n = 0; n < N; ++n) {
+    double s = 0.0;
+    for (int k = 0; k < nb; ++k) s += part[(((long long)n * nb + k) * G + g) * 256 + t];
+    const float ci = (float)(s / HW);
+    cov_in[((long long)n * G + g) * 256 + t] = ci;
+    const double mi = mu_in[(long long)n * C + g * 16 + i], mj = mu_in[(long long)n * C + g * 16 + j];
+    s2 += (double)ci + mi * mj;
+    if (t < 16) s1 += mu_in[(long long)n * C + g * 16 + t];
+  }
+  moments[(long long)g * SW_MOM + 16 + t] = s2;
+  if (t < 16) moments[(long long)g * SW_MOM + t] = s1;
+}
+
+// One block per group: batch mean/cov from the (possibly all-reduced) moments over
+// `count` instances (or the running statistics in eval), running-stat update, and
+// for every local instance the Newton-Schulz whitening matrix folded with the affine.
+__global__ __launch_bounds__(256) void sw_finalize(const double* __restrict__ moments, double count, int N, int C,
+                                                   int T, float eps, float momentum, const float* mean_w,
+                                                   const float* var_w, const float* gamma, const float* beta,
+                                                   float* running_mean, float* running_cov, int training,
+                                                   float* __restrict__ save) {
   __shared__ SwLds L;
   const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
   float* mu_in = save;
@@ -231,29 +258,16 @@ __global__ __launch_bounds__(256) void sw_stats_finalize(const float* __restrict
   float* cov_bn = mu_bn + C;
   float* aff = cov_bn + (long long)G * 256;
   float* bias = aff + (long long)N * G * 256;
-  // instance covariances and batch statistics
-  float mb = 0.f;  // thread t < 16: batch mean of channel t
-  if (t < 16) {
-    for (int n = 0; n < N; ++n) mb += mu_in[(long long)n * C + g * 16 + t];
-    mb /= N;
-    L.vec[0][t] = mb;
-  }
+  __shared__ double mbd[16];
+  if (t < 16) mbd[t] = moments[(long long)g * SW_MOM + t] / count;
   __syncthreads();
-  double cb = 0.0;
-  for (int n = 0; n < N; ++n) {
-    double s = 0.0;
-    for (int k = 0; k < nb; ++k) s += part[(((long long)n * nb + k) * G + g) * 256 + t];
-    const float ci = (float)(s / HW);
-    cov_in[((long long)n * G + g) * 256 + t] = ci;
-    const float di = mu_in[(long long)n * C + g * 16 + i] - L.vec[0][i];
-    const float dj = mu_in[(long long)n * C + g * 16 + j] - L.vec[0][j];
-    cb += (double)ci + (double)di * dj;
-  }
-  float cbn = (float)(cb / N);
-  __syncthreads();
+  float mb, cbn;
   if (training) {
+    cbn = (float)(moments[(long long)g * SW_MOM + 16 + t] / count - mbd[i] * mbd[j]);
     if (t < 16) {
+      mb = (float)mbd[t];
       mu_bn[g * 16 + t] = mb;
+      L.vec[0][t] = mb;
       float* rm = running_mean + g * 16 + t;
       *rm = *rm * momentum + (1.f - momentum) * mb;
     }
@@ -285,9 +299,9 @@ __global__ __launch_bounds__(256) void sw_stats_finalize(const float* __restrict
     __syncthreads();
     aff[((long long)n * G + g) * 256 + t] = L.X[t];
     if (t < 16) {
-      float s = 0.f;
-      for (int k = 0; k < 16; ++k) s = fmaf(L.X[t * 16 + k], L.vec[1][k], s);
-      bias[(long long)n * C + g * 16 + t] = (beta ? beta[g * 16 + t] : 0.f) - s;
+      float sacc = 0.f;
+      for (int k = 0; k < 16; ++k) sacc = fmaf(L.X[t * 16 + k], L.vec[1][k], sacc);
+      bias[(long long)n * C + g * 16 + t] = (beta ? beta[g * 16 + t] : 0.f) - sacc;
     }
     __syncthreads();
   }
@@ -382,7 +396,7 @@ __global__ __launch_bounds__(256) void sw_bwd_partial(const T* __restrict__ gy, 
   }
 }
 
-// One block per group: exact adjoint of sw_stats_finalize for every instance.
+// One block per group: exact adjoint of sw_finalize for every instance (phase A).
 // coef layout: [n][g][ K(256) | L(256) | c(16) ]  so that
 //   dx_p = K ge_p + L (x_p - mu_n) + c.
 // wpart[g][4] = (da0, da1, db0, db1) partial over n; dgamma/dbeta written.
@@ -390,7 +404,7 @@ __global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ pa
                                                     float eps, const float* mean_w, const float* var_w,
                                                     const float* gamma, const float* __restrict__ save,
                                                     float* __restrict__ coef, float* __restrict__ wpart,
-                                                    float* dgamma, float* dbeta) {
+                                                    double* __restrict__ bmoments, float* dgamma, float* dbeta) {
   __shared__ SwLds L;
   __shared__ float Ps[(SW_MAXT + 1) * 256];
   __shared__ float mv[4][16];  // mu_bn, mixed mean, mu_n, sgy
@@ -492,23 +506,10 @@ __global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ pa
     }
     __syncthreads();
   }
-  // Esym = (dcov_bn + dcov_bn^T) / (N HW)
-  L.X[t] = dcov_bn;
-  if (t < 16) mv[3][t] = dmu_bn / ((float)N * HW);
-  __syncthreads();
-  const float E = (dcov_bn + L.X[j * 16 + i]) / ((float)N * HW);
-  L.Y[t] = E;
-  __syncthreads();
-  for (int n = 0; n < N; ++n) {
-    float* cf = coef + ((long long)n * G + g) * 528;
-    cf[256 + t] += E;
-    if (t < 16) {
-      // c = E (mu_n - mu_bn) + dmu_n/HW + dmu_bn/(N HW)
-      float s = 0.f;
-      for (int k = 0; k < 16; ++k) s = fmaf(L.Y[t * 16 + k], mu_in[(long long)n * C + g * 16 + k] - mv[0][k], s);
-      cf[512 + t] += s + mv[3][t];
-    }
-  }
+  // the batch-statistics adjoints leave through bmoments (all-reduced over ranks by
+  // SyncSwitchWhiten); sw_bwd_coef completes the per-instance coefficients.
+  bmoments[(long long)g * SW_MOM + 16 + t] = dcov_bn;
+  if (t < 16) bmoments[(long long)g * SW_MOM + t] = dmu_bn;
   if (j == 0) {
     if (dgamma) dgamma[g * 16 + i] = dgam;
     if (dbeta) dbeta[g * 16 + i] = dbet;
@@ -520,6 +521,34 @@ __global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ pa
     wpart[g * 4 + 1] = s1;
     wpart[g * 4 + 2] = db0;
     wpart[g * 4 + 3] = db1;
+  }
+}
+
+// Completes coef with the batch terms: Esym = (dC + dC^T)/(count HW) added to L,
+// c += Esym (mu_n - mu_bn) + dmu_bn/(count HW); count = images over all ranks.
+__global__ __launch_bounds__(256) void sw_bwd_coef(const double* __restrict__ bmoments, double count, int N, int HW,
+                                                   int C, const float* __restrict__ save, float* __restrict__ coef) {
+  __shared__ float E[256];
+  __shared__ float mb[16], dmu[16];
+  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  const float* mu_in = save;
+  const float* mu_bn = mu_in + (long long)N * C + (long long)N * G * 256;
+  const double* bm = bmoments + (long long)g * SW_MOM;
+  const double den = count * (double)HW;
+  E[t] = (float)((bm[16 + t] + bm[16 + j * 16 + i]) / den);
+  if (t < 16) {
+    mb[t] = mu_bn[g * 16 + t];
+    dmu[t] = (float)(bm[t] / den);
+  }
+  __syncthreads();
+  for (int n = 0; n < N; ++n) {
+    float* cf = coef + ((long long)n * G + g) * 528;
+    cf[256 + t] += E[t];
+    if (t < 16) {
+      float sacc = 0.f;
+      for (int k = 0; k < 16; ++k) sacc = fmaf(E[t * 16 + k], mu_in[(long long)n * C + g * 16 + k] - mb[k], sacc);
+      cf[512 + t] += sacc + dmu[t];
+    }
   }
 }
 
@@ -643,13 +672,23 @@ extern "C" int64_t dg_sw_save_size(int N, int C) {
   return (2 * (int64_t)N * C + 2 * (int64_t)N * G * 256 + C + G * 256) * 4;
 }
 
-extern "C" int64_t dg_sw_workspace(int N, int HW, int C) {
-  if (N <= 0 || HW <= 0 || C <= 0 || C % SWC) return DG_ERR_INVALID;
+extern "C" int64_t dg_sw_moments_size(int C) {
+  if (C <= 0 || C % SWC) return DG_ERR_INVALID;
+  return (int64_t)(C / SWC) * SW_MOM * 8;
+}
+
+static int64_t sw_ws_core(int N, int HW, int C) {  // partials + coefficients, 8-B aligned
   const int64_t G = C / SWC, nb = sw_nb(HW);
   const int64_t fwd = std::max<int64_t>(dg_instnorm_workspace(N, HW, C), 0) + (int64_t)N * C * 4 +
                       (int64_t)N * nb * G * 256 * 4;
   const int64_t bwd = (int64_t)N * nb * G * 272 * 4 + (int64_t)N * G * 528 * 4 + G * 4 * 4;
-  return std::max(fwd, bwd);
+  return (std::max(fwd, bwd) + 7) / 8 * 8;
+}
+
+// workspace of dg_sw_fwd/bwd (and of the split phases): core + one moments block
+extern "C" int64_t dg_sw_workspace(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0 || C % SWC) return DG_ERR_INVALID;
+  return sw_ws_core(N, HW, C) + (int64_t)(C / SWC) * SW_MOM * 8;
 }
 
 #define SW_DISPATCH_G(KERNEL, T, ...)                                                                \
@@ -662,19 +701,20 @@ extern "C" int64_t dg_sw_workspace(int N, int HW, int C) {
       hipLaunchKernelGGL((KERNEL<T, 4>), __VA_ARGS__);                                              \
   } while (0)
 
-// SwitchWhiten2d forward (sw_type 2).  mean_w/var_w: the raw sw_mean_weight /
-// sw_var_weight parameters (softmax taken here).  save: dg_sw_save_size bytes,
-// consumed by dg_sw_bwd.  training: batch statistics + running-stat update;
-// otherwise running_mean/running_cov replace the batch statistics.
-extern "C" int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T, float eps,
-                         float momentum, const float* mean_w, const float* var_w, const float* gamma,
-                         const float* beta, float* running_mean, float* running_cov, int training, int act,
-                         float* save, void* y, int64_t ldy, void* workspace, void* stream) {
-  DG_REQUIRE(x && y && save && workspace && mean_w && var_w && running_mean && running_cov);
-  DG_REQUIRE(N > 0 && HW > 0 && C > 0 && T >= 0 && (!gamma || beta));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
-  DG_SUPPORTED(C % SWC == 0 && C <= 256 && T <= SW_MAXT && ldx % V == 0 && ldy % V == 0);
+#define SW_CHECK_SHAPE(dtype, C, T_, ...)                                                           \
+  do {                                                                                              \
+    DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);                                                \
+    const int V_ = dtype == DG_BF16 ? 8 : 4;                                                        \
+    DG_SUPPORTED(C % SWC == 0 && C <= 256 && (T_) <= SW_MAXT);                                      \
+    for (int64_t ld_ : {__VA_ARGS__}) DG_SUPPORTED(ld_ % V_ == 0);                                  \
+  } while (0)
+
+// SwitchWhiten2d statistics, phase 1 (per rank): instance means/covariances into
+// `save` and the batch moments [G][272] doubles into `moments`.
+extern "C" int dg_sw_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float* save,
+                               double* moments, void* workspace, void* stream) {
+  DG_REQUIRE(x && save && moments && workspace && N > 0 && HW > 0 && C > 0);
+  SW_CHECK_SHAPE(dtype, C, 0, ldx);
   hipStream_t st = (hipStream_t)stream;
   const int G = C / SWC, nb = sw_nb(HW), ppb = dg_cdiv(HW, nb);
   float* mu = save;  // mu_in is the first save slot
@@ -689,7 +729,24 @@ extern "C" int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, i
   else
     SW_DISPATCH_G(sw_cov_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)x, ldx, HW, C, ppb, mu, part);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sw_stats_finalize, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, T, eps, momentum, mean_w,
+  hipLaunchKernelGGL(sw_inst_stats, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, save, moments);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// Phase 2: batch statistics from `moments` summed over `count` images (all ranks),
+// running-stat update (training), whitening matrices, fused whiten+affine(+ReLU) apply.
+extern "C" int dg_sw_fwd_finish(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T, float eps,
+                                float momentum, const float* mean_w, const float* var_w, const float* gamma,
+                                const float* beta, float* running_mean, float* running_cov, int training, int act,
+                                int64_t count, const double* moments, float* save, void* y, int64_t ldy,
+                                void* stream) {
+  DG_REQUIRE(x && y && save && moments && mean_w && var_w && running_mean && running_cov && count > 0);
+  DG_REQUIRE(N > 0 && HW > 0 && C > 0 && T >= 0 && (!gamma || beta));
+  SW_CHECK_SHAPE(dtype, C, T, ldx, ldy);
+  hipStream_t st = (hipStream_t)stream;
+  const int G = C / SWC;
+  hipLaunchKernelGGL(sw_finalize, dim3(G), dim3(256), 0, st, moments, (double)count, N, C, T, eps, momentum, mean_w,
                      var_w, gamma, beta, running_mean, running_cov, training, save);
   DG_CHECK_LAUNCH();
   const float* aff = save + (int64_t)N * C + (int64_t)N * G * 256 + C + (int64_t)G * 256;
@@ -707,21 +764,29 @@ extern "C" int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, i
   return DG_OK;
 }
 
-// Backward of dg_sw_fwd (training mode).  gy: upstream gradient of y; y: the
-// forward output (ReLU mask when act == 1); x: forward input.  Writes dx (+=
-// when accumulate), dgamma/dbeta, d(sw_mean_weight), d(sw_var_weight) (each
-// may be NULL).
-extern "C" int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
-                         int64_t ldx, int N, int HW, int C, int T, float eps, const float* mean_w,
-                         const float* var_w, const float* gamma, int act, const float* save, void* dx, int64_t lddx,
-                         int accumulate, float* dgamma, float* dbeta, float* dmean_w, float* dvar_w,
-                         void* workspace, void* stream) {
-  DG_REQUIRE(gy && x && dx && save && workspace && mean_w && var_w && (act == 0 || y));
+// SwitchWhiten2d forward (sw_type 2), one rank: phase 1 + phase 2 with count = N.
+// The moments live at the end of the workspace.
+extern "C" int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T, float eps,
+                         float momentum, const float* mean_w, const float* var_w, const float* gamma,
+                         const float* beta, float* running_mean, float* running_cov, int training, int act,
+                         float* save, void* y, int64_t ldy, void* workspace, void* stream) {
+  DG_REQUIRE(workspace && N > 0 && HW > 0 && C > 0 && C % SWC == 0);
+  double* moments = (double*)((char*)workspace + sw_ws_core(N, HW, C));
+  int rc = dg_sw_fwd_stats(dtype, x, ldx, N, HW, C, save, moments, workspace, stream);
+  if (rc) return rc;
+  return dg_sw_fwd_finish(dtype, x, ldx, N, HW, C, T, eps, momentum, mean_w, var_w, gamma, beta, running_mean,
+                          running_cov, training, act, N, moments, save, y, ldy, stream);
+}
+
+// Backward phase 1 (per rank): per-instance adjoints into the workspace, the batch
+// adjoints (dcov_bn, dmu_bn) into `bmoments` [G][272] doubles, dgamma/dbeta.
+extern "C" int dg_sw_bwd_stats(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+                               int64_t ldx, int N, int HW, int C, int T, float eps, const float* mean_w,
+                               const float* var_w, const float* gamma, int act, const float* save, double* bmoments,
+                               float* dgamma, float* dbeta, void* workspace, void* stream) {
+  DG_REQUIRE(gy && x && save && bmoments && workspace && mean_w && var_w && (act == 0 || y));
   DG_REQUIRE(N > 0 && HW > 0 && C > 0 && T >= 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
-  DG_SUPPORTED(C % SWC == 0 && C <= 256 && T <= SW_MAXT && ldx % V == 0 && ldg % V == 0 && lddx % V == 0 &&
-               (act == 0 || ldy % V == 0));
+  SW_CHECK_SHAPE(dtype, C, T, ldx, ldg, act ? ldy : ldx);
   hipStream_t st = (hipStream_t)stream;
   const int G = C / SWC, nb = sw_nb(HW), ppb = dg_cdiv(HW, nb);
   const float* mu = save;
@@ -736,7 +801,27 @@ extern "C" int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, 
                   (const float*)x, ldx, HW, C, ppb, act, mu, part);
   DG_CHECK_LAUNCH();
   hipLaunchKernelGGL(sw_bwd_small, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, T, eps, mean_w, var_w, gamma, save,
-                     coef, wpart, dgamma, dbeta);
+                     coef, wpart, bmoments, dgamma, dbeta);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// Backward phase 2: batch adjoints summed over ranks (`count` images in total) ->
+// coefficients -> dx (+= when accumulate); mixing-weight gradients (this rank's part).
+extern "C" int dg_sw_bwd_finish(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+                                int64_t ldx, int N, int HW, int C, int act, const float* mean_w, const float* var_w,
+                                const float* save, int64_t count, const double* bmoments, void* dx, int64_t lddx,
+                                int accumulate, float* dmean_w, float* dvar_w, void* workspace, void* stream) {
+  DG_REQUIRE(gy && x && dx && save && bmoments && workspace && mean_w && var_w && (act == 0 || y) && count > 0);
+  DG_REQUIRE(N > 0 && HW > 0 && C > 0);
+  SW_CHECK_SHAPE(dtype, C, 0, ldx, ldg, lddx, act ? ldy : ldx);
+  hipStream_t st = (hipStream_t)stream;
+  const int G = C / SWC, nb = sw_nb(HW);
+  const float* mu = save;
+  float* part = (float*)workspace;
+  float* coef = part + (int64_t)N * nb * G * 272;
+  float* wpart = coef + (int64_t)N * G * 528;
+  hipLaunchKernelGGL(sw_bwd_coef, dim3(G), dim3(256), 0, st, bmoments, (double)count, N, HW, C, save, coef);
   DG_CHECK_LAUNCH();
   hipLaunchKernelGGL(sw_bwd_weights, dim3(1), dim3(64), 0, st, wpart, G, mean_w, var_w, dmean_w, dvar_w);
   DG_CHECK_LAUNCH();
@@ -751,4 +836,19 @@ extern "C" int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, 
                        ldy, (const float*)x, ldx, HW, C, appb, act, mu, coef, (float*)dx, lddx, accumulate);
   DG_CHECK_LAUNCH();
   return DG_OK;
+}
+
+// Backward of dg_sw_fwd (training mode, one rank): phase 1 + phase 2 with count = N.
+extern "C" int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+                         int64_t ldx, int N, int HW, int C, int T, float eps, const float* mean_w,
+                         const float* var_w, const float* gamma, int act, const float* save, void* dx, int64_t lddx,
+                         int accumulate, float* dgamma, float* dbeta, float* dmean_w, float* dvar_w,
+                         void* workspace, void* stream) {
+  DG_REQUIRE(workspace && N > 0 && HW > 0 && C > 0 && C % SWC == 0);
+  double* bm = (double*)((char*)workspace + sw_ws_core(N, HW, C));
+  int rc = dg_sw_bwd_stats(dtype, gy, ldg, y, ldy, x, ldx, N, HW, C, T, eps, mean_w, var_w, gamma, act, save, bm,
+                           dgamma, dbeta, workspace, stream);
+  if (rc) return rc;
+  return dg_sw_bwd_finish(dtype, gy, ldg, y, ldy, x, ldx, N, HW, C, act, mean_w, var_w, save, N, bm, dx, lddx,
+                          accumulate, dmean_w, dvar_w, workspace, stream);
 }

@@ -47,3 +47,15 @@ def broadcast_module_(module: torch.nn.Module, src: int = 0) -> None:
     if world() > 1:
         for t in module.state_dict().values():
             dist.broadcast(t, src)
+
+
+def sum_moments(n_local: int):
+    """Reducer for SyncSwitchWhiten2d (models/SW/ops/sync_switchwhiten.py:13-56):
+    t -> (t summed over ranks, n_local * world).  Like the reference's SyncMeanCov it
+    assumes every rank holds the same number of images."""
+    def reduce(t: torch.Tensor):
+        n = world()
+        if n > 1:
+            dist.all_reduce(t)
+        return t, n_local * n
+    return reduce

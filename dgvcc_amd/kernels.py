@@ -381,6 +381,44 @@ def sw_fwd(x: Act, mean_w, var_w, gamma, beta, running_mean, running_cov, traini
     return save
 
 
+def sw_fwd_sync(x: Act, mean_w, var_w, gamma, beta, running_mean, running_cov, training: bool,
+                act: int, y: Act, reduce_fn, T: int = 5, eps: float = 1e-5, momentum: float = 0.9):
+    """SyncSwitchWhiten2d forward: reduce_fn(moments f64 tensor) -> (moments summed over ranks,
+    total image count) sits between the statistics and the whitening phases.
+    Returns (save, workspace) for sw_bwd_sync."""
+    HW = x.H * x.W
+    dev = x.buf.device
+    save = torch.empty(query("dg_sw_save_size", x.N, x.C) // 4, dtype=torch.float32, device=dev)
+    ws = query("dg_sw_workspace", x.N, HW, x.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
+    mom = torch.empty(query("dg_sw_moments_size", x.C) // 8, dtype=torch.float64, device=dev)
+    count = x.N
+    if training:
+        call("dg_sw_fwd_stats", x.dt, x.ptr, x.ld, x.N, HW, x.C, ptr(save), ptr(mom), ptr(work), stream())
+        mom, count = reduce_fn(mom)
+    else:
+        call("dg_sw_fwd_stats", x.dt, x.ptr, x.ld, x.N, HW, x.C, ptr(save), ptr(mom), ptr(work), stream())
+    call("dg_sw_fwd_finish", x.dt, x.ptr, x.ld, x.N, HW, x.C, int(T), float(eps), float(momentum),
+         ptr(mean_w), ptr(var_w), ptr(gamma), ptr(beta), ptr(running_mean), ptr(running_cov),
+         int(training), act, int(count), ptr(mom), ptr(save), y.ptr, y.ld, stream())
+    return save, work, count
+
+
+def sw_bwd_sync(gy: Act, y: Act | None, x: Act, save, work, mean_w, var_w, gamma, act: int, dx: Act,
+                reduce_fn, dgamma=None, dbeta=None, dmean_w=None, dvar_w=None, accumulate=False,
+                T: int = 5, eps: float = 1e-5):
+    HW = x.H * x.W
+    bm = torch.empty(query("dg_sw_moments_size", x.C) // 8, dtype=torch.float64, device=x.buf.device)
+    call("dg_sw_bwd_stats", x.dt, gy.ptr, gy.ld, y.ptr if y is not None else None,
+         y.ld if y is not None else 0, x.ptr, x.ld, x.N, HW, x.C, int(T), float(eps), ptr(mean_w),
+         ptr(var_w), ptr(gamma), act, ptr(save), ptr(bm), ptr(dgamma), ptr(dbeta), ptr(work), stream())
+    bm, count = reduce_fn(bm)
+    call("dg_sw_bwd_finish", x.dt, gy.ptr, gy.ld, y.ptr if y is not None else None,
+         y.ld if y is not None else 0, x.ptr, x.ld, x.N, HW, x.C, act, ptr(mean_w), ptr(var_w),
+         ptr(save), int(count), ptr(bm), dx.ptr, dx.ld, int(accumulate), ptr(dmean_w), ptr(dvar_w),
+         ptr(work), stream())
+
+
 def sw_bwd(gy: Act, y: Act | None, x: Act, save, mean_w, var_w, gamma, act: int, dx: Act,
            dgamma=None, dbeta=None, dmean_w=None, dvar_w=None, accumulate=False, T: int = 5,
            eps: float = 1e-5):

@@ -209,25 +209,39 @@ class SwitchWhiten2d(nn.Module):
         nn.init.zeros_(self.bias)
 
 
+class SyncSwitchWhiten2d(SwitchWhiten2d):
+    """models/SW/ops/sync_switchwhiten.py:59-183: the batch (BW) mean/covariance are
+    synchronised over the data-parallel ranks (SyncMeanCov).  On the HIP path the
+    statistics and whitening kernels are split and the [G][272] batch moments (and, in
+    backward, their adjoints) are all-reduced over RCCL in between; with one rank it
+    is SwitchWhiten2d."""
+    sync = True
+
+    def __init__(self, num_features, num_pergroup=16, sw_type=2, T=5, tie_weight=False, eps=1e-5,
+                 momentum=0.99, affine=True):
+        super().__init__(num_features, num_pergroup, sw_type, T, tie_weight, eps, momentum, affine)
+
+
 SW_CFG = dict(type="SW", sw_type=2, num_pergroup=16, T=5, tie_weight=False, momentum=0.9, affine=True)
 
 
-def _make_sw():
-    return lambda c: SwitchWhiten2d(c, num_pergroup=16, sw_type=2, T=5, tie_weight=False, eps=1e-5,
-                                    momentum=0.9, affine=True)
+def _make_sw(sync=False):
+    cls = SyncSwitchWhiten2d if sync else SwitchWhiten2d
+    return lambda c: cls(c, num_pergroup=16, sw_type=2, T=5, tie_weight=False, eps=1e-5,
+                         momentum=0.9, affine=True)
 
 
 class Bottleneck_SW(nn.Module):
     """SW/backbones/resnet.py:75-118: norm2 is SwitchWhiten2d ('sw2') when with_sw."""
     expansion = 4
 
-    def __init__(self, inplanes, planes, stride=1, downsample=None, with_sw=False):
+    def __init__(self, inplanes, planes, stride=1, downsample=None, with_sw=False, sync=False):
         super().__init__()
         self.norm2_name = "sw2" if with_sw else "bn2"
         self.conv1 = nn.Conv2d(inplanes, planes, kernel_size=1, bias=False)
         self.add_module("bn1", nn.BatchNorm2d(planes))
         self.conv2 = nn.Conv2d(planes, planes, kernel_size=3, stride=stride, padding=1, bias=False)
-        self.add_module(self.norm2_name, _make_sw()(planes) if with_sw else nn.BatchNorm2d(planes))
+        self.add_module(self.norm2_name, _make_sw(sync)(planes) if with_sw else nn.BatchNorm2d(planes))
         self.conv3 = nn.Conv2d(planes, planes * 4, kernel_size=1, bias=False)
         self.add_module("bn3", nn.BatchNorm2d(planes * 4))
         self.relu = nn.ReLU(inplace=True)
@@ -242,10 +256,10 @@ class Bottleneck_SW(nn.Module):
                         ds[1] if ds is not None else None)
 
 
-def _sw_backbone():
+def _sw_backbone(sync=False):
     """children()[:7] of SW resnet50(sw_cfg): conv1, sw1, relu, maxpool, layer1-3."""
     conv1 = nn.Conv2d(3, 64, kernel_size=7, stride=2, padding=3, bias=False)
-    mods = [conv1, _make_sw()(64), nn.ReLU(inplace=True), nn.MaxPool2d(kernel_size=3, stride=2, padding=1)]
+    mods = [conv1, _make_sw(sync)(64), nn.ReLU(inplace=True), nn.MaxPool2d(kernel_size=3, stride=2, padding=1)]
     inplanes = 64
     for planes, nblk, stride in LAYERS[:3]:
         ds = None
@@ -254,7 +268,7 @@ def _sw_backbone():
         blocks = [Bottleneck_SW(inplanes, planes, stride, ds, with_sw=False)]
         inplanes = planes * 4
         for i in range(1, nblk):
-            blocks.append(Bottleneck_SW(inplanes, planes, with_sw=(i % 2 == 1)))
+            blocks.append(Bottleneck_SW(inplanes, planes, with_sw=(i % 2 == 1), sync=sync))
         mods.append(nn.Sequential(*blocks))
     bb = nn.Sequential(*mods)
     for m in bb.modules():
@@ -267,12 +281,14 @@ def _sw_backbone():
 
 
 class SWCounter_ResNet(_CounterBase):
-    """models/SW/__init__.py:24-42."""
+    """models/SW/__init__.py:24-42.  sync=True builds SyncSwitchWhiten2d layers (batch
+    whitening statistics shared over the data-parallel ranks; an extension — the
+    reference's SW counter uses SwitchWhiten2d)."""
 
-    def __init__(self, pretrained=True):
+    def __init__(self, pretrained=True, sync=False):
         super().__init__()
         self._init_precision()
-        self.backbone = _sw_backbone()
+        self.backbone = _sw_backbone(sync)
         _load_local(self.backbone, "resnet50", pretrained)
         self.head = _counter_head()
         self._plan = None

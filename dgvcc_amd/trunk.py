@@ -20,6 +20,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from . import dist as D
 from . import kernels as K
 from .engine import ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum
 from .kernels import Act
@@ -113,6 +114,12 @@ class Norm:
             K.instnorm_apply(z, st, g, b, act, y)
             return st
         m = self.m  # sw
+        if getattr(m, "sync", False) and D.world() > 1:  # SyncSwitchWhiten2d over RCCL
+            save, work, _ = K.sw_fwd_sync(z, m.sw_mean_weight.detach(), m.sw_var_weight.detach(),
+                                          m.weight.detach(), m.bias.detach(), m.running_mean,
+                                          m.running_cov, training, act, y, D.sum_moments(z.N), T=m.T,
+                                          eps=m.eps, momentum=m.momentum)
+            return ("sync", save, work)
         return K.sw_fwd(z, m.sw_mean_weight.detach(), m.sw_var_weight.detach(), m.weight.detach(),
                         m.bias.detach(), m.running_mean, m.running_cov, training, act, y, T=m.T,
                         eps=m.eps, momentum=m.momentum)
@@ -143,9 +150,15 @@ class Norm:
             m = self.m
             d = {p: torch.empty(p.shape, dtype=torch.float32, device=dev)
                  for p in (m.weight, m.bias, m.sw_mean_weight, m.sw_var_weight)}
-            K.sw_bwd(g, y, z, st, m.sw_mean_weight.detach(), m.sw_var_weight.detach(),
-                     m.weight.detach(), act, dz, d[m.weight], d[m.bias], d[m.sw_mean_weight],
-                     d[m.sw_var_weight], T=m.T, eps=m.eps)
+            if isinstance(st, tuple):  # synchronized statistics: all-reduce the batch adjoints
+                _, save, work = st
+                K.sw_bwd_sync(g, y, z, save, work, m.sw_mean_weight.detach(), m.sw_var_weight.detach(),
+                              m.weight.detach(), act, dz, D.sum_moments(z.N), d[m.weight], d[m.bias],
+                              d[m.sw_mean_weight], d[m.sw_var_weight], T=m.T, eps=m.eps)
+            else:
+                K.sw_bwd(g, y, z, st, m.sw_mean_weight.detach(), m.sw_var_weight.detach(),
+                         m.weight.detach(), act, dz, d[m.weight], d[m.bias], d[m.sw_mean_weight],
+                         d[m.sw_var_weight], T=m.T, eps=m.eps)
             for p, v in d.items():
                 _acc(grads, p, v)
 

@@ -174,6 +174,29 @@ int dg_sw_fwd(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T
               float momentum, const float* mean_w, const float* var_w, const float* gamma,
               const float* beta, float* running_mean, float* running_cov, int training, int act,
               float* save, void* y, int64_t ldy, void* workspace, void* stream);
+/* Split phases for SyncSwitchWhiten2d (models/SW/ops/sync_switchwhiten.py:9-56): the batch
+ * moments moments[G][272] (doubles: sum_n mu_n | sum_n cov_n + mu_n mu_n^T) are the only
+ * cross-instance quantities, so a caller can all-reduce them between the phases; `count` =
+ * images over all ranks.  dg_sw_fwd == stats + finish(count = N).  `workspace` (dg_sw_workspace
+ * bytes) must be the same buffer across a stats/finish pair. */
+int64_t dg_sw_moments_size(int C);
+int dg_sw_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float* save,
+                    double* moments, void* workspace, void* stream);
+int dg_sw_fwd_finish(int dtype, const void* x, int64_t ldx, int N, int HW, int C, int T, float eps,
+                     float momentum, const float* mean_w, const float* var_w, const float* gamma,
+                     const float* beta, float* running_mean, float* running_cov, int training, int act,
+                     int64_t count, const double* moments, float* save, void* y, int64_t ldy,
+                     void* stream);
+/* Backward phases: bmoments[G][272] = (dL/dmu_bn | dL/dcov_bn) of this rank, summed over ranks
+ * by the caller (SyncMeanCov.backward all-reduces grad_mean/grad_cov) before finish. */
+int dg_sw_bwd_stats(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+                    int64_t ldx, int N, int HW, int C, int T, float eps, const float* mean_w,
+                    const float* var_w, const float* gamma, int act, const float* save, double* bmoments,
+                    float* dgamma, float* dbeta, void* workspace, void* stream);
+int dg_sw_bwd_finish(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,
+                     int64_t ldx, int N, int HW, int C, int act, const float* mean_w, const float* var_w,
+                     const float* save, int64_t count, const double* bmoments, void* dx, int64_t lddx,
+                     int accumulate, float* dmean_w, float* dvar_w, void* workspace, void* stream);
 /* Exact adjoint (batch statistics, Newton-Schulz iterations recomputed). y = forward
  * output (ReLU mask when act == 1). Any of dgamma/dbeta/dmean_w/dvar_w may be NULL. */
 int dg_sw_bwd(int dtype, const void* gy, int64_t ldg, const void* y, int64_t ldy, const void* x,

@@ -321,3 +321,22 @@ def test_bias_relu_bwd_no_norm(dev, dtype):
     assert torch.equal(dz.buf.float().cpu(), ref.to(dtype).float())
     assert relerr(db, ref.sum(dim=(0, 1, 2))) < 1e-5
     assert relerr(dbias, ref.sum(dim=(0, 1, 2))) < 1e-5
+
+
+def test_sync_switch_whiten_two_ranks(dev):
+    """SyncSwitchWhiten2d (a17): 2 ranks (gloo, one GPU) on half batches each reproduce
+    the full-batch SwitchWhiten2d forward, running statistics, input and parameter
+    gradients (batch moments and their adjoints all-reduced between kernel phases)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={port}",
+                        os.path.join(here, "sync_sw_worker.py")],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.count("OK") == 2, (r.stdout[-2000:], r.stderr[-3000:])
