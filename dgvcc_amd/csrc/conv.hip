@@ -532,6 +532,11 @@ static bool pipe_wide() {
   return v == 1;
 }
 
+static bool use_tap3() {
+  const char* e = getenv("DGVCC_TAP3");
+  return !(e && e[0] == '0');
+}
+
 static bool use_wgrad_pipe() {
   const char* e = getenv("DGVCC_WGRAD_PIPE");
   return e && e[0] == '1';
@@ -544,6 +549,116 @@ static bool use_pipe() {
     v = (e && e[0] == '0') ? 0 : 1;
   }
   return v == 1;
+}
+
+// ---------------------------------------------------------------------------
+// bf16 forward/dgrad for Cout = 64, 3x3 / stride 1 / pad 1, W % 256 == 0:
+// a tile is 256 output pixels of ONE image row x 64 channels; a K-step is one
+// kernel row dh and 64 input channels, staging the 3 taps' filters and ONE
+// 264-pixel X strip that the 3 taps read at row offsets 0/1/2 (3x fewer staged
+// X bytes than one tap per step).  Single LDS stage (57 KB), two blocks per CU
+// overlap each other's loads and MFMAs.
+// ---------------------------------------------------------------------------
+constexpr int T3_XROWS = 264;
+
+__global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
+  using T = bf16;
+  constexpr int BN = 64, BM = 256;
+  constexpr int A_BYTES = 3 * BN * 128, X_BYTES = T3_XROWS * 128;
+  constexpr int A_INST = A_BYTES / 1024, X_INST = X_BYTES / 1024;   // 24 + 33
+  constexpr int N_INST = A_INST + X_INST;
+  constexpr int TI = 4, TJ = 4;                                      // wave tile 64 px x 64 co
+  __shared__ __attribute__((aligned(1024))) char smem[A_BYTES + X_BYTES];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int px0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+  const int n = px0 / HW, rem = px0 - n * HW;
+  const int pr = rem / a.W, q0 = rem - pr * a.W;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lrow = lane >> 3;
+  const int xlo = max(0, px0 - a.W - 8), xhi = min(M, px0 + BM + a.W + 8);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * 2), 0, (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 2),
+      0x00020000);
+  const long long ldw = 9ll * a.C;
+  __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, (unsigned)(BN * ldw * 2), 0x00020000);
+  const int CB = a.C / 64;
+  const int KT = 3 * CB;
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wpx = wid * 64;
+  const int fr = lane & 15, fc = lane >> 4;
+  const char* As = smem;
+  const char* Xs = smem + A_BYTES;
+
+  for (int t = 0; t < KT; ++t) {
+    const int dh = t % 3, cb = t / 3;
+    for (int ii = wid; ii < N_INST; ii += 4) {
+      if (ii < A_INST) {  // filter rows: tap s = ii / 8, co rows (ii % 8) * 8 + lrow
+        const int sw = ii >> 3, row = (ii & 7) * 8 + lrow;
+        const int ch = (lane & 7) ^ (row & 7);
+        lds_dma16(wr, As + ii * 1024,
+                  (unsigned)(((long long)row * ldw + (dh * 3 + sw) * a.C + cb * 64 + ch * 8) * 2));
+      } else {            // X strip rows: pixel q0 - 4 + row of image row pr + dh - 1
+        const int jj = ii - A_INST, row = jj * 8 + lrow;
+        const int ch = (lane & 7) ^ (row & 7);
+        const int h = pr + dh - 1, w = q0 - 4 + row;
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+        const long long pin = (long long)n * HW + (long long)h * a.W + w - xlo;
+        lds_dma16(xr, Xs + jj * 1024, ok ? (unsigned)((pin * a.ldx + cb * 64 + ch * 8) * 2) : 0xFFFFFFF0u);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int sw = 0; sw < 3; ++sw) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = 4 * ks + fc;
+        u4v af[TI], bfr[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Xs + swz(wpx + 16 * j + fr + sw + 3, ch));
+#pragma unroll
+        for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + sw * BN * 128 + swz(16 * i + fr, ch));
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  T* y = (T*)a.y;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      st4(yrow + co, v);
+    }
+  }
 }
 
 template <typename T>
@@ -560,7 +675,9 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         else if (var == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2>), dim3(G_), dim3(512), 0, st, a); \
         else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 0>), dim3(G_), dim3(512), 0, st, a); \
       } while (0)
-      if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
+      if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
+        hipLaunchKernelGGL(conv_fwd_tap3_kernel, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+      } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
       else PIPE_LAUNCH(64, 3, np * (a.Cout / 64));
 #undef PIPE_LAUNCH
