@@ -310,17 +310,18 @@ template <typename T>
 int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int M, int C, const float* gamma,
                 const float* mean, const float* inv, const float* scale, const float* shift, int act,
                 const float* drop, int HW, void* dz, long long lddz, float* dgamma, float* dbeta, float* dbias,
-                void* ws, hipStream_t st) {
+                void* ws, hipStream_t st, float* coef_out = nullptr) {
   const int nblk = bn_nblk(M);
   const int ppb = dg_cdiv(M, nblk);
   float* part = (float*)ws;
-  float* coef = part + (long long)nblk * 3 * C;
+  float* coef = coef_out ? coef_out : part + (long long)nblk * 3 * C;
   hipLaunchKernelGGL(bn_bwd_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C, ppb,
                      mean, inv, scale, shift, act, drop, HW, part);
   DG_CHECK_LAUNCH();
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, inv, dgamma,
                      dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
+  if (!dz) return DG_OK;  // coefficients only (a fused consumer applies them)
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
   hipLaunchKernelGGL(bn_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
                      mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz);
@@ -388,4 +389,21 @@ extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, i
                                  lddz, dgamma, dbeta, dbias, workspace, st)
              : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
                                   dz, lddz, dgamma, dbeta, dbias, workspace, st);
+}
+
+extern "C" int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                              const float* gamma, const float* save_mean, const float* save_invstd,
+                              const float* scale, const float* shift, int act, const float* drop, int HW,
+                              float* coef, float* dgamma, float* dbeta, float* dbias, void* workspace,
+                              void* stream) {
+  DG_REQUIRE(g && z && coef && workspace && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
+  DG_REQUIRE(!drop || HW > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz));
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16
+             ? bn_bwd_impl<bf16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+                                 nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef)
+             : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+                                  nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef);
 }

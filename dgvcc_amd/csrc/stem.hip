@@ -1,0 +1,461 @@
+// First VGG16-BN layer (features[0:3] = Conv2d(3, 64, 3, pad 1) + BatchNorm2d +
+// ReLU, models/models.py:35-36) fused for the bf16 perf path.
+//
+// The generic route materialised a [N*H*W][64] im2col buffer (27 taps padded to
+// 64) and ran the K=64 GEMM on it, then read the conv output again for the BN
+// statistics: ~3.5 GB of HBM traffic per 16 frames at 768x1024 for 0.1 TFLOP.
+// Here:
+//   forward  stem_fwd_kernel  gathers the 27 taps straight from the NCHW f32
+//            image into MFMA B fragments (v_mfma_f32_16x16x32_bf16, K = 27 -> 32),
+//            adds the bias, writes z (bf16 NHWC) and keeps per-channel shifted
+//            sums of the stored values -> per-block (n, mean, M2) partials;
+//            bn_part_finalize merges them (Chan) in double.
+//   backward stem_bwd_kernel recomputes dz = BN/ReLU backward (the same float
+//            arithmetic as bn_bwd_apply in norm.hip) from g and z, stages dz and
+//            the image im2col tile in LDS and accumulates dW = dz^T . col on MFMA
+//            (transposed ds_read_b64_tr_b16 fragments).  dz never reaches HBM
+//            (the first layer has no input gradient).
+#include "dg_common.h"
+#include <algorithm>
+
+namespace {
+
+constexpr int SNT = 256;     // 4 waves
+constexpr int SCO = 64;      // output channels of the stem
+constexpr int SK = 32;       // 27 taps padded to one bf16 MFMA k-step
+
+__device__ __forceinline__ unsigned short bfbits(float x) { return f2bf(x); }
+
+// Wave-independent row segments (W % 64 == 0): a segment is 64 consecutive
+// pixels of one image row.  The 3 channels x 3 rows x 66 columns it needs are
+// loaded coalesced (one float per lane and row, prefetched a segment ahead) and
+// staged in the wave's own LDS slice as bf16; B fragments are then gathered from
+// LDS.  The output fragment (16 px x 64 co) is transposed through LDS so every
+// global store is a full 16-B lane / 1-KB wave write.
+constexpr int TROW = 72;                       // staged image row: 66 used (q0-1 .. q0+64)
+constexpr int T_BYTES = 9 * TROW * 2;          // [c][r][TROW] bf16
+constexpr int O_BYTES = 16 * 128;              // [16 px][64 co] bf16, 16-B chunks XOR-swizzled by row
+constexpr int FW_LDS = T_BYTES + O_BYTES;
+
+__device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restrict__ img, int H, int W,
+                                                          const bf16* __restrict__ wp, const float* __restrict__ bias,
+                                                          bf16* __restrict__ z, long long ldz, long long nseg,
+                                                          float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * FW_LDS];
+  __shared__ float sh[4][3][SCO];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int h = lane >> 4, col = lane & 15;
+  char* T = smem + wid * FW_LDS;
+  char* O = T + T_BYTES;
+  const int spr = W / 64;  // segments per image row
+  // LDS byte offsets of this lane's 8 taps (k = 8h + j) relative to pixel column x
+  int toff[8];
+  unsigned kmask = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 8 * h + j;
+    const int t = k / 3, c = k - 3 * t, r = t / 3, s2 = t - 3 * r;
+    toff[j] = ((c * 3 + r) * TROW + s2) * 2;
+    if (k < 27) kmask |= 1u << j;
+  }
+  u4v wa[4];
+  float bs[4][4];
+#pragma unroll
+  for (int cf = 0; cf < 4; ++cf) {
+    wa[cf] = *(const u4v*)(wp + (16 * cf + col) * SK + 8 * h);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bs[cf][i] = bias ? bias[16 * cf + 4 * h + i] : 0.f;
+  }
+  float K[16], S1[16], S2[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { K[e] = 0.f; S1[e] = 0.f; S2[e] = 0.f; }
+
+  float raw[9], rawt[9];
+  auto gload = [&](long long seg) {
+    const int row_id = (int)(seg / spr);            // n*H + p
+    const int q0 = (int)(seg - (long long)row_id * spr) * 64;
+    const int n = row_id / H, p = row_id - n * H;
+    const int qa = q0 - 1 + lane, qb = q0 + 63 + lane;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int pr = p + r - 1;
+        const bool rok = (unsigned)pr < (unsigned)H;
+        const float* src = img + ((long long)(n * 3 + c) * H + pr) * W;
+        raw[c * 3 + r] = (rok && qa >= 0) ? src[qa] : 0.f;
+        rawt[c * 3 + r] = (rok && lane < 2 && qb < W) ? src[qb] : 0.f;
+      }
+  };
+  long long seg = (long long)blockIdx.x * 4 + wid;
+  const long long sstride = (long long)gridDim.x * 4;
+  if (seg < nseg) gload(seg);
+  long long nloc = 0;
+  bool first = true;
+  for (; seg < nseg; seg += sstride) {
+    // stage the image rows (bf16), then prefetch the next segment's
+    unsigned short* Ts = (unsigned short*)T;
+#pragma unroll
+    for (int e = 0; e < 9; ++e) {
+      Ts[e * TROW + lane] = bfbits(raw[e]);
+      if (lane < 2) Ts[e * TROW + 64 + lane] = bfbits(rawt[e]);
+    }
+    lds_fence();
+    if (seg + sstride < nseg) gload(seg + sstride);
+    const long long m0 = seg * 64;
+#pragma unroll
+    for (int pf = 0; pf < 4; ++pf) {
+      const int x2 = (16 * pf + col) * 2;
+      unsigned short v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (kmask >> j) & 1 ? *(const unsigned short*)(T + toff[j] + x2) : 0;
+      const u4v b = u4v{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16), v[4] | ((unsigned)v[5] << 16),
+                        v[6] | ((unsigned)v[7] << 16)};
+      f4v acc[4];
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf)
+        acc[cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s8v, wa[cf]), __builtin_bit_cast(s8v, b),
+                                                          f4v{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf) {
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = bf2f(bfbits(acc[cf][i] + bs[cf][i]));  // the stored value
+        const int chunk = 2 * cf + (h >> 1);
+        *(u2v*)(O + col * 128 + ((chunk ^ (col & 7)) << 4) + (h & 1) * 8) =
+            u2v{pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])};
+        if (first && pf == 0) {  // per-channel shift: the wave's first pixel (lane col 0 of its group)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) K[cf * 4 + i] = __shfl(o[i], lane & 48, 64);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float d = o[i] - K[cf * 4 + i];
+          S1[cf * 4 + i] += d;
+          S2[cf * 4 + i] = fmaf(d, d, S2[cf * 4 + i]);
+        }
+      }
+      lds_fence();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int row = (lane >> 3) + 8 * u, chunk = lane & 7;
+        const u4v ov = *(const u4v*)(O + row * 128 + ((chunk ^ (row & 7)) << 4));
+        *(u4v*)(z + (m0 + 16 * pf + row) * ldz + chunk * 8) = ov;
+      }
+    }
+    first = false;
+    nloc += 64;
+  }
+  // reduce over the 16 pixel lanes of each group
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      S1[e] += __shfl_xor(S1[e], o, 64);
+      S2[e] += __shfl_xor(S2[e], o, 64);
+    }
+  }
+  if (col == 0) {
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 16 * cf + 4 * h + i, e = cf * 4 + i;
+        const float nn = (float)nloc;
+        sh[wid][0][c] = nn;
+        sh[wid][1][c] = nloc ? K[e] + S1[e] / nn : 0.f;
+        sh[wid][2][c] = nloc ? fmaxf(S2[e] - S1[e] * S1[e] / nn, 0.f) : 0.f;
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < SCO) {  // Chan merge of the 4 waves
+    const int c = threadIdx.x;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float nb = sh[w][0][c];
+      if (nb == 0.f) continue;
+      const float mb = sh[w][1][c];
+      const float nt = n + nb;
+      const float d = mb - mean;
+      mean += d * (nb / nt);
+      m2 += sh[w][2][c] + d * d * (n * nb / nt);
+      n = nt;
+    }
+    float* o = part + (long long)blockIdx.x * 3 * SCO;
+    o[c] = n;
+    o[SCO + c] = mean;
+    o[2 * SCO + c] = m2;
+  }
+}
+
+// Backward, wave-independent 32-pixel row segments: dW[co][k] = sum_px dz[px][co] col[px][k].
+// Per wave LDS: dz tile [32 px][64 co] bf16 (128-B rows, read transposed) and the
+// transposed im2col tile colT[32 k][32 px] bf16 (64-B rows; rows 27..31 stay zero).
+// Lane roles: dz for channels 8*(lane&7).. of pixels (lane>>3) + 8u; colT rows
+// k = 2i + (lane>>5) at pixel lane&31.  Loads are prefetched a segment ahead.
+constexpr int BDZ = 32 * 128, BCOL = 32 * 64, BW_LDS = BDZ + BCOL;
+
+__global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
+    const float* __restrict__ img, int H, int W, const bf16* __restrict__ g, long long ldg, const bf16* __restrict__ z,
+    long long ldz, const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ coef, long long nseg, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * BW_LDS];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  char* DZ = smem + wid * BW_LDS;
+  char* CT = DZ + BDZ;
+  const int spr = W / 32;
+  const int c0 = (lane & 7) * 8;
+  float sc[8], sf[8], mu[8], is[8], k1[8], k2[8], k3[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+    k1[e] = coef[c0 + e]; k2[e] = coef[SCO + c0 + e]; k3[e] = coef[2 * SCO + c0 + e];
+  }
+  // colT rows of this lane: k = 2i + (lane>>5), i = 0..13 (k = 27 -> zero); px = lane & 31
+  const int half = lane >> 5, xq = lane & 31;
+  for (int r = 28 + half; r < 32; r += 2) *(unsigned short*)(CT + r * 64 + xq * 2) = 0;
+
+  u4v gr[4], zr[4];
+  float cv[14];
+  auto gload = [&](long long seg) {
+    const int row_id = (int)(seg / spr);
+    const int q0 = (int)(seg - (long long)row_id * spr) * 32;
+    const int n = row_id / H, p = row_id - n * H;
+    const long long m0 = (long long)row_id * W + q0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long long m = m0 + (lane >> 3) + 8 * u;
+      gr[u] = *(const u4v*)(g + m * ldg + c0);
+      zr[u] = *(const u4v*)(z + m * ldz + c0);
+    }
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      const int k = 2 * i + half;
+      const int t = k / 3, c = k - 3 * t, r = t / 3, s2 = t - 3 * r;
+      const int pr = p + r - 1, qq = q0 + xq + s2 - 1;
+      const bool in = k < 27 && (unsigned)pr < (unsigned)H && (unsigned)qq < (unsigned)W;
+      cv[i] = in ? img[((long long)(n * 3 + c) * H + pr) * W + qq] : 0.f;
+    }
+  };
+  f4v acc[4][2];
+#pragma unroll
+  for (int cf = 0; cf < 4; ++cf) acc[cf][0] = acc[cf][1] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3, li = lane & 15;
+  long long seg = (long long)blockIdx.x * 4 + wid;
+  const long long sstride = (long long)gridDim.x * 4;
+  if (seg < nseg) gload(seg);
+  for (; seg < nseg; seg += sstride) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float gv[8], zv[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        gv[2 * i] = __uint_as_float(gr[u][i] << 16); gv[2 * i + 1] = __uint_as_float(gr[u][i] & 0xffff0000u);
+        zv[2 * i] = __uint_as_float(zr[u][i] << 16); zv[2 * i + 1] = __uint_as_float(zr[u][i] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {  // bn_bwd_load + bn_bwd_apply of norm.hip (act = relu, no dropout)
+        if (!(fmaf(zv[e], sc[e], sf[e]) > 0.f)) gv[e] = 0.f;
+        const float xh = (zv[e] - mu[e]) * is[e];
+        gv[e] = k1[e] * gv[e] - k2[e] * xh - k3[e];
+      }
+      const int px = (lane >> 3) + 8 * u;
+      *(u4v*)(DZ + px * 128 + c0 * 2) =
+          u4v{pack_bf2(gv[0], gv[1]), pack_bf2(gv[2], gv[3]), pack_bf2(gv[4], gv[5]), pack_bf2(gv[6], gv[7])};
+    }
+#pragma unroll
+    for (int i = 0; i < 14; ++i) *(unsigned short*)(CT + (2 * i + half) * 64 + xq * 2) = bfbits(cv[i]);
+    lds_fence();
+    if (seg + sstride < nseg) gload(seg + sstride);
+    // A = dz^T (transposed reads): logical k = 8*gq + j <-> pixel 4*gq + (j&3) + 16*(j>>2)
+    s8v bfv[2];
+#pragma unroll
+    for (int kf = 0; kf < 2; ++kf) {
+      const char* rp = CT + (16 * kf + li) * 64;
+      const u2v lo = *(const u2v*)(rp + 8 * gq), hi = *(const u2v*)(rp + 32 + 8 * gq);
+      bfv[kf] = __builtin_bit_cast(s8v, u4v{lo[0], lo[1], hi[0], hi[1]});
+    }
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) {
+      const int ca = (16 * cf + 4 * p4) * 2;
+      s4v alo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(DZ + (4 * gq + q4) * 128 + ca));
+      s4v ahi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(DZ + (16 + 4 * gq + q4) * 128 + ca));
+      const s8v af = s8v{alo[0], alo[1], alo[2], alo[3], ahi[0], ahi[1], ahi[2], ahi[3]};
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf) acc[cf][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[kf], acc[cf][kf], 0, 0, 0);
+    }
+  }
+  // combine the 4 waves in a fixed order (deterministic), then one slab row per block
+  __syncthreads();
+  float* red = (float*)smem;  // [64 co][32 k]
+  for (int w = 0; w < 4; ++w) {
+    if (wid == w) {
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf)
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float* d = red + (16 * cf + 4 * gq + i) * SK + 16 * kf + li;
+            *d = (w == 0 ? 0.f : *d) + acc[cf][kf][i];
+          }
+    }
+    __syncthreads();
+  }
+  float* o = slab + (long long)blockIdx.x * SCO * SK;
+  for (int e = threadIdx.x; e < SCO * SK; e += SNT) o[e] = red[e];
+}
+
+// out[rb][c] = sum of rows [rb*rpb, (rb+1)*rpb) of in[rows][cols]; grid (cols/256, ceil(rows/rpb)).
+__global__ __launch_bounds__(SNT) void colsum_rows_kernel(const float* __restrict__ in, int rows, int cols, int rpb,
+                                                          float* __restrict__ out) {
+  const int c = blockIdx.x * SNT + threadIdx.x;
+  if (c >= cols) return;
+  const int r0 = blockIdx.y * rpb, r1 = min(rows, r0 + rpb);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += in[(long long)r * cols + c];
+  out[(long long)blockIdx.y * cols + c] = s;
+}
+
+// dw[co][c][r][s] (torch layout) = sum_b slab[b][co][k], k = (r*3+s)*3+c; one block per co.
+__global__ __launch_bounds__(SNT) void stem_wgrad_reduce(const float* __restrict__ slab, int nblk,
+                                                         float* __restrict__ dw, int accumulate) {
+  __shared__ float sh[8][SK];
+  const int co = blockIdx.x, k = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  float s = 0.f;
+  for (int b = rg; b < nblk; b += 8) s += slab[((long long)b * SCO + co) * SK + k];
+  sh[rg][k] = s;
+  __syncthreads();
+  if (threadIdx.x < 27) {
+    float t = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) t += sh[r][k];
+    const int tap = k / 3, c = k - 3 * tap;
+    float* d = dw + (co * 3 + c) * 9 + tap;
+    *d = accumulate ? *d + t : t;
+  }
+}
+
+// Merge per-block (n, mean, M2) rows [nblk][3][C] into the BN batch statistics
+// (Chan et al.; double), then the same outputs as bn_stats_finalize (norm.hip).
+__global__ __launch_bounds__(SNT) void bn_part_finalize(const float* __restrict__ part, int nblk, int C,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float* running_mean,
+                                                        float* running_var, float momentum, float eps,
+                                                        float* save_mean, float* save_invstd, float* scale,
+                                                        float* shift) {
+  __shared__ double sh[2][SNT];
+  __shared__ double smean;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const long long row = 3LL * C;
+  double n = 0.0, s = 0.0;
+  for (int b = tid; b < nblk; b += SNT) {
+    const double nb = part[b * row + c];
+    n += nb;
+    s += nb * part[b * row + C + c];
+  }
+  sh[0][tid] = n; sh[1][tid] = s;
+  __syncthreads();
+  for (int o = SNT / 2; o > 0; o >>= 1) {
+    if (tid < o) { sh[0][tid] += sh[0][tid + o]; sh[1][tid] += sh[1][tid + o]; }
+    __syncthreads();
+  }
+  const double M = sh[0][0];
+  if (tid == 0) smean = sh[1][0] / M;
+  __syncthreads();
+  const double mean = smean;
+  double m2 = 0.0;
+  for (int b = tid; b < nblk; b += SNT) {
+    const double nb = part[b * row + c];
+    if (nb == 0.0) continue;
+    const double d = part[b * row + C + c] - mean;
+    m2 += part[b * row + 2 * C + c] + nb * d * d;
+  }
+  __syncthreads();
+  sh[0][tid] = m2;
+  __syncthreads();
+  for (int o = SNT / 2; o > 0; o >>= 1) {
+    if (tid < o) sh[0][tid] += sh[0][tid + o];
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  const double var = sh[0][0] / M;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  save_mean[c] = (float)mean;
+  save_invstd[c] = invstd;
+  const float sc = gamma ? gamma[c] * invstd : invstd;
+  scale[c] = sc;
+  shift[c] = (beta ? beta[c] : 0.f) - (float)mean * sc;
+  if (running_mean) {
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    const double unb = M > 1 ? var * M / (M - 1) : var;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unb;
+  }
+}
+
+inline int stem_fwd_grid(long long nseg) { return (int)std::max(1LL, std::min(512LL, (nseg + 3) / 4)); }
+inline int stem_bwd_grid(long long nseg) { return (int)std::max(1LL, std::min(512LL, (nseg + 3) / 4)); }
+constexpr int STEM_RPB = 32;  // slab rows per first-stage reduce block
+
+}  // namespace
+
+extern "C" int64_t dg_stem_part_rows(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return DG_ERR_INVALID;
+  return stem_fwd_grid((long long)N * H * (W / 64));
+}
+
+extern "C" int dg_stem_fwd(const float* img, int N, int H, int W, const void* wpack, const float* bias, void* z,
+                           int64_t ldz, float* part, void* stream) {
+  DG_REQUIRE(img && wpack && z && part && N > 0 && H > 0 && W > 0 && ldz >= SCO);
+  DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldz % 8 == 0);
+  const long long nseg = (long long)N * H * (W / 64);
+  hipLaunchKernelGGL(stem_fwd_kernel, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
+                     (const bf16*)wpack, bias, (bf16*)z, (long long)ldz, nseg, part);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_part_finalize(const float* part, int nblk, int C, const float* gamma, const float* beta,
+                                   float* running_mean, float* running_var, float momentum, float eps,
+                                   float* save_mean, float* save_invstd, float* scale, float* shift, void* stream) {
+  DG_REQUIRE(part && nblk > 0 && C > 0 && save_mean && save_invstd && scale && shift);
+  DG_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
+  hipLaunchKernelGGL(bn_part_finalize, dim3(C), dim3(SNT), 0, (hipStream_t)stream, part, nblk, C, gamma, beta,
+                     running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_stem_bwd_workspace(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return DG_ERR_INVALID;
+  const int grid = stem_bwd_grid((long long)N * H * (W / 32));
+  return ((int64_t)grid + dg_cdiv(grid, STEM_RPB)) * SCO * SK * 4;
+}
+
+extern "C" int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
+                           int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
+                           const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,
+                           int accumulate, void* stream) {
+  DG_REQUIRE(img && g && z && save_mean && save_invstd && scale && shift && coef && dw && workspace);
+  DG_REQUIRE(N > 0 && H > 0 && W > 0 && ldg >= SCO && ldz >= SCO);
+  DG_SUPPORTED(W % 32 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldg % 8 == 0 && ldz % 8 == 0);
+  const long long nseg = (long long)N * H * (W / 32);
+  const int grid = stem_bwd_grid(nseg);
+  const int nred = dg_cdiv(grid, STEM_RPB);
+  DG_REQUIRE(ws_bytes >= ((int64_t)grid + nred) * SCO * SK * 4);
+  hipStream_t st = (hipStream_t)stream;
+  float* slab = (float*)workspace;
+  float* slab2 = slab + (long long)grid * SCO * SK;
+  hipLaunchKernelGGL(stem_bwd_kernel, dim3(grid), dim3(SNT), 0, st, img, H, W, (const bf16*)g, (long long)ldg,
+                     (const bf16*)z, (long long)ldz, save_mean, save_invstd, scale, shift, coef, nseg, slab);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3(SCO * SK / SNT, nred), dim3(SNT), 0, st, (const float*)slab, grid,
+                     SCO * SK, STEM_RPB, slab2);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(stem_wgrad_reduce, dim3(SCO), dim3(SNT), 0, st, (const float*)slab2, nred, dw, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}

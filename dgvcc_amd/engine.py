@@ -56,17 +56,44 @@ class ConvLayer:
             return K.pack_weight(w, dt, cpad=self.Cin, row_len=64)
         return K.pack_weight(w, dt)
 
-    def forward(self, x: Act, out: Act, training: bool, tape: dict | None,
+    def stem_ok(self, dt) -> bool:
+        """bf16 first layer with BN + ReLU: fused conv/statistics and BN-backward/wgrad kernels."""
+        return (self.first and dt == torch.bfloat16 and self.bn is not None and self.act == ACT_RELU
+                and self.Cin == 3 and self.Cout == 64 and self.R == 3)
+
+    @staticmethod
+    def stem_shape_ok(W: int) -> bool:  # row segments of 64 pixels (dg_stem_fwd)
+        return W % 64 == 0
+
+    def forward(self, x, out: Act, training: bool, tape: dict | None,
                 drop: torch.Tensor | None = None):
-        dt = x.buf.dtype
-        wp = self._pack(dt)
+        """x: NHWC Act, or for the fused bf16 stem the NCHW f32 image itself."""
+        stem = isinstance(x, torch.Tensor)
+        dt = out.buf.dtype
         bias = self.conv.bias.detach() if self.conv.bias is not None else None
+        bn = self.bn
+        if stem:
+            N, _, H, W = x.shape
+            wp = K.pack_weight(self.conv.weight.detach(), dt, cpad=3, row_len=32)
+            z = Act(K.nhwc(N, H, W, self.Cout, dt, x.device))
+            part, nblk = K.stem_fwd(x, wp, bias, z)
+            if training:
+                bn.num_batches_tracked.add_(1)
+                stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
+                                           bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+            else:
+                stats = K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                        bn.running_var, bn.eps)
+            K.bn_apply(z, stats, self.act, out, drop)
+            if tape is not None:
+                tape[self] = (x, z, stats, wp, drop, training)
+            return
+        wp = self._pack(dt)
         z = Act(K.nhwc(x.N, x.H, x.W, self.Cout, dt, x.buf.device))
         if self.first:
             K.conv_fwd(x, wp, self.Cout, 1, 0, z, bias=bias, k_alg=9 * self.Cin)
         else:
             K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
-        bn = self.bn
         if bn is not None:
             if training:
                 bn.num_batches_tracked.add_(1)
@@ -95,6 +122,14 @@ class ConvLayer:
         dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) \
             if self.conv.bias is not None else None
         gamma = self.bn.weight.detach() if self.bn is not None else None
+        if isinstance(x, torch.Tensor):  # fused bf16 stem: coefficients, then BN-backward + wgrad in one pass
+            coef = K.bn_bwd_coef(g, z, gamma, stats, self.act, dgamma, dbeta, dbias, drop)
+            dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
+            K.stem_bwd(x, g, z, stats, coef, dw)
+            grads = {self.conv.weight: dw, self.bn.weight: dgamma, self.bn.bias: dbeta}
+            if self.conv.bias is not None:
+                grads[self.conv.bias] = dbias
+            return grads
         K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta,
                  dbias, drop)
         dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
@@ -141,8 +176,11 @@ class FeaturePlan:
         E, D = self.enc, self.dec
         nh = lambda h, w, c: Act(K.nhwc(N, h, w, c, dt, dev))  # noqa: E731
         s = {}
-        col = Act(K.im2col_c3(img.float(), dt))
-        a = nh(H, W, 64); E[0].forward(col, a, training, tape)
+        a = nh(H, W, 64)
+        if E[0].stem_ok(dt) and ConvLayer.stem_shape_ok(W):
+            E[0].forward(img.float().contiguous(), a, training, tape)
+        else:
+            E[0].forward(Act(K.im2col_c3(img.float(), dt)), a, training, tape)
         b = nh(H, W, 64); E[1].forward(a, b, training, tape)
         p1 = nh(H // 2, W // 2, 64); K.maxpool_fwd(b, p1)
         a2 = nh(H // 2, W // 2, 128); E[2].forward(p1, a2, training, tape)

@@ -137,6 +137,50 @@ def unpack_c3_grad(dwcol: torch.Tensor, dw: torch.Tensor, accumulate=False):
     call("dg_unpack_c3_grad", ptr(dwcol), dw.shape[0], ptr(dw), int(accumulate), stream())
 
 
+def stem_fwd(img: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor | None, z: Act) -> tuple:
+    """Fused first layer (bf16): z = conv3x3(img NCHW f32, 3->64) + bias, plus BN partials."""
+    N, _, H, W = img.shape
+    rows = query("dg_stem_part_rows", N, H, W)
+    part = torch.empty((rows, 3, 64), dtype=torch.float32, device=img.device)
+    flops = 2.0 * N * H * W * 27 * 64
+    nbytes = 4.0 * img.numel() + 2.0 * N * H * W * 64
+    _timed("stem", flops, lambda: call("dg_stem_fwd", ptr(img), N, H, W, ptr(wp), ptr(bias), z.ptr, z.ld,
+                                       ptr(part), stream()), nbytes)
+    return part, rows
+
+
+def bn_part_finalize(part: torch.Tensor, nblk: int, C: int, gamma, beta, running_mean, running_var,
+                     momentum, eps):
+    stats = torch.empty((4, C), dtype=torch.float32, device=part.device)
+    call("dg_bn_part_finalize", ptr(part), nblk, C, ptr(gamma), ptr(beta), ptr(running_mean),
+         ptr(running_var), float(momentum), float(eps), ptr(stats[0]), ptr(stats[1]), ptr(stats[2]),
+         ptr(stats[3]), stream())
+    return stats
+
+
+def bn_bwd_coef(g: Act, z: Act, gamma, stats, act: int, dgamma, dbeta, dbias=None,
+                drop: torch.Tensor | None = None) -> torch.Tensor:
+    ws = query("dg_bn_workspace", z.M, z.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
+    coef = torch.empty((3, z.C), dtype=torch.float32, device=z.buf.device)
+    call("dg_bn_bwd_coef", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma), ptr(stats[0]),
+         ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, ptr(coef),
+         ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), stream())
+    return coef
+
+
+def stem_bwd(img: torch.Tensor, g: Act, z: Act, stats, coef, dw: torch.Tensor, accumulate=False):
+    N, _, H, W = img.shape
+    ws = query("dg_stem_bwd_workspace", N, H, W)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=img.device)
+    flops = 2.0 * N * H * W * 27 * 64
+    nbytes = 2.0 * (g.M * g.C + z.M * z.C) + 4.0 * img.numel()
+    _timed("stem_wgrad", flops, lambda: call("dg_stem_bwd", ptr(img), N, H, W, g.ptr, g.ld, z.ptr, z.ld,
+                                             ptr(stats[0]), ptr(stats[1]), ptr(stats[2]), ptr(stats[3]),
+                                             ptr(coef), ptr(dw), ptr(work), ws, int(accumulate),
+                                             stream()), nbytes)
+
+
 # ---------------------------------------------------------------- BN -------
 def bn_fwd_train(z: Act, gamma, beta, running_mean, running_var, momentum, eps):
     C = z.C

@@ -126,6 +126,38 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
               void* workspace, void* stream);
 
+/* Coefficients of the BN backward without the dz pass: coef[3][C] = (k1, k2, k3) with
+ * dz = k1*act'(g) - k2*xhat - k3 (the bn_bwd_apply arithmetic), plus dgamma/dbeta/dbias.
+ * For fused consumers (dg_stem_bwd). */
+int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                   const float* gamma, const float* save_mean, const float* save_invstd,
+                   const float* scale, const float* shift, int act, const float* drop, int HW,
+                   float* coef, float* dgamma, float* dbeta, float* dbias, void* workspace,
+                   void* stream);
+
+/* Merge per-block BN partials part[nblk][3][C] = (n, mean, M2) (Chan, double) into the
+ * batch statistics: same outputs and running-stat update as dg_bn_fwd_train. */
+int dg_bn_part_finalize(const float* part, int nblk, int C, const float* gamma, const float* beta,
+                        float* running_mean, float* running_var, float momentum, float eps,
+                        float* save_mean, float* save_invstd, float* scale, float* shift, void* stream);
+
+/* ---- fused first layer (bf16): Conv2d(3,64,3,pad 1) of vgg16_bn.features[0]
+ * (models/models.py:35-36) read straight from the NCHW f32 image (no im2col buffer).
+ * dg_stem_fwd: z[N,H,W,64] (pixel stride ldz, bf16) = conv + bias, and the BN statistics
+ * partials part[dg_stem_part_rows][3][64] for dg_bn_part_finalize.  wpack: bf16 [64][32]
+ * (dg_pack_weight Cpad=3, row_len=32: k = (r*3+s)*3+c).  N*H*W % 64 == 0.
+ * dg_stem_bwd: dW [64][3][3][3] f32 (torch layout) of the conv from the BN+ReLU
+ * backward (g = dL/dy, z, the forward statistics and dg_bn_bwd_coef's coef), dz never
+ * materialised. */
+int64_t dg_stem_part_rows(int N, int H, int W);
+int dg_stem_fwd(const float* img, int N, int H, int W, const void* wpack, const float* bias,
+                void* z, int64_t ldz, float* part, void* stream);
+int64_t dg_stem_bwd_workspace(int N, int H, int W);
+int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
+                int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
+                const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,
+                int accumulate, void* stream);
+
 /* ---- ResNet bottleneck joins and InstanceNorm (IBN-b / ISW / SW trunks) --------
  * Residual join out = act(bn3(z1) + bn_ds(z2) | z2) of Bottleneck.forward
  * (models/ibnnet/resnet_ibn.py:96-107, models/ISW/Resnet.py:187-216,
