@@ -218,9 +218,11 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
   const int half = lane >> 5, xq = lane & 31;
   for (int r = 28 + half; r < 32; r += 2) *(unsigned short*)(CT + r * 64 + xq * 2) = 0;
 
-  u4v gr[4], zr[4];
-  float cv[14];
-  auto gload = [&](long long seg) {
+  struct Regs {
+    u4v gr[4], zr[4];
+    float cv[14];
+  };
+  auto gload = [&](Regs& R, long long seg) {
     const int row_id = (int)(seg / spr);
     const int q0 = (int)(seg - (long long)row_id * spr) * 32;
     const int n = row_id / H, p = row_id - n * H;
@@ -228,8 +230,8 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const long long m = m0 + (lane >> 3) + 8 * u;
-      gr[u] = *(const u4v*)(g + m * ldg + c0);
-      zr[u] = *(const u4v*)(z + m * ldz + c0);
+      R.gr[u] = *(const u4v*)(g + m * ldg + c0);
+      R.zr[u] = *(const u4v*)(z + m * ldz + c0);
     }
 #pragma unroll
     for (int i = 0; i < 14; ++i) {
@@ -237,24 +239,21 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
       const int t = k / 3, c = k - 3 * t, r = t / 3, s2 = t - 3 * r;
       const int pr = p + r - 1, qq = q0 + xq + s2 - 1;
       const bool in = k < 27 && (unsigned)pr < (unsigned)H && (unsigned)qq < (unsigned)W;
-      cv[i] = in ? img[((long long)(n * 3 + c) * H + pr) * W + qq] : 0.f;
+      R.cv[i] = in ? img[((long long)(n * 3 + c) * H + pr) * W + qq] : 0.f;
     }
   };
   f4v acc[4][2];
 #pragma unroll
   for (int cf = 0; cf < 4; ++cf) acc[cf][0] = acc[cf][1] = f4v{0.f, 0.f, 0.f, 0.f};
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3, li = lane & 15;
-  long long seg = (long long)blockIdx.x * 4 + wid;
-  const long long sstride = (long long)gridDim.x * 4;
-  if (seg < nseg) gload(seg);
-  for (; seg < nseg; seg += sstride) {
+  auto process = [&](const Regs& R) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float gv[8], zv[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        gv[2 * i] = __uint_as_float(gr[u][i] << 16); gv[2 * i + 1] = __uint_as_float(gr[u][i] & 0xffff0000u);
-        zv[2 * i] = __uint_as_float(zr[u][i] << 16); zv[2 * i + 1] = __uint_as_float(zr[u][i] & 0xffff0000u);
+        gv[2 * i] = __uint_as_float(R.gr[u][i] << 16); gv[2 * i + 1] = __uint_as_float(R.gr[u][i] & 0xffff0000u);
+        zv[2 * i] = __uint_as_float(R.zr[u][i] << 16); zv[2 * i + 1] = __uint_as_float(R.zr[u][i] & 0xffff0000u);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {  // bn_bwd_load + bn_bwd_apply of norm.hip (act = relu, no dropout)
@@ -267,9 +266,8 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
           u4v{pack_bf2(gv[0], gv[1]), pack_bf2(gv[2], gv[3]), pack_bf2(gv[4], gv[5]), pack_bf2(gv[6], gv[7])};
     }
 #pragma unroll
-    for (int i = 0; i < 14; ++i) *(unsigned short*)(CT + (2 * i + half) * 64 + xq * 2) = bfbits(cv[i]);
+    for (int i = 0; i < 14; ++i) *(unsigned short*)(CT + (2 * i + half) * 64 + xq * 2) = bfbits(R.cv[i]);
     lds_fence();
-    if (seg + sstride < nseg) gload(seg + sstride);
     // A = dz^T (transposed reads): logical k = 8*gq + j <-> pixel 4*gq + (j&3) + 16*(j>>2)
     s8v bfv[2];
 #pragma unroll
@@ -287,6 +285,19 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
 #pragma unroll
       for (int kf = 0; kf < 2; ++kf) acc[cf][kf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[kf], acc[cf][kf], 0, 0, 0);
     }
+  };
+  // two register sets: segment i+1's loads are issued before segment i is processed
+  Regs RA, RB;
+  long long seg = (long long)blockIdx.x * 4 + wid;
+  const long long sstride = (long long)gridDim.x * 4;
+  if (seg < nseg) gload(RA, seg);
+  for (; seg < nseg; seg += 2 * sstride) {
+    const long long s1 = seg + sstride;
+    if (s1 < nseg) gload(RB, s1);
+    process(RA);
+    if (s1 >= nseg) break;
+    if (s1 + sstride < nseg) gload(RA, s1 + sstride);
+    process(RB);
   }
   // combine the 4 waves in a fixed order (deterministic), then one slab row per block
   __syncthreads();
