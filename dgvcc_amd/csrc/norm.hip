@@ -287,6 +287,206 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const T* __restrict__ g, long
   }
 }
 
+// ---------------------------------------------------------------------------
+// BN(+ReLU) fused with the following MaxPool2d(2, 2) (vgg16_bn.features[5:7],
+// [12:14], [22:24], [32:34]; models/models.py:35-38).  One thread = one pooled
+// pixel x one 16-B channel chunk; the 2x2 window's four z vectors give the four
+// activations y_k = rnd(act(z*scale + shift) * drop) exactly as bn_apply_kernel
+// stores them, and the pooled value is their first-max (ATen scan order, NaN
+// propagates).  The backward recomputes the same y_k to route the pooled
+// gradient to the window's argmax, so neither y nor the full-resolution
+// gradient of y is ever materialised (only a direct full-resolution gradient,
+// when y also feeds another consumer, e.g. x1/x2 into the decoder concats).
+// ---------------------------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ float rnd_t(float v) { return to_f(from_f<T>(v)); }
+
+__device__ __forceinline__ void pool_window(long long pp, int H, int W, long long pos[4]) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int wo = (int)(pp % Wo);
+  const long long t = pp / Wo;
+  const int ho = (int)(t % Ho);
+  const long long n = t / Ho;
+  const long long p00 = (n * H + 2 * ho) * W + 2 * wo;
+  pos[0] = p00; pos[1] = p00 + 1; pos[2] = p00 + W; pos[3] = p00 + W + 1;
+}
+
+// first max of the four window values (same rule as resample.hip argmax4)
+__device__ __forceinline__ int first_max4(float a, float b, float c, float d) {
+  int k = 0;
+  float m = a;
+  if (b > m || isnan(b)) { m = b; k = 1; }
+  if (c > m || isnan(c)) { m = c; k = 2; }
+  if (d > m || isnan(d)) { m = d; k = 3; }
+  return k;
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__ z, long long ldz, int H, int W,
+                                                           long long Mp, int C, const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int act,
+                                                           const float* __restrict__ drop, int HW, T* __restrict__ y,
+                                                           long long ldy, T* __restrict__ yp, long long ldyp) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const int c0 = (int)(gt % tpp) * V;
+  const long long pstride = (long long)gridDim.x * NT / tpp;
+  float sc[V], sf[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
+  for (long long pp = gt / tpp; pp < Mp; pp += pstride) {
+    long long pos[4];
+    pool_window(pp, H, W, pos);
+    float v[4][V];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ldv(z + pos[k] * ldz + c0, v[k]);
+    const float* d = drop ? drop + (pos[0] / HW) * C + c0 : nullptr;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        float t = fmaf(v[k][e], sc[e], sf[e]);
+        if (act == 1) t = t > 0.f ? t : 0.f;
+        if (d) t *= d[e];
+        v[k][e] = rnd_t<T>(t);
+      }
+      if (y) stv(y + pos[k] * ldy + c0, v[k]);
+    }
+    float o[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = v[first_max4(v[0][e], v[1][e], v[2][e], v[3][e])][e];
+    stv(yp + pp * ldyp + c0, o);
+  }
+}
+
+// Upstream gradient of the BN output at the window's four pixels: the pooled
+// gradient at the recomputed argmax (+ the direct gradient gd), times drop,
+// zeroed where the ReLU was inactive (bn_bwd_load's rule).
+template <typename T, int V>
+__device__ __forceinline__ void bn_pool_bwd_load(const T* gp, long long ldgp, const T* gd, long long ldgd, const T* z,
+                                                 long long ldz, long long pp, const long long pos[4], int c0, int C,
+                                                 const ChanParams<V>& cp, int act, const float* drop, int HW,
+                                                 float gv[4][V], float zv[4][V]) {
+  float gpv[V];
+  ldv(gp + pp * ldgp + c0, gpv);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    ldv(z + pos[k] * ldz + c0, zv[k]);
+    if (gd) ldv(gd + pos[k] * ldgd + c0, gv[k]);
+    else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) gv[k][e] = 0.f;
+    }
+  }
+  const float* d = drop ? drop + (pos[0] / HW) * C + c0 : nullptr;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    float y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float t = fmaf(zv[k][e], cp.sc[e], cp.sf[e]);
+      if (act == 1) t = t > 0.f ? t : 0.f;
+      if (d) t *= d[e];
+      y[k] = rnd_t<T>(t);
+    }
+    const int am = first_max4(y[0], y[1], y[2], y[3]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k == am) gv[k][e] += gpv[e];
+      if (d) gv[k][e] *= d[e];
+      if (act == 1 && !(fmaf(zv[k][e], cp.sc[e], cp.sf[e]) > 0.f)) gv[k][e] = 0.f;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ gp, long long ldgp,
+                                                          const T* __restrict__ gd, long long ldgd,
+                                                          const T* __restrict__ z, long long ldz, int H, int W,
+                                                          long long Mp, int C, long long ppb, const float* mean,
+                                                          const float* invstd, const float* scale, const float* shift,
+                                                          int act, const float* drop, int HW, float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[3][NT * V];
+  const int tpp = C / V;
+  const int rows = NT / tpp;
+  const int tid = threadIdx.x;
+  const int ch = tid % tpp, pl = tid / tpp;
+  const int c0 = ch * V;
+  float sg[V], sgx[V], sx[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { sg[e] = 0.f; sgx[e] = 0.f; sx[e] = 0.f; }
+  const long long p0 = blockIdx.x * ppb, p1 = min(Mp, p0 + ppb);
+  if (pl < rows) {
+    ChanParams<V> cp;
+    cp.load(c0, scale, shift, mean, invstd);
+    for (long long pp = p0 + pl; pp < p1; pp += rows) {
+      long long pos[4];
+      pool_window(pp, H, W, pos);
+      float gv[4][V], zv[4][V];
+      bn_pool_bwd_load<T, V>(gp, ldgp, gd, ldgd, z, ldz, pp, pos, c0, C, cp, act, drop, HW, gv, zv);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float xh = (zv[k][e] - cp.mu[e]) * cp.is[e];
+          sg[e] += gv[k][e];
+          sgx[e] = fmaf(gv[k][e], xh, sgx[e]);
+          sx[e] += xh;
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      sh[0][pl * C + c0 + e] = sg[e];
+      sh[1][pl * C + c0 + e] = sgx[e];
+      sh[2][pl * C + c0 + e] = sx[e];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f, d = 0.f;
+    for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; d += sh[2][r * C + c]; }
+    float* o = part + (long long)blockIdx.x * 3 * C;
+    o[c] = a; o[C + c] = b; o[2 * C + c] = d;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp, long long ldgp,
+                                                        const T* __restrict__ gd, long long ldgd,
+                                                        const T* __restrict__ z, long long ldz, int H, int W,
+                                                        long long Mp, int C, const float* mean, const float* invstd,
+                                                        const float* scale, const float* shift, int act,
+                                                        const float* drop, int HW, const float* __restrict__ coef,
+                                                        T* __restrict__ dz, long long lddz) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const int c0 = (int)(gt % tpp) * V;
+  const long long pstride = (long long)gridDim.x * NT / tpp;
+  ChanParams<V> cp;
+  cp.load(c0, scale, shift, mean, invstd);
+  float k1[V], k2[V], k3[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { k1[e] = coef[c0 + e]; k2[e] = coef[C + c0 + e]; k3[e] = coef[2 * C + c0 + e]; }
+  for (long long pp = gt / tpp; pp < Mp; pp += pstride) {
+    long long pos[4];
+    pool_window(pp, H, W, pos);
+    float gv[4][V], zv[4][V];
+    bn_pool_bwd_load<T, V>(gp, ldgp, gd, ldgd, z, ldz, pp, pos, c0, C, cp, act, drop, HW, gv, zv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float xh = (zv[k][e] - cp.mu[e]) * cp.is[e];
+        gv[k][e] = k1[e] * gv[k][e] - k2[e] * xh - k3[e];
+      }
+      stv(dz + pos[k] * lddz + c0, gv[k]);
+    }
+  }
+}
+
 inline int ew_grid(long long n) {
   long long g = (n + NT - 1) / NT;
   return (int)std::max<long long>(1, std::min<long long>(g, 8192));
@@ -406,4 +606,68 @@ extern "C" int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void*
                                  nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef)
              : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
                                   nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef);
+}
+
+extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, int H, int W, int C,
+                                const float* scale, const float* shift, int act, const float* drop, void* y,
+                                int64_t ldy, void* yp, int64_t ldyp, void* stream) {
+  DG_REQUIRE(z && yp && scale && shift && N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
+  DG_REQUIRE(ldz >= C && ldyp >= C && (!y || ldy >= C));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, ldyp) &&
+               (!y || BN_SHAPE_OK(dtype, C, ldy)));
+  hipStream_t st = (hipStream_t)stream;
+  const long long Mp = (long long)N * (H / 2) * (W / 2);
+  const long long total = Mp * (C / (dtype == DG_BF16 ? 8 : 4));
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_apply_pool_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, H, W,
+                       Mp, C, scale, shift, act, drop, H * W, (bf16*)y, ldy, (bf16*)yp, ldyp);
+  else
+    hipLaunchKernelGGL(bn_apply_pool_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, H,
+                       W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+template <typename T>
+static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long long ldgd, const void* z,
+                            long long ldz, int N, int H, int W, int C, const float* gamma, const float* mean,
+                            const float* inv, const float* scale, const float* shift, int act, const float* drop,
+                            void* dz, long long lddz, float* dgamma, float* dbeta, float* dbias, void* ws,
+                            hipStream_t st) {
+  const long long M = (long long)N * H * W, Mp = M / 4;
+  const int nblk = bn_nblk((int)Mp);
+  const long long ppb = (Mp + nblk - 1) / nblk;
+  float* part = (float*)ws;
+  float* coef = part + (long long)nblk * 3 * C;
+  hipLaunchKernelGGL(bn_pool_bwd_partial<T>, dim3(nblk), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd, ldgd,
+                     (const T*)z, ldz, H, W, Mp, C, ppb, mean, inv, scale, shift, act, drop, H * W, part);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, (int)M, C, gamma, inv,
+                     dgamma, dbeta, dbias, coef);
+  DG_CHECK_LAUNCH();
+  const long long total = Mp * (C / (16 / (int)sizeof(T)));
+  hipLaunchKernelGGL(bn_pool_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd,
+                     ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop, H * W, coef, (T*)dz,
+                     lddz);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd, const void* z,
+                              int64_t ldz, int N, int H, int W, int C, const float* gamma, const float* save_mean,
+                              const float* save_invstd, const float* scale, const float* shift, int act,
+                              const float* drop, void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
+                              void* workspace, void* stream) {
+  DG_REQUIRE(gp && z && dz && workspace && save_mean && save_invstd && scale && shift);
+  DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldgp) &&
+               BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz) && (!gd || BN_SHAPE_OK(dtype, C, ldgd)));
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16
+             ? bn_pool_bwd_impl<bf16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
+                                      shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st)
+             : bn_pool_bwd_impl<float>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
+                                       shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st);
 }

@@ -65,11 +65,13 @@ class ConvLayer:
     def stem_shape_ok(W: int) -> bool:  # row segments of 64 pixels (dg_stem_fwd)
         return W % 64 == 0
 
-    def forward(self, x, out: Act, training: bool, tape: dict | None,
-                drop: torch.Tensor | None = None):
-        """x: NHWC Act, or for the fused bf16 stem the NCHW f32 image itself."""
+    def forward(self, x, out: Act | None, training: bool, tape: dict | None,
+                drop: torch.Tensor | None = None, pool: Act | None = None):
+        """x: NHWC Act, or for the fused bf16 stem the NCHW f32 image itself.
+        pool: also apply the following MaxPool2d(2,2) into `pool` (BN/ReLU/pool in one pass);
+        `out` (the un-pooled activation) may then be None when nothing else reads it."""
         stem = isinstance(x, torch.Tensor)
-        dt = out.buf.dtype
+        dt = (out if out is not None else pool).buf.dtype
         bias = self.conv.bias.detach() if self.conv.bias is not None else None
         bn = self.bn
         if stem:
@@ -84,7 +86,7 @@ class ConvLayer:
             else:
                 stats = K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                                         bn.running_var, bn.eps)
-            K.bn_apply(z, stats, self.act, out, drop)
+            self._apply(z, stats, out, drop, pool)
             if tape is not None:
                 tape[self] = (x, z, stats, wp, drop, training)
             return
@@ -107,11 +109,20 @@ class ConvLayer:
             stats = torch.zeros((4, C), dtype=torch.float32, device=x.buf.device)
             stats[1].fill_(1.0)
             stats[2].fill_(1.0)
-        K.bn_apply(z, stats, self.act, out, drop)
+        self._apply(z, stats, out, drop, pool)
         if tape is not None:
             tape[self] = (x, z, stats, wp, drop, training)
 
-    def backward(self, tape: dict, g: Act, gx: Act | None, accumulate_gx: bool = False) -> dict:
+    def _apply(self, z: Act, stats, out: Act | None, drop, pool: Act | None):
+        if pool is not None:
+            K.bn_apply_pool(z, stats, self.act, out, pool, drop)
+        else:
+            K.bn_apply(z, stats, self.act, out, drop)
+
+    def backward(self, tape: dict, g: Act | None, gx: Act | None, accumulate_gx: bool = False,
+                 g_pool: Act | None = None) -> dict:
+        """g: gradient of the layer output (None if only the pooled output was used);
+        g_pool: gradient of the pooled output when the forward ran with `pool`."""
         x, z, stats, wp, drop, training = tape.pop(self)
         if self.bn is not None and not training:
             raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
@@ -130,8 +141,13 @@ class ConvLayer:
             if self.conv.bias is not None:
                 grads[self.conv.bias] = dbias
             return grads
-        K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta,
-                 dbias, drop)
+        if g_pool is not None:
+            if self.bn is None:
+                raise RuntimeError("pooled backward needs a BatchNorm layer")
+            K.bn_bwd_pool(g_pool, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
+        else:
+            K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta,
+                     dbias, drop)
         dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
         if self.first:
             dwcol = torch.empty((self.Cout, 64, 1, 1), dtype=torch.float32, device=dev)
@@ -181,21 +197,21 @@ class FeaturePlan:
             E[0].forward(img.float().contiguous(), a, training, tape)
         else:
             E[0].forward(Act(K.im2col_c3(img.float(), dt)), a, training, tape)
-        b = nh(H, W, 64); E[1].forward(a, b, training, tape)
-        p1 = nh(H // 2, W // 2, 64); K.maxpool_fwd(b, p1)
+        # conv -> BN -> ReLU -> MaxPool run as conv + one BN/ReLU/pool pass (the un-pooled
+        # activation is written only where the decoder also reads it: x1, x2)
+        p1 = nh(H // 2, W // 2, 64); E[1].forward(a, None, training, tape, pool=p1)
         a2 = nh(H // 2, W // 2, 128); E[2].forward(p1, a2, training, tape)
-        b2 = nh(H // 2, W // 2, 128); E[3].forward(a2, b2, training, tape)
-        p2 = nh(H // 4, W // 4, 128); K.maxpool_fwd(b2, p2)
+        p2 = nh(H // 4, W // 4, 128); E[3].forward(a2, None, training, tape, pool=p2)
         a4 = nh(H // 4, W // 4, 256); E[4].forward(p2, a4, training, tape)
         a5 = nh(H // 4, W // 4, 256); E[5].forward(a4, a5, training, tape)
         dec1in = K.nhwc(N, H // 4, W // 4, 512, dt, dev)
-        x1 = Act(dec1in, 256, 256); E[6].forward(a5, x1, training, tape)
-        p3 = nh(H // 8, W // 8, 256); K.maxpool_fwd(x1, p3)
+        x1 = Act(dec1in, 256, 256)
+        p3 = nh(H // 8, W // 8, 256); E[6].forward(a5, x1, training, tape, pool=p3)
         a7 = nh(H // 8, W // 8, 512); E[7].forward(p3, a7, training, tape)
         a8 = nh(H // 8, W // 8, 512); E[8].forward(a7, a8, training, tape)
         dec2in = K.nhwc(N, H // 8, W // 8, 1024, dt, dev)
-        x2 = Act(dec2in, 512, 512); E[9].forward(a8, x2, training, tape)
-        p4 = nh(H // 16, W // 16, 512); K.maxpool_fwd(x2, p4)
+        x2 = Act(dec2in, 512, 512)
+        p4 = nh(H // 16, W // 16, 512); E[9].forward(a8, x2, training, tape, pool=p4)
         a10 = nh(H // 16, W // 16, 512); E[10].forward(p4, a10, training, tape)
         a11 = nh(H // 16, W // 16, 512); E[11].forward(a10, a11, training, tape)
         x3 = nh(H // 16, W // 16, 512); E[12].forward(a11, x3, training, tape)
@@ -212,8 +228,7 @@ class FeaturePlan:
         a17 = nh(H // 4, W // 4, 256); D[4].forward(Act(dec1in), a17, training, tape)
         D[5].forward(a17, Act(ycat, 0, 128), training, tape)
         if tape is not None:
-            tape[self] = dict(b=b, b2=b2, x1=x1, x2=x2, dec1in=dec1in, dec2in=dec2in,
-                              shape=(N, H, W), dt=dt)
+            tape[self] = dict(dec1in=dec1in, dec2in=dec2in, shape=(N, H, W), dt=dt)
         return ycat, x3.buf
 
     def backward(self, tape: dict, g_ycat: torch.Tensor, g_x3: torch.Tensor | None) -> dict:
@@ -251,21 +266,19 @@ class FeaturePlan:
         g_a11 = nh(H // 16, W // 16, 512); grads.update(E[12].backward(tape, gx3, g_a11))
         g_a10 = nh(H // 16, W // 16, 512); grads.update(E[11].backward(tape, g_a11, g_a10))
         g_p4 = nh(H // 16, W // 16, 512); grads.update(E[10].backward(tape, g_a10, g_p4))
-        K.maxpool_bwd(s["x2"], g_p4, Act(g_dec2in, 512, 512), accumulate=True)
-        # enc2
-        g_a8 = nh(H // 8, W // 8, 512); grads.update(E[9].backward(tape, Act(g_dec2in, 512, 512), g_a8))
+        # enc2 (the pooled gradients are routed inside the BN backward of the pooled layers)
+        g_a8 = nh(H // 8, W // 8, 512)
+        grads.update(E[9].backward(tape, Act(g_dec2in, 512, 512), g_a8, g_pool=g_p4))
         g_a7 = nh(H // 8, W // 8, 512); grads.update(E[8].backward(tape, g_a8, g_a7))
         g_p3 = nh(H // 8, W // 8, 256); grads.update(E[7].backward(tape, g_a7, g_p3))
-        K.maxpool_bwd(s["x1"], g_p3, Act(g_dec1in, 256, 256), accumulate=True)
         # enc1
-        g_a5 = nh(H // 4, W // 4, 256); grads.update(E[6].backward(tape, Act(g_dec1in, 256, 256), g_a5))
+        g_a5 = nh(H // 4, W // 4, 256)
+        grads.update(E[6].backward(tape, Act(g_dec1in, 256, 256), g_a5, g_pool=g_p3))
         g_a4 = nh(H // 4, W // 4, 256); grads.update(E[5].backward(tape, g_a5, g_a4))
         g_p2 = nh(H // 4, W // 4, 128); grads.update(E[4].backward(tape, g_a4, g_p2))
-        g_b2 = nh(H // 2, W // 2, 128); K.maxpool_bwd(s["b2"], g_p2, g_b2)
-        g_a2 = nh(H // 2, W // 2, 128); grads.update(E[3].backward(tape, g_b2, g_a2))
+        g_a2 = nh(H // 2, W // 2, 128); grads.update(E[3].backward(tape, None, g_a2, g_pool=g_p2))
         g_p1 = nh(H // 2, W // 2, 64); grads.update(E[2].backward(tape, g_a2, g_p1))
-        g_b = nh(H, W, 64); K.maxpool_bwd(s["b"], g_p1, g_b)
-        g_a = nh(H, W, 64); grads.update(E[1].backward(tape, g_b, g_a))
+        g_a = nh(H, W, 64); grads.update(E[1].backward(tape, None, g_a, g_pool=g_p1))
         grads.update(E[0].backward(tape, g_a, None))
         return (), grads
 

@@ -217,6 +217,24 @@ def bn_bwd(g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), stream())
 
 
+def bn_apply_pool(z: Act, stats, act: int, y: Act | None, yp: Act, drop: torch.Tensor | None = None):
+    """y = act(BN(z)) [* drop] (only written when y is given) and yp = maxpool2x2(y)."""
+    call("dg_bn_apply_pool", z.dt, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(stats[2]), ptr(stats[3]), act,
+         ptr(drop), y.ptr if y is not None else None, y.ld if y is not None else 0, yp.ptr, yp.ld, stream())
+
+
+def bn_bwd_pool(gp: Act, gd: Act | None, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta,
+                dbias=None, drop: torch.Tensor | None = None):
+    """BN backward with the upstream gradient = maxpool2x2 backward of gp (argmax recomputed
+    from z) [+ the direct gradient gd]."""
+    ws = query("dg_bn_workspace", z.M, z.C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
+    call("dg_bn_bwd_pool", z.dt, gp.ptr, gp.ld, gd.ptr if gd is not None else None,
+         gd.ld if gd is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(gamma), ptr(stats[0]),
+         ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), dz.ptr, dz.ld, ptr(dgamma),
+         ptr(dbeta), ptr(dbias), ptr(work), stream())
+
+
 # ---------------------------------------------------------------- resample -
 def maxpool_fwd(x: Act, y: Act):
     call("dg_maxpool2_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, y.ptr, y.ld, stream())

@@ -126,6 +126,21 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
               void* workspace, void* stream);
 
+/* BN(+ReLU) fused with the following MaxPool2d(2,2) (vgg16_bn.features[5:7] etc.,
+ * models/models.py:35-38).  Apply: y = act(z*scale+shift)*drop (written only when y != NULL,
+ * e.g. x1/x2 that also feed the decoder) and yp [N,H/2,W/2,C] = first-max of each 2x2 window
+ * of y (ATen rule).  Backward: gp = dL/dyp, gd = direct dL/dy (NULL = none); the pooled
+ * gradient is routed to the recomputed argmax, then the BN/ReLU backward as dg_bn_bwd.
+ * H, W even; workspace of dg_bn_workspace(N*H*W, C) bytes. */
+int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, int H, int W, int C,
+                     const float* scale, const float* shift, int act, const float* drop, void* y,
+                     int64_t ldy, void* yp, int64_t ldyp, void* stream);
+int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
+                   const void* z, int64_t ldz, int N, int H, int W, int C, const float* gamma,
+                   const float* save_mean, const float* save_invstd, const float* scale,
+                   const float* shift, int act, const float* drop, void* dz, int64_t lddz,
+                   float* dgamma, float* dbeta, float* dbias, void* workspace, void* stream);
+
 /* Coefficients of the BN backward without the dz pass: coef[3][C] = (k1, k2, k3) with
  * dz = k1*act'(g) - k2*xhat - k3 (the bn_bwd_apply arithmetic), plus dgamma/dbeta/dbias.
  * For fused consumers (dg_stem_bwd). */

@@ -84,3 +84,64 @@ def test_stem_fwd_bwd(dev, N, H, W):
     wref = torch.nn.grad.conv2d_weight(img.bfloat16().double(), (64, 3, 3, 3), dz64, padding=1)
     assert relerr(dw, wref) < 1e-4
     assert relerr(dw, dw0) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("with_y,with_gd", [(False, False), (True, True)])
+@pytest.mark.parametrize("C,H,W", [(64, 8, 12), (256, 6, 4), (512, 4, 8)])
+def test_bn_relu_pool_fused(dev, dtype, with_y, with_gd, C, H, W):
+    """dg_bn_apply_pool / dg_bn_bwd_pool vs the unfused BN apply + maxpool (+ their backward),
+    and vs float64 autograd of BatchNorm2d(train) -> ReLU -> MaxPool2d(2,2) in f32."""
+    K = _k()
+    N = 2
+    g = torch.Generator().manual_seed(3)
+    z = torch.randn(N, C, H, W, generator=g)
+    z[:, :, :, 1::2] = z[:, :, :, 0::2]  # exact ties inside the pooling windows
+    gam = torch.rand(C, generator=g) + 0.5
+    bet = torch.randn(C, generator=g) * 0.2
+    gp = torch.randn(N, C, H // 2, W // 2, generator=g)
+    gd = torch.randn(N, C, H, W, generator=g) if with_gd else None
+    if dtype == torch.bfloat16:
+        z, gp = z.bfloat16().float(), gp.bfloat16().float()
+        gd = gd.bfloat16().float() if gd is not None else None
+    zd = K.Act(to_nhwc(z).to(dev, dtype))
+    stats = K.bn_fwd_train(zd, gam.to(dev), bet.to(dev), torch.zeros(C, device=dev),
+                           torch.ones(C, device=dev), 0.1, 1e-5)
+    # fused
+    y = K.Act(K.nhwc(N, H, W, C, dtype, dev)) if with_y else None
+    yp = K.Act(K.nhwc(N, H // 2, W // 2, C, dtype, dev))
+    K.bn_apply_pool(zd, stats, 1, y, yp)
+    gpd = K.Act(to_nhwc(gp).to(dev, dtype))
+    gdd = K.Act(to_nhwc(gd).to(dev, dtype)) if gd is not None else None
+    dz = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    dg, db = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    K.bn_bwd_pool(gpd, gdd, zd, gam.to(dev), stats, 1, dz, dg, db)
+    # unfused
+    y0 = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    K.bn_apply(zd, stats, 1, y0)
+    yp0 = K.Act(K.nhwc(N, H // 2, W // 2, C, dtype, dev))
+    K.maxpool_fwd(y0, yp0)
+    gy0 = K.Act(gdd.buf.clone()) if gdd is not None else K.Act(K.nhwc(N, H, W, C, dtype, dev, zero=True))
+    K.maxpool_bwd(y0, gpd, gy0, accumulate=True)
+    dz0 = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    dg0, db0 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    K.bn_bwd(gy0, zd, gam.to(dev), stats, 1, dz0, dg0, db0)
+    torch.cuda.synchronize()
+    assert torch.equal(yp.buf, yp0.buf)
+    if with_y:
+        assert torch.equal(y.buf, y0.buf)
+    # bf16 with a direct gradient: the unfused route rounds gd + routed gp to bf16 before the BN
+    # backward, the fused one adds them in f32
+    tol = 1e-5 if (dtype == torch.float32 or not with_gd) else 1e-2
+    assert relerr(dg, dg0) < tol and relerr(db, db0) < tol
+    assert relerr(dz.buf, dz0.buf) < (1e-5 if dtype == torch.float32 else 1e-2)
+    if dtype == torch.float32:  # float64 autograd reference
+        zr = z.double().requires_grad_()
+        gr, br = gam.double().requires_grad_(), bet.double().requires_grad_()
+        a = F.relu(F.batch_norm(zr, None, None, gr, br, training=True, eps=1e-5))
+        out = F.max_pool2d(a, 2)
+        loss = (out * gp.double()).sum() + ((a * gd.double()).sum() if gd is not None else 0.0)
+        loss.backward()
+        assert relerr(yp.buf.permute(0, 3, 1, 2), out.detach()) < 1e-5
+        assert relerr(dz.buf.permute(0, 3, 1, 2), zr.grad) < 1e-4
+        assert relerr(dg, gr.grad) < 1e-4 and relerr(db, br.grad) < 1e-4
