@@ -893,8 +893,16 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
     const long long t = o / C;
     const int rs = (int)(t % RS);
     const int co = (int)(t / RS);
-    float sum = 0.f;
-    for (int sp = 0; sp < splits; ++sp) sum += slab[(long long)sp * Cout * ldk + o];
+    // 8 independent loads in flight per thread (fixed pairing order: deterministic)
+    const long long sstr = (long long)Cout * ldk;
+    float acc8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int sp = 0;
+    for (; sp + 8 <= splits; sp += 8) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc8[u] += slab[(long long)(sp + u) * sstr + o];
+    }
+    for (int u = 0; sp < splits; ++sp, ++u) acc8[u] += slab[(long long)sp * sstr + o];
+    const float sum = ((acc8[0] + acc8[1]) + (acc8[2] + acc8[3])) + ((acc8[4] + acc8[5]) + (acc8[6] + acc8[7]));
     float* d = dw + ((long long)co * C + c) * RS + rs;
     *d = accumulate ? *d + sum : sum;
   }

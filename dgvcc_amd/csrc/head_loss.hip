@@ -109,13 +109,22 @@ __global__ __launch_bounds__(NT) void head_bwd_kernel(const T* __restrict__ x, l
   }
 }
 
-__global__ void colsum_kernel(const float* __restrict__ part, int nblk, int ncol, float* out0, int n0, float* out1) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= ncol) return;
+// One block per column: 256 threads stride the rows, then a fixed-order tree (deterministic).
+__global__ __launch_bounds__(NT) void colsum_kernel(const float* __restrict__ part, int nblk, int ncol, float* out0,
+                                                    int n0, float* out1) {
+  __shared__ double sh[NT];
+  const int c = blockIdx.x;
   double a = 0.0;
-  for (int k = 0; k < nblk; ++k) a += part[(long long)k * ncol + c];
-  if (c < n0) out0[c] = (float)a;
-  else if (out1) out1[c - n0] = (float)a;
+  for (int k = threadIdx.x; k < nblk; k += NT) a += part[(long long)k * ncol + c];
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = NT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  if (c < n0) out0[c] = (float)sh[0];
+  else if (out1) out1[c - n0] = (float)sh[0];
 }
 
 inline int head_nblk(int M) { return std::max(1, std::min(1024, dg_cdiv(M, 64))); }
@@ -390,7 +399,7 @@ extern "C" int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, 
     hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(nblk), dim3(NT), 0, st, (const float*)x, ldx, M, C, w, act, y, gy,
                        (float*)gx, ldgx, accumulate_gx, ppb, part);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_kernel, dim3(dg_cdiv(C + 1, 256)), dim3(256), 0, st, part, nblk, C + 1, gw, C, gbias);
+  hipLaunchKernelGGL(colsum_kernel, dim3(C + 1), dim3(NT), 0, st, part, nblk, C + 1, gw, C, gbias);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

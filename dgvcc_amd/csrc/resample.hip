@@ -323,6 +323,107 @@ __global__ __launch_bounds__(NT) void upsample_bwd_kernel(const T* __restrict__ 
   }
 }
 
+// den_dec of the DGModel family on the decomposed decoder concatenation
+// (models/models.py:84, 89-90):
+//   conv1x1(cat[y1, up2(y2), up4(y3)]) = conv1x1(y1; W1) + up2(conv1x1(y2; W2)) + up4(conv1x1(y3; W3))
+// since bilinear resampling acts on pixels and the 1x1 conv on channels (both linear).
+// z = z1 + up2(z2) + up4(z3) + bias (bilinear, align_corners=False, as upsample_fwd_kernel),
+// stored in T, plus the BN statistics partials (n, mean, M2) of the stored values per block
+// (per-block shift = the block's first pixel, recomputed by every thread).
+template <typename T>
+__device__ __forceinline__ void cat_combine_px(const T* z1, long long ldz1, const T* z2, long long ldz2, const T* z3,
+                                               long long ldz3, int H, int W, long long p, int c0, const float* bias,
+                                               float o[16 / sizeof(T)]) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int HW = H * W;  // N*H*W < 2^31 (checked by the ABI)
+  const int n = (int)p / HW;
+  const int rem = (int)p - n * HW;
+  const int ho = rem / W, wo = rem - ho * W;
+  ldv(z1 + p * ldz1 + c0, o);
+#pragma unroll
+  for (int lv = 0; lv < 2; ++lv) {
+    const int sc = lv == 0 ? 2 : 4, h = H / sc, w = W / sc;
+    const T* zz = lv == 0 ? z2 : z3;
+    const long long ld = lv == 0 ? ldz2 : ldz3;
+    const Tap th = src_tap(ho, h, H, sc, 0), tw = src_tap(wo, w, W, sc, 0);
+    const float h1l = th.l1, h0l = 1.f - th.l1, w1l = tw.l1, w0l = 1.f - tw.l1;
+    const T* base = zz + (long long)n * h * w * ld + c0;
+    float a[V], b[V], c[V], d[V];
+    ldv(base + ((long long)th.i0 * w + tw.i0) * ld, a);
+    ldv(base + ((long long)th.i0 * w + tw.i1) * ld, b);
+    ldv(base + ((long long)th.i1 * w + tw.i0) * ld, c);
+    ldv(base + ((long long)th.i1 * w + tw.i1) * ld, d);
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] += h0l * (w0l * a[e] + w1l * b[e]) + h1l * (w0l * c[e] + w1l * d[e]);
+  }
+  if (bias) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] += bias[c0 + e];
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) o[e] = to_f(from_f<T>(o[e]));  // the stored value
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void cat_combine_kernel(const T* z1, long long ldz1,
+                                                         const T* __restrict__ z2, long long ldz2,
+                                                         const T* __restrict__ z3, long long ldz3, int H, int W,
+                                                         long long M, int C, long long ppb,
+                                                         const float* __restrict__ bias, T* z, long long ldz,
+                                                         float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[2][NT * V];
+  __shared__ float shK[NT * V];
+  const int tpp = C / V;
+  const int rows = NT / tpp;
+  const int tid = threadIdx.x;
+  const int ch = tid % tpp, pl = tid / tpp;
+  const int c0 = ch * V;
+  const long long p0 = blockIdx.x * ppb, p1 = min(M, p0 + ppb);
+  float K[V], s1[V], s2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  // per-channel shift = the block's first pixel, computed before any store (z may alias z1)
+  if (pl == 0 && p0 < p1) {
+    cat_combine_px<T>(z1, ldz1, z2, ldz2, z3, ldz3, H, W, p0, c0, bias, K);
+#pragma unroll
+    for (int e = 0; e < V; ++e) shK[c0 + e] = K[e];
+  }
+  __syncthreads();
+  if (pl < rows && p0 < p1) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) K[e] = shK[c0 + e];
+    for (long long p = p0 + pl; p < p1; p += rows) {
+      float o[V];
+      cat_combine_px<T>(z1, ldz1, z2, ldz2, z3, ldz3, H, W, p, c0, bias, o);
+      stv(z + p * ldz + c0, o);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const float dd = o[e] - K[e];
+        s1[e] += dd;
+        s2[e] = fmaf(dd, dd, s2[e]);
+      }
+    }
+  }
+  if (pl < rows) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) { sh[0][pl * C + c0 + e] = s1[e]; sh[1][pl * C + c0 + e] = s2[e]; }
+  }
+  __syncthreads();
+  if (!part) return;
+  for (int c = tid; c < C; c += NT) {
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; }
+    const float n = (float)max(0LL, p1 - p0);
+    float* out = part + (long long)blockIdx.x * 3 * C;
+    out[c] = n;
+    out[C + c] = n > 0.f ? shK[c] + a / n : 0.f;
+    out[2 * C + c] = n > 0.f ? fmaxf(b - a * a / n, 0.f) : 0.f;
+  }
+}
+
+inline int cat_nblk(long long M) { return (int)std::max(1LL, std::min(1024LL, (M + 63) / 64)); }
+
 template <typename T>
 int up_fwd(const void* x, long long ldx, int N, int H, int W, int C, int scale, int mode, void* y, long long ldy,
            hipStream_t st) {
@@ -447,6 +548,36 @@ extern "C" int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void*
   else
     hipLaunchKernelGGL(maxpool_gen_bwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx,
                        (const float*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (float*)gx, ldgx, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_cat_combine_part_rows(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return DG_ERR_INVALID;
+  return cat_nblk((long long)N * H * W);
+}
+
+extern "C" int dg_cat_combine(int dtype, const void* z1, int64_t ldz1, const void* z2, int64_t ldz2, const void* z3,
+                              int64_t ldz3, int N, int H, int W, int C, const float* bias, void* z, int64_t ldz,
+                              float* part, void* stream) {
+  DG_REQUIRE(z1 && z2 && z3 && z && N > 0 && H > 0 && W > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(H % 4 == 0 && W % 4 == 0 && (long long)N * H * W < (1LL << 31) && C % V == 0 && 256 % (C / V) == 0 &&
+               ldz1 % V == 0 && ldz2 % V == 0 &&
+               ldz3 % V == 0 && ldz % V == 0);
+  const long long M = (long long)N * H * W;
+  const int nblk = cat_nblk(M);
+  const long long ppb = (M + nblk - 1) / nblk;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(cat_combine_kernel<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)z1, (long long)ldz1,
+                       (const bf16*)z2, (long long)ldz2, (const bf16*)z3, (long long)ldz3, H, W, M, C, ppb, bias,
+                       (bf16*)z, (long long)ldz, part);
+  else
+    hipLaunchKernelGGL(cat_combine_kernel<float>, dim3(nblk), dim3(NT), 0, st, (const float*)z1, (long long)ldz1,
+                       (const float*)z2, (long long)ldz2, (const float*)z3, (long long)ldz3, H, W, M, C, ppb, bias,
+                       (float*)z, (long long)ldz, part);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

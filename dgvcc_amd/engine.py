@@ -166,11 +166,140 @@ class ConvLayer:
         return grads
 
 
+class CatParts:
+    """The decoder concatenation y_cat = cat[y1, up2(y2), up4(y3)] (models/models.py:84) kept
+    as its parts (NHWC Acts at their own resolutions) instead of a materialised
+    [N, H/4, W/4, 896] tensor."""
+    SCALES = (1, 2, 4)
+
+    def __init__(self, y1: Act, y2: Act, y3: Act):
+        self.parts = (y1, y2, y3)
+        for p, sc in zip(self.parts, self.SCALES):
+            if (p.H * sc, p.W * sc) != (y1.H, y1.W):
+                raise ValueError("CatParts: part resolutions must be y1, y1/2, y1/4")
+
+    @property
+    def N(self):
+        return self.parts[0].N
+
+    @property
+    def H(self):
+        return self.parts[0].H
+
+    @property
+    def W(self):
+        return self.parts[0].W
+
+    @property
+    def C(self):
+        return sum(p.C for p in self.parts)
+
+    def empty_like(self) -> "CatParts":
+        return CatParts(*(Act(torch.empty(p.N, p.H, p.W, p.C, dtype=p.buf.dtype, device=p.buf.device))
+                          for p in self.parts))
+
+    def tensors(self):
+        return tuple(p.buf for p in self.parts)
+
+
+def as_cat(x):
+    """A head plan's concatenation input: a (y1, y2, y3) tuple of NHWC tensors -> CatParts,
+    or a materialised NHWC y_cat tensor -> Act."""
+    if isinstance(x, (tuple, list)):
+        return CatParts(*(Act(t) for t in x))
+    return Act(x)
+
+
+def cat_empty_like(cat):
+    return cat.empty_like() if isinstance(cat, CatParts) else Act(torch.empty_like(cat.buf))
+
+
+def cat_grads(gcat) -> tuple:
+    return gcat.tensors() if isinstance(gcat, CatParts) else (gcat.buf,)
+
+
+class CatConvLayer(ConvLayer):
+    """den_dec (1x1 Conv + BN + ReLU [+ Dropout2d], models/models.py:55-58) applied to the decoder
+    concatenation.  On CatParts the 1x1 conv runs on each part at the part's own resolution
+    and the bilinear upsampling moves behind it (both are linear):
+        W . cat[y1, up2(y2), up4(y3)] = W1 y1 + up2(W2 y2) + up4(W3 y3),
+    so neither y_cat (896 channels at H/4 x W/4) nor its gradient is ever materialised and the
+    conv FLOPs drop 4x.  One pass (dg_cat_combine) sums the parts and emits the BN partials;
+    the backward downsamples dz once per part (U^T) and runs the per-part dgrad/wgrad."""
+
+    def forward(self, x, out, training, tape, drop=None, pool=None):
+        if not isinstance(x, CatParts):
+            return super().forward(x, out, training, tape, drop=drop, pool=pool)
+        if self.R != 1 or self.bn is None or pool is not None or x.C != self.Cin:
+            raise ValueError("CatConvLayer: decomposed path needs a 1x1 conv with BatchNorm")
+        dt = out.buf.dtype
+        dev = out.buf.device
+        w = self.conv.weight.detach()
+        zs, wps, lo = [], [], 0
+        for part in x.parts:
+            wp = K.pack_weight(w[:, lo:lo + part.C].contiguous(), dt)
+            zk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dt, dev))
+            K.conv_fwd(part, wp, self.Cout, 1, 0, zk)
+            zs.append(zk)
+            wps.append(wp)
+            lo += part.C
+        z = zs[0]
+        bias = self.conv.bias.detach() if self.conv.bias is not None else None
+        rows = K.query("dg_cat_combine_part_rows", z.N, z.H, z.W)
+        part = torch.empty((rows, 3, self.Cout), dtype=torch.float32, device=dev)
+        K.call("dg_cat_combine", z.dt, z.ptr, z.ld, zs[1].ptr, zs[1].ld, zs[2].ptr, zs[2].ld, z.N, z.H, z.W,
+               self.Cout, K.ptr(bias), z.ptr, z.ld, K.ptr(part), K.stream())
+        bn = self.bn
+        if training:
+            bn.num_batches_tracked.add_(1)
+            stats = K.bn_part_finalize(part, rows, self.Cout, bn.weight.detach(), bn.bias.detach(),
+                                       bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+        else:
+            stats = K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                    bn.running_var, bn.eps)
+        K.bn_apply(z, stats, self.act, out, drop)
+        if tape is not None:
+            tape[self] = (x, z, stats, wps, drop, training)
+
+    def backward(self, tape, g, gx, accumulate_gx=False, g_pool=None):
+        if not isinstance(tape[self][0], CatParts):
+            return super().backward(tape, g, gx, accumulate_gx=accumulate_gx, g_pool=g_pool)
+        x, z, stats, wps, drop, training = tape.pop(self)
+        if not training:
+            raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
+        dev = z.buf.device
+        dz = Act(torch.empty_like(z.buf))
+        dgamma = torch.empty(self.Cout, dtype=torch.float32, device=dev)
+        dbeta = torch.empty(self.Cout, dtype=torch.float32, device=dev)
+        dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) if self.conv.bias is not None else None
+        K.bn_bwd(g, z, self.bn.weight.detach(), stats, self.act, dz, dgamma, dbeta, dbias, drop)
+        gzs = [dz]
+        for part, sc in zip(x.parts[1:], CatParts.SCALES[1:]):  # U^T dz at the part's resolution
+            gk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dz.buf.dtype, dev))
+            K.upsample_bwd(dz, sc, K.UP_BILINEAR, gk)
+            gzs.append(gk)
+        dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
+        lo = 0
+        for k, part in enumerate(x.parts):
+            dwk = torch.empty((self.Cout, part.C, 1, 1), dtype=torch.float32, device=dev)
+            K.conv_wgrad(part, gzs[k], 1, 0, dwk)
+            dw[:, lo:lo + part.C] = dwk
+            if gx is not None:
+                K.conv_dgrad(gzs[k], wps[k], part.C, 1, 0, gx.parts[k], accumulate=accumulate_gx)
+            lo += part.C
+        grads = {self.conv.weight: dw, self.bn.weight: dgamma, self.bn.bias: dbeta}
+        if self.conv.bias is not None:
+            grads[self.conv.bias] = dbias
+        return grads
+
+
 # ---------------------------------------------------------------------------
 # VGG16-BN encoder (features[0:43]) + density decoder (models/models.py:35-87)
 # ---------------------------------------------------------------------------
 class FeaturePlan:
-    """forward_fe of DGModel_base: img [N,3,H,W] f32 -> (y_cat NHWC [N,H/4,W/4,896], x3 NHWC)."""
+    """forward_fe of DGModel_base: img [N,3,H,W] f32 -> (y1, y2, y3, x3) NHWC, where the
+    reference's y_cat = cat[y1, up2(y2), up4(y3)] (models/models.py:84) is left to the heads'
+    CatConvLayer (never materialised on the hot path)."""
 
     def __init__(self, model):
         feats = list(model.enc1) + list(model.enc2) + list(model.enc3)
@@ -218,42 +347,44 @@ class FeaturePlan:
         # decoder
         a13 = nh(H // 16, W // 16, 1024); D[0].forward(x3, a13, training, tape)
         y3 = nh(H // 16, W // 16, 512); D[1].forward(a13, y3, training, tape)
-        ycat = K.nhwc(N, H // 4, W // 4, 896, dt, dev)
         K.upsample_fwd(y3, 2, K.UP_BILINEAR, Act(dec2in, 0, 512))
-        K.upsample_fwd(y3, 4, K.UP_BILINEAR, Act(ycat, 384, 512))
         a15 = nh(H // 8, W // 8, 512); D[2].forward(Act(dec2in), a15, training, tape)
         y2 = nh(H // 8, W // 8, 256); D[3].forward(a15, y2, training, tape)
         K.upsample_fwd(y2, 2, K.UP_BILINEAR, Act(dec1in, 0, 256))
-        K.upsample_fwd(y2, 2, K.UP_BILINEAR, Act(ycat, 128, 256))
         a17 = nh(H // 4, W // 4, 256); D[4].forward(Act(dec1in), a17, training, tape)
-        D[5].forward(a17, Act(ycat, 0, 128), training, tape)
+        y1 = nh(H // 4, W // 4, 128); D[5].forward(a17, y1, training, tape)
         if tape is not None:
             tape[self] = dict(dec1in=dec1in, dec2in=dec2in, shape=(N, H, W), dt=dt)
-        return ycat, x3.buf
+        return y1.buf, y2.buf, y3.buf, x3.buf
 
-    def backward(self, tape: dict, g_ycat: torch.Tensor, g_x3: torch.Tensor | None) -> dict:
+    def backward(self, tape: dict, g_y1, g_y2, g_y3, g_x3) -> dict:
+        """Gradients of (y1, y2, y3, x3) from the heads (None = unused)."""
         s = tape.pop(self)
         N, H, W = s["shape"]
         dt = s["dt"]
-        dev = g_ycat.device
+        dev = s["dec1in"].device
         E, D = self.enc, self.dec
         nh = lambda h, w, c: Act(K.nhwc(N, h, w, c, dt, dev))  # noqa: E731
-        g_ycat = g_ycat.contiguous()
+
+        def own(g, h, w, c):  # a writable NHWC gradient buffer (zeros when the output was unused)
+            if g is None:
+                return Act(K.nhwc(N, h, w, c, dt, dev, zero=True))
+            return Act(g.to(dt).contiguous().clone())
+
         grads = {}
         # decoder
         g_a17 = nh(H // 4, W // 4, 256)
-        grads.update(D[5].backward(tape, Act(g_ycat, 0, 128), g_a17))
+        grads.update(D[5].backward(tape, own(g_y1, H // 4, W // 4, 128), g_a17))
         g_dec1in = K.nhwc(N, H // 4, W // 4, 512, dt, dev)
         grads.update(D[4].backward(tape, g_a17, Act(g_dec1in)))
-        g_y2 = nh(H // 8, W // 8, 256)
-        K.upsample_bwd(Act(g_dec1in, 0, 256), 2, K.UP_BILINEAR, g_y2, gy2=Act(g_ycat, 128, 256))
+        gy2 = own(g_y2, H // 8, W // 8, 256)
+        K.upsample_bwd(Act(g_dec1in, 0, 256), 2, K.UP_BILINEAR, gy2, accumulate=True)
         g_a15 = nh(H // 8, W // 8, 512)
-        grads.update(D[3].backward(tape, g_y2, g_a15))
+        grads.update(D[3].backward(tape, gy2, g_a15))
         g_dec2in = K.nhwc(N, H // 8, W // 8, 1024, dt, dev)
         grads.update(D[2].backward(tape, g_a15, Act(g_dec2in)))
-        g_y3 = nh(H // 16, W // 16, 512)
-        K.upsample_bwd(Act(g_dec2in, 0, 512), 2, K.UP_BILINEAR, g_y3)
-        K.upsample_bwd(Act(g_ycat, 384, 512), 4, K.UP_BILINEAR, g_y3, accumulate=True)
+        g_y3 = own(g_y3, H // 16, W // 16, 512)
+        K.upsample_bwd(Act(g_dec2in, 0, 512), 2, K.UP_BILINEAR, g_y3, accumulate=True)
         g_a13 = nh(H // 16, W // 16, 1024)
         grads.update(D[1].backward(tape, g_y3, g_a13))
         if g_x3 is not None:
@@ -341,7 +472,7 @@ class DensityPlan:
     """ycat NHWC [N,h,w,896] -> d [N,1,4h,4w] f32."""
 
     def __init__(self, den_dec_block, den_head_block, dropout_p: float = 0.0):
-        self.dec = ConvLayer(den_dec_block.conv, den_dec_block.bn, ACT_RELU)
+        self.dec = CatConvLayer(den_dec_block.conv, den_dec_block.bn, ACT_RELU)
         hc = den_head_block.conv
         self.head_w = hc.weight
         self.head_b = hc.bias
@@ -354,24 +485,26 @@ class DensityPlan:
             ps.append(self.head_b)
         return ps
 
-    def forward(self, ycat: torch.Tensor, training: bool, tape: dict | None = None):
-        N, h, w, C = ycat.shape
-        dt = ycat.dtype
-        dev = ycat.device
+    def forward(self, ycat, training: bool, tape: dict | None = None):
+        """ycat: (y1, y2, y3) NHWC parts (CatParts) or a materialised NHWC y_cat tensor."""
+        cat = as_cat(ycat)
+        N, h, w = cat.N, cat.H, cat.W
+        dt = cat.parts[0].buf.dtype if isinstance(cat, CatParts) else cat.buf.dtype
+        dev = cat.parts[0].buf.device if isinstance(cat, CatParts) else cat.buf.device
         drop = dropout2d_mask(N, self.dec.Cout, self.p, dev) if training else None
         yden = Act(K.nhwc(N, h, w, self.dec.Cout, dt, dev))
-        self.dec.forward(Act(ycat), yden, training, tape, drop=drop)
+        self.dec.forward(cat, yden, training, tape, drop=drop)
         hb = self.head_b.detach() if self.head_b is not None else None
         yh = K.head_fwd(yden, self.head_w.detach().reshape(-1), hb, self.head_act)
         d = torch.empty((N, 4 * h, 4 * w, 1), dtype=torch.float32, device=dev)
         K.upsample_fwd(Act(yh.view(N, h, w, 1)), 4, K.UP_BILINEAR, Act(d))
         if tape is not None:
-            tape[self] = (ycat.shape, dt, yden, yh)
+            tape[self] = (cat, dt, yden, yh)
         return d.view(N, 1, 4 * h, 4 * w)
 
     def backward(self, tape: dict, g_d: torch.Tensor):
-        shape, dt, yden, yh = tape.pop(self)
-        N, h, w, C = shape
+        cat, dt, yden, yh = tape.pop(self)
+        N, h, w = cat.N, cat.H, cat.W
         dev = g_d.device
         g_h = torch.empty((N, h, w, 1), dtype=torch.float32, device=dev)
         K.upsample_bwd(Act(g_d.contiguous().view(N, 4 * h, 4 * w, 1)), 4, K.UP_BILINEAR, Act(g_h))
@@ -380,12 +513,12 @@ class DensityPlan:
         gb = torch.empty(1, dtype=torch.float32, device=dev) if self.head_b is not None else None
         K.head_bwd(yden, self.head_w.detach().reshape(-1), self.head_act, yh, g_h.view(N, h, w),
                    g_yden, gw, gb)
-        g_ycat = torch.empty(shape, dtype=dt, device=dev)
-        grads = self.dec.backward(tape, g_yden, Act(g_ycat))
+        g_cat = cat_empty_like(cat)
+        grads = self.dec.backward(tape, g_yden, g_cat)
         grads[self.head_w] = gw.view_as(self.head_w)
         if gb is not None:
             grads[self.head_b] = gb
-        return (g_ycat,), grads
+        return cat_grads(g_cat), grads
 
 
 # ---------------------------------------------------------------------------
@@ -444,7 +577,7 @@ class _Heads:
 
     def __init__(self, model, mem: bool, cls: bool):
         dd = model.den_dec[0]
-        self.den = ConvLayer(dd.conv, dd.bn, ACT_RELU)
+        self.den = CatConvLayer(dd.conv, dd.bn, ACT_RELU)
         self.den_drop_module = next((m for m in model.den_dec if isinstance(m, nn.Dropout2d)), None)
         hc = model.den_head[0].conv
         self.head_w, self.head_b = hc.weight, hc.bias
@@ -535,14 +668,16 @@ class SinglePlan(_Heads):
     ycat, x3 (NHWC) [, c_gt] -> d  or  (dc, c)."""
 
     def forward(self, ycat, x3, c_gt, training, tape=None):
-        N, h, w, _ = ycat.shape
-        dt, dev = ycat.dtype, ycat.device
+        """ycat: (y1, y2, y3) NHWC parts or a materialised NHWC y_cat tensor."""
+        cat = as_cat(ycat)
+        N, h, w = cat.N, cat.H, cat.W
+        dt, dev = x3.dtype, x3.device
         p = self.den_drop_module.p if (self.den_drop_module is not None and training) else 0.0
         drop = dropout2d_mask(N, self.den.Cout, p, dev)
         sub = {} if tape is not None else None
         yden = Act(K.nhwc(N, h, w, self.den.Cout, dt, dev))
-        self.den.forward(Act(ycat), yden, training, sub, drop=drop)
-        st = {"sub": sub, "yden": yden, "shape": ycat.shape}
+        self.den.forward(cat, yden, training, sub, drop=drop)
+        st = {"sub": sub, "yden": yden, "cat": cat}
         y = yden
         if self.memr is not None:
             memT_s, mem_p, scale = self.memr.packs(dt)
@@ -573,7 +708,8 @@ class SinglePlan(_Heads):
     def backward(self, tape, *gouts):
         st = tape.pop(self)
         sub = st["sub"]
-        N, h, w, Cy = st["shape"]
+        cat = st["cat"]
+        N, h, w = cat.N, cat.H, cat.W
         grads = {}
         g_d = gouts[0]
         g_x3 = None
@@ -590,14 +726,15 @@ class SinglePlan(_Heads):
                 K.call("dg_softmax_bwd", gP.dt, st["P"].ptr, gP.ptr, gP.M, gP.C, gL.ptr, K.stream())
                 g_y, dmem_b = self.memr.bwd_logits(gL, st["yden"], st["mem_p"], st["scale"], dt)
                 _acc(grads, self.memr.mem, (dmem_a + dmem_b).view_as(self.memr.mem))
-            g_ycat = torch.empty(st["shape"], dtype=y.buf.dtype, device=y.buf.device)
-            for p, g in self.den.backward(sub, g_y, Act(g_ycat)).items():
+            g_cat = cat_empty_like(cat)
+            for p, g in self.den.backward(sub, g_y, g_cat).items():
                 _acc(grads, p, g)
+            g_cat = cat_grads(g_cat)
         else:
-            g_ycat = None
+            g_cat = (None,) * (3 if isinstance(cat, CatParts) else 1)
         if self.cls is not None and len(gouts) > 1 and gouts[1] is not None:
             g_x3 = self.cls_bwd(sub, "cls", gouts[1], grads)
-        return (g_ycat, g_x3), grads
+        return (*g_cat, g_x3), grads
 
 
 class PairPlan(_Heads):
@@ -611,9 +748,11 @@ class PairPlan(_Heads):
         self.nondiff = (4,) if cls else ()
 
     def forward(self, ycat1, ycat2, x3_1, x3_2, c_gt, p_drop, err_thrs, tape=None):
-        N, h, w, _ = ycat1.shape
+        """ycat1/2: (y1, y2, y3) NHWC parts or materialised NHWC y_cat tensors."""
+        cat1, cat2 = as_cat(ycat1), as_cat(ycat2)
+        N, h, w = cat1.N, cat1.H, cat1.W
         HW = h * w
-        dt, dev = ycat1.dtype, ycat1.device
+        dt, dev = x3_1.dtype, x3_1.device
         training = True
         sub = {} if tape is not None else None
         C = self.den.Cout
@@ -621,8 +760,8 @@ class PairPlan(_Heads):
         y2 = Act(K.nhwc(N, h, w, C, dt, dev))
         s1 = {} if tape is not None else None
         s2 = {} if tape is not None else None
-        self.den.forward(Act(ycat1), y1, training, s1)
-        self.den.forward(Act(ycat2), y2, training, s2)
+        self.den.forward(cat1, y1, training, s1)
+        self.den.forward(cat2, y2, training, s2)
         # instance-norm statistics -> e_mask (detached) -> masked, dropped features
         stats = torch.empty((4, N * C), dtype=torch.float32, device=dev)
         ws = K.query("dg_instnorm_workspace", N, HW, C)
@@ -652,7 +791,7 @@ class PairPlan(_Heads):
         yn1 = self.memr.readout(P1, mem_p, dt)
         yn2 = self.memr.readout(P2, mem_p, dt)
         yh1, yh2 = self.head(yn1), self.head(yn2)
-        st = dict(s1=s1, s2=s2, shape=ycat1.shape, mask=mask, d1=d1, d2=d2, m1=m1, m2=m2, P1=P1,
+        st = dict(s1=s1, s2=s2, cat1=cat1, cat2=cat2, mask=mask, d1=d1, d2=d2, m1=m1, m2=m2, P1=P1,
                   P2=P2, yn1=yn1, yn2=yn2, yh1=yh1, yh2=yh2, mem_p=mem_p, scale=scale)
         if self.cls is None:
             outs = (_up4(yh1, N, h, w), _up4(yh2, N, h, w), loss_con)
@@ -676,7 +815,7 @@ class PairPlan(_Heads):
 
     def backward(self, tape, *gouts):
         st = tape.pop(self)
-        N, h, w, Cy = st["shape"]
+        N, h, w = st["cat1"].N, st["cat1"].H, st["cat1"].W
         HW = h * w
         grads = {}
         if self.cls is None:
@@ -719,11 +858,10 @@ class PairPlan(_Heads):
         g_y2 = Act(K.nhwc(N, h, w, C, dt, dev))
         K.call("dg_emask_bwd", g_m1.dt, g_m1.ptr, g_m2.ptr, N, HW, C, K.ptr(st["mask"]), K.ptr(st["d1"]),
                K.ptr(st["d2"]), g_y1.ptr, g_y2.ptr, g_y1.ld, K.stream())
-        g_ycat1 = torch.empty(st["shape"], dtype=dt, device=dev)
-        g_ycat2 = torch.empty(st["shape"], dtype=dt, device=dev)
-        for p, g in self.den.backward(st["s1"], g_y1, Act(g_ycat1)).items():
+        g_cat1, g_cat2 = cat_empty_like(st["cat1"]), cat_empty_like(st["cat2"])
+        for p, g in self.den.backward(st["s1"], g_y1, g_cat1).items():
             _acc(grads, p, g)
-        for p, g in self.den.backward(st["s2"], g_y2, Act(g_ycat2)).items():
+        for p, g in self.den.backward(st["s2"], g_y2, g_cat2).items():
             _acc(grads, p, g)
         g_x3_1 = g_x3_2 = None
         if self.cls is not None:
@@ -731,4 +869,4 @@ class PairPlan(_Heads):
                 g_x3_1 = self.cls_bwd(st["sub"], "c1", g_c1, grads)
             if g_c2 is not None:
                 g_x3_2 = self.cls_bwd(st["sub"], "c2", g_c2, grads)
-        return (g_ycat1, g_ycat2, g_x3_1, g_x3_2), grads
+        return (*cat_grads(g_cat1), *cat_grads(g_cat2), g_x3_1, g_x3_2), grads

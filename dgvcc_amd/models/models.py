@@ -96,6 +96,39 @@ class _SingleConvPlan:
         return (gx.buf.permute(0, 3, 1, 2),), grads
 
 
+class _CatPlan:
+    """Materialise y_cat = cat[y1, up2(y2), up4(y3)] (NHWC) for forward_fe callers, with its
+    backward (slice + bilinear U^T), on the HIP resample kernels."""
+
+    def params(self):
+        return []
+
+    def __call__(self, y1, y2, y3):
+        def fwd(a, b, c, tape):
+            from .. import kernels as K
+            N, h, w, c1 = a.shape
+            out = K.nhwc(N, h, w, c1 + b.shape[3] + c.shape[3], a.dtype, a.device)
+            out[..., :c1] = a
+            K.upsample_fwd(K.Act(b.contiguous()), 2, K.UP_BILINEAR, K.Act(out, c1, b.shape[3]))
+            K.upsample_fwd(K.Act(c.contiguous()), 4, K.UP_BILINEAR, K.Act(out, c1 + b.shape[3], c.shape[3]))
+            if tape is not None:
+                tape[self] = (a.shape, b.shape, c.shape)
+            return out
+
+        return E.run_plan(self, fwd, (y1, y2, y3), [])
+
+    def backward(self, tape, g):
+        from .. import kernels as K
+        sa, sb, sc = tape.pop(self)
+        g = g.contiguous()
+        ga = g[..., :sa[3]].contiguous()
+        gb = K.nhwc(*sb, g.dtype, g.device)
+        gc = K.nhwc(*sc, g.dtype, g.device)
+        K.upsample_bwd(K.Act(g, sa[3], sb[3]), 2, K.UP_BILINEAR, K.Act(gb))
+        K.upsample_bwd(K.Act(g, sa[3] + sb[3], sc[3]), 4, K.UP_BILINEAR, K.Act(gc))
+        return (ga, gb, gc), {}
+
+
 def upsample(x, scale_factor=2, mode="bilinear"):
     """reference models/models.py:23-27 on NCHW tensors (HIP resample kernel)."""
     from .. import kernels as K
@@ -175,21 +208,24 @@ class DGModel_base(_DGBase):
         return E.run_plan(fe, fwd, (x,), fe.params())
 
     def forward_fe(self, x):
-        ycat, x3 = self._forward_fe_nhwc(x)
+        """(y_cat, x3) NCHW as the reference returns them (models/models.py:64-87); y_cat is
+        materialised here only — the model's own forward keeps it as its parts."""
+        y1, y2, y3, x3 = self._forward_fe_nhwc(x)
+        ycat = _CatPlan()(y1, y2, y3)
         return ycat.permute(0, 3, 1, 2), x3.permute(0, 3, 1, 2)
 
-    def _density(self, ycat):
+    def _density(self, cat):
         den = self._get_plans()["den"]
         den.p = self.den_dropout
 
-        def fwd(yc, tape):
-            return den.forward(yc, self.training, tape)
+        def fwd(y1, y2, y3, tape):
+            return den.forward((y1, y2, y3), self.training, tape)
 
-        return E.run_plan(den, fwd, (ycat,), den.params())
+        return E.run_plan(den, fwd, tuple(cat), den.params())
 
     def forward(self, x):
-        ycat, _ = self._forward_fe_nhwc(x)
-        return self._density(ycat)
+        y1, y2, y3, _ = self._forward_fe_nhwc(x)
+        return self._density((y1, y2, y3))
 
 
 class DGModel_mem(DGModel_base):
@@ -226,17 +262,17 @@ class DGModel_mem(DGModel_base):
         yn = plan.memr.readout(P, mem_p, dt)
         return yn.buf.permute(0, 3, 1, 2), L.buf.view(b, h * w, -1).transpose(1, 2)
 
-    def _single(self, ycat, x3, c_gt=None):
+    def _single(self, cat, x3, c_gt=None):
         plan = self._get_plans()["single"]
 
-        def fwd(yc, x, tape):
-            return plan.forward(yc, x, c_gt, self.training, tape)
+        def fwd(y1, y2, y3, x, tape):
+            return plan.forward((y1, y2, y3), x, c_gt, self.training, tape)
 
-        return E.run_plan(plan, fwd, (ycat, x3), plan.params())
+        return E.run_plan(plan, fwd, (*cat, x3), plan.params())
 
     def forward(self, x):
-        ycat, x3 = self._forward_fe_nhwc(x)
-        return self._single(ycat, x3)
+        y1, y2, y3, x3 = self._forward_fe_nhwc(x)
+        return self._single((y1, y2, y3), x3)
 
 
 class _PairMixin:
@@ -246,16 +282,16 @@ class _PairMixin:
         return F.mse_loss(F.softmax(logits1, dim=1), F.softmax(logits2, dim=1))
 
     def _pair(self, img1, img2, c_gt):
-        ycat1, x3_1 = self._forward_fe_nhwc(img1)
-        ycat2, x3_2 = self._forward_fe_nhwc(img2)
+        *cat1, x3_1 = self._forward_fe_nhwc(img1)
+        *cat2, x3_2 = self._forward_fe_nhwc(img2)
         plan = self._get_plans()["pair"]
         p = float(self.den_dropout)
         thr = float(self.err_thrs)
 
-        def fwd(y1, y2, a, b, tape):
-            return plan.forward(y1, y2, a, b, c_gt, p, thr, tape)
+        def fwd(a1, a2, a3, b1, b2, b3, xa, xb, tape):
+            return plan.forward((a1, a2, a3), (b1, b2, b3), xa, xb, c_gt, p, thr, tape)
 
-        return E.run_plan(plan, fwd, (ycat1, ycat2, x3_1, x3_2), plan.params())
+        return E.run_plan(plan, fwd, (*cat1, *cat2, x3_1, x3_2), plan.params())
 
 
 class DGModel_memadd(_PairMixin, DGModel_mem):
@@ -304,8 +340,8 @@ class DGModel_cls(DGModel_base):
     _single = DGModel_mem._single
 
     def forward(self, x, c_gt=None):
-        ycat, x3 = self._forward_fe_nhwc(x)
-        return self._single(ycat, x3, c_gt)
+        y1, y2, y3, x3 = self._forward_fe_nhwc(x)
+        return self._single((y1, y2, y3), x3, c_gt)
 
 
 class DGModel_memcls(DGModel_mem):
@@ -325,8 +361,8 @@ class DGModel_memcls(DGModel_mem):
     transform_cls_map = DGModel_cls.transform_cls_map
 
     def forward(self, x, c_gt=None):
-        ycat, x3 = self._forward_fe_nhwc(x)
-        return self._single(ycat, x3, c_gt)
+        y1, y2, y3, x3 = self._forward_fe_nhwc(x)
+        return self._single((y1, y2, y3), x3, c_gt)
 
 
 class DGModel_final(_PairMixin, DGModel_memcls):

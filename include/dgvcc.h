@@ -276,6 +276,17 @@ int dg_upsample_bwd(int dtype, const void* gy, int64_t ldgy, const void* gy2, in
                     int N, int H, int W, int C, int scale, int mode, void* gx, int64_t ldgx,
                     int accumulate, void* stream);
 
+/* den_dec on the decomposed decoder concatenation (models/models.py:84,89-90):
+ * conv1x1(cat[y1, up2(y2), up4(y3)]) = z1 + up2(z2) + up4(z3) with zk = conv1x1(yk; W[:, slice k]).
+ * z [N,H,W,C] = z1 + up2(z2 [N,H/2,W/2,C]) + up4(z3 [N,H/4,W/4,C]) + bias (bilinear,
+ * align_corners=False), stored in dtype; part (may be NULL) receives the BN statistics
+ * partials [dg_cat_combine_part_rows][3][C] = (n, mean, M2) of the stored z for
+ * dg_bn_part_finalize.  z may alias z1. */
+int64_t dg_cat_combine_part_rows(int N, int H, int W);
+int dg_cat_combine(int dtype, const void* z1, int64_t ldz1, const void* z2, int64_t ldz2,
+                   const void* z3, int64_t ldz3, int N, int H, int W, int C, const float* bias,
+                   void* z, int64_t ldz, float* part, void* stream);
+
 /* ---- density head: 1x1 conv C->1 (+ReLU) --------------------------------------
  * den_head (models/models.py:60-62) / cls_head tail (models/models.py:241-242). */
 int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w,
