@@ -303,11 +303,12 @@ __device__ __forceinline__ float rnd_t(float v) { return to_f(from_f<T>(v)); }
 
 __device__ __forceinline__ void pool_window(long long pp, int H, int W, long long pos[4]) {
   const int Ho = H / 2, Wo = W / 2;
-  const int wo = (int)(pp % Wo);
-  const long long t = pp / Wo;
-  const int ho = (int)(t % Ho);
-  const long long n = t / Ho;
-  const long long p00 = (n * H + 2 * ho) * W + 2 * wo;
+  const int p32 = (int)pp;  // N*H*W < 2^31 (checked by the ABI): 32-bit division
+  const int wo = p32 % Wo;
+  const int t = p32 / Wo;
+  const int ho = t % Ho;
+  const int n = t / Ho;
+  const long long p00 = ((long long)n * H + 2 * ho) * W + 2 * wo;
   pos[0] = p00; pos[1] = p00 + 1; pos[2] = p00 + W; pos[3] = p00 + W + 1;
 }
 
@@ -614,8 +615,8 @@ extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, in
   DG_REQUIRE(z && yp && scale && shift && N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
   DG_REQUIRE(ldz >= C && ldyp >= C && (!y || ldy >= C));
   DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, ldyp) &&
-               (!y || BN_SHAPE_OK(dtype, C, ldy)));
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldz) &&
+               BN_SHAPE_OK(dtype, C, ldyp) && (!y || BN_SHAPE_OK(dtype, C, ldy)));
   hipStream_t st = (hipStream_t)stream;
   const long long Mp = (long long)N * (H / 2) * (W / 2);
   const long long total = Mp * (C / (dtype == DG_BF16 ? 8 : 4));

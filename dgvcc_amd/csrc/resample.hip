@@ -215,12 +215,23 @@ __global__ __launch_bounds__(NT) void upsample_fwd_kernel(const T* __restrict__ 
                                                           long long ldy) {
   const int Ho = H * scale, Wo = W * scale, tpp = C / V;
   const long long total = (long long)N * Ho * Wo * tpp;
+  const bool small = total < (1LL << 31);
   for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const int ch = (int)(i % tpp);
-    long long t = i / tpp;
-    const int wo = (int)(t % Wo); t /= Wo;
-    const int ho = (int)(t % Ho);
-    const int n = (int)(t / Ho);
+    int ch, wo, ho, n;
+    if (small) {  // 32-bit index math (64-bit division is a long software sequence)
+      const int ii = (int)i;
+      ch = ii % tpp;
+      int t = ii / tpp;
+      wo = t % Wo; t /= Wo;
+      ho = t % Ho;
+      n = t / Ho;
+    } else {
+      ch = (int)(i % tpp);
+      long long t = i / tpp;
+      wo = (int)(t % Wo); t /= Wo;
+      ho = (int)(t % Ho);
+      n = (int)(t / Ho);
+    }
     const Tap th = src_tap(ho, H, Ho, scale, mode), tw = src_tap(wo, W, Wo, scale, mode);
     const float h1l = th.l1, h0l = 1.f - th.l1, w1l = tw.l1, w0l = 1.f - tw.l1;
     const T* base = x + (long long)n * H * W * ldx + ch * V;
@@ -440,13 +451,83 @@ int up_fwd(const void* x, long long ldx, int N, int H, int W, int C, int scale, 
   return DG_OK;
 }
 
+// Specialised backward for bilinear align_corners=False at a compile-time scale SC
+// (the decoder's x2 / x4): the output pixels that touch input i lie in the exact window
+// [SC*i - SC/2, SC*i + 3*SC/2) (2*SC per axis, checked against the generic tap rule),
+// so the per-axis weights are computed once and the gather loop has fixed trip counts.
+// Same (oh, ow) accumulation order as upsample_bwd_kernel -> identical results.
+template <typename T, int V, int SC>
+__global__ __launch_bounds__(NT) void upsample_bwd_bl_kernel(const T* __restrict__ gy, long long ldgy,
+                                                             const T* __restrict__ gy2, long long ldgy2, int N, int H,
+                                                             int W, int C, T* __restrict__ gx, long long ldgx,
+                                                             int accumulate) {
+  constexpr int WN = 2 * SC;
+  const int Ho = H * SC, Wo = W * SC, tpp = C / V;
+  const int total = N * H * W * tpp;  // < 2^31 (checked by the launcher)
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int ch = i % tpp;
+    int t = i / tpp;
+    const int iw = t % W; t /= W;
+    const int ih = t % H;
+    const int n = t / H;
+    const int oh0 = SC * ih - SC / 2, ow0 = SC * iw - SC / 2;
+    float wh[WN], ww[WN];
+#pragma unroll
+    for (int k = 0; k < WN; ++k) {
+      const int oh = oh0 + k, ow = ow0 + k;
+      wh[k] = (oh >= 0 && oh < Ho) ? tap_weight(src_tap(oh, H, Ho, SC, 0), ih) : 0.f;
+      ww[k] = (ow >= 0 && ow < Wo) ? tap_weight(src_tap(ow, W, Wo, SC, 0), iw) : 0.f;
+    }
+    float acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int kh = 0; kh < WN; ++kh) {
+      if (wh[kh] == 0.f) continue;
+      const long long rowp = (long long)(n * Ho + oh0 + kh) * Wo;
+#pragma unroll
+      for (int kw = 0; kw < WN; ++kw) {
+        if (ww[kw] == 0.f) continue;
+        const float wgt = wh[kh] * ww[kw];
+        const long long op = rowp + ow0 + kw;
+        float g[V];
+        ldv(gy + op * ldgy + ch * V, g);
+        if (gy2) {
+          float g2[V];
+          ldv(gy2 + op * ldgy2 + ch * V, g2);
+#pragma unroll
+          for (int e = 0; e < V; ++e) g[e] += g2[e];
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = fmaf(wgt, g[e], acc[e]);
+      }
+    }
+    T* dst = gx + ((long long)(n * H + ih) * W + iw) * ldgx + ch * V;
+    if (accumulate) {
+      float o[V];
+      ldv(dst, o);
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] += o[e];
+    }
+    stv(dst, acc);
+  }
+}
+
 template <typename T>
 int up_bwd(const void* gy, long long ldgy, const void* gy2, long long ldgy2, int N, int H, int W, int C, int scale,
            int mode, void* gx, long long ldgx, int acc, hipStream_t st) {
   constexpr int V = 16 / (int)sizeof(T);
   const bool vec = (C % V == 0) && (ldgy % V == 0) && (ldgx % V == 0) && (!gy2 || ldgy2 % V == 0);
   const long long total = (long long)N * H * W * (vec ? C / V : C);
-  if (vec)
+  if (vec && mode == 0 && (scale == 2 || scale == 4) && total < (1LL << 31) &&
+      (long long)N * H * scale * W * scale < (1LL << 31)) {
+    if (scale == 2)
+      hipLaunchKernelGGL((upsample_bwd_bl_kernel<T, V, 2>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gy, ldgy,
+                         (const T*)gy2, ldgy2, N, H, W, C, (T*)gx, ldgx, acc);
+    else
+      hipLaunchKernelGGL((upsample_bwd_bl_kernel<T, V, 4>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gy, ldgy,
+                         (const T*)gy2, ldgy2, N, H, W, C, (T*)gx, ldgx, acc);
+  } else if (vec)
     hipLaunchKernelGGL((upsample_bwd_kernel<T, V>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gy, ldgy,
                        (const T*)gy2, ldgy2, N, H, W, C, scale, mode, (T*)gx, ldgx, acc);
   else
