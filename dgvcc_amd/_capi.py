@@ -90,6 +90,12 @@ def call(name: str, *args) -> int:
     return r
 
 
+def lib_call_status(name: str, *args) -> int:
+    """Invoke an entry point and return its status code unchecked (for callers that
+    handle DG_ERR_UNSUPPORTED themselves)."""
+    return int(getattr(lib(), name)(*args))
+
+
 def query(name: str, *args) -> int:
     r = getattr(lib(), name)(*args)
     if r < 0:

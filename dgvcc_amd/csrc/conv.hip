@@ -26,7 +26,85 @@ struct FwdArgs {
   const float* bias;
   char* y; long long ldy;
   int accumulate;
+  float* part;  // bf16 pipe/tap3 only: BN statistics partials [ceil(M/256)][3][Cout] (NULL = none)
 };
+
+// Sum over the 16 lanes of a DPP row, result in every lane: quad butterflies (xor 1, 2)
+// then rotations by 4 and 8 (VALU-only, no LDS crossbar traffic).
+#define DG_DPP(x, ctrl) __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), (ctrl), 0xf, 0xf, true))
+__device__ __forceinline__ float row16_sum(float x) {
+  x += DG_DPP(x, 0xB1);   // quad_perm [1,0,3,2]
+  x += DG_DPP(x, 0x4E);   // quad_perm [2,3,0,1]
+  x += DG_DPP(x, 0x124);  // row_ror:4
+  x += DG_DPP(x, 0x128);  // row_ror:8
+  return x;
+}
+
+// Workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not wait for
+// this wave's outstanding global stores (the epilogue's y stores keep draining).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// Epilogue BN statistics of the stored (bf16-rounded) conv outputs, replacing the
+// separate statistics pass over z (norm.hip bn_stats_partial).  acc holds the stored
+// values; lane (fr, fc) has channels cw + 16i + 4fc + r of pixel 16j + fr of its wave.
+// Per wave and channel: count, mean and M2 over its valid pixels (DPP row sums over
+// the 16 pixel lanes, two passes over registers), then a Chan merge of the NPW pixel
+// waves through LDS into one partial row (n, mean, M2) per block.
+template <int TI, int TJ, int NPW, int BN>
+__device__ __forceinline__ void epi_stats(f4v (&acc)[TI][TJ], const bool (&valid)[TJ], int pw, int cw, char* lds,
+                                          float* part_row, int Cout, int co0, int tid, int fr, int fc) {
+  float cnt = 0.f;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) cnt += valid[j] ? 1.f : 0.f;
+  cnt = row16_sum(cnt);
+  const float rcnt = cnt > 0.f ? 1.f / cnt : 0.f;
+  float* sh = (float*)lds;  // [NPW][3][BN]
+  lds_barrier();            // every wave is done reading the operand ring
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float sm = 0.f;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) sm += valid[j] ? acc[i][j][r] : 0.f;
+      const float mean = row16_sum(sm) * rcnt;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const float d = acc[i][j][r] - mean;
+        q = valid[j] ? fmaf(d, d, q) : q;
+      }
+      q = row16_sum(q);
+      if (fr == 0) {
+        const int c = cw + 16 * i + 4 * fc + r;
+        sh[(pw * 3 + 0) * BN + c] = cnt;
+        sh[(pw * 3 + 1) * BN + c] = mean;
+        sh[(pw * 3 + 2) * BN + c] = q;
+      }
+    }
+  lds_barrier();
+  for (int c = tid; c < BN; c += 64 * 4 * NPW) {
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) {
+      const float nb = sh[(w * 3 + 0) * BN + c];
+      if (nb == 0.f) continue;
+      const float mb = sh[(w * 3 + 1) * BN + c];
+      const float nt = n + nb;
+      const float d = mb - mean;
+      mean += d * (nb / nt);
+      m2 += sh[(w * 3 + 2) * BN + c] + d * d * (n * nb / nt);
+      n = nt;
+    }
+    part_row[co0 + c] = n;
+    part_row[Cout + co0 + c] = mean;
+    part_row[2 * Cout + co0 + c] = m2;
+  }
+}
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
@@ -491,9 +569,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 #undef PIPE_ISSUE
 
   T* y = (T*)a.y;
+  bool valid[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
+    valid[j] = px < M;
     if (px >= M) continue;
     T* yrow = y + (long long)px * a.ldy;
 #pragma unroll
@@ -510,8 +590,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
         v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       st4(yrow + co, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
     }
   }
+  if (a.part)
+    epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / PBM) * 3 * a.Cout, a.Cout,
+                             co0, tid, fr, fc);
 }
 
 static int pipe_var() {
@@ -639,9 +724,11 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
   }
 
   T* y = (T*)a.y;
+  bool valid[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
+    valid[j] = true;  // M % 256 == 0 on this path
     T* yrow = y + (long long)px * a.ldy;
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -657,8 +744,13 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
         v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       st4(yrow + co, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
     }
   }
+  if (a.part)
+    epi_stats<TI, TJ, 4, BN>(acc, valid, wid, 0, smem, a.part + (long long)(px0 / BM) * 3 * a.Cout, a.Cout, 0, tid,
+                             fr, fc);
 }
 
 template <typename T>
@@ -1464,6 +1556,29 @@ extern "C" int dg_conv_fwd(int dtype, const void* x, int64_t ldx, int N, int H, 
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate};
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+}
+
+// Which forward kernel serves this shape (bf16): 1 = pipelined / fused 3-tap (epilogue
+// statistics available), 0 = register-staged.
+static bool fwd_has_epi_stats(int C, int Cout, long long ldx, int R, int S) {
+  return use_pipe() && C % 64 == 0 && ldx % 8 == 0 && (long long)Cout * R * S * C * 2 < (1ll << 31);
+}
+
+extern "C" int64_t dg_conv_stats_rows(int N, int H, int W) {
+  if (N <= 0 || H <= 0 || W <= 0) return DG_ERR_INVALID;
+  return dg_cdiv((long long)N * H * W, 256);
+}
+
+extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                                 int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy, float* part,
+                                 void* stream) {
+  DG_REQUIRE(x && w && y && part && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
+  DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldy % 4 == 0);
+  DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
+  FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, 0, part};
+  return launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 
 extern "C" int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream) {

@@ -407,6 +407,49 @@ __global__ __launch_bounds__(SNT) void bn_part_finalize(const float* __restrict_
   }
 }
 
+// First stage of the partial merge for long partial lists: rows [64b, 64b+64) of
+// part[nblk][3][C] -> out row b (Chan, float), 64 channels x 4 row groups per block.
+constexpr int PMG = 64;
+__global__ __launch_bounds__(SNT) void bn_part_merge(const float* __restrict__ part, int nblk, int C,
+                                                     float* __restrict__ out) {
+  __shared__ float sh[3][4][64];
+  const int cl = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const long long row = 3LL * C;
+  const int r0 = blockIdx.y * PMG, r1 = min(nblk, r0 + PMG);
+  float n = 0.f, mean = 0.f, m2 = 0.f;
+  if (c < C) {
+    for (int b = r0 + rg; b < r1; b += 4) {
+      const float nb = part[b * row + c];
+      if (nb == 0.f) continue;
+      const float mb = part[b * row + C + c];
+      const float nt = n + nb;
+      const float d = mb - mean;
+      mean += d * (nb / nt);
+      m2 += part[b * row + 2 * C + c] + d * d * (n * nb / nt);
+      n = nt;
+    }
+  }
+  sh[0][rg][cl] = n; sh[1][rg][cl] = mean; sh[2][rg][cl] = m2;
+  __syncthreads();
+  if (rg != 0 || c >= C) return;
+  n = 0.f; mean = 0.f; m2 = 0.f;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const float nb = sh[0][g][cl];
+    if (nb == 0.f) continue;
+    const float nt = n + nb;
+    const float d = sh[1][g][cl] - mean;
+    mean += d * (nb / nt);
+    m2 += sh[2][g][cl] + d * d * (n * nb / nt);
+    n = nt;
+  }
+  float* o = out + (long long)blockIdx.y * row;
+  o[c] = n; o[C + c] = mean; o[2 * C + c] = m2;
+}
+
+inline int part_rows2(int nblk) { return nblk > 1024 ? dg_cdiv(nblk, PMG) : 0; }
+
 inline int stem_fwd_grid(long long nseg) { return (int)std::max(1LL, std::min(512LL, (nseg + 3) / 4)); }
 inline int stem_bwd_grid(long long nseg) { return (int)std::max(1LL, std::min(512LL, (nseg + 3) / 4)); }
 constexpr int STEM_RPB = 32;  // slab rows per first-stage reduce block
@@ -429,13 +472,28 @@ extern "C" int dg_stem_fwd(const float* img, int N, int H, int W, const void* wp
   return DG_OK;
 }
 
+extern "C" int64_t dg_bn_part_workspace(int nblk, int C) {
+  if (nblk <= 0 || C <= 0) return DG_ERR_INVALID;
+  return std::max<int64_t>(16, (int64_t)part_rows2(nblk) * 3 * C * 4);
+}
+
 extern "C" int dg_bn_part_finalize(const float* part, int nblk, int C, const float* gamma, const float* beta,
                                    float* running_mean, float* running_var, float momentum, float eps,
-                                   float* save_mean, float* save_invstd, float* scale, float* shift, void* stream) {
+                                   float* save_mean, float* save_invstd, float* scale, float* shift, void* workspace,
+                                   void* stream) {
   DG_REQUIRE(part && nblk > 0 && C > 0 && save_mean && save_invstd && scale && shift);
   DG_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
-  hipLaunchKernelGGL(bn_part_finalize, dim3(C), dim3(SNT), 0, (hipStream_t)stream, part, nblk, C, gamma, beta,
-                     running_mean, running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+  hipStream_t st = (hipStream_t)stream;
+  const int r2 = part_rows2(nblk);
+  if (r2) {  // long list: merge groups of 64 rows first
+    DG_REQUIRE(workspace);
+    hipLaunchKernelGGL(bn_part_merge, dim3(dg_cdiv(C, 64), r2), dim3(SNT), 0, st, part, nblk, C, (float*)workspace);
+    DG_CHECK_LAUNCH();
+    part = (const float*)workspace;
+    nblk = r2;
+  }
+  hipLaunchKernelGGL(bn_part_finalize, dim3(C), dim3(SNT), 0, st, part, nblk, C, gamma, beta, running_mean,
+                     running_var, momentum, eps, save_mean, save_invstd, scale, shift);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -92,11 +92,20 @@ class ConvLayer:
             return
         wp = self._pack(dt)
         z = Act(K.nhwc(x.N, x.H, x.W, self.Cout, dt, x.buf.device))
+        epi = None
         if self.first:
             K.conv_fwd(x, wp, self.Cout, 1, 0, z, bias=bias, k_alg=9 * self.Cin)
+        elif bn is not None and training:  # BN statistics from the conv epilogue where available
+            epi = K.conv_fwd_stats(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
+            if epi is None:
+                K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
         else:
             K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
-        if bn is not None:
+        if epi is not None:
+            bn.num_batches_tracked.add_(1)
+            stats = K.bn_part_finalize(epi[0], epi[1], self.Cout, bn.weight.detach(), bn.bias.detach(),
+                                       bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+        elif bn is not None:
             if training:
                 bn.num_batches_tracked.add_(1)
                 stats = K.bn_fwd_train(z, bn.weight.detach(), bn.bias.detach(), bn.running_mean,

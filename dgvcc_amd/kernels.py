@@ -10,7 +10,7 @@ from dataclasses import dataclass
 
 import torch
 
-from ._capi import DGError, call, dtype_code, ptr, query, stream
+from ._capi import DGError, call, dtype_code, lib_call_status, ptr, query, stream
 
 F32, BF16 = 0, 1
 
@@ -152,10 +152,41 @@ def stem_fwd(img: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor | None, z: 
 def bn_part_finalize(part: torch.Tensor, nblk: int, C: int, gamma, beta, running_mean, running_var,
                      momentum, eps):
     stats = torch.empty((4, C), dtype=torch.float32, device=part.device)
+    ws = query("dg_bn_part_workspace", nblk, C)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=part.device)
     call("dg_bn_part_finalize", ptr(part), nblk, C, ptr(gamma), ptr(beta), ptr(running_mean),
          ptr(running_var), float(momentum), float(eps), ptr(stats[0]), ptr(stats[1]), ptr(stats[2]),
-         ptr(stats[3]), stream())
+         ptr(stats[3]), ptr(work), stream())
     return stats
+
+
+_EPI_STATS_OFF = __import__("os").environ.get("DGVCC_EPI_STATS", "1") == "0"
+
+
+def conv_fwd_stats(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
+                   bias: torch.Tensor | None = None):
+    """conv_fwd with the BN statistics partials of y from the conv epilogue; returns
+    (part, rows), or None (nothing launched) when the shape is served by a kernel without
+    epilogue statistics."""
+    rows = query("dg_conv_stats_rows", x.N, x.H, x.W)
+    part = torch.empty((rows, 3, Cout), dtype=torch.float32, device=x.buf.device)
+    flops = 2.0 * x.M * x.C * R * R * Cout
+    es = x.buf.element_size()
+    nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout)
+    res = []
+
+    def launch():
+        res.append(lib_call_status("dg_conv_fwd_stats", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
+                                   R, R, pad, ptr(bias), y.ptr, y.ld, ptr(part), stream()))
+
+    if x.dt != 1 or _EPI_STATS_OFF:
+        return None
+    _timed("fwd", flops, launch, nbytes)
+    if res[0] == -2:  # DG_ERR_UNSUPPORTED: nothing was launched
+        return None
+    if res[0] != 0:
+        raise DGError(f"dg_conv_fwd_stats failed with status {res[0]}")
+    return part, rows
 
 
 def bn_bwd_coef(g: Act, z: Act, gamma, stats, act: int, dgamma, dbeta, dbias=None,

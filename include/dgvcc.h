@@ -51,6 +51,16 @@ int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, 
                   const void* w, int C, int R, int S, int pad, void* wflip,
                   void* dx, int64_t lddx, int accumulate, void* stream);
 
+/* Forward conv (bf16, pipelined kernels) with the BatchNorm2d statistics of the stored
+ * output computed in the epilogue: part[dg_conv_stats_rows][3][Cout] = (n, mean, M2) per
+ * 256-pixel tile, for dg_bn_part_finalize (replaces the statistics pass over y).
+ * Returns DG_ERR_UNSUPPORTED (nothing launched) where only the register-staged kernel
+ * serves the shape; the caller then runs dg_conv_fwd + dg_bn_fwd_train. */
+int64_t dg_conv_stats_rows(int N, int H, int W);
+int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                      const void* w, int Cout, int R, int S, int pad, const float* bias,
+                      void* y, int64_t ldy, float* part, void* stream);
+
 /* wflip[C][R][S][Cout] = w[Cout][R-1-r][S-1-s][C] (packed filters of dtype). */
 int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream);
 
@@ -152,9 +162,11 @@ int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t
 
 /* Merge per-block BN partials part[nblk][3][C] = (n, mean, M2) (Chan, double) into the
  * batch statistics: same outputs and running-stat update as dg_bn_fwd_train. */
+int64_t dg_bn_part_workspace(int nblk, int C);
 int dg_bn_part_finalize(const float* part, int nblk, int C, const float* gamma, const float* beta,
                         float* running_mean, float* running_var, float momentum, float eps,
-                        float* save_mean, float* save_invstd, float* scale, float* shift, void* stream);
+                        float* save_mean, float* save_invstd, float* scale, float* shift,
+                        void* workspace, void* stream);
 
 /* ---- fused first layer (bf16): Conv2d(3,64,3,pad 1) of vgg16_bn.features[0]
  * (models/models.py:35-36) read straight from the NCHW f32 image (no im2col buffer).

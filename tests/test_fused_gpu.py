@@ -145,3 +145,38 @@ def test_bn_relu_pool_fused(dev, dtype, with_y, with_gd, C, H, W):
         assert relerr(yp.buf.permute(0, 3, 1, 2), out.detach()) < 1e-5
         assert relerr(dz.buf.permute(0, 3, 1, 2), zr.grad) < 1e-4
         assert relerr(dg, gr.grad) < 1e-4 and relerr(db, br.grad) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout", [
+    (2, 24, 40, 64, 256),     # pipelined 256-wide tiles, M % 256 != 0 (partial last tile)
+    (2, 20, 24, 128, 128),    # pipelined 128-wide tiles
+    (1, 8, 256, 64, 64),      # fused 3-tap kernel
+    (3, 256, 512, 64, 64),    # fused 3-tap, 1536 partial rows: two-stage merge
+    (1, 12, 12, 512, 1024),   # several co tiles
+])
+def test_conv_epilogue_bn_stats(dev, N, H, W, C, Cout):
+    """dg_conv_fwd_stats (statistics in the conv epilogue) + dg_bn_part_finalize against
+    dg_conv_fwd + dg_bn_fwd_train on the same inputs: z bit-identical, statistics ~1e-6."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
+    b = (torch.randn(Cout, generator=g) + 3.0).to(dev)  # |mean| >> std
+    gam, bet = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    wp = K.pack_weight(w, bf)
+    z = K.Act(K.nhwc(N, H, W, Cout, bf, dev))
+    res = K.conv_fwd_stats(K.Act(x), wp, Cout, 3, 1, z, bias=b)
+    assert res is not None
+    rm, rv = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    st = K.bn_part_finalize(res[0], res[1], Cout, gam, bet, rm, rv, 0.1, 1e-5)
+    z0 = K.Act(K.nhwc(N, H, W, Cout, bf, dev))
+    K.conv_fwd(K.Act(x), wp, Cout, 3, 1, z0, bias=b)
+    rm0, rv0 = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    st0 = K.bn_fwd_train(z0, gam, bet, rm0, rv0, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    assert torch.equal(z.buf, z0.buf)
+    zf = z.buf.double().reshape(-1, Cout)
+    assert relerr(st[0], zf.mean(0)) < 1e-6
+    assert relerr(st[1], 1.0 / (zf.var(0, unbiased=False) + 1e-5).sqrt()) < 2e-6
+    assert relerr(st, st0) < 2e-6 and relerr(rv, rv0) < 2e-6 and relerr(rm, rm0) < 2e-6
