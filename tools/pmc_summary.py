@@ -34,11 +34,14 @@ for k in sorted(set(fetch) | set(write), key=lambda k: -fetch.get(k, [0, 1])[0])
     out[k] = {"dispatches": n, "fetch_bytes_per_dispatch_corrected": 2 * f * 1024 / max(nf, 1),
               "write_bytes_per_dispatch": w * 1024 / max(nw, 1)}
 json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
-conv = [v for k, v in out.items() if "conv_fwd_kernel" in k]
+# the launches bench.py's roofline times (kinds fwd + dgrad): every forward-GEMM kernel variant
+FWD_KERNELS = ("conv_fwd_pipe_kernel", "conv_fwd_tap3_kernel", "conv_fwd_kernel")
+conv = [v for k, v in out.items() if any(f in k for f in FWD_KERNELS)]
 if conv:
     n = sum(v["dispatches"] for v in conv)
     tot = sum((v["fetch_bytes_per_dispatch_corrected"] + v["write_bytes_per_dispatch"]) * v["dispatches"] for v in conv)
-    json.dump({"kernel": "conv_fwd_kernel (all tile variants)", "dispatches": n,
+    json.dump({"kernel": "implicit-GEMM conv forward/dgrad (conv_fwd_pipe_kernel, conv_fwd_tap3_kernel)",
+               "dispatches": n,
                "hbm_bytes_per_launch": tot / n,
                "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB->bytes, averaged over dispatches of a 2-step bench run"},
               open(os.path.join(os.path.dirname(dst), "conv_traffic.json"), "w"), indent=1)
