@@ -93,8 +93,16 @@ class DGTrainer(Trainer):
         model([img, img2], cal_covstat=True)
         return cnt
 
+    def prepare_batch(self, batch):
+        """A `DenClsDataset.collate` RawDenClsBatch -> the reference's batch layout, with the
+        pixel augmentation run on this trainer's device; reference-layout batches pass through."""
+        from ..datasets.augment import DeviceAugment, RawDenClsBatch
+        if isinstance(batch, RawDenClsBatch):
+            return DeviceAugment(self.device)(batch)
+        return batch
+
     def train_step(self, model, loss, optimizer, batch, epoch):
-        imgs1, imgs2, gt_datas = batch
+        imgs1, imgs2, gt_datas = self.prepare_batch(batch)
         imgs1 = imgs1.to(self.device, non_blocking=True)
         imgs2 = imgs2.to(self.device, non_blocking=True)
         gt_cmaps = gt_datas[-1].to(self.device, non_blocking=True)
@@ -138,8 +146,18 @@ class DGTrainer(Trainer):
         optimizer.step()
         return loss_total.detach().item()
 
+    def _val_batch(self, batch):
+        """DenClsDataset val/test samples collated with batch size 1 carry the uint8 image and
+        the parameter record: run their pixel transforms on the device."""
+        img = batch[0]
+        if isinstance(img, torch.Tensor) and img.dtype == torch.uint8:
+            from ..datasets.augment import augment_den_cls
+            img1, img2 = augment_den_cls(img.to(self.device), batch[1])
+            return (img1, img2, *batch[2:])
+        return batch
+
     def val_step(self, model, batch):
-        img1, img2, gt, _, _ = batch
+        img1, img2, gt, _, _ = self._val_batch(batch)
         img1 = img1.to(self.device)
         img2 = img2.to(self.device)
         if self.mode == "isw":
@@ -151,7 +169,7 @@ class DGTrainer(Trainer):
         return np.abs(pred - n), {"mse": (pred - n) ** 2}
 
     def test_step(self, model, batch):
-        img1, _, gt, _, _ = batch
+        img1, _, gt, _, _ = self._val_batch(batch)
         pred = self.predict(model, img1.to(self.device))
         n = gt.shape[1]
         return {"mae": np.abs(pred - n), "mse": (pred - n) ** 2}

@@ -299,6 +299,20 @@ int dg_cat_combine(int dtype, const void* z1, int64_t ldz1, const void* z2, int6
                    const void* z3, int64_t ldz3, int N, int H, int W, int C, const float* bias,
                    void* z, int64_t ldz, float* part, void* stream);
 
+/* ---- device-side training augmentation (DenClsDataset, datasets/den_cls_dataset.py:29-35,
+ * 77-158) -------------------------------------------------------------------------------
+ * imgs: B uint8 RGB crops [B][H][W][3] (HBM-resident); params: [B][16] f32 per-sample
+ * decisions drawn on the host in the reference's RNG order (dgvcc_amd/datasets/augment.py):
+ * grey, hflip, ColorJitter (applied, op order, factors, uint8 hue shift), GaussianBlur
+ * (applied, 1-D weights), RandomAdjustSharpness (applied, factor).
+ * img1 = Normalize(ToTensor(grey/flip(img))), img2 = Normalize(ToTensor(more_transform(...)))
+ * as NCHW f32 [B][3][H][W], bit-identical to the PIL/torchvision host pipeline (see augment.hip).
+ * dg_block_map: bmap [B][h/16][w/16] = (16x16 block sums of dmap [B][h][w] > 0). */
+int64_t dg_augment_workspace(int B, int H, int W);
+int dg_augment_den_cls(const unsigned char* imgs, int B, int H, int W, const float* params,
+                       float* img1, float* img2, void* workspace, int64_t ws_bytes, void* stream);
+int dg_block_map(const float* dmap, int B, int h, int w, float* bmap, void* stream);
+
 /* ---- density head: 1x1 conv C->1 (+ReLU) --------------------------------------
  * den_head (models/models.py:60-62) / cls_head tail (models/models.py:241-242). */
 int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w,
