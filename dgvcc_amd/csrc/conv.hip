@@ -1182,7 +1182,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(WgArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int W9_XROWS = 72;
 
-template <int BCO>
+// WT = 1 (BCO 128): wave tile 64 co x 16 c (TI 4, TJ 1) instead of 32 x 32: the 9 taps' B
+// fragments are read once per 4 A fragments (fewer transposed LDS reads per MFMA).
+template <int BCO, int WT = 0>
 __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int BKP = 64, BC = 64;
   constexpr int RA = BCO * 2, RX = BC * 2;                    // bytes per LDS row
@@ -1193,7 +1195,8 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int N_INST = A_INST + X_INST;
   constexpr int A_BYTES = BKP * RA, X_BYTES = W9_XROWS * RX;
   constexpr int STAGE = A_BYTES + 3 * X_BYTES;
-  constexpr int TI = 2, TJ = BCO == 128 ? 2 : 1;             // wave tile: 32 co x 16*TJ c, 9 taps
+  constexpr bool WIDE = BCO == 128 && WT == 1;
+  constexpr int TI = WIDE ? 4 : 2, TJ = (BCO == 128 && !WIDE) ? 2 : 1;  // wave tile: 16*TI co x 16*TJ c, 9 taps
   __shared__ __attribute__((aligned(1024))) char smem[PSTAGES * STAGE];
 
   const int HW = a.H * a.W;
@@ -1252,8 +1255,8 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[tp][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-  const int wco = BCO == 128 ? (wid & 3) * 32 : (wid & 1) * 32;
-  const int wc = BCO == 128 ? (wid >> 2) * 32 : (wid >> 1) * 16;
+  const int wco = WIDE ? (wid & 1) * 64 : (BCO == 128 ? (wid & 3) * 32 : (wid & 1) * 32);
+  const int wc = WIDE ? (wid >> 1) * 16 : (BCO == 128 ? (wid >> 2) * 32 : (wid >> 1) * 16);
   const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
   const int hb = (p4 & 1) * 8;
 
@@ -1332,6 +1335,15 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
       }
 }
 
+static bool wg9_wide() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_WG9_TILE");
+    v = (e && e[0] == '0') ? 0 : 1;  // default: the 64 co x 16 c wave tile (A/B: +2% on the 128-co layers)
+  }
+  return v == 1;
+}
+
 static bool wg9_ok(int C, int Cout, int R, int S, int W, int pad) {
   return use_pipe() && R == 3 && S == 3 && pad == 1 && W % 64 == 0 && C % 64 == 0 && Cout % 64 == 0;
 }
@@ -1389,7 +1401,8 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
     if (a.stride == 1 && !a.whole_x && wg9_ok(a.C, a.Cout, a.R, a.S, a.W, a.pad)) {
       const int b9 = a.Cout % 128 == 0 ? 128 : 64;
       const dim3 g9((a.Cout / b9) * (a.C / 64) * a.splits);
-      if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
+      if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1>), g9, dim3(512), 0, st, a);
+      else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((conv_wgrad9_kernel<64>), g9, dim3(512), 0, st, a);
       done = true;
     } else if (use_wgrad_pipe()) {  // opt-in: measured slower than the register-staged kernel (round 1)
