@@ -57,3 +57,38 @@ def test_block_map(dev):
     d[d < 0.995] = 0
     ref = (d.reshape(3, 1, 4, 16, 3, 16).sum(dim=(3, 5)) > 0).float()
     assert torch.equal(block_map(d.to(dev)).cpu(), ref)
+
+
+def test_train_step_on_raw_batch(dev, tmp_path):
+    """DenClsDataset -> collate -> DGTrainer.train_step (GPU augmentation inside) on DGModel_final."""
+    import os
+    import random
+    from PIL import Image
+    from dgvcc_amd.datasets import DenClsDataset
+    from dgvcc_amd.losses import MSELoss
+    from dgvcc_amd.models.models import DGModel_final
+    from dgvcc_amd.optim import AdamW
+    from dgvcc_amd.trainers.dgtrainer import DGTrainer
+    rng = np.random.default_rng(2)
+    root = tmp_path / "ds"
+    (root / "train").mkdir(parents=True)
+    for i in range(2):
+        Image.fromarray(rng.integers(0, 256, (80, 96, 3), dtype=np.uint8)).save(root / "train" / f"a{i}.jpg")
+        np.save(root / "train" / f"a{i}.npy", np.stack([rng.uniform(0, 96, 9), rng.uniform(0, 80, 9)], 1))
+        np.save(root / "train" / f"a{i}_dmap.npy", rng.random((80, 96)).astype(np.float32) * 1e-3)
+    random.seed(0)
+    torch.manual_seed(0)
+    ds = DenClsDataset(str(root), 64, 1, "train", False, 16)
+    raw = DenClsDataset.collate([ds[0], ds[1]])
+    model = DGModel_final(pretrained=False).to(dev).set_precision("bf16").train()
+    opt = AdamW(model.parameters(), lr=1e-4)
+    cwd = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        tr = DGTrainer(2112, "t", dev, 1000, 10000, "final")
+        loss = tr.train_step(model, MSELoss(), opt, raw, 0)
+    finally:
+        os.chdir(cwd)
+    assert np.isfinite(loss)
+    img1, img2, (pts, dmaps, bmaps) = tr.prepare_batch(raw)
+    assert img1.shape == (2, 3, 64, 64) and bmaps.shape == (2, 1, 4, 4) and len(pts) == 2
