@@ -7,12 +7,25 @@
 // variance does not cancel when |mean| >> std.
 #include "dg_common.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
 constexpr int NT = 256;
 
 inline int bn_nblk(int M) { return std::max(1, std::min(1024, dg_cdiv(M, 64))); }
+// pooled BN backward partials: more, smaller blocks (each thread walks 2x2 windows; more
+// loads in flight per CU)
+inline int pool_nblk_cap() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_POOL_NBLK");
+    v = e ? atoi(e) : 2048;
+    if (v < 1) v = 1;
+  }
+  return v;
+}
+inline int pool_nblk(long long Mp) { return (int)std::max(1LL, std::min((long long)pool_nblk_cap(), (Mp + 31) / 32)); }
 
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_stats_partial(const T* __restrict__ z, long long ldz, int M, int C, int ppb,
@@ -384,10 +397,12 @@ __device__ __forceinline__ void bn_pool_bwd_load(const T* gp, long long ldgp, co
 #pragma unroll
   for (int e = 0; e < V; ++e) {
     float y[4];
+    bool on[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float t = fmaf(zv[k][e], cp.sc[e], cp.sf[e]);
-      if (act == 1) t = t > 0.f ? t : 0.f;
+      on[k] = t > 0.f;  // the ReLU mask of bn_bwd_load: fmaf(z, scale, shift) > 0
+      if (act == 1) t = on[k] ? t : 0.f;
       if (d) t *= d[e];
       y[k] = rnd_t<T>(t);
     }
@@ -396,7 +411,7 @@ __device__ __forceinline__ void bn_pool_bwd_load(const T* gp, long long ldgp, co
     for (int k = 0; k < 4; ++k) {
       if (k == am) gv[k][e] += gpv[e];
       if (d) gv[k][e] *= d[e];
-      if (act == 1 && !(fmaf(zv[k][e], cp.sc[e], cp.sf[e]) > 0.f)) gv[k][e] = 0.f;
+      if (act == 1 && !on[k]) gv[k][e] = 0.f;
     }
   }
 }
@@ -422,6 +437,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
   if (pl < rows) {
     ChanParams<V> cp;
     cp.load(c0, scale, shift, mean, invstd);
+#pragma unroll 2
     for (long long pp = p0 + pl; pp < p1; pp += rows) {
       long long pos[4];
       pool_window(pp, H, W, pos);
@@ -534,7 +550,7 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
 
 extern "C" int64_t dg_bn_workspace(int M, int C) {
   if (M <= 0 || C <= 0) return DG_ERR_INVALID;
-  return ((int64_t)bn_nblk(M) * 3 + 3) * C * 4;
+  return ((int64_t)std::max(bn_nblk(M), pool_nblk(M / 4)) * 3 + 3) * C * 4;
 }
 
 // C/V must divide NT (power of two <= 256): every thread then owns one channel chunk.
@@ -637,7 +653,7 @@ static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long
                             void* dz, long long lddz, float* dgamma, float* dbeta, float* dbias, void* ws,
                             hipStream_t st) {
   const long long M = (long long)N * H * W, Mp = M / 4;
-  const int nblk = bn_nblk((int)Mp);
+  const int nblk = pool_nblk(Mp);
   const long long ppb = (Mp + nblk - 1) / nblk;
   float* part = (float*)ws;
   float* coef = part + (long long)nblk * 3 * C;
