@@ -1505,20 +1505,30 @@ __global__ void im2col_c3_kernel(const float* __restrict__ img, int N, int H, in
 template <typename T>
 __global__ void im2col_c3_ex_kernel(const float* __restrict__ img, int N, int H, int W, int R, int S, int stride,
                                     int pad, int P, int Q, int Kpad, T* __restrict__ out) {
-  const long long total = (long long)N * P * Q * Kpad;
+  // one thread per (output pixel, 16-byte chunk of k); 32-bit index math (ABI checks the sizes)
+  constexpr int E = 16 / (int)sizeof(T);
+  const int nch = Kpad / E, PQ = P * Q, RS3 = R * S * 3;
+  const long long total = (long long)N * PQ * nch;
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < total;
        o += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(o % Kpad);
-    const long long m = o / Kpad;
-    float v = 0.f;
-    if (k < R * S * 3) {
-      const int c = k % 3, rs = k / 3, r = rs / S, s = rs % S;
-      const int n = (int)(m / ((long long)P * Q));
-      const int rem = (int)(m % ((long long)P * Q));
-      const int h = (rem / Q) * stride - pad + r, w = (rem % Q) * stride - pad + s;
-      if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) v = img[(((long long)n * 3 + c) * H + h) * W + w];
+    const int m = (int)(o / nch), chk = (int)(o - (long long)m * nch);
+    const int n = m / PQ, rem = m - n * PQ;
+    const int p = rem / Q, q = rem - p * Q;
+    const int h0 = p * stride - pad, w0 = q * stride - pad;
+    const float* base = img + (long long)n * 3 * H * W;
+    float v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int k = chk * E + e;
+      float x = 0.f;
+      if (k < RS3) {
+        const int rs = k / 3, c = k - 3 * rs, r = rs / S, s2 = rs - r * S;
+        const int h = h0 + r, w = w0 + s2;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) x = base[((long long)c * H + h) * W + w];
+      }
+      v[e] = x;
     }
-    out[o] = from_f<T>(v);
+    stv(out + (long long)m * Kpad + chk * E, v);
   }
 }
 
@@ -1779,8 +1789,9 @@ extern "C" int dg_im2col_c3(int dtype, const float* img, int N, int H, int W, in
   DG_REQUIRE(img && out && N > 0 && H > 0 && W > 0 && R > 0 && S > 0 && stride >= 1 && Kpad >= R * S * 3);
   const int P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
   DG_REQUIRE(P > 0 && Q > 0);
+  DG_SUPPORTED(Kpad % 8 == 0 && (long long)N * P * Q < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  const long long total = (long long)N * P * Q * Kpad;
+  const long long total = (long long)N * P * Q * (Kpad / (dtype == DG_BF16 ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(im2col_c3_ex_kernel<bf16>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
                        R, S, stride, pad, P, Q, Kpad, (bf16*)out);

@@ -182,6 +182,94 @@ __global__ __launch_bounds__(NT) void maxpool_gen_bwd(const T* __restrict__ x, l
   }
 }
 
+// The same pool recording each window's argmax (uint8 offset r*k + s of the first max,
+// same scan order and NaN rule): the backward is then a gather of at most ceil(k/st)^2
+// (index, gradient) pairs per input instead of re-scanning every overlapping window
+// (9 x-loads per window for the ResNet 3x3/2 stem pool).
+template <typename T>
+__global__ __launch_bounds__(NT) void maxpool_idx_fwd(const T* __restrict__ x, long long ldx, int N, int H, int W,
+                                                      int C, int k, int st, int pad, int P, int Q, T* __restrict__ y,
+                                                      long long ldy, unsigned char* __restrict__ idx) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const int total = N * P * Q * tpp;  // < 2^30 (checked by the ABI)
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int ch = i % tpp;
+    int t = i / tpp;
+    const int q = t % Q; t /= Q;
+    const int p = t % P;
+    const int n = t / P;
+    float m[V];
+    int am[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { m[e] = -INFINITY; am[e] = -1; }
+    for (int r = 0; r < k; ++r) {
+      const int h = p * st - pad + r;
+      if ((unsigned)h >= (unsigned)H) continue;
+      for (int s = 0; s < k; ++s) {
+        const int w = q * st - pad + s;
+        if ((unsigned)w >= (unsigned)W) continue;
+        float v[V];
+        ldv(x + ((long long)(n * H + h) * W + w) * ldx + ch * V, v);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (v[e] > m[e] || isnan(v[e]) || am[e] < 0) { m[e] = v[e]; am[e] = r * k + s; }
+      }
+    }
+    const long long o = (long long)(n * P + p) * Q + q;
+    stv(y + o * ldy + ch * V, m);
+    unsigned int pk[V / 4];
+#pragma unroll
+    for (int e = 0; e < V / 4; ++e)
+      pk[e] = (unsigned)am[4 * e] | ((unsigned)am[4 * e + 1] << 8) | ((unsigned)am[4 * e + 2] << 16) |
+              ((unsigned)am[4 * e + 3] << 24);
+    unsigned int* ip = reinterpret_cast<unsigned int*>(idx + o * C + ch * V);
+#pragma unroll
+    for (int e = 0; e < V / 4; ++e) ip[e] = pk[e];
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(NT) void maxpool_idx_bwd(const unsigned char* __restrict__ idx, const T* __restrict__ gy,
+                                                      long long ldgy, int N, int H, int W, int C, int k, int st,
+                                                      int pad, int P, int Q, T* __restrict__ gx, long long ldgx,
+                                                      int accumulate) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const int total = N * H * W * tpp;  // < 2^30 (checked by the ABI)
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int ch = i % tpp;
+    int t = i / tpp;
+    const int w = t % W; t /= W;
+    const int h = t % H;
+    const int n = t / H;
+    float acc[V];
+    T* dst = gx + ((long long)(n * H + h) * W + w) * ldgx + ch * V;
+    if (accumulate) ldv(dst, acc);
+    else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = 0.f;
+    }
+    const int plo = max(0, (h + pad - k + st) / st), phi = min(P - 1, (h + pad) / st);
+    const int qlo = max(0, (w + pad - k + st) / st), qhi = min(Q - 1, (w + pad) / st);
+    for (int p = plo; p <= phi; ++p)
+      for (int q = qlo; q <= qhi; ++q) {
+        const unsigned mine = (unsigned)((h - (p * st - pad)) * k + (w - (q * st - pad)));
+        const long long o = (long long)(n * P + p) * Q + q;
+        const unsigned int* ip = reinterpret_cast<const unsigned int*>(idx + o * C + ch * V);
+        unsigned int pk[V / 4];
+#pragma unroll
+        for (int e = 0; e < V / 4; ++e) pk[e] = ip[e];
+        float g[V];
+        ldv(gy + o * ldgy + ch * V, g);
+#pragma unroll
+        for (int e = 0; e < V; ++e)
+          if (((pk[e >> 2] >> (8 * (e & 3))) & 0xffu) == mine) acc[e] += g[e];
+      }
+    stv(dst, acc);
+  }
+}
+
 // Source taps of output index o along one axis.
 struct Tap { int i0, i1; float l1; };
 __device__ __forceinline__ Tap src_tap(int o, int in, int out, int scale, int mode) {
@@ -629,6 +717,47 @@ extern "C" int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void*
   else
     hipLaunchKernelGGL(maxpool_gen_bwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx,
                        (const float*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (float*)gx, ldgx, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_maxpool_fwd_idx(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int k, int stride,
+                                  int pad, void* y, int64_t ldy, unsigned char* idx, void* stream) {
+  DG_REQUIRE(x && y && idx && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && k <= 15 && stride > 0 && pad >= 0 &&
+             2 * pad <= k);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ldx % V == 0 && ldy % V == 0 && (long long)N * H * W * (C / V) < (1LL << 30));
+  const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * P * Q * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(maxpool_idx_fwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, H, W, C, k,
+                       stride, pad, P, Q, (bf16*)y, ldy, idx);
+  else
+    hipLaunchKernelGGL(maxpool_idx_fwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, H, W,
+                       C, k, stride, pad, P, Q, (float*)y, ldy, idx);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_maxpool_bwd_idx(int dtype, const unsigned char* idx, const void* gy, int64_t ldgy, int N, int H,
+                                  int W, int C, int k, int stride, int pad, void* gx, int64_t ldgx, int accumulate,
+                                  void* stream) {
+  DG_REQUIRE(idx && gy && gx && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && k <= 15 && stride > 0 && pad >= 0 &&
+             2 * pad <= k);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ldgy % V == 0 && ldgx % V == 0 && (long long)N * H * W * (C / V) < (1LL << 30));
+  const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * H * W * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(maxpool_idx_bwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, idx, (const bf16*)gy, ldgy, N, H,
+                       W, C, k, stride, pad, P, Q, (bf16*)gx, ldgx, accumulate);
+  else
+    hipLaunchKernelGGL(maxpool_idx_bwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, idx, (const float*)gy, ldgy, N,
+                       H, W, C, k, stride, pad, P, Q, (float*)gx, ldgx, accumulate);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -69,6 +69,17 @@ __global__ __launch_bounds__(NT) void relu_bwd_kernel(const T* __restrict__ g, l
 }
 
 // ---------------------------------------------------------------- IN apply --
+// Grid for the channel-stationary elementwise kernels below: gridDim.x * NT is a multiple of
+// tpp = C/V, so every thread keeps one channel chunk c0 for its whole pixel loop and holds
+// that chunk's per-(n, c) parameters in registers, reloading them only when n changes.
+inline int cs_grid(long long total, int tpp) {
+  int q = tpp, a = NT;  // q = tpp / gcd(tpp, NT)
+  while (a) { const int t = q % a; q = a; a = t; }
+  q = tpp / q;
+  const int g = ew_grid(total);
+  return (g + q - 1) / q * q;
+}
+
 // y = act((x - mu[n,c]) * is[n,c] * gamma[c] + beta[c])
 template <typename T>
 __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, long long ldx, int N, int HW, int C,
@@ -77,18 +88,30 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
                                                       int act, T* __restrict__ y, long long ldy) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const long long total = (long long)N * HW * tpp;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const long long p = i / tpp;
-    const int c0 = (int)(i % tpp) * V;
-    const int n = (int)(p / HW);
+  const int gt = blockIdx.x * NT + threadIdx.x;
+  const int c0 = (gt % tpp) * V;
+  const int pstride = gridDim.x * NT / tpp;
+  const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
+  float ga[V], be[V], m[V], s[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    ga[e] = gamma ? gamma[c0 + e] : 1.f;
+    be[e] = gamma ? beta[c0 + e] : 0.f;
+  }
+  int cur = -1;
+  for (int p = gt / tpp; p < M; p += pstride) {
+    const int n = p / HW;
+    if (n != cur) {
+      cur = n;
+#pragma unroll
+      for (int e = 0; e < V; ++e) { m[e] = mu[n * C + c0 + e]; s[e] = is[n * C + c0 + e]; }
+    }
     float v[V];
     ldv(x + p * ldx + c0, v);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int nc = n * C + c0 + e;
-      float t = (v[e] - mu[nc]) * is[nc];
-      if (gamma) t = fmaf(t, gamma[c0 + e], beta[c0 + e]);
+      float t = (v[e] - m[e]) * s[e];
+      if (gamma) t = fmaf(t, ga[e], be[e]);
       if (act == 1) t = t > 0.f ? t : 0.f;
       v[e] = t;
     }
@@ -140,28 +163,44 @@ __global__ __launch_bounds__(NT) void in_bwd_partial(const T* __restrict__ g, lo
 }
 
 // coef[n][c] = (k1, k2, k3): dx = k1*g - k2*xhat - k3 ; dgamma/dbeta summed over n
-__global__ void in_bwd_finalize(const float* __restrict__ part, int N, int nb, int HW, int C,
-                                const float* __restrict__ is, const float* __restrict__ gamma, float* dgamma,
-                                float* dbeta, float* __restrict__ coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
+// Block of FIN_CH channels x FIN_KS partial slices: the nb partials of each (n, c) are
+// summed by FIN_KS threads in parallel (coalesced across c) and combined in LDS in a fixed
+// order, so the result is deterministic.
+constexpr int FIN_CH = 16, FIN_KS = 16;
+__global__ __launch_bounds__(FIN_CH * FIN_KS) void in_bwd_finalize(const float* __restrict__ part, int N, int nb,
+                                                                   int HW, int C, const float* __restrict__ is,
+                                                                   const float* __restrict__ gamma, float* dgamma,
+                                                                   float* dbeta, float* __restrict__ coef) {
+  __shared__ double sh[2][FIN_KS][FIN_CH];
+  const int cl = threadIdx.x % FIN_CH, ks = threadIdx.x / FIN_CH;
+  const int c = blockIdx.x * FIN_CH + cl;
   double tg = 0.0, tx = 0.0;
   for (int n = 0; n < N; ++n) {
     double a = 0.0, b = 0.0;
-    for (int k = 0; k < nb; ++k) {
-      const float* o = part + ((long long)n * nb + k) * 2 * C;
-      a += o[c]; b += o[C + c];
+    if (c < C)
+      for (int k = ks; k < nb; k += FIN_KS) {
+        const float* o = part + ((long long)n * nb + k) * 2 * C;
+        a += o[c]; b += o[C + c];
+      }
+    sh[0][ks][cl] = a; sh[1][ks][cl] = b;
+    __syncthreads();
+    if (ks == 0 && c < C) {
+      a = 0.0; b = 0.0;
+      for (int r = 0; r < FIN_KS; ++r) { a += sh[0][r][cl]; b += sh[1][r][cl]; }
+      tg += a; tx += b;
+      const float gm = gamma ? gamma[c] : 1.f;
+      const float k1 = gm * is[n * C + c];
+      float* cf = coef + ((long long)n * C + c) * 3;
+      cf[0] = k1;
+      cf[1] = (float)(k1 * b / HW);
+      cf[2] = (float)(k1 * a / HW);
     }
-    tg += a; tx += b;
-    const float gm = gamma ? gamma[c] : 1.f;
-    const float k1 = gm * is[n * C + c];
-    float* cf = coef + ((long long)n * C + c) * 3;
-    cf[0] = k1;
-    cf[1] = (float)(k1 * b / HW);
-    cf[2] = (float)(k1 * a / HW);
+    __syncthreads();
   }
-  if (dgamma) dgamma[c] = (float)tx;
-  if (dbeta) dbeta[c] = (float)tg;
+  if (ks == 0 && c < C) {
+    if (dgamma) dgamma[c] = (float)tx;
+    if (dbeta) dbeta[c] = (float)tg;
+  }
 }
 
 template <typename T>
@@ -171,21 +210,31 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
                                                    T* __restrict__ dx, long long lddx, int accumulate) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const long long total = (long long)N * HW * tpp;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const long long p = i / tpp;
-    const int c0 = (int)(i % tpp) * V;
-    const int n = (int)(p / HW);
+  const int gt = blockIdx.x * NT + threadIdx.x;
+  const int c0 = (gt % tpp) * V;
+  const int pstride = gridDim.x * NT / tpp;
+  const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
+  float m[V], s[V], k1[V], k2[V], k3[V];
+  int cur = -1;
+  for (int p = gt / tpp; p < M; p += pstride) {
+    const int n = p / HW;
+    if (n != cur) {
+      cur = n;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int nc = n * C + c0 + e;
+        m[e] = mu[nc]; s[e] = is[nc];
+        k1[e] = coef[nc * 3]; k2[e] = coef[nc * 3 + 1]; k3[e] = coef[nc * 3 + 2];
+      }
+    }
     float gv[V], xv[V], o[V];
     ldv(g + p * ldg + c0, gv);
     ldv(x + p * ldx + c0, xv);
     if (accumulate) ldv(dx + p * lddx + c0, o);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int nc = n * C + c0 + e;
-      const float* cf = coef + (long long)nc * 3;
-      const float xh = (xv[e] - mu[nc]) * is[nc];
-      const float d = cf[0] * gv[e] - cf[1] * xh - cf[2];
+      const float xh = (xv[e] - m[e]) * s[e];
+      const float d = k1[e] * gv[e] - k2[e] * xh - k3[e];
       o[e] = accumulate ? o[e] + d : d;
     }
     stv(dx + p * lddx + c0, o);
@@ -239,14 +288,15 @@ extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, i
   DG_REQUIRE(x && y && mean && invstd && N > 0 && HW > 0 && C > 0 && (!gamma || beta));
   DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
   const int V = dtype == DG_BF16 ? 8 : 4;
-  DG_SUPPORTED(VOK(dtype, C, ldx) && VOK(dtype, C, ldy));
-  hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * HW * (C / V);
+  DG_SUPPORTED(VOK(dtype, C, ldx) && VOK(dtype, C, ldy) && total < (1LL << 30));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = cs_grid(total, C / V);
   if (dtype == DG_BF16)
-    hipLaunchKernelGGL(in_apply_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, HW, C,
+    hipLaunchKernelGGL(in_apply_kernel<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (bf16*)y, ldy);
   else
-    hipLaunchKernelGGL(in_apply_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, HW, C,
+    hipLaunchKernelGGL(in_apply_kernel<float>, dim3(grid), dim3(NT), 0, st, (const float*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (float*)y, ldy);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -266,29 +316,30 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
   DG_REQUIRE(g && x && dx && mean && invstd && workspace && N > 0 && HW > 0 && C > 0);
   DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
   const int V = dtype == DG_BF16 ? 8 : 4;
-  DG_SUPPORTED(VOK(dtype, C, ldg) && VOK(dtype, C, ldx) && VOK(dtype, C, lddx) && C / V <= NT);
+  const long long total = (long long)N * HW * (C / V);
+  DG_SUPPORTED(VOK(dtype, C, ldg) && VOK(dtype, C, ldx) && VOK(dtype, C, lddx) && C / V <= NT &&
+               total < (1LL << 30));
   hipStream_t st = (hipStream_t)stream;
   const int nb = in_nb(HW), ppb = dg_cdiv(HW, nb);
   float* part = (float*)workspace;
   float* coef = part + (long long)N * nb * 2 * C;
-  const long long total = (long long)N * HW * (C / V);
+  const int grid = cs_grid(total, C / V);
+  const dim3 fgrid(dg_cdiv(C, FIN_CH)), fblk(FIN_CH * FIN_KS);
   if (dtype == DG_BF16) {
     hipLaunchKernelGGL(in_bwd_partial<bf16>, dim3(nb, N), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x, ldx,
                        HW, C, ppb, mean, invstd, part);
     DG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, part, N, nb, HW, C, invstd, gamma,
-                       dgamma, dbeta, coef);
+    hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
     DG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(in_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x,
+    hipLaunchKernelGGL(in_bwd_apply<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x,
                        ldx, N, HW, C, mean, invstd, coef, (bf16*)dx, lddx, accumulate);
   } else {
     hipLaunchKernelGGL(in_bwd_partial<float>, dim3(nb, N), dim3(NT), 0, st, (const float*)g, ldg, (const float*)x,
                        ldx, HW, C, ppb, mean, invstd, part);
     DG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(in_bwd_finalize, dim3(dg_cdiv(C, 256)), dim3(256), 0, st, part, N, nb, HW, C, invstd, gamma,
-                       dgamma, dbeta, coef);
+    hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
     DG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(in_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+    hipLaunchKernelGGL(in_bwd_apply<float>, dim3(grid), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)x, ldx, N, HW, C, mean, invstd, coef, (float*)dx, lddx, accumulate);
   }
   DG_CHECK_LAUNCH();

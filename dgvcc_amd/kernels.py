@@ -407,6 +407,19 @@ def maxpool_k_bwd(x: Act, gy: Act, k: int, stride: int, pad: int, gx: Act, accum
          gx.ptr, gx.ld, int(accumulate), stream())
 
 
+def maxpool_k_fwd_idx(x: Act, k: int, stride: int, pad: int, y: Act) -> torch.Tensor:
+    """maxpool_k_fwd that also records each window's argmax (uint8 [N,P,Q,C]) for maxpool_k_bwd_idx."""
+    idx = torch.empty((y.N, y.H, y.W, x.C), dtype=torch.uint8, device=x.buf.device)
+    call("dg_maxpool_fwd_idx", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, k, stride, pad, y.ptr, y.ld,
+         ptr(idx), stream())
+    return idx
+
+
+def maxpool_k_bwd_idx(idx: torch.Tensor, gy: Act, k: int, stride: int, pad: int, gx: Act, accumulate=False):
+    call("dg_maxpool_bwd_idx", gx.dt, ptr(idx), gy.ptr, gy.ld, gx.N, gx.H, gx.W, gx.C, k, stride, pad,
+         gx.ptr, gx.ld, int(accumulate), stream())
+
+
 def bn_add_apply(z1: Act, st1, z2: Act, st2, act: int, y: Act):
     """y = act(bn1(z1) + (bn2(z2) if st2 is not None else z2)) — Bottleneck join."""
     call("dg_bn_add_apply", z1.dt, z1.ptr, z1.ld, z1.M, z1.C, ptr(st1[2]), ptr(st1[3]), z2.ptr,

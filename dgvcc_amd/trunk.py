@@ -324,11 +324,11 @@ class CounterPlan:
             st0 = self.stem.forward(z0, y0, training, ACT_RELU)
         Pm, Qm = K.conv_out(P, 3, 2, 1), K.conv_out(Q, 3, 2, 1)
         x = Act(K.nhwc(N, Pm, Qm, 64, dt, dev))
-        K.maxpool_k_fwd(y0, 3, 2, 1, x)
+        pidx = K.maxpool_k_fwd_idx(y0, 3, 2, 1, x)
         for b in self.blocks:
             x = b.forward(x, training, tape, ws)
         if tape is not None:
-            tape[self] = dict(col=col, z0=z0, st0=st0, y0=y0, w0=w0, shape=(N, H, W), dt=dt)
+            tape[self] = dict(col=col, z0=z0, st0=st0, y0=y0, w0=w0, pidx=pidx, shape=(N, H, W), dt=dt)
         return x, ws
 
     def head_fwd(self, x: Act, training: bool, tape: dict | None):
@@ -397,7 +397,7 @@ class CounterPlan:
         # maxpool, stem
         y0 = s["y0"]
         g_y0 = Act(torch.empty_like(y0.buf))
-        K.maxpool_k_bwd(y0, g_x, 3, 2, 1, g_y0)
+        K.maxpool_k_bwd_idx(s["pidx"], g_x, 3, 2, 1, g_y0)
         g_z0 = Act(torch.empty_like(s["z0"].buf))
         if self.stem.kind == "iw":
             w0 = s["w0"]

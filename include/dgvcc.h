@@ -280,6 +280,13 @@ int dg_maxpool_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, i
 int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy, int N,
                    int H, int W, int C, int k, int stride, int pad, void* gx, int64_t ldgx,
                    int accumulate, void* stream);
+/* The same pool recording the argmax: idx [N,P,Q,C] uint8 = r*k + s of each window's first
+ * maximum (k <= 15); the backward gathers (idx, gy) pairs instead of re-scanning windows. */
+int dg_maxpool_fwd_idx(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int k,
+                       int stride, int pad, void* y, int64_t ldy, unsigned char* idx, void* stream);
+int dg_maxpool_bwd_idx(int dtype, const unsigned char* idx, const void* gy, int64_t ldgy, int N,
+                       int H, int W, int C, int k, int stride, int pad, void* gx, int64_t ldgx,
+                       int accumulate, void* stream);
 /* mode: 0 bilinear(align_corners=False), 1 bilinear(align_corners=True), 2 nearest */
 int dg_upsample_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int scale,
                     int mode, void* y, int64_t ldy, void* stream);

@@ -141,6 +141,13 @@ def test_maxpool_3x3_s2(dev, dtype, shape):
     assert torch.equal(to_nchw(y.buf.float()).cpu(), yr.detach())
     tol = 1e-6 if dtype == torch.float32 else 1e-2  # bf16: sums of up to 4 window grads
     assert relerr(to_nchw(gx.buf.float()), xr.grad) < tol
+    # argmax-recording variant: identical pooled values and gradients (same summation order)
+    y2 = K.Act(K.nhwc(N, P, Q, C, dtype, dev))
+    idx = K.maxpool_k_fwd_idx(xd, 3, 2, 1, y2)
+    gx2 = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+    K.maxpool_k_bwd_idx(idx, K.Act(to_nhwc(gy).to(dev, dtype)), 3, 2, 1, gx2)
+    torch.cuda.synchronize()
+    assert torch.equal(y2.buf, y.buf) and torch.equal(gx2.buf, gx.buf)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
