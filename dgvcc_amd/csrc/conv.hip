@@ -26,7 +26,9 @@ struct FwdArgs {
   const float* bias;
   char* y; long long ldy;
   int accumulate;
-  float* part;  // bf16 pipe/tap3 only: BN statistics partials [ceil(M/256)][3][Cout] (NULL = none)
+  float* part = nullptr;   // bf16 pipe/tap3 only: BN statistics partials [ceil(M/256)][3][Cout]
+  int ksplit = 1;          // bf16 pipe only: > 1 splits the K loop over blocks, f32 partials into kpart
+  float* kpart = nullptr;  // [ksplit][M][Cout]; splitk_reduce_kernel finishes bias/accumulate/stats
 };
 
 // Sum over the 16 lanes of a DPP row, result in every lane: quad butterflies (xor 1, 2)
@@ -468,7 +470,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   const int HW = a.H * a.W;
   const int M = a.N * HW;
   const int nco = a.Cout / BN;
-  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int ntile = (M + PBM - 1) / PBM * nco;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / ntile;  // K-slice of a split-K launch (0 otherwise)
+  bid -= split * ntile;
   const int co0 = (bid % nco) * BN;
   const int px0 = (bid / nco) * PBM;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -501,12 +506,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   for (int i = 0; i < AI; ++i) aoff[i] = (unsigned)((((wid * AI + i) * 8 + lrow) * ldw + gchunk * 8) * 2);
 
   const int CB = a.C / BK;
-  const int KT = a.R * a.S * CB;
+  const int KTA = a.R * a.S * CB;
+  const int kt0 = (int)((long long)split * KTA / a.ksplit);
+  const int KT = (int)((long long)(split + 1) * KTA / a.ksplit) - kt0;  // this block's K-steps
   const unsigned cbytes = (unsigned)(gchunk * 16);
 
-#define PIPE_ISSUE(t_, stage_) \
+#define PIPE_ISSUE(u_, stage_) \
   do { \
-    const int rs = (t_) / CB, cb = (t_) - rs * CB; \
+    const int rs = (kt0 + (u_)) / CB, cb = (kt0 + (u_)) - rs * CB; \
     const int r = rs / a.S, s = rs - r * a.S; \
     char* As = smem + (stage_) * STAGE; \
     char* Bs = As + BN * 128; \
@@ -568,6 +575,17 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   }
 #undef PIPE_ISSUE
 
+  if (a.ksplit > 1) {  // raw f32 partial sums of this K-slice
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      float* kp = a.kpart + ((long long)split * M + px) * a.Cout + co0 + wco + 4 * fc;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) *(f4v*)(kp + 16 * i) = acc[i][j];
+    }
+    return;
+  }
   T* y = (T*)a.y;
   bool valid[TJ];
 #pragma unroll
@@ -597,6 +615,128 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   if (a.part)
     epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / PBM) * 3 * a.Cout, a.Cout,
                              co0, tid, fr, fc);
+}
+
+// Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored
+// as T, and — when part != NULL — the BN statistics partials of the stored values in the
+// epilogue's format (one (n, mean, M2) row per 256-pixel block, two passes over registers).
+// Block = 256 pixels x 64 channels, 1024 threads: one channel quad x 4 pixels (stride 64)
+// each, so even the smallest layers put ~16 waves per tile in flight on the loads.
+constexpr int SKR_PL = 64;
+template <typename T>
+__global__ __launch_bounds__(1024) void splitk_reduce_kernel(const float* __restrict__ kpart, int ksplit, int M,
+                                                             int Cout, const float* __restrict__ bias,
+                                                             T* __restrict__ y, long long ldy, int accumulate,
+                                                             float* __restrict__ part) {
+  constexpr int PXT = 256 / SKR_PL;
+  __shared__ float sh[2][SKR_PL][64];
+  const int tid = threadIdx.x, cq = tid & 15, pl = tid >> 4;
+  const int px0 = blockIdx.x * 256, c0 = blockIdx.y * 64 + 4 * cq;
+  const long long slab = (long long)M * Cout;
+  float b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (bias) {
+    const f4v bv = *(const f4v*)(bias + c0);
+    b[0] = bv[0]; b[1] = bv[1]; b[2] = bv[2]; b[3] = bv[3];
+  }
+  float v[PXT][4];
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < PXT; ++k) {
+    const int px = px0 + pl + SKR_PL * k;
+    if (px >= M) {
+      v[k][0] = v[k][1] = v[k][2] = v[k][3] = 0.f;
+      continue;
+    }
+    const float* src = kpart + (long long)px * Cout + c0;
+    f4v a = *(const f4v*)src;
+    int sp = 1;
+    for (; sp + 1 < ksplit; sp += 2) {  // two slabs in flight per step
+      const f4v t0 = *(const f4v*)(src + sp * slab);
+      const f4v t1 = *(const f4v*)(src + (sp + 1) * slab);
+      a[0] += t0[0]; a[1] += t0[1]; a[2] += t0[2]; a[3] += t0[3];
+      a[0] += t1[0]; a[1] += t1[1]; a[2] += t1[2]; a[3] += t1[3];
+    }
+    if (sp < ksplit) {
+      const f4v t0 = *(const f4v*)(src + sp * slab);
+      a[0] += t0[0]; a[1] += t0[1]; a[2] += t0[2]; a[3] += t0[3];
+    }
+    float o[4] = {a[0] + b[0], a[1] + b[1], a[2] + b[2], a[3] + b[3]};
+    T* dst = y + (long long)px * ldy + c0;
+    if (accumulate) {
+      float q[4];
+      ld4(dst, q);
+      o[0] += q[0]; o[1] += q[1]; o[2] += q[2]; o[3] += q[3];
+    }
+    st4(dst, o);
+    ++cnt;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      v[k][r] = std::is_same<T, bf16>::value ? bf2f(f2bf(o[r])) : o[r];  // the stored value
+      s[r] += v[k][r];
+    }
+  }
+  if (!part) return;
+  const int n = min(256, M - px0);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sh[0][pl][4 * cq + r] = s[r];
+  __syncthreads();
+  float mean[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = 0.f;
+    for (int l = 0; l < SKR_PL; ++l) t += sh[0][l][4 * cq + r];
+    mean[r] = t / (float)n;
+  }
+  float q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < PXT; ++k)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = v[k][r] - mean[r];
+      q[r] = (k < cnt) ? fmaf(d, d, q[r]) : q[r];
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) sh[1][pl][4 * cq + r] = q[r];
+  __syncthreads();
+  if (pl == 0) {
+    float* row = part + (long long)blockIdx.x * 3 * Cout;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float m2 = 0.f;
+      for (int l = 0; l < SKR_PL; ++l) m2 += sh[1][l][4 * cq + r];
+      row[c0 + r] = (float)n;
+      row[Cout + c0 + r] = mean[r];
+      row[2 * Cout + c0 + r] = m2;
+    }
+  }
+}
+
+// K-slices for a pipelined bf16 forward whose tile grid cannot fill the chip (deep
+// layers at small batch: 3k-25k pixels): the split minimising a cost model of the K loop
+// against the reduce traffic, keeping one wave of blocks (<= 256, one 128-KB-LDS block per
+// CU) and at least 3 K-steps per slice.
+static int fwd_ksplit(long long M, int Cout, int C, int R, int S) {
+  const char* e = getenv("DGVCC_SPLITK");
+  if (e && e[0] == '0') return 1;
+  if (C % 64 != 0) return 1;
+  const int BN = Cout % 256 == 0 ? 256 : (Cout % 128 == 0 ? 128 : 64);
+  if (Cout == 64 || BN == 64) return 1;
+  const long long nblk = (M + 255) / 256 * (Cout / BN);
+  if (nblk >= 128) return 1;
+  const int KT = R * S * (C / 64);
+  // cost model (us), measured on MI355X: ~2.2 us per K-step of a 256x256 tile (1.2 for
+  // 128-wide), one wave of blocks; the reduce moves 8 B per partial element at ~4 TB/s.
+  const double tstep = BN == 256 ? 2.2 : 1.2;
+  const double red = (double)M * Cout * 8.0 / 4.0e6;
+  int best = 1;
+  double tbest = KT * tstep;
+  const int smax = (int)std::min<long long>(256 / nblk, KT / 3);
+  for (int ks = 2; ks <= std::min(smax, 32); ++ks) {
+    const double t = (double)((KT + ks - 1) / ks) * tstep + 3.0 + ks * red;
+    if (t < tbest) { tbest = t; best = ks; }
+  }
+  return best;
 }
 
 static int pipe_var() {
@@ -767,7 +907,15 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         else if (var == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2>), dim3(G_), dim3(512), 0, st, a); \
         else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 0>), dim3(G_), dim3(512), 0, st, a); \
       } while (0)
-      if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
+      if (a.ksplit > 1) {  // BN and stage count as the unsplit choice below
+        const unsigned g = (unsigned)(np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : 128)) * a.ksplit);
+        if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, g);
+        else PIPE_LAUNCH(128, 3, g);
+        DG_CHECK_LAUNCH();
+        hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3((unsigned)dg_cdiv(M, 256), a.Cout / 64), dim3(1024), 0, st,
+                           (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (bf16*)a.y, a.ldy, a.accumulate,
+                           a.part);
+      } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
         hipLaunchKernelGGL(conv_fwd_tap3_kernel, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
@@ -1602,6 +1750,39 @@ extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, i
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, 0, part};
   return launch_fwd<bf16>(a, (hipStream_t)stream);
+}
+
+extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
+  const long long M = (long long)N * H * W;
+  if (dtype != DG_BF16 || !fwd_has_epi_stats(C, Cout, C, R, S)) return 0;
+  const int ks = fwd_ksplit(M, Cout, C, R, S);
+  return ks > 1 ? (int64_t)ks * M * Cout * 4 : 0;
+}
+
+// dg_conv_fwd / dg_conv_fwd_stats with a workspace: part may be NULL (no statistics);
+// a workspace of dg_conv_fwd_workspace bytes lets a small-grid shape split its K loop.
+extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                              int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
+                              int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream) {
+  DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
+  DG_SUPPORTED(dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0));
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
+  DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
+  if (part) DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate, part};
+  if (dtype == DG_BF16 && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
+    const long long M = (long long)N * H * W;
+    const int ks = fwd_ksplit(M, Cout, C, R, S);
+    if (ks > 1 && ws_bytes >= (int64_t)ks * M * Cout * 4) {
+      a.ksplit = ks;
+      a.kpart = (float*)workspace;
+    }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
 }
 
 extern "C" int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream) {

@@ -25,10 +25,45 @@ from .kernels import Act
 ACT_NONE, ACT_RELU = 0, 1
 
 
+_FROZEN_GEN = [0]
+
+
+def invalidate_frozen():
+    """Weights may have changed behind torch's back (a train()/eval() switch, a fused
+    optimizer step writing the flat parameter buffer through a raw pointer)."""
+    _FROZEN_GEN[0] += 1
+
+
+def frozen(owner, name, srcs, build):
+    """Eval-mode memo of a weight-derived tensor (packed filters, BN scale/shift): rebuilt
+    when a source tensor is replaced or modified in place, or after invalidate_frozen().
+    Saves the per-frame repacking and the per-layer running-stat math of evaluation."""
+    key = (_FROZEN_GEN[0],) + tuple((t.data_ptr(), t._version) for t in srcs)
+    memo = owner.__dict__.setdefault("_frozen", {})
+    ent = memo.get(name)
+    if ent is None or ent[0] != key:
+        ent = (key, build())
+        memo[name] = ent
+    return ent[1]
+
+
+def bn_eval_cached(owner, bn: nn.BatchNorm2d) -> torch.Tensor:
+    return frozen(owner, "bn_eval", (bn.weight, bn.bias, bn.running_mean, bn.running_var),
+                  lambda: K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                                          bn.running_var, bn.eps))
+
+
 def _bn_momentum(bn: nn.BatchNorm2d) -> float:
     if bn.momentum is None:  # cumulative moving average (torch semantics)
         return 1.0 / float(bn.num_batches_tracked.item())
     return float(bn.momentum)
+
+
+def _ident_stats(C, dev):
+    st = torch.zeros((4, C), dtype=torch.float32, device=dev)
+    st[1].fill_(1.0)
+    st[2].fill_(1.0)
+    return st
 
 
 class ConvLayer:
@@ -76,7 +111,8 @@ class ConvLayer:
         bn = self.bn
         if stem:
             N, _, H, W = x.shape
-            wp = K.pack_weight(self.conv.weight.detach(), dt, cpad=3, row_len=32)
+            build = lambda: K.pack_weight(self.conv.weight.detach(), dt, cpad=3, row_len=32)  # noqa: E731
+            wp = build() if training else frozen(self, ("stem", dt), (self.conv.weight,), build)
             z = Act(K.nhwc(N, H, W, self.Cout, dt, x.device))
             part, nblk = K.stem_fwd(x, wp, bias, z)
             if training:
@@ -84,13 +120,12 @@ class ConvLayer:
                 stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                            bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
             else:
-                stats = K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
-                                        bn.running_var, bn.eps)
+                stats = bn_eval_cached(self, bn)
             self._apply(z, stats, out, drop, pool)
             if tape is not None:
                 tape[self] = (x, z, stats, wp, drop, training)
             return
-        wp = self._pack(dt)
+        wp = self._pack(dt) if training else frozen(self, ("w", dt), (self.conv.weight,), lambda: self._pack(dt))
         z = Act(K.nhwc(x.N, x.H, x.W, self.Cout, dt, x.buf.device))
         epi = None
         if self.first:
@@ -111,13 +146,9 @@ class ConvLayer:
                 stats = K.bn_fwd_train(z, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                                        bn.running_var, _bn_momentum(bn), bn.eps)
             else:
-                stats = K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
-                                        bn.running_var, bn.eps)
+                stats = bn_eval_cached(self, bn)
         else:
-            C = self.Cout
-            stats = torch.zeros((4, C), dtype=torch.float32, device=x.buf.device)
-            stats[1].fill_(1.0)
-            stats[2].fill_(1.0)
+            stats = frozen(self, ("ident", x.buf.device), (), lambda: _ident_stats(self.Cout, x.buf.device))
         self._apply(z, stats, out, drop, pool)
         if tape is not None:
             tape[self] = (x, z, stats, wp, drop, training)
@@ -246,7 +277,8 @@ class CatConvLayer(ConvLayer):
         w = self.conv.weight.detach()
         zs, wps, lo = [], [], 0
         for part in x.parts:
-            wp = K.pack_weight(w[:, lo:lo + part.C].contiguous(), dt)
+            build = lambda lo=lo, c=part.C: K.pack_weight(w[:, lo:lo + c].contiguous(), dt)  # noqa: E731
+            wp = build() if training else frozen(self, ("cat", dt, lo), (self.conv.weight,), build)
             zk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dt, dev))
             K.conv_fwd(part, wp, self.Cout, 1, 0, zk)
             zs.append(zk)
@@ -264,8 +296,7 @@ class CatConvLayer(ConvLayer):
             stats = K.bn_part_finalize(part, rows, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                        bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
         else:
-            stats = K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
-                                    bn.running_var, bn.eps)
+            stats = bn_eval_cached(self, bn)
         K.bn_apply(z, stats, self.act, out, drop)
         if tape is not None:
             tape[self] = (x, z, stats, wps, drop, training)
@@ -539,7 +570,9 @@ class MemRead:
     def __init__(self, mem: nn.Parameter):
         self.mem = mem  # [1, k, slots]
 
-    def packs(self, dt):
+    def packs(self, dt, training=True):
+        if not training:
+            return frozen(self, ("packs", dt), (self.mem,), lambda: self.packs(dt))
         m = self.mem.detach()[0]  # [k, slots]
         k, S = m.shape
         scale = 1.0 / float(k) ** 0.5
@@ -689,7 +722,7 @@ class SinglePlan(_Heads):
         st = {"sub": sub, "yden": yden, "cat": cat}
         y = yden
         if self.memr is not None:
-            memT_s, mem_p, scale = self.memr.packs(dt)
+            memT_s, mem_p, scale = self.memr.packs(dt, training)
             L = self.memr.logits(yden, memT_s, dt)
             P = Act(torch.empty_like(L.buf))
             K.call("dg_softmax_fwd", L.dt, L.ptr, L.M, L.C, P.ptr, K.stream())

@@ -99,9 +99,24 @@ def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
     flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * Cout
     es = x.buf.element_size()
     nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout * (2 if accumulate else 1))  # x, w, y (+y read)
-    _timed(kind, flops, lambda: call("dg_conv_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
-                                     Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate),
-                                     stream()), nbytes)
+    ws, work = _fwd_workspace(x, Cout, R)
+    _timed(kind, flops, lambda: call("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
+                                     Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate), None,
+                                     ptr(work), ws, stream()), nbytes)
+
+
+_FWD_WS: dict = {}
+
+
+def _fwd_workspace(x: Act, Cout: int, R: int):
+    """Split-K partials for small-grid forward/dgrad shapes (deep layers at small batch)."""
+    key = (x.dt, x.N, x.H, x.W, x.C, Cout, R)
+    ws = _FWD_WS.get(key)
+    if ws is None:
+        ws = _FWD_WS[key] = query("dg_conv_fwd_workspace", x.dt, x.N, x.H, x.W, x.C, Cout, R, R)
+    if ws == 0:
+        return 0, None
+    return ws, torch.empty(ws, dtype=torch.uint8, device=x.buf.device)
 
 
 def flip_weight(wp: torch.Tensor, Cout: int, C: int, R: int) -> torch.Tensor:
@@ -175,17 +190,19 @@ def conv_fwd_stats(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act
     nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout)
     res = []
 
-    def launch():
-        res.append(lib_call_status("dg_conv_fwd_stats", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
-                                   R, R, pad, ptr(bias), y.ptr, y.ld, ptr(part), stream()))
-
     if x.dt != 1 or _EPI_STATS_OFF:
         return None
+    ws, work = _fwd_workspace(x, Cout, R)
+
+    def launch():
+        res.append(lib_call_status("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
+                                   R, R, pad, ptr(bias), y.ptr, y.ld, 0, ptr(part), ptr(work), ws, stream()))
+
     _timed("fwd", flops, launch, nbytes)
     if res[0] == -2:  # DG_ERR_UNSUPPORTED: nothing was launched
         return None
     if res[0] != 0:
-        raise DGError(f"dg_conv_fwd_stats failed with status {res[0]}")
+        raise DGError(f"dg_conv_fwd_ex failed with status {res[0]}")
     return part, rows
 
 

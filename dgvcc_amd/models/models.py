@@ -157,6 +157,11 @@ class _DGBase(nn.Module):
     def compute_dtype(self):
         return _PRECISIONS[self.precision]
 
+    def train(self, mode: bool = True):
+        from ..engine import invalidate_frozen
+        invalidate_frozen()  # eval-mode packed weights are rebuilt after any mode switch
+        return super().train(mode)
+
 
 class DGModel_base(_DGBase):
     """reference models/models.py:29-96."""
@@ -255,7 +260,7 @@ class DGModel_mem(DGModel_base):
         plan = self._get_plans()["single"]
         dt = self.compute_dtype
         ya = K.Act(y.detach().permute(0, 2, 3, 1).contiguous().to(dt))
-        memT_s, mem_p, _ = plan.memr.packs(dt)
+        memT_s, mem_p, _ = plan.memr.packs(dt, self.training)
         L = plan.memr.logits(ya, memT_s, dt)
         P = K.Act(torch.empty_like(L.buf))
         K.call("dg_softmax_fwd", L.dt, L.ptr, L.M, L.C, P.ptr, K.stream())

@@ -1,7 +1,7 @@
 """Fused AdamW over one flat fp32 buffer (torch.optim.AdamW semantics,
 reference main.py:85-86), with the data-parallel gradient all-reduce folded in.
 
-At construction every parameter's storage is moved into a flat buffer per
+At the first step every parameter's storage is moved into a flat buffer per
 param group (`p.data` becomes a view), so one HIP launch updates the whole
 model.  Gradients are gathered into a flat buffer by one launch
 (`dg_gather_flat`); when torch.distributed is initialised that buffer is
@@ -14,6 +14,7 @@ import torch
 
 from . import kernels as K
 from .dist import average_flat_
+from .engine import invalidate_frozen
 from ._capi import call, ptr, stream
 
 
@@ -27,25 +28,44 @@ class AdamW(torch.optim.Optimizer):
         self.allreduce = allreduce
         for group in self.param_groups:
             ps = group["params"]
-            dev = ps[0].device
-            if any(p.dtype != torch.float32 or p.device != dev for p in ps):
+            if any(p.dtype != torch.float32 or p.device != ps[0].device for p in ps):
                 raise ValueError("fused AdamW needs fp32 params on one device")
-            sizes = [p.numel() for p in ps]
-            total = sum(sizes)
-            flat = torch.empty(total, dtype=torch.float32, device=dev)
-            offs = [0]
-            for p, n in zip(ps, sizes):
-                flat[offs[-1]:offs[-1] + n].copy_(p.detach().reshape(-1))
-                offs.append(offs[-1] + n)
-            for p, o, n in zip(ps, offs, sizes):
-                p.data = flat[o:o + n].view_as(p)
-            group["_flat"] = flat
-            group["_offs"] = offs
-            group["_m"] = torch.zeros_like(flat)
-            group["_v"] = torch.zeros_like(flat)
-            group["_g"] = torch.empty_like(flat)
-            group["_step"] = 0
-            group["_offs_dev"] = torch.tensor(offs, dtype=torch.int64, device=dev)
+
+    @staticmethod
+    def _is_flat(group):
+        flat = group.get("_flat")
+        if flat is None:
+            return False
+        base = flat.data_ptr()
+        return all(p.device == flat.device and p.data_ptr() == base + 4 * o
+                   for p, o in zip(group["params"], group["_offs"]))
+
+    def _ensure_flat(self, group):
+        """Move every parameter's storage into one flat buffer per group (`p.data` becomes a
+        view).  Done at the first step, and again if the parameters were re-homed since
+        (`model.to(device)` after the optimizer was built, as the reference's main.py
+        does); the moments follow the parameters."""
+        if self._is_flat(group):
+            return
+        ps = group["params"]
+        dev = ps[0].device
+        if any(p.dtype != torch.float32 or p.device != dev for p in ps):
+            raise ValueError("fused AdamW needs fp32 params on one device")
+        sizes = [p.numel() for p in ps]
+        flat = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
+        offs = [0]
+        for p, n in zip(ps, sizes):
+            flat[offs[-1]:offs[-1] + n].copy_(p.detach().reshape(-1))
+            offs.append(offs[-1] + n)
+        for p, o, n in zip(ps, offs, sizes):
+            p.data = flat[o:o + n].view_as(p)
+        group["_flat"] = flat
+        group["_offs"] = offs
+        group["_m"] = group["_m"].to(dev) if "_m" in group else torch.zeros_like(flat)
+        group["_v"] = group["_v"].to(dev) if "_v" in group else torch.zeros_like(flat)
+        group["_g"] = torch.empty_like(flat)
+        group.setdefault("_step", 0)
+        group.pop("_live_cache", None)
 
     def _gather(self, group):
         """Gather live gradients into the flat buffer; returns the [start, end) runs of
@@ -89,9 +109,11 @@ class AdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        invalidate_frozen()  # the update below writes parameters behind torch's version counters
         for group in self.param_groups:
             if all(p.grad is None for p in group["params"]):
                 continue
+            self._ensure_flat(group)
             runs = self._gather(group)
             g = group["_g"]
             if self.allreduce:

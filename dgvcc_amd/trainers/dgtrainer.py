@@ -70,25 +70,31 @@ class DGTrainer(Trainer):
         h, w = img.shape[2:]
         ps = self.patch_size
         if h >= ps or w >= ps:
-            total = torch.zeros((), device=img.device)
             patches, _, _ = divide_img_into_patches(img, ps)
-            for p in patches:
-                total = total + self._pred(model, p).sum()
-            return total.item() / self.log_para  # one sync instead of one per patch
+            return self._count([self._pred(model, p).sum() for p in patches])
         return self._pred(model, img).sum().item() / self.log_para
+
+    def _count(self, sums):
+        """The reference adds `torch.sum(pred).item() / log_para` per patch in Python
+        floats; same arithmetic and order here, with one device->host copy instead of one
+        synchronising .item() per patch."""
+        total = 0
+        for s in torch.stack(sums).cpu().tolist():
+            total += s / self.log_para
+        return total
 
     def predict2(self, model, img, img2):
         """predict + ISW covariance statistics pass (dgtrainer.py:86-102)."""
         h, w = img.shape[2:]
         ps = self.patch_size
         if h >= ps or w >= ps:
-            total = torch.zeros((), device=img.device)
             p1, _, _ = divide_img_into_patches(img, ps)
             p2, _, _ = divide_img_into_patches(img2, ps)
+            sums = []
             for a, b in zip(p1, p2):
-                total = total + self._pred(model, a).sum()
+                sums.append(self._pred(model, a).sum())
                 model([a, b], cal_covstat=True)
-            return total.item() / self.log_para
+            return self._count(sums)
         cnt = self._pred(model, img).sum().item() / self.log_para
         model([img, img2], cal_covstat=True)
         return cnt

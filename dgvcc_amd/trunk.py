@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from . import dist as D
 from . import kernels as K
-from .engine import ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum
+from .engine import ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_cached, frozen
 from .kernels import Act
 
 STEM_KPAD = 192  # 7*7*3 = 147 taps, padded to a multiple of 64 for the MFMA K loop
@@ -40,8 +40,9 @@ class TConv:
         self.Cin, self.Cout = conv.in_channels, conv.out_channels
         self.same = self.stride == 1 and 2 * self.pad == self.R - 1
 
-    def pack(self, dt):
-        return K.pack_weight(self.conv.weight.detach(), dt)
+    def pack(self, dt, training=True):
+        build = lambda: K.pack_weight(self.conv.weight.detach(), dt)  # noqa: E731
+        return build() if training else frozen(self, ("w", dt), (self.conv.weight,), build)
 
     def out_hw(self, H, W):
         return K.conv_out(H, self.R, self.stride, self.pad), K.conv_out(W, self.R, self.stride, self.pad)
@@ -72,8 +73,7 @@ def bn_stats(z: Act, bn: nn.BatchNorm2d, training: bool) -> torch.Tensor:
         bn.num_batches_tracked.add_(1)
         return K.bn_fwd_train(z, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                               bn.running_var, _bn_momentum(bn), bn.eps)
-    return K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean, bn.running_var,
-                           bn.eps)
+    return bn_eval_cached(bn, bn)
 
 
 def _identity_stats(C, dev):
@@ -188,7 +188,7 @@ class Block:
         dt, dev = x.buf.dtype, x.buf.device
         N = x.N
         nh = lambda h, w, c: Act(K.nhwc(N, h, w, c, dt, dev))  # noqa: E731
-        wp1, wp2, wp3 = self.c1.pack(dt), self.c2.pack(dt), self.c3.pack(dt)
+        wp1, wp2, wp3 = self.c1.pack(dt, training), self.c2.pack(dt, training), self.c3.pack(dt, training)
         z1 = nh(x.H, x.W, self.c1.Cout); self.c1.fwd(x, wp1, z1)
         st1 = bn_stats(z1, self.bn1, training)
         a1 = nh(x.H, x.W, self.c1.Cout); K.bn_apply(z1, st1, ACT_RELU, a1)
@@ -199,7 +199,7 @@ class Block:
         st3 = bn_stats(z3, self.bn3, training)
         wpd = zd = std = None
         if self.cd is not None:
-            wpd = self.cd.pack(dt)
+            wpd = self.cd.pack(dt, training)
             zd = nh(P, Q, self.cd.Cout); self.cd.fwd(x, wpd, zd)
             std = bn_stats(zd, self.bnd, training)
         out = nh(P, Q, self.c3.Cout)
@@ -308,7 +308,8 @@ class CounterPlan:
             raise ValueError(f"input H,W must be multiples of 16 (got {H}x{W})")
         dev = img.device
         col = Act(K.im2col_c3_general(img.float(), dt, 7, 2, 3, STEM_KPAD))
-        wp0 = K.pack_weight(self.conv1.weight.detach(), dt, cpad=3, row_len=STEM_KPAD)
+        build = lambda: K.pack_weight(self.conv1.weight.detach(), dt, cpad=3, row_len=STEM_KPAD)  # noqa: E731
+        wp0 = build() if training else frozen(self, ("stem", dt), (self.conv1.weight,), build)
         P, Q = col.H, col.W
         z0 = Act(K.nhwc(N, P, Q, 64, dt, dev))
         K.conv_fwd(col, wp0, 64, 1, 0, z0, k_alg=147)

@@ -60,6 +60,15 @@ int64_t dg_conv_stats_rows(int N, int H, int W);
 int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                       const void* w, int Cout, int R, int S, int pad, const float* bias,
                       void* y, int64_t ldy, float* part, void* stream);
+/* Split-K workspace (bytes, 0 = none needed) for the bf16 forward of a shape whose tile
+ * grid cannot fill the GPU (deep layers at small batch). */
+int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S);
+/* dg_conv_fwd + dg_conv_fwd_stats in one entry: part may be NULL; with a workspace of
+ * dg_conv_fwd_workspace bytes the K loop is split over blocks and reduced deterministically
+ * (bias, accumulate and the statistics partials in the reduce pass). */
+int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                   int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
+                   int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream);
 
 /* wflip[C][R][S][Cout] = w[Cout][R-1-r][S-1-s][C] (packed filters of dtype). */
 int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream);

@@ -203,3 +203,47 @@ def test_bf16_model_fallback_shapes(dev, H, W):
         assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in model.parameters())
         outs.append(d.sum().item())
     assert abs(outs[1] - outs[0]) / abs(outs[0]) < 0.1
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,acc", [
+    (1, 24, 32, 512, 512, False),   # conv5-like at batch 1: 6 tiles -> split 24
+    (1, 48, 64, 256, 512, True),    # conv4-like, accumulate into y
+    (2, 20, 24, 128, 128, False),   # 128-wide tiles
+])
+def test_conv_splitk_matches_unsplit(dev, monkeypatch, N, H, W, C, Cout, acc):
+    """Small-grid bf16 forwards split their K loop over blocks (f32 partials + a reduce
+    pass): same result as the unsplit kernel to f32 summation-order rounding, against a
+    float64 reference, with bias, accumulate and the epilogue statistics."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    y0 = torch.randn(N, H, W, Cout, generator=g).to(dev, bf)
+    wp = K.pack_weight(w, bf)
+    assert K.query("dg_conv_fwd_workspace", 1, N, H, W, C, Cout, 3, 3) > 0
+    outs = []
+    for split in ("1", "0"):
+        monkeypatch.setenv("DGVCC_SPLITK", split)
+        K._FWD_WS.clear()
+        z = K.Act(y0.clone())
+        K.conv_fwd(K.Act(x), wp, Cout, 3, 1, z, bias=b, accumulate=acc)
+        zs = K.Act(K.nhwc(N, H, W, Cout, bf, dev))
+        res = K.conv_fwd_stats(K.Act(x), wp, Cout, 3, 1, zs, bias=b)
+        outs.append((z.buf.clone(), zs.buf.clone(), res))
+    K._FWD_WS.clear()
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + y0.double()
+    for z, zs, _ in outs:
+        assert relerr(z, ref) < 1e-2
+    assert relerr(outs[0][0], outs[1][0]) < 1e-2
+    part, rows = outs[0][2]
+    rm, rv = torch.zeros(Cout, device=dev), torch.ones(Cout, device=dev)
+    st = K.bn_part_finalize(part, rows, Cout, torch.ones(Cout, device=dev), torch.zeros(Cout, device=dev), rm, rv,
+                            0.1, 1e-5)
+    zf = outs[0][1].double().reshape(-1, Cout)
+    assert relerr(st[0], zf.mean(0)) < 1e-6
+    assert relerr(st[1], 1.0 / (zf.var(0, unbiased=False) + 1e-5).sqrt()) < 2e-6
