@@ -948,6 +948,7 @@ struct WgArgs {
   int splits, pps;     // pixels per split (multiple of BKP)
   int stride, P, Q;    // output grid of dy (stride 1: P = H, Q = W)
   int whole_x;         // 1: descriptor over the whole x (strided convs)
+  int pad_ok = 0;      // 1: the plan may be the padded 9-tap kernel's (dg_conv_wgrad)
 };
 
 template <typename T> struct WgCfg;
@@ -1332,7 +1333,12 @@ constexpr int W9_XROWS = 72;
 
 // WT = 1 (BCO 128): wave tile 64 co x 16 c (TI 4, TJ 1) instead of 32 x 32: the 9 taps' B
 // fragments are read once per 4 A fragments (fewer transposed LDS reads per MFMA).
-template <int BCO, int WT = 0>
+// PADK = 1 (W % 64 != 0, the 40/20-wide deep layers of 320-px crops): the K index runs over
+// the zero-padded image, u = (n, p+1, q+1) in N x (H+2) x (W+2), so a K-step of 64 u may
+// span rows and every shifted strip read lands on a zero pad cell exactly where the conv's
+// padding is: dy rows of pad cells are zero, x rows outside the image are zero.  Costs
+// (H+2)(W+2)/HW more K (10% at 40x40) instead of falling back to the per-tap kernel.
+template <int BCO, int WT = 0, int PADK = 0>
 __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int BKP = 64, BC = 64;
   constexpr int RA = BCO * 2, RX = BC * 2;                    // bytes per LDS row
@@ -1355,24 +1361,59 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   const int split = bid / tiles;
   const int t0 = bid - split * tiles;
   const int co0 = (t0 % nco) * BCO, c0 = (t0 / nco) * BC;
+  const int PW = a.W + 2, PHW = (a.H + 2) * PW;
+  const int U = PADK ? a.N * PHW : M;                        // K index space
   const int kbeg = split * a.pps;
-  const int kend = min(M, kbeg + a.pps);
-  const int nkt = (kend - kbeg) / BKP;
+  const int kend = min(U, kbeg + a.pps);
+  const int nkt = PADK ? (kend - kbeg + BKP - 1) / BKP : (kend - kbeg) / BKP;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-  const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 2);
+  const int dylo = PADK ? 0 : kbeg, dyhi = PADK ? M : kend;
+  const unsigned dy_bytes = (unsigned)(((long long)(dyhi - dylo - 1) * a.lddy + a.Cout) * 2);
   __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.dy + (long long)kbeg * a.lddy * 2), 0, dy_bytes, 0x00020000);
+      (void*)(a.dy + (long long)dylo * a.lddy * 2), 0, dy_bytes, 0x00020000);
   const int halo = a.W + 8;
-  const int xlo = max(0, kbeg - halo), xhi = min(M, kend + halo);
+  const int xlo = PADK ? 0 : max(0, kbeg - halo), xhi = PADK ? M : min(M, kend + halo);
   const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 2);
   __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.x + (long long)xlo * a.ldx * 2), 0, x_bytes, 0x00020000);
   const int my_inst = (N_INST - wid + 7) / 8;                 // wave-uniform DMA count per step
 
+  // padded index -> image pixel (or -1 on a pad cell / outside [0, U))
+  auto unpad = [&](int u) -> int {
+    if (u < 0 || u >= U) return -1;
+    const int n = u / PHW, r = u - n * PHW;
+    const int pp = r / PW, qq = r - pp * PW;
+    if (pp < 1 || pp > a.H || qq < 1 || qq > a.W) return -1;
+    return n * HW + (pp - 1) * a.W + (qq - 1);
+  };
+
+#define W9_ISSUE_PAD(kt_, stage_) \
+  do { \
+    const int u0 = kbeg + (kt_) * BKP; \
+    char* As = smem + (stage_) * STAGE; \
+    char* Xs = As + A_BYTES; \
+    for (int ii = wid; ii < N_INST; ii += 8) { \
+      if (ii < A_INST) { \
+        const int row = ii * RPIA + lane / CPRA; \
+        const int ch = (lane % CPRA) ^ wg_swz<CPRA>(row); \
+        const int px = (u0 + row < kend) ? unpad(u0 + row) : -1; \
+        lds_dma16(dyr, As + ii * 1024, px >= 0 ? (unsigned)(((long long)px * a.lddy + co0 + ch * 8) * 2) : 0xFFFFFFF0u); \
+      } else { \
+        const int jj = ii - A_INST; \
+        const int dhi = jj / 9, sub = jj - dhi * 9; \
+        const int row = sub * 8 + (lane >> 3); \
+        const int ch = (lane & 7) ^ wg_swz<CPRX>(row); \
+        const int px = unpad(u0 - 4 + row + (dhi - 1) * PW); \
+        lds_dma16(xr, Xs + dhi * X_BYTES + sub * 1024, px >= 0 ? (unsigned)(((long long)px * a.ldx + c0 + ch * 8) * 2) : 0xFFFFFFF0u); \
+      } \
+    } \
+  } while (0)
+
 #define W9_ISSUE(kt_, stage_) \
   do { \
+    if constexpr (PADK) { W9_ISSUE_PAD(kt_, stage_); break; } \
     const int px0 = kbeg + (kt_) * BKP; \
     const int n = px0 / HW, rem = px0 - n * HW; \
     const int pr = rem / a.W, q0 = rem - pr * a.W; \
@@ -1465,6 +1506,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
     }
   }
 #undef W9_ISSUE
+#undef W9_ISSUE_PAD
 
   const long long ldk = 9ll * a.C;
   float* out = a.slab + (long long)split * a.Cout * ldk;
@@ -1496,18 +1538,33 @@ static bool wg9_ok(int C, int Cout, int R, int S, int W, int pad) {
   return use_pipe() && R == 3 && S == 3 && pad == 1 && W % 64 == 0 && C % 64 == 0 && Cout % 64 == 0;
 }
 
+// the padded-K variant: any W; whole-tensor buffer descriptors (32-bit byte offsets)
+static bool wg9p_ok(int N, int H, int W, int C, int Cout, int R, int S, int pad, long long ldx, long long lddy) {
+  const char* e = getenv("DGVCC_WG9_PAD");
+  if (e && e[0] == '0') return false;
+  const long long M = (long long)N * H * W;
+  return use_pipe() && R == 3 && S == 3 && pad == 1 && W % 64 != 0 && C % 64 == 0 && Cout % 64 == 0 &&
+         M * std::max(ldx, lddy) * 2 < (1ll << 31) && (long long)N * (H + 2) * (W + 2) < (1ll << 30);
+}
+
 struct WgPlan { int splits, pps; };
 
 // splits for the fused-tap kernel: >= 8 K-steps per block, block count chosen for
-// whole rounds of one block per CU (tail efficiency >= 90% where possible).
-static WgPlan wg9_plan(int N, int H, int W, int C, int Cout) {
-  const long long M = (long long)N * H * W;
-  const long long steps = M / 64;
+// whole rounds of one block per CU (tail efficiency >= 90% where possible), starting from
+// one round: every extra round doubles the f32 slab written and re-read by the reduce.
+// units: the K index space (pixels, or padded cells for the PADK variant).
+static WgPlan wg9_plan(long long units, int C, int Cout) {
+  const long long steps = (units + 63) / 64;
   const int bco = Cout % 128 == 0 ? 128 : 64;
   const long long tiles = (long long)(Cout / bco) * (C / 64);
   long long best = 1;
   double best_eff = -1.0;
-  for (int rounds = 2; rounds <= 12; ++rounds) {
+  static int rmin = -1;
+  if (rmin < 0) {
+    const char* e = getenv("DGVCC_WG9_ROUNDS");
+    rmin = e ? std::max(1, atoi(e)) : 1;  // A/B (MI355X): 1 round beats 2 by 2% (768x1024) / 8% (320 crops)
+  }
+  for (int rounds = rmin; rounds <= 12; ++rounds) {
     long long sp = (256ll * rounds + tiles - 1) / tiles;
     sp = std::max(1ll, std::min(sp, std::max(1ll, steps / 8)));
     const long long blocks = tiles * sp;
@@ -1520,10 +1577,17 @@ static WgPlan wg9_plan(int N, int H, int W, int C, int Cout) {
   return WgPlan{(int)splits, (int)(sps * 64)};
 }
 
+// ld* < 0: the shape-only plan of the workspace query (assumes the padded 9-tap kernel is
+// eligible); pad_ok = false: callers whose launch never takes the padded kernel.
 template <typename T>
-WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S) {  // H, W: output grid
+WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S, long long ldx = -1, long long lddy = -1,
+               bool pad_ok = false) {  // H, W: output grid
   constexpr int BKP = WgCfg<T>::BKP;
-  if (std::is_same<T, bf16>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2)) return wg9_plan(N, H, W, C, Cout);
+  if (std::is_same<T, bf16>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2))
+    return wg9_plan((long long)N * H * W, C, Cout);
+  if (std::is_same<T, bf16>::value && pad_ok &&
+      wg9p_ok(N, H, W, C, Cout, R, S, (R - 1) / 2, ldx < 0 ? C : ldx, lddy < 0 ? Cout : lddy))
+    return wg9_plan((long long)N * (H + 2) * (W + 2), C, Cout);
   const long long M = (long long)N * H * W;
   const int bco = (Cout % 128 == 0) ? 128 : 64;
   const int bc = (C % 128 == 0) ? 128 : 64;
@@ -1546,12 +1610,21 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   const dim3 grid(tiles * a.splits);
   bool done = false;
   if constexpr (std::is_same<T, bf16>::value) {
-    if (a.stride == 1 && !a.whole_x && wg9_ok(a.C, a.Cout, a.R, a.S, a.W, a.pad)) {
+    const bool w9 = a.stride == 1 && !a.whole_x && wg9_ok(a.C, a.Cout, a.R, a.S, a.W, a.pad);
+    const bool w9p = a.stride == 1 && !a.whole_x && !w9 && a.pad_ok &&
+                     wg9p_ok(a.N, a.H, a.W, a.C, a.Cout, a.R, a.S, a.pad, a.ldx, a.lddy);
+    if (w9 || w9p) {
       const int b9 = a.Cout % 128 == 0 ? 128 : 64;
       const dim3 g9((a.Cout / b9) * (a.C / 64) * a.splits);
-      if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1>), g9, dim3(512), 0, st, a);
-      else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad9_kernel<64>), g9, dim3(512), 0, st, a);
+      if (w9) {
+        if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad9_kernel<64>), g9, dim3(512), 0, st, a);
+      } else {
+        if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 1>), g9, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1>), g9, dim3(512), 0, st, a);
+      }
       done = true;
     } else if (use_wgrad_pipe()) {  // opt-in: measured slower than the register-staged kernel (round 1)
       const int RS = a.R * a.S;
@@ -1822,8 +1895,12 @@ extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int
 
 extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
-  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : wg_plan<float>(N, H, W, C, Cout, R, S);
-  return (int64_t)p.splits * Cout * C * R * S * 4;
+  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S, -1, -1, true)
+                              : wg_plan<float>(N, H, W, C, Cout, R, S);
+  // the padded 9-tap plan may be refused at launch (pixel strides too large): cover the
+  // fallback plan too
+  WgPlan q = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
+  return (int64_t)std::max(p.splits, q.splits) * Cout * C * R * S * 4;
 }
 
 extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,
@@ -1836,10 +1913,14 @@ extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H
   DG_REQUIRE(ldx % 8 == 0 && lddy % 8 == 0 && ldx >= C && lddy >= Cout);
   const int64_t need = dg_conv_wgrad_workspace(dtype, N, H, W, C, Cout, R, S);
   DG_REQUIRE(ws_bytes >= need);
-  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : wg_plan<float>(N, H, W, C, Cout, R, S);
-  DG_SUPPORTED((long long)(p.pps + 2 * pad * (W + 1)) * std::max(ldx, lddy) * 4 < (1ll << 31));
+  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S, ldx, lddy, true)
+                              : wg_plan<float>(N, H, W, C, Cout, R, S);
+  const bool padk = dtype == DG_BF16 && !wg9_ok(C, Cout, R, S, W, pad) &&
+                    wg9p_ok(N, H, W, C, Cout, R, S, pad, ldx, lddy);
+  if (!padk) DG_SUPPORTED((long long)(p.pps + 2 * pad * (W + 1)) * std::max(ldx, lddy) * 4 < (1ll << 31));
   WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
            1, H, W, 0};
+  a.pad_ok = 1;
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
 }

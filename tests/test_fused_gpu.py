@@ -247,3 +247,30 @@ def test_conv_splitk_matches_unsplit(dev, monkeypatch, N, H, W, C, Cout, acc):
     zf = outs[0][1].double().reshape(-1, Cout)
     assert relerr(st[0], zf.mean(0)) < 1e-6
     assert relerr(st[1], 1.0 / (zf.var(0, unbiased=False) + 1e-5).sqrt()) < 2e-6
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout", [
+    (16, 40, 40, 256, 512),   # conv4 of a 320-px crop
+    (16, 20, 20, 512, 512),   # conv5 of a 320-px crop
+    (3, 7, 24, 64, 128),      # ragged: K-steps span rows and images, last step partial
+])
+def test_wgrad9_padded_k(dev, monkeypatch, N, H, W, C, Cout):
+    """Fused 9-tap bf16 wgrad over the zero-padded K index (W % 64 != 0) against float64
+    and against the per-tap kernel it replaces."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    dy = torch.randn(N, H, W, Cout, generator=g).to(dev, bf)
+    outs = []
+    for pad in ("1", "0"):
+        monkeypatch.setenv("DGVCC_WG9_PAD", pad)
+        dw = torch.empty(Cout, C, 3, 3, device=dev)
+        K.conv_wgrad(K.Act(x), K.Act(dy), 3, 1, dw)
+        outs.append(dw)
+    torch.cuda.synchronize()
+    xr = x.double().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = torch.zeros(Cout, C, 3, 3, dtype=torch.float64, device=dev, requires_grad=True)
+    F.conv2d(xr, wr, padding=1).backward(dy.double().permute(0, 3, 1, 2))
+    assert relerr(outs[0], wr.grad) < 1e-5
+    assert relerr(outs[0], outs[1]) < 1e-5

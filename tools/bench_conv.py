@@ -6,7 +6,8 @@ from dgvcc_amd import kernels as K
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 dt = torch.bfloat16 if (len(sys.argv) < 3 or sys.argv[2] == "bf16") else torch.float32
-H0, W0 = 768, 1024
+H0 = int(sys.argv[3]) if len(sys.argv) > 3 else 768
+W0 = int(sys.argv[4]) if len(sys.argv) > 4 else 1024
 layers = [  # (H, W, C, Cout, R)
     (H0, W0, 64, 64, 3), (H0 // 2, W0 // 2, 64, 128, 3), (H0 // 2, W0 // 2, 128, 128, 3),
     (H0 // 4, W0 // 4, 128, 256, 3), (H0 // 4, W0 // 4, 256, 256, 3),
