@@ -374,6 +374,21 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
   }
 }
 
+// The pooled backward keeps 4 pixels x V channels of z and g live per thread: V = 4
+// (8-B bf16 loads) holds the two kernels under ~100 VGPRs, 4-5 waves per SIMD instead of 2
+// at V = 8, which is what a latency-bound gather of 4 rows needs.
+constexpr int POOL_V = 4;
+template <int V, typename T>
+__device__ __forceinline__ void ldn(const T* p, float* v) {
+  if constexpr (V == 4) ld4(p, v);
+  else ldv(p, v);
+}
+template <int V, typename T>
+__device__ __forceinline__ void stn(T* p, const float* v) {
+  if constexpr (V == 4) st4(p, v);
+  else stv(p, v);
+}
+
 // Upstream gradient of the BN output at the window's four pixels: the pooled
 // gradient at the recomputed argmax (+ the direct gradient gd), times drop,
 // zeroed where the ReLU was inactive (bn_bwd_load's rule).
@@ -383,11 +398,11 @@ __device__ __forceinline__ void bn_pool_bwd_load(const T* gp, long long ldgp, co
                                                  const ChanParams<V>& cp, int act, const float* drop, int HW,
                                                  float gv[4][V], float zv[4][V]) {
   float gpv[V];
-  ldv(gp + pp * ldgp + c0, gpv);
+  ldn<V>(gp + pp * ldgp + c0, gpv);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    ldv(z + pos[k] * ldz + c0, zv[k]);
-    if (gd) ldv(gd + pos[k] * ldgd + c0, gv[k]);
+    ldn<V>(z + pos[k] * ldz + c0, zv[k]);
+    if (gd) ldn<V>(gd + pos[k] * ldgd + c0, gv[k]);
     else {
 #pragma unroll
       for (int e = 0; e < V; ++e) gv[k][e] = 0.f;
@@ -423,7 +438,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
                                                           long long Mp, int C, long long ppb, const float* mean,
                                                           const float* invstd, const float* scale, const float* shift,
                                                           int act, const float* drop, int HW, float* __restrict__ part) {
-  constexpr int V = 16 / (int)sizeof(T);
+  constexpr int V = POOL_V;
   __shared__ float sh[3][NT * V];
   const int tpp = C / V;
   const int rows = NT / tpp;
@@ -437,7 +452,6 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
   if (pl < rows) {
     ChanParams<V> cp;
     cp.load(c0, scale, shift, mean, invstd);
-#pragma unroll 2
     for (long long pp = p0 + pl; pp < p1; pp += rows) {
       long long pos[4];
       pool_window(pp, H, W, pos);
@@ -477,7 +491,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
                                                         const float* scale, const float* shift, int act,
                                                         const float* drop, int HW, const float* __restrict__ coef,
                                                         T* __restrict__ dz, long long lddz) {
-  constexpr int V = 16 / (int)sizeof(T);
+  constexpr int V = POOL_V;
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
@@ -499,7 +513,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
         const float xh = (zv[k][e] - cp.mu[e]) * cp.is[e];
         gv[k][e] = k1[e] * gv[k][e] - k2[e] * xh - k3[e];
       }
-      stv(dz + pos[k] * lddz + c0, gv[k]);
+      stn<V>(dz + pos[k] * lddz + c0, gv[k]);
     }
   }
 }
@@ -663,7 +677,7 @@ static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, (int)M, C, gamma, inv,
                      dgamma, dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
-  const long long total = Mp * (C / (16 / (int)sizeof(T)));
+  const long long total = Mp * (C / POOL_V);
   hipLaunchKernelGGL(bn_pool_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd,
                      ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop, H * W, coef, (T*)dz,
                      lddz);
@@ -680,7 +694,8 @@ extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const voi
   DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
   DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldgp) &&
-               BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz) && (!gd || BN_SHAPE_OK(dtype, C, ldgd)));
+               BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz) && (!gd || BN_SHAPE_OK(dtype, C, ldgd)) &&
+               C % POOL_V == 0 && NT % (C / POOL_V) == 0);
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16
              ? bn_pool_bwd_impl<bf16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
