@@ -13,7 +13,15 @@ namespace {
 
 constexpr int NT = 256;
 
-inline int bn_nblk(int M) { return std::max(1, std::min(1024, dg_cdiv(M, 64))); }
+inline int bn_nblk_cap() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_BN_NBLK");
+    v = e ? std::max(64, atoi(e)) : 1024;
+  }
+  return v;
+}
+inline int bn_nblk(int M) { return std::max(1, std::min(bn_nblk_cap(), dg_cdiv(M, 64))); }
 // pooled BN backward partials: more, smaller blocks (each thread walks 2x2 windows; more
 // loads in flight per CU)
 inline int pool_nblk_cap() {
