@@ -29,6 +29,14 @@ struct FwdArgs {
   float* part = nullptr;   // bf16 pipe/tap3 only: BN statistics partials [ceil(M/256)][3][Cout]
   int ksplit = 1;          // bf16 pipe only: > 1 splits the K loop over blocks, f32 partials into kpart
   float* kpart = nullptr;  // [ksplit][M][Cout]; splitk_reduce_kernel finishes bias/accumulate/stats
+  // bf16 pipe only, dgrad launches: the BatchNorm-backward partial sums of the layer whose
+  // output gradient this launch produces (norm.hip bn_bwd_partial's three rows per
+  // 256-pixel tile: sum g', sum g' xhat, sum xhat with g' = g * drop * relu'(bn(z)))
+  const char* bz = nullptr;
+  long long ldbz = 0;
+  const float *bsc = nullptr, *bsf = nullptr, *bmu = nullptr, *bis = nullptr, *bdrop = nullptr;
+  int bact = 0, bHW = 1;
+  float* bpart = nullptr;
 };
 
 // Sum over the 16 lanes of a DPP row, result in every lane: quad butterflies (xor 1, 2)
@@ -105,6 +113,69 @@ __device__ __forceinline__ void epi_stats(f4v (&acc)[TI][TJ], const bool (&valid
     part_row[co0 + c] = n;
     part_row[Cout + co0 + c] = mean;
     part_row[2 * Cout + co0 + c] = m2;
+  }
+}
+
+// Epilogue BatchNorm-backward partial sums of the stored (bf16-rounded) gradient tile:
+// the separate pass over (g, z) of norm.hip's bn_bwd_partial, computed where g is
+// produced; z is read here at the tile's pixels (8-B loads), once.
+template <int TI, int TJ, int NPW, int BN>
+__device__ __forceinline__ void epi_bnbwd(f4v (&acc)[TI][TJ], const bool (&valid)[TJ], int pw, int cw, int wpx,
+                                          char* lds, const FwdArgs& a, int px0, int co0, int tid, int fr, int fc) {
+  float* sh = (float*)lds;  // [NPW][3][BN]
+  lds_barrier();            // every wave is done reading the operand ring
+  const bf16* z = (const bf16*)a.bz;
+#pragma unroll
+  for (int i = 0; i < TI; ++i) {
+    const int cl = cw + 16 * i + 4 * fc;
+    const int c = co0 + cl;
+    float sc[4], sf[4], mu[4], is[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { sc[r] = a.bsc[c + r]; sf[r] = a.bsf[c + r]; mu[r] = a.bmu[c + r]; is[r] = a.bis[c + r]; }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f}, s3[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      if (!valid[j]) continue;
+      const int px = px0 + wpx + 16 * j + fr;
+      float zv[4];
+      ld4(z + (long long)px * a.ldbz + c, zv);
+      float d[4] = {1.f, 1.f, 1.f, 1.f};
+      if (a.bdrop) {
+        const float* dp = a.bdrop + (long long)(px / a.bHW) * a.Cout + c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) d[r] = dp[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float g = acc[i][j][r];
+        if (a.bdrop) g *= d[r];
+        if (a.bact == 1 && !(fmaf(zv[r], sc[r], sf[r]) > 0.f)) g = 0.f;
+        const float xh = (zv[r] - mu[r]) * is[r];
+        s1[r] += g;
+        s2[r] = fmaf(g, xh, s2[r]);
+        s3[r] += xh;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s1[r] = row16_sum(s1[r]);
+      s2[r] = row16_sum(s2[r]);
+      s3[r] = row16_sum(s3[r]);
+      if (fr == 0) {
+        sh[(pw * 3 + 0) * BN + cl + r] = s1[r];
+        sh[(pw * 3 + 1) * BN + cl + r] = s2[r];
+        sh[(pw * 3 + 2) * BN + cl + r] = s3[r];
+      }
+    }
+  }
+  lds_barrier();
+  float* row = a.bpart + (long long)(px0 / 256) * 3 * a.Cout;
+  for (int t = tid; t < 3 * BN; t += 512) {  // the pipe kernel's 512 threads
+    const int k = t / BN, c = t - k * BN;
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < NPW; ++w) v += sh[(w * 3 + k) * BN + c];
+    row[k * a.Cout + co0 + c] = v;
   }
 }
 
@@ -615,6 +686,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   if (a.part)
     epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / PBM) * 3 * a.Cout, a.Cout,
                              co0, tid, fr, fc);
+  else if (a.bpart)
+    epi_bnbwd<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, wpx, smem, a, px0, co0, tid, fr, fc);
 }
 
 // Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored
@@ -1856,6 +1929,33 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   }
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+}
+
+// dgrad (or any bf16 pipelined forward) that also emits the BatchNorm-backward partial sums
+// of the layer whose output gradient y is: bpart[dg_conv_stats_rows][3][Cout] for
+// dg_bn_bwd_from_part.  z/ldz, scale/shift/mean/invstd, act, drop, HW describe that layer
+// (dg_bn_bwd's arguments).  DG_ERR_UNSUPPORTED (nothing launched) where the shape is not
+// served by the pipelined kernel in one pass (no split-K here): the caller then runs
+// dg_conv_fwd + dg_bn_bwd.
+extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                                 int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
+                                 const float* scale, const float* shift, const float* mean, const float* invstd,
+                                 int act, const float* drop, int HW, float* bpart, void* stream) {
+  DG_REQUIRE(x && w && y && z && bpart && scale && shift && mean && invstd && N > 0 && H > 0 && W > 0 && C > 0 &&
+             Cout > 0 && R > 0 && S > 0 && (act == 0 || act == 1) && (!drop || HW > 0));
+  DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 128 == 0);  // the pipe kernel's 128/256 tiles
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldy % 4 == 0 && ldz >= Cout && ldz % 4 == 0);
+  DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
+  const long long M = (long long)N * H * W;
+  DG_SUPPORTED(fwd_ksplit(M, Cout, C, R, S) == 1);
+  FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, nullptr, (char*)y, ldy, 0};
+  a.bz = (const char*)z;
+  a.ldbz = ldz;
+  a.bsc = scale; a.bsf = shift; a.bmu = mean; a.bis = invstd; a.bdrop = drop;
+  a.bact = act; a.bHW = drop ? HW : 1;
+  a.bpart = bpart;
+  return launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 
 extern "C" int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream) {

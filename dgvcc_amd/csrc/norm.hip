@@ -630,6 +630,35 @@ extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, i
                                   dz, lddz, dgamma, dbeta, dbias, workspace, st);
 }
 
+// dg_bn_bwd with the partial sums already computed by the producer of g (the dgrad
+// epilogue, dg_conv_fwd_bnbwd): finalize + apply.  part[nblk][3][C]; workspace >= 3*C floats.
+extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const void* g, int64_t ldg, const void* z,
+                                   int64_t ldz, int M, int C, const float* gamma, const float* save_mean,
+                                   const float* save_invstd, const float* scale, const float* shift, int act,
+                                   const float* drop, int HW, void* dz, int64_t lddz, float* dgamma, float* dbeta,
+                                   float* dbias, float* coef, void* stream) {
+  DG_REQUIRE(part && nblk > 0 && g && z && dz && coef && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
+  DG_REQUIRE(!drop || HW > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, save_invstd,
+                     dgamma, dbeta, dbias, coef);
+  DG_CHECK_LAUNCH();
+  if (dtype == DG_BF16) {
+    const long long total = (long long)M * (C / 8);
+    hipLaunchKernelGGL(bn_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
+  } else {
+    const long long total = (long long)M * (C / 4);
+    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+                       (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
+                       (float*)dz, lddz);
+  }
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
 extern "C" int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
                               const float* gamma, const float* save_mean, const float* save_invstd,
                               const float* scale, const float* shift, int act, const float* drop, int HW,

@@ -160,10 +160,13 @@ class ConvLayer:
             K.bn_apply(z, stats, self.act, out, drop)
 
     def backward(self, tape: dict, g: Act | None, gx: Act | None, accumulate_gx: bool = False,
-                 g_pool: Act | None = None) -> dict:
+                 g_pool: Act | None = None, gx_bn: "ConvLayer | None" = None) -> dict:
         """g: gradient of the layer output (None if only the pooled output was used);
-        g_pool: gradient of the pooled output when the forward ran with `pool`."""
+        g_pool: gradient of the pooled output when the forward ran with `pool`;
+        gx_bn: the layer whose whole output gradient gx is (its BN-backward partial sums
+        then come from this layer's dgrad epilogue)."""
         x, z, stats, wp, drop, training = tape.pop(self)
+        pre = tape.pop(("bnpart", self), None)
         if self.bn is not None and not training:
             raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
         dev = z.buf.device
@@ -185,6 +188,8 @@ class ConvLayer:
             if self.bn is None:
                 raise RuntimeError("pooled backward needs a BatchNorm layer")
             K.bn_bwd_pool(g_pool, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
+        elif pre is not None:
+            K.bn_bwd_from_part(pre, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
         else:
             K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta,
                      dbias, drop)
@@ -196,7 +201,16 @@ class ConvLayer:
         else:
             K.conv_wgrad(x, dz, self.R, self.pad, dw)
             if gx is not None:
-                K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, gx, accumulate=accumulate_gx)
+                res = None
+                if gx_bn is not None and not accumulate_gx and gx_bn.bn is not None:
+                    xn, zn, stn, _, dropn, trn = tape[gx_bn]
+                    if trn and not isinstance(xn, torch.Tensor) and zn.C == gx.C:
+                        res = K.conv_dgrad_bnpart(dz, wp, self.Cin, self.R, self.pad, gx, zn, stn, gx_bn.act,
+                                                  dropn)
+                        if res is not None:
+                            tape[("bnpart", gx_bn)] = res
+                if res is None:
+                    K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, gx, accumulate=accumulate_gx)
         grads = {self.conv.weight: dw}
         if self.conv.bias is not None:
             grads[self.conv.bias] = dbias if self.bn is not None else dbeta
@@ -414,40 +428,40 @@ class FeaturePlan:
         grads = {}
         # decoder
         g_a17 = nh(H // 4, W // 4, 256)
-        grads.update(D[5].backward(tape, own(g_y1, H // 4, W // 4, 128), g_a17))
+        grads.update(D[5].backward(tape, own(g_y1, H // 4, W // 4, 128), g_a17, gx_bn=D[4]))
         g_dec1in = K.nhwc(N, H // 4, W // 4, 512, dt, dev)
         grads.update(D[4].backward(tape, g_a17, Act(g_dec1in)))
         gy2 = own(g_y2, H // 8, W // 8, 256)
         K.upsample_bwd(Act(g_dec1in, 0, 256), 2, K.UP_BILINEAR, gy2, accumulate=True)
         g_a15 = nh(H // 8, W // 8, 512)
-        grads.update(D[3].backward(tape, gy2, g_a15))
+        grads.update(D[3].backward(tape, gy2, g_a15, gx_bn=D[2]))
         g_dec2in = K.nhwc(N, H // 8, W // 8, 1024, dt, dev)
         grads.update(D[2].backward(tape, g_a15, Act(g_dec2in)))
         g_y3 = own(g_y3, H // 16, W // 16, 512)
         K.upsample_bwd(Act(g_dec2in, 0, 512), 2, K.UP_BILINEAR, g_y3, accumulate=True)
         g_a13 = nh(H // 16, W // 16, 1024)
-        grads.update(D[1].backward(tape, g_y3, g_a13))
+        grads.update(D[1].backward(tape, g_y3, g_a13, gx_bn=D[0]))
         if g_x3 is not None:
             gx3 = Act(g_x3.to(dt).contiguous().clone())
             grads.update(D[0].backward(tape, g_a13, gx3, accumulate_gx=True))
         else:
             gx3 = nh(H // 16, W // 16, 512)
-            grads.update(D[0].backward(tape, g_a13, gx3))
+            grads.update(D[0].backward(tape, g_a13, gx3, gx_bn=E[12]))
         # enc3
-        g_a11 = nh(H // 16, W // 16, 512); grads.update(E[12].backward(tape, gx3, g_a11))
-        g_a10 = nh(H // 16, W // 16, 512); grads.update(E[11].backward(tape, g_a11, g_a10))
+        g_a11 = nh(H // 16, W // 16, 512); grads.update(E[12].backward(tape, gx3, g_a11, gx_bn=E[11]))
+        g_a10 = nh(H // 16, W // 16, 512); grads.update(E[11].backward(tape, g_a11, g_a10, gx_bn=E[10]))
         g_p4 = nh(H // 16, W // 16, 512); grads.update(E[10].backward(tape, g_a10, g_p4))
         # enc2 (the pooled gradients are routed inside the BN backward of the pooled layers)
         g_a8 = nh(H // 8, W // 8, 512)
         grads.update(E[9].backward(tape, Act(g_dec2in, 512, 512), g_a8, g_pool=g_p4))
-        g_a7 = nh(H // 8, W // 8, 512); grads.update(E[8].backward(tape, g_a8, g_a7))
+        g_a7 = nh(H // 8, W // 8, 512); grads.update(E[8].backward(tape, g_a8, g_a7, gx_bn=E[7]))
         g_p3 = nh(H // 8, W // 8, 256); grads.update(E[7].backward(tape, g_a7, g_p3))
         # enc1
         g_a5 = nh(H // 4, W // 4, 256)
         grads.update(E[6].backward(tape, Act(g_dec1in, 256, 256), g_a5, g_pool=g_p3))
-        g_a4 = nh(H // 4, W // 4, 256); grads.update(E[5].backward(tape, g_a5, g_a4))
+        g_a4 = nh(H // 4, W // 4, 256); grads.update(E[5].backward(tape, g_a5, g_a4, gx_bn=E[4]))
         g_p2 = nh(H // 4, W // 4, 128); grads.update(E[4].backward(tape, g_a4, g_p2))
-        g_a2 = nh(H // 2, W // 2, 128); grads.update(E[3].backward(tape, None, g_a2, g_pool=g_p2))
+        g_a2 = nh(H // 2, W // 2, 128); grads.update(E[3].backward(tape, None, g_a2, g_pool=g_p2, gx_bn=E[2]))
         g_p1 = nh(H // 2, W // 2, 64); grads.update(E[2].backward(tape, g_a2, g_p1))
         g_a = nh(H, W, 64); grads.update(E[1].backward(tape, None, g_a, g_pool=g_p1))
         grads.update(E[0].backward(tape, g_a, None))

@@ -131,6 +131,50 @@ def conv_dgrad(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, acc
     conv_fwd(dy, wflip, C, R, R - 1 - pad, dx, accumulate=accumulate, kind="dgrad")
 
 
+# Opt-in: measured slower on MI355X (the pipelined conv runs one 128-KB-LDS block per CU, so
+# the epilogue's z loads and reductions are fully exposed: +1.3 ms of dgrad per step against
+# the 0.75 ms partial pass it removes at 768x1024, A/B in DESIGN.md).
+_BNPART_OFF = __import__("os").environ.get("DGVCC_DGRAD_BNPART", "0") != "1"
+
+
+def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, z: Act, stats,
+                      act: int, drop: torch.Tensor | None = None):
+    """conv_dgrad (no accumulate) whose epilogue also emits the BatchNorm-backward partial
+    sums of the layer whose output gradient dx is (z, stats, act, drop: that layer's);
+    returns (part, rows) for bn_bwd_from_part, or None (nothing launched) when the shape is
+    not served that way."""
+    if dy.dt != 1 or _BNPART_OFF or stats is None:
+        return None
+    wflip = flip_weight(wp, dy.C, C, R)
+    rows = query("dg_conv_stats_rows", dy.N, dy.H, dy.W)
+    part = torch.empty((rows, 3, C), dtype=torch.float32, device=dy.buf.device)
+    flops = 2.0 * dy.M * dy.C * R * R * C
+    nbytes = dy.buf.element_size() * (dy.M * dy.C + wflip.numel() + 2 * dy.M * C)
+    res = []
+
+    def launch():
+        res.append(lib_call_status("dg_conv_fwd_bnbwd", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W, dy.C, ptr(wflip), C,
+                                   R, R, R - 1 - pad, dx.ptr, dx.ld, z.ptr, z.ld, ptr(stats[2]), ptr(stats[3]),
+                                   ptr(stats[0]), ptr(stats[1]), act, ptr(drop), z.H * z.W, ptr(part), stream()))
+
+    _timed("dgrad", flops, launch, nbytes)
+    if res[0] == -2:
+        return None
+    if res[0] != 0:
+        raise DGError(f"dg_conv_fwd_bnbwd failed with status {res[0]}")
+    return part, rows
+
+
+def bn_bwd_from_part(pre, g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias=None,
+                     drop: torch.Tensor | None = None):
+    """bn_bwd with the partial sums from conv_dgrad_bnpart."""
+    part, rows = pre
+    coef = torch.empty((3, z.C), dtype=torch.float32, device=z.buf.device)
+    call("dg_bn_bwd_from_part", z.dt, ptr(part), rows, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma),
+         ptr(stats[0]), ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, dz.ptr, dz.ld,
+         ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), stream())
+
+
 def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=False, k_alg=None):
     ws = query("dg_conv_wgrad_workspace", x.dt, x.N, x.H, x.W, x.C, dy.C, R, R)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)

@@ -69,6 +69,16 @@ int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, i
 int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                    int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                    int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream);
+/* bf16 forward (used for dgrad: flipped filters) that also emits the BatchNorm-backward
+ * partial sums of the layer whose output gradient y is, from the epilogue:
+ * bpart[dg_conv_stats_rows][3][Cout] for dg_bn_bwd_from_part (replaces dg_bn_bwd's
+ * partial pass over g and z).  z, scale/shift/mean/invstd, act, drop, HW: that layer's
+ * dg_bn_bwd arguments.  DG_ERR_UNSUPPORTED (nothing launched) when the shape is not served
+ * in one pipelined pass. */
+int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                      int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
+                      const float* scale, const float* shift, const float* mean, const float* invstd,
+                      int act, const float* drop, int HW, float* bpart, void* stream);
 
 /* wflip[C][R][S][Cout] = w[Cout][R-1-r][S-1-s][C] (packed filters of dtype). */
 int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream);
@@ -144,6 +154,13 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               const float* scale, const float* shift, int act, const float* drop, int HW,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
               void* workspace, void* stream);
+/* dg_bn_bwd from precomputed partial sums part[nblk][3][C] (dg_conv_fwd_bnbwd): finalize +
+ * apply; coef: caller workspace of 3*C floats. */
+int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const void* g, int64_t ldg, const void* z,
+                        int64_t ldz, int M, int C, const float* gamma, const float* save_mean,
+                        const float* save_invstd, const float* scale, const float* shift, int act,
+                        const float* drop, int HW, void* dz, int64_t lddz, float* dgamma, float* dbeta,
+                        float* dbias, float* coef, void* stream);
 
 /* BN(+ReLU) fused with the following MaxPool2d(2,2) (vgg16_bn.features[5:7] etc.,
  * models/models.py:35-38).  Apply: y = act(z*scale+shift)*drop (written only when y != NULL,

@@ -274,3 +274,42 @@ def test_wgrad9_padded_k(dev, monkeypatch, N, H, W, C, Cout):
     F.conv2d(xr, wr, padding=1).backward(dy.double().permute(0, 3, 1, 2))
     assert relerr(outs[0], wr.grad) < 1e-5
     assert relerr(outs[0], outs[1]) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,C,Cin_next,act,use_drop", [
+    (2, 128, 128, 256, 256, 1, False),   # 256-wide tiles (grids large enough not to split K)
+    (2, 120, 140, 128, 256, 1, True),    # 128-wide tiles, ragged last tile, Dropout2d mask
+    (1, 128, 128, 512, 512, 0, False),   # two channel tiles, no ReLU
+])
+def test_dgrad_epilogue_bn_partials(dev, monkeypatch, N, H, W, C, Cin_next, act, use_drop):
+    """dg_conv_fwd_bnbwd (BN-backward partial sums in the dgrad epilogue) + dg_bn_bwd_from_part
+    against dg_conv_dgrad + dg_bn_bwd on the same inputs: gx bit-identical, dz/dgamma/dbeta
+    to f32 summation-order rounding."""
+    K = _k()
+    monkeypatch.setattr(K, "_BNPART_OFF", False)
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(9)
+    dz_next = torch.randn(N, H, W, Cin_next, generator=g).to(dev, bf)
+    w = (torch.randn(Cin_next, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
+    z = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    gam, bet = torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev)
+    rm, rv = torch.zeros(C, device=dev), torch.ones(C, device=dev)
+    st = K.bn_fwd_train(K.Act(z), gam, bet, rm, rv, 0.1, 1e-5)
+    drop = ((torch.rand(N, C, generator=g) > 0.3).float() / 0.7).to(dev) if use_drop else None
+    wp = K.pack_weight(w, bf)
+    gx1 = K.Act(K.nhwc(N, H, W, C, bf, dev))
+    pre = K.conv_dgrad_bnpart(K.Act(dz_next), wp, C, 3, 1, gx1, K.Act(z), st, act, drop)
+    assert pre is not None
+    dz1 = K.Act(K.nhwc(N, H, W, C, bf, dev))
+    dg1, db1 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    K.bn_bwd_from_part(pre, gx1, K.Act(z), gam, st, act, dz1, dg1, db1, None, drop)
+    gx0 = K.Act(K.nhwc(N, H, W, C, bf, dev))
+    K.conv_dgrad(K.Act(dz_next), wp, C, 3, 1, gx0)
+    dz0 = K.Act(K.nhwc(N, H, W, C, bf, dev))
+    dg0, db0 = torch.empty(C, device=dev), torch.empty(C, device=dev)
+    K.bn_bwd(gx0, K.Act(z), gam, st, act, dz0, dg0, db0, None, drop)
+    torch.cuda.synchronize()
+    assert torch.equal(gx1.buf, gx0.buf)
+    assert relerr(dg1, dg0) < 1e-5 and relerr(db1, db0) < 1e-5
+    assert relerr(dz1.buf, dz0.buf) < 1e-2  # bf16 storage: rare 1-ulp flips from the coefficients
+    assert (dz1.buf.float() - dz0.buf.float()).abs().max() <= 2 * dz0.buf.float().abs().max() * 2 ** -8
