@@ -37,7 +37,23 @@ struct FwdArgs {
   const float *bsc = nullptr, *bsf = nullptr, *bmu = nullptr, *bis = nullptr, *bdrop = nullptr;
   int bact = 0, bHW = 1;
   float* bpart = nullptr;
+  // eval-mode BatchNorm (+ReLU) in the epilogue: y = act(conv*escale + eshift), applied after
+  // bias/accumulate exactly as dg_bn_apply applies it to a stored f32 z
+  const float* escale = nullptr;
+  const float* eshift = nullptr;
+  int eact = 0;
 };
+
+__device__ __forceinline__ void epi_affine(float v[4], const FwdArgs& a, int co) {
+  if (!a.escale) return;
+  const f4v sc = *(const f4v*)(a.escale + co), sf = *(const f4v*)(a.eshift + co);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float t = fmaf(v[r], sc[r], sf[r]);
+    if (a.eact == 1) t = t > 0.f ? t : 0.f;
+    v[r] = t;
+  }
+}
 
 // Sum over the 16 lanes of a DPP row, result in every lane: quad butterflies (xor 1, 2)
 // then rotations by 4 and 8 (VALU-only, no LDS crossbar traffic).
@@ -327,6 +343,7 @@ _Pragma("unroll") \
         ld4(yrow + co, o);
         v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
+      epi_affine(v, a, co);
       st4(yrow + co, v);
     }
   }
@@ -678,6 +695,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
         ld4(yrow + co, o);
         v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
+      epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
@@ -700,7 +718,8 @@ template <typename T>
 __global__ __launch_bounds__(1024) void splitk_reduce_kernel(const float* __restrict__ kpart, int ksplit, int M,
                                                              int Cout, const float* __restrict__ bias,
                                                              T* __restrict__ y, long long ldy, int accumulate,
-                                                             float* __restrict__ part) {
+                                                             float* __restrict__ part, const float* escale,
+                                                             const float* eshift, int eact) {
   constexpr int PXT = 256 / SKR_PL;
   __shared__ float sh[2][SKR_PL][64];
   const int tid = threadIdx.x, cq = tid & 15, pl = tid >> 4;
@@ -740,6 +759,13 @@ __global__ __launch_bounds__(1024) void splitk_reduce_kernel(const float* __rest
       float q[4];
       ld4(dst, q);
       o[0] += q[0]; o[1] += q[1]; o[2] += q[2]; o[3] += q[3];
+    }
+    if (escale) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = fmaf(o[r], escale[c0 + r], eshift[c0 + r]);
+        o[r] = (eact == 1 && !(t > 0.f)) ? 0.f : t;
+      }
     }
     st4(dst, o);
     ++cnt;
@@ -956,6 +982,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
         ld4(yrow + co, o);
         v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
+      epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
@@ -987,7 +1014,7 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         DG_CHECK_LAUNCH();
         hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3((unsigned)dg_cdiv(M, 256), a.Cout / 64), dim3(1024), 0, st,
                            (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (bf16*)a.y, a.ldy, a.accumulate,
-                           a.part);
+                           a.part, a.escale, a.eshift, a.eact);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
         hipLaunchKernelGGL(conv_fwd_tap3_kernel, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
@@ -1937,6 +1964,37 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
 // (dg_bn_bwd's arguments).  DG_ERR_UNSUPPORTED (nothing launched) where the shape is not
 // served by the pipelined kernel in one pass (no split-K here): the caller then runs
 // dg_conv_fwd + dg_bn_bwd.
+// Eval-mode Conv + BatchNorm(running statistics) [+ ReLU] in one pass: the BN scale/shift
+// (gamma/sqrt(running_var+eps), beta - running_mean*scale) and the activation are applied in the conv
+// epilogue, so z is never written and re-read.  The f32 result equals dg_conv_fwd followed
+// by dg_bn_apply bit for bit (same fmaf on the same f32 value); bf16 skips z's rounding.
+extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                                   int Cout, int R, int S, int pad, const float* bias, const float* scale,
+                                   const float* shift, int act, void* y, int64_t ldy, void* workspace,
+                                   int64_t ws_bytes, void* stream) {
+  DG_REQUIRE(x && w && y && scale && shift && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0 &&
+             (act == 0 || act == 1));
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
+  DG_SUPPORTED(dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0));
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
+  DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
+  FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, 0};
+  a.escale = scale;
+  a.eshift = shift;
+  a.eact = act;
+  if (dtype == DG_BF16 && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
+    const long long M = (long long)N * H * W;
+    const int ks = fwd_ksplit(M, Cout, C, R, S);
+    if (ks > 1 && ws_bytes >= (int64_t)ks * M * Cout * 4) {
+      a.ksplit = ks;
+      a.kpart = (float*)workspace;
+    }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+}
+
 extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                                  int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
                                  const float* scale, const float* shift, const float* mean, const float* invstd,

@@ -26,6 +26,7 @@ ACT_NONE, ACT_RELU = 0, 1
 
 
 _FROZEN_GEN = [0]
+_EVAL_FUSE = __import__("os").environ.get("DGVCC_EVAL_FUSE", "1") != "0"
 
 
 def invalidate_frozen():
@@ -126,6 +127,11 @@ class ConvLayer:
                 tape[self] = (x, z, stats, wp, drop, training)
             return
         wp = self._pack(dt) if training else frozen(self, ("w", dt), (self.conv.weight,), lambda: self._pack(dt))
+        if (_EVAL_FUSE and not training and bn is not None and pool is None and drop is None
+                and out is not None and not self.first and tape is None):
+            # evaluation: BN from the running statistics (+ReLU) in the conv epilogue, no z pass
+            K.conv_fwd_bn_eval(x, wp, self.Cout, self.R, self.pad, out, bias, bn_eval_cached(self, bn), self.act)
+            return
         z = Act(K.nhwc(x.N, x.H, x.W, self.Cout, dt, x.buf.device))
         epi = None
         if self.first:

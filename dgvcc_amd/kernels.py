@@ -105,6 +105,16 @@ def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
                                      ptr(work), ws, stream()), nbytes)
 
 
+def conv_fwd_bn_eval(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act, bias, stats, act: int):
+    """Eval-mode Conv + BN(running stats) [+ ReLU] in one launch: y = act((conv + bias)*scale + shift)."""
+    flops = 2.0 * x.M * x.C * R * R * Cout
+    nbytes = x.buf.element_size() * (x.M * x.C + wp.numel() + x.M * Cout)
+    ws, work = _fwd_workspace(x, Cout, R)
+    _timed("fwd", flops, lambda: call("dg_conv_fwd_bn_eval", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
+                                      R, R, pad, ptr(bias), ptr(stats[2]), ptr(stats[3]), act, y.ptr, y.ld,
+                                      ptr(work), ws, stream()), nbytes)
+
+
 _FWD_WS: dict = {}
 
 

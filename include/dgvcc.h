@@ -69,6 +69,14 @@ int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, i
 int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                    int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                    int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream);
+/* Eval-mode Conv + BatchNorm(running stats) [+ ReLU]: y = act((conv(x) + bias) * scale + shift)
+ * with scale = gamma/sqrt(running_var+eps), shift = beta - running_mean*scale applied in the conv
+ * epilogue (z never stored);
+ * f32 results equal dg_conv_fwd + dg_bn_apply bit for bit.  Workspace as dg_conv_fwd_ex. */
+int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                        int Cout, int R, int S, int pad, const float* bias, const float* scale,
+                        const float* shift, int act, void* y, int64_t ldy, void* workspace, int64_t ws_bytes,
+                        void* stream);
 /* bf16 forward (used for dgrad: flipped filters) that also emits the BatchNorm-backward
  * partial sums of the layer whose output gradient y is, from the epilogue:
  * bpart[dg_conv_stats_rows][3][Cout] for dg_bn_bwd_from_part (replaces dg_bn_bwd's

@@ -313,3 +313,32 @@ def test_dgrad_epilogue_bn_partials(dev, monkeypatch, N, H, W, C, Cin_next, act,
     assert relerr(dg1, dg0) < 1e-5 and relerr(db1, db0) < 1e-5
     assert relerr(dz1.buf, dz0.buf) < 1e-2  # bf16 storage: rare 1-ulp flips from the coefficients
     assert (dz1.buf.float() - dz0.buf.float()).abs().max() <= 2 * dz0.buf.float().abs().max() * 2 ** -8
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("N,H,W,C,Cout,act", [(1, 24, 32, 256, 512, 1), (2, 16, 256, 64, 64, 1), (1, 32, 48, 128, 128, 0)])
+def test_conv_bn_eval_epilogue(dev, dtype, N, H, W, C, Cout, act):
+    """dg_conv_fwd_bn_eval (eval BN + ReLU in the conv epilogue) against dg_conv_fwd +
+    dg_bn_apply: f32 bit-identical; bf16 within one bf16 ulp (z is no longer rounded)."""
+    K = _k()
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, dtype)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    gam, bet = torch.rand(Cout, device=dev) + 0.5, torch.randn(Cout, device=dev)
+    rm, rv = torch.randn(Cout, device=dev) * 0.1, torch.rand(Cout, device=dev) + 0.5
+    st = K.bn_eval_stats(gam, bet, rm, rv, 1e-5)
+    wp = K.pack_weight(w, dtype)
+    y1 = K.Act(K.nhwc(N, H, W, Cout, dtype, dev))
+    K.conv_fwd_bn_eval(K.Act(x), wp, Cout, 3, 1, y1, b, st, act)
+    z = K.Act(K.nhwc(N, H, W, Cout, dtype, dev))
+    K.conv_fwd(K.Act(x), wp, Cout, 3, 1, z, bias=b)
+    y0 = K.Act(K.nhwc(N, H, W, Cout, dtype, dev))
+    K.bn_apply(z, st, act, y0)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert torch.equal(y1.buf, y0.buf)
+    else:  # the unfused route rounds z to bf16 before scaling: error ~ |z * scale| * 2^-8
+        d = (y1.buf.float() - y0.buf.float()).abs()
+        zs = (z.buf.float() * st[2]).abs()
+        assert (d <= zs * 2 ** -7 + y0.buf.float().abs() * 2 ** -7 + 1e-3).all()
