@@ -885,6 +885,12 @@ static bool use_pipe() {
 // ---------------------------------------------------------------------------
 constexpr int T3_XROWS = 264;
 
+// PADK = 1 (W % 256 != 0: 320-px crops, evaluation frames): the 256-wide tile runs over the
+// zero-padded pixel index u = (n, p+1, q+1) in N x (H+2) x (W+2) instead of one image row, so
+// a tile may span rows and images; each kernel row's X strip is contiguous in u and the taps'
+// +-1 shifts land on zero pad cells exactly where the convolution pads.  Outputs on pad cells
+// are computed and dropped ((H+2)(W+2)/HW more MFMA work: +1.3% at 320x320).
+template <int PADK = 0>
 __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
   using T = bf16;
   constexpr int BN = 64, BM = 256;
@@ -896,16 +902,25 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
 
   const int HW = a.H * a.W;
   const int M = a.N * HW;
-  const int px0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+  const int PW = a.W + 2, PHW = (a.H + 2) * PW;
+  const int U = PADK ? a.N * PHW : M;
+  const int px0 = xcd_remap(blockIdx.x, gridDim.x) * BM;  // tile origin (padded index when PADK)
   const int n = px0 / HW, rem = px0 - n * HW;
   const int pr = rem / a.W, q0 = rem - pr * a.W;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lrow = lane >> 3;
-  const int xlo = max(0, px0 - a.W - 8), xhi = min(M, px0 + BM + a.W + 8);
+  const int xlo = PADK ? 0 : max(0, px0 - a.W - 8), xhi = PADK ? M : min(M, px0 + BM + a.W + 8);
   __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.x + (long long)xlo * a.ldx * 2), 0, (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 2),
       0x00020000);
+  auto unpad = [&](int u) -> int {  // padded index -> pixel, -1 on a pad cell / outside [0, U)
+    if (u < 0 || u >= U) return -1;
+    const int nn = u / PHW, r = u - nn * PHW;
+    const int pp = r / PW, qq = r - pp * PW;
+    if (pp < 1 || pp > a.H || qq < 1 || qq > a.W) return -1;
+    return nn * HW + (pp - 1) * a.W + (qq - 1);
+  };
   const long long ldw = 9ll * a.C;
   __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, (unsigned)(BN * ldw * 2), 0x00020000);
   const int CB = a.C / 64;
@@ -929,6 +944,12 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
         const int ch = (lane & 7) ^ (row & 7);
         lds_dma16(wr, As + ii * 1024,
                   (unsigned)(((long long)row * ldw + (dh * 3 + sw) * a.C + cb * 64 + ch * 8) * 2));
+      } else if (PADK) {  // X strip rows: padded index px0 - 4 + row of kernel row dh
+        const int jj = ii - A_INST, row = jj * 8 + lrow;
+        const int ch = (lane & 7) ^ (row & 7);
+        const int pin = unpad(px0 - 4 + row + (dh - 1) * PW);
+        lds_dma16(xr, Xs + jj * 1024,
+                  pin >= 0 ? (unsigned)(((long long)pin * a.ldx + cb * 64 + ch * 8) * 2) : 0xFFFFFFF0u);
       } else {            // X strip rows: pixel q0 - 4 + row of image row pr + dh - 1
         const int jj = ii - A_INST, row = jj * 8 + lrow;
         const int ch = (lane & 7) ^ (row & 7);
@@ -966,8 +987,9 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
   bool valid[TJ];
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int px = px0 + wpx + 16 * j + fr;
-    valid[j] = true;  // M % 256 == 0 on this path
+    const int px = PADK ? unpad(px0 + wpx + 16 * j + fr) : px0 + wpx + 16 * j + fr;
+    valid[j] = px >= 0;  // unpadded path: M % 256 == 0
+    if (px < 0) continue;
     T* yrow = y + (long long)px * a.ldy;
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
@@ -993,6 +1015,15 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
                              fr, fc);
 }
 
+// the padded 3-tap variant: whole-tensor x descriptor (32-bit byte offsets), no split-K
+static bool tap3_pad_ok(const FwdArgs& a) {
+  const char* e = getenv("DGVCC_TAP3_PAD");
+  if (e && e[0] == '0') return false;
+  if (!use_tap3() || a.ksplit > 1 || a.W % 256 == 0 || a.bpart) return false;
+  const long long M = (long long)a.N * a.H * a.W;
+  return M * a.ldx * 2 < (1ll << 31) && (long long)a.N * (a.H + 2) * (a.W + 2) < (1ll << 30);
+}
+
 template <typename T>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
@@ -1016,7 +1047,10 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
                            (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (bf16*)a.y, a.ldy, a.accumulate,
                            a.part, a.escale, a.eshift, a.eact);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
-        hipLaunchKernelGGL(conv_fwd_tap3_kernel, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+        hipLaunchKernelGGL(conv_fwd_tap3_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+      } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && !a.part && tap3_pad_ok(a)) {
+        const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
+        hipLaunchKernelGGL(conv_fwd_tap3_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
       else PIPE_LAUNCH(64, 3, np * (a.Cout / 64));
@@ -1922,6 +1956,11 @@ extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, i
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, 0, part};
+  {
+    FwdArgs q = a;
+    q.part = nullptr;
+    if (Cout == 64 && R == 3 && S == 3 && pad == 1 && tap3_pad_ok(q)) return DG_ERR_UNSUPPORTED;
+  }
   return launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 
@@ -1946,6 +1985,13 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   if (part) DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate, part};
+  {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
+     // runs dg_conv_fwd + the statistics pass instead
+    FwdArgs q = a;
+    q.part = nullptr;
+    if (part && dtype == DG_BF16 && Cout == 64 && R == 3 && S == 3 && pad == 1 && tap3_pad_ok(q))
+      return DG_ERR_UNSUPPORTED;
+  }
   if (dtype == DG_BF16 && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
     const long long M = (long long)N * H * W;
     const int ks = fwd_ksplit(M, Cout, C, R, S);

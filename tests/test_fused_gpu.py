@@ -342,3 +342,34 @@ def test_conv_bn_eval_epilogue(dev, dtype, N, H, W, C, Cout, act):
         d = (y1.buf.float() - y0.buf.float()).abs()
         zs = (z.buf.float() * st[2]).abs()
         assert (d <= zs * 2 ** -7 + y0.buf.float().abs() * 2 ** -7 + 1e-3).all()
+
+
+@pytest.mark.parametrize("N,H,W,C,acc", [(2, 20, 40, 64, False), (3, 7, 24, 128, True), (1, 320, 320, 64, False)])
+def test_tap3_padded_index(dev, monkeypatch, N, H, W, C, acc):
+    """Cout = 64 bf16 3x3 forward with W % 256 != 0 on the 3-tap kernel over the padded pixel
+    index (tiles spanning rows and images) against float64 and against the per-tap kernel;
+    the epilogue-statistics entry point declines such shapes (the caller then runs the
+    statistics pass)."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    w = (torch.randn(64, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
+    b = torch.randn(64, generator=g).to(dev)
+    y0 = torch.randn(N, H, W, 64, generator=g).to(dev, bf)
+    wp = K.pack_weight(w, bf)
+    outs = []
+    for pad in ("1", "0"):
+        monkeypatch.setenv("DGVCC_TAP3_PAD", pad)
+        y = K.Act(y0.clone())
+        K.conv_fwd(K.Act(x), wp, 64, 3, 1, y, bias=b, accumulate=acc)
+        outs.append(y.buf)
+    zs = K.Act(K.nhwc(N, H, W, 64, bf, dev))
+    monkeypatch.setenv("DGVCC_TAP3_PAD", "1")
+    assert K.conv_fwd_stats(K.Act(x), wp, 64, 3, 1, zs, bias=b) is None
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + y0.double()
+    assert relerr(outs[0], ref) < 1e-2
+    assert relerr(outs[0], outs[1]) < 1e-2
