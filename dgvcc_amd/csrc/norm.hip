@@ -659,6 +659,18 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
   return DG_OK;
 }
 
+// bn_bwd_finalize on caller-made partial sums part[nblk][3][C] (sum g', sum g' xhat,
+// sum xhat): the BN-backward coefficients coef[3][C] and dgamma/dbeta/dbias.
+extern "C" int dg_bn_bwd_finalize_part(const float* part, int nblk, int M, int C, const float* gamma,
+                                       const float* save_invstd, float* dgamma, float* dbeta, float* dbias,
+                                       float* coef, void* stream) {
+  DG_REQUIRE(part && nblk > 0 && M > 0 && C > 0 && save_invstd && coef);
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, (hipStream_t)stream, part, nblk, M, C,
+                     gamma, save_invstd, dgamma, dbeta, dbias, coef);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
 extern "C" int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
                               const float* gamma, const float* save_mean, const float* save_invstd,
                               const float* scale, const float* shift, int act, const float* drop, int HW,

@@ -18,6 +18,10 @@
 #include "dg_common.h"
 #include <algorithm>
 
+extern "C" int dg_bn_bwd_finalize_part(const float* part, int nblk, int M, int C, const float* gamma,
+                                       const float* save_invstd, float* dgamma, float* dbeta, float* dbias,
+                                       float* coef, void* stream);  // norm.hip
+
 namespace {
 
 constexpr int SNT = 256;     // 4 waves
@@ -39,15 +43,34 @@ constexpr int FW_LDS = T_BYTES + O_BYTES;
 
 __device__ __forceinline__ void lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// MODE 0: write z and the BN statistics partials; 1: statistics only (z is recomputed by
+// its consumers instead of stored); 2: y = relu(bn(z)) with z recomputed (the stored bf16 z
+// value, then dg_bn_apply's arithmetic) written to `z`, no statistics; 3: the BN-backward
+// partial sums of g (sum g', sum g' xhat, sum xhat; g' = g relu'(bn(z))) with z recomputed:
+// plain per-block sums for bn_bwd_finalize.
+struct StemBn {
+  const float *sc, *sf, *mu, *is;  // BN scale/shift and saved mean/invstd
+  const bf16* g;                   // MODE 3: gradient of y
+  long long ldg;
+};
+
+template <int MODE>
 __global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restrict__ img, int H, int W,
                                                           const bf16* __restrict__ wp, const float* __restrict__ bias,
                                                           bf16* __restrict__ z, long long ldz, long long nseg,
-                                                          float* __restrict__ part) {
+                                                          float* __restrict__ part, StemBn bn) {
   __shared__ __attribute__((aligned(16))) char smem[4 * FW_LDS];
   __shared__ float sh[4][3][SCO];
+  __shared__ __attribute__((aligned(16))) float bnp[4][SCO];  // MODE 2/3: scale, shift, mean, invstd
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int h = lane >> 4, col = lane & 15;
   char* T = smem + wid * FW_LDS;
+  if constexpr (MODE >= 2) {
+    const int k = threadIdx.x / SCO, c = threadIdx.x - k * SCO;  // 256 threads = 4 x 64
+    const float* src = k == 0 ? bn.sc : k == 1 ? bn.sf : k == 2 ? bn.mu : bn.is;
+    bnp[k][c] = src ? src[c] : 0.f;
+    __syncthreads();
+  }
   char* O = T + T_BYTES;
   const int spr = W / 64;  // segments per image row
   // LDS byte offsets of this lane's 8 taps (k = 8h + j) relative to pixel column x
@@ -105,8 +128,17 @@ __global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restric
     lds_fence();
     if (seg + sstride < nseg) gload(seg + sstride);
     const long long m0 = seg * 64;
-#pragma unroll
+    // MODE 3 keeps 3 x 16 accumulators and the pixel group's g live: the pixel-group loop
+    // stays rolled there (fully unrolled it spills)
+    constexpr int PFU = MODE == 3 ? 1 : 4;
+#pragma unroll PFU
     for (int pf = 0; pf < 4; ++pf) {
+      u2v graw[4];  // MODE 3: this pixel group's g, 4 loads issued before the first use
+      if constexpr (MODE == 3) {
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf)
+          graw[cf] = *(const u2v*)(bn.g + (m0 + 16 * pf + col) * bn.ldg + 16 * cf + 4 * h);
+      }
       const int x2 = (16 * pf + col) * 2;
       unsigned short v[8];
 #pragma unroll
@@ -123,31 +155,63 @@ __global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restric
         float o[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) o[i] = bf2f(bfbits(acc[cf][i] + bs[cf][i]));  // the stored value
-        const int chunk = 2 * cf + (h >> 1);
-        *(u2v*)(O + col * 128 + ((chunk ^ (col & 7)) << 4) + (h & 1) * 8) =
-            u2v{pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])};
-        if (first && pf == 0) {  // per-channel shift: the wave's first pixel (lane col 0 of its group)
+        const int cb = 16 * cf + 4 * h;
+        if constexpr (MODE == 2) {  // dg_bn_apply: relu(fmaf(z, scale, shift))
+          const f4v sc4 = *(const f4v*)&bnp[0][cb], sf4 = *(const f4v*)&bnp[1][cb];
 #pragma unroll
-          for (int i = 0; i < 4; ++i) K[cf * 4 + i] = __shfl(o[i], lane & 48, 64);
+          for (int i = 0; i < 4; ++i) {
+            const float t = fmaf(o[i], sc4[i], sf4[i]);
+            o[i] = t > 0.f ? t : 0.f;
+          }
         }
+        if constexpr (MODE == 0 || MODE == 2) {
+          const int chunk = 2 * cf + (h >> 1);
+          *(u2v*)(O + col * 128 + ((chunk ^ (col & 7)) << 4) + (h & 1) * 8) =
+              u2v{pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])};
+        }
+        if constexpr (MODE == 0 || MODE == 1) {
+          if (first && pf == 0) {  // per-channel shift: the wave's first pixel (lane col 0 of its group)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float d = o[i] - K[cf * 4 + i];
-          S1[cf * 4 + i] += d;
-          S2[cf * 4 + i] = fmaf(d, d, S2[cf * 4 + i]);
+            for (int i = 0; i < 4; ++i) K[cf * 4 + i] = __shfl(o[i], lane & 48, 64);
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float d = o[i] - K[cf * 4 + i];
+            S1[cf * 4 + i] += d;
+            S2[cf * 4 + i] = fmaf(d, d, S2[cf * 4 + i]);
+          }
+        }
+        if constexpr (MODE == 3) {  // bn_bwd_load + bn_bwd_partial of norm.hip (act = relu, no dropout)
+          const u2v gr = graw[cf];
+          const float gv[4] = {__uint_as_float(gr[0] << 16), __uint_as_float(gr[0] & 0xffff0000u),
+                               __uint_as_float(gr[1] << 16), __uint_as_float(gr[1] & 0xffff0000u)};
+          const f4v sc4 = *(const f4v*)&bnp[0][cb], sf4 = *(const f4v*)&bnp[1][cb];
+          const f4v mu4 = *(const f4v*)&bnp[2][cb], is4 = *(const f4v*)&bnp[3][cb];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float gg = gv[i];
+            if (!(fmaf(o[i], sc4[i], sf4[i]) > 0.f)) gg = 0.f;
+            const float xh = (o[i] - mu4[i]) * is4[i];
+            S1[cf * 4 + i] += gg;
+            S2[cf * 4 + i] = fmaf(gg, xh, S2[cf * 4 + i]);
+            K[cf * 4 + i] += xh;
+          }
         }
       }
-      lds_fence();
+      if constexpr (MODE == 0 || MODE == 2) {
+        lds_fence();
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int row = (lane >> 3) + 8 * u, chunk = lane & 7;
-        const u4v ov = *(const u4v*)(O + row * 128 + ((chunk ^ (row & 7)) << 4));
-        *(u4v*)(z + (m0 + 16 * pf + row) * ldz + chunk * 8) = ov;
+        for (int u = 0; u < 2; ++u) {
+          const int row = (lane >> 3) + 8 * u, chunk = lane & 7;
+          const u4v ov = *(const u4v*)(O + row * 128 + ((chunk ^ (row & 7)) << 4));
+          *(u4v*)(z + (m0 + 16 * pf + row) * ldz + chunk * 8) = ov;
+        }
       }
     }
     first = false;
     nloc += 64;
   }
+  if constexpr (MODE == 2) return;
   // reduce over the 16 pixel lanes of each group
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
@@ -155,7 +219,27 @@ __global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restric
     for (int o = 1; o < 16; o <<= 1) {
       S1[e] += __shfl_xor(S1[e], o, 64);
       S2[e] += __shfl_xor(S2[e], o, 64);
+      if constexpr (MODE == 3) K[e] += __shfl_xor(K[e], o, 64);
     }
+  }
+  if constexpr (MODE == 3) {  // plain sums: 4 waves in a fixed order -> one part row per block
+    if (col == 0) {
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int c = 16 * cf + 4 * h + i, e = cf * 4 + i;
+          sh[wid][0][c] = S1[e];
+          sh[wid][1][c] = S2[e];
+          sh[wid][2][c] = K[e];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 * SCO) {
+      const int k = threadIdx.x / SCO, c = threadIdx.x - k * SCO;
+      part[(long long)blockIdx.x * 3 * SCO + k * SCO + c] = sh[0][k][c] + sh[1][k][c] + sh[2][k][c] + sh[3][k][c];
+    }
+    return;
   }
   if (col == 0) {
 #pragma unroll
@@ -196,16 +280,33 @@ __global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restric
 // transposed im2col tile colT[32 k][32 px] bf16 (64-B rows; rows 27..31 stay zero).
 // Lane roles: dz for channels 8*(lane&7).. of pixels (lane>>3) + 8u; colT rows
 // k = 2i + (lane>>5) at pixel lane&31.  Loads are prefetched a segment ahead.
-constexpr int BDZ = 32 * 128, BCOL = 32 * 64, BW_LDS = BDZ + BCOL;
+// RECOMP = 1: z is not read from HBM but recomputed from the staged im2col tile (the same
+// MFMA on the same bf16 operands as stem_fwd_kernel, so the same bits), transposed through
+// a third per-wave LDS tile into the dz lane layout.
+constexpr int CTS = 72;  // colT row stride (B): the 4 k-groups of a B-fragment gather hit distinct banks
+constexpr int BDZ = 32 * 128, BCOL = 32 * CTS, BZT = 32 * 128;
 
+template <int RECOMP>
 __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
     const float* __restrict__ img, int H, int W, const bf16* __restrict__ g, long long ldg, const bf16* __restrict__ z,
     long long ldz, const float* __restrict__ mean, const float* __restrict__ invstd, const float* __restrict__ scale,
-    const float* __restrict__ shift, const float* __restrict__ coef, long long nseg, float* __restrict__ slab) {
+    const float* __restrict__ shift, const float* __restrict__ coef, long long nseg, float* __restrict__ slab,
+    const bf16* __restrict__ wpk, const float* __restrict__ bias) {
+  constexpr int BW_LDS = BDZ + BCOL + (RECOMP ? BZT : 0);
   __shared__ __attribute__((aligned(16))) char smem[4 * BW_LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   char* DZ = smem + wid * BW_LDS;
   char* CT = DZ + BDZ;
+  char* ZT = CT + BCOL;  // RECOMP: z tile [32 px][64 co] bf16
+  u4v wa[4];             // RECOMP: filter fragments (A operand) as stem_fwd_kernel
+  __shared__ __attribute__((aligned(16))) float bsl[SCO];  // RECOMP: conv bias (LDS: registers are full)
+  if constexpr (RECOMP) {
+    const int col = lane & 15, hh = lane >> 4;
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) wa[cf] = *(const u4v*)(wpk + (16 * cf + col) * SK + 8 * hh);
+    if (threadIdx.x < SCO) bsl[threadIdx.x] = bias ? bias[threadIdx.x] : 0.f;
+    __syncthreads();
+  }
   const int spr = W / 32;
   const int c0 = (lane & 7) * 8;
   float sc[8], sf[8], mu[8], is[8], k1[8], k2[8], k3[8];
@@ -216,7 +317,7 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
   }
   // colT rows of this lane: k = 2i + (lane>>5), i = 0..13 (k = 27 -> zero); px = lane & 31
   const int half = lane >> 5, xq = lane & 31;
-  for (int r = 28 + half; r < 32; r += 2) *(unsigned short*)(CT + r * 64 + xq * 2) = 0;
+  for (int r = 28 + half; r < 32; r += 2) *(unsigned short*)(CT + r * CTS + xq * 2) = 0;
 
   struct Regs {
     u4v gr[4], zr[4];
@@ -231,7 +332,7 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
     for (int u = 0; u < 4; ++u) {
       const long long m = m0 + (lane >> 3) + 8 * u;
       R.gr[u] = *(const u4v*)(g + m * ldg + c0);
-      R.zr[u] = *(const u4v*)(z + m * ldz + c0);
+      if constexpr (!RECOMP) R.zr[u] = *(const u4v*)(z + m * ldz + c0);
     }
 #pragma unroll
     for (int i = 0; i < 14; ++i) {
@@ -247,13 +348,51 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
   for (int cf = 0; cf < 4; ++cf) acc[cf][0] = acc[cf][1] = f4v{0.f, 0.f, 0.f, 0.f};
   const int gq = lane >> 4, q4 = (lane & 15) >> 2, p4 = lane & 3, li = lane & 15;
   auto process = [&](const Regs& R) {
+    u4v zrow[4];
+    if constexpr (RECOMP) {
+      // im2col tile first; z = W . colT on MFMA (B fragments gathered as stem_fwd_kernel does)
+#pragma unroll
+      for (int i = 0; i < 14; ++i) *(unsigned short*)(CT + (2 * i + half) * CTS + xq * 2) = bfbits(R.cv[i]);
+      lds_fence();
+      const int col = lane & 15, hh = lane >> 4;
+#pragma unroll
+      for (int pb = 0; pb < 2; ++pb) {
+        unsigned short v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = *(const unsigned short*)(CT + (8 * hh + j) * CTS + (16 * pb + col) * 2);
+        const u4v b = u4v{v[0] | ((unsigned)v[1] << 16), v[2] | ((unsigned)v[3] << 16),
+                          v[4] | ((unsigned)v[5] << 16), v[6] | ((unsigned)v[7] << 16)};
+#pragma unroll
+        for (int cf = 0; cf < 4; ++cf) {
+          const f4v a4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s8v, wa[cf]),
+                                                                 __builtin_bit_cast(s8v, b), f4v{0.f, 0.f, 0.f, 0.f},
+                                                                 0, 0, 0);
+          const f4v b4 = *(const f4v*)&bsl[16 * cf + 4 * hh];
+          float o[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o[i] = bf2f(bfbits(a4[i] + b4[i]));  // stem_fwd's stored value
+          const int zr = 16 * pb + col, chunk = 2 * cf + (hh >> 1);  // 16-B chunks XOR-swizzled by row
+          *(u2v*)(ZT + zr * 128 + ((chunk ^ (zr & 7)) << 4) + (hh & 1) * 8) =
+              u2v{pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3])};
+        }
+      }
+      lds_fence();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int zr = (lane >> 3) + 8 * u, chunk = lane & 7;
+        zrow[u] = *(const u4v*)(ZT + zr * 128 + ((chunk ^ (zr & 7)) << 4));
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) zrow[u] = R.zr[u];
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float gv[8], zv[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         gv[2 * i] = __uint_as_float(R.gr[u][i] << 16); gv[2 * i + 1] = __uint_as_float(R.gr[u][i] & 0xffff0000u);
-        zv[2 * i] = __uint_as_float(R.zr[u][i] << 16); zv[2 * i + 1] = __uint_as_float(R.zr[u][i] & 0xffff0000u);
+        zv[2 * i] = __uint_as_float(zrow[u][i] << 16); zv[2 * i + 1] = __uint_as_float(zrow[u][i] & 0xffff0000u);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {  // bn_bwd_load + bn_bwd_apply of norm.hip (act = relu, no dropout)
@@ -265,14 +404,16 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
       *(u4v*)(DZ + px * 128 + c0 * 2) =
           u4v{pack_bf2(gv[0], gv[1]), pack_bf2(gv[2], gv[3]), pack_bf2(gv[4], gv[5]), pack_bf2(gv[6], gv[7])};
     }
+    if constexpr (!RECOMP) {
 #pragma unroll
-    for (int i = 0; i < 14; ++i) *(unsigned short*)(CT + (2 * i + half) * 64 + xq * 2) = bfbits(R.cv[i]);
+      for (int i = 0; i < 14; ++i) *(unsigned short*)(CT + (2 * i + half) * CTS + xq * 2) = bfbits(R.cv[i]);
+    }
     lds_fence();
     // A = dz^T (transposed reads): logical k = 8*gq + j <-> pixel 4*gq + (j&3) + 16*(j>>2)
     s8v bfv[2];
 #pragma unroll
     for (int kf = 0; kf < 2; ++kf) {
-      const char* rp = CT + (16 * kf + li) * 64;
+      const char* rp = CT + (16 * kf + li) * CTS;
       const u2v lo = *(const u2v*)(rp + 8 * gq), hi = *(const u2v*)(rp + 32 + 8 * gq);
       bfv[kf] = __builtin_bit_cast(s8v, u4v{lo[0], lo[1], hi[0], hi[1]});
     }
@@ -466,10 +607,56 @@ extern "C" int dg_stem_fwd(const float* img, int N, int H, int W, const void* wp
   DG_REQUIRE(img && wpack && z && part && N > 0 && H > 0 && W > 0 && ldz >= SCO);
   DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldz % 8 == 0);
   const long long nseg = (long long)N * H * (W / 64);
-  hipLaunchKernelGGL(stem_fwd_kernel, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
-                     (const bf16*)wpack, bias, (bf16*)z, (long long)ldz, nseg, part);
+  hipLaunchKernelGGL(stem_fwd_kernel<0>, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
+                     (const bf16*)wpack, bias, (bf16*)z, (long long)ldz, nseg, part, StemBn{});
   DG_CHECK_LAUNCH();
   return DG_OK;
+}
+
+// Statistics only (z not stored; its consumers recompute it from the image).
+extern "C" int dg_stem_stats(const float* img, int N, int H, int W, const void* wpack, const float* bias, float* part,
+                             void* stream) {
+  DG_REQUIRE(img && wpack && part && N > 0 && H > 0 && W > 0);
+  DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31));
+  const long long nseg = (long long)N * H * (W / 64);
+  hipLaunchKernelGGL(stem_fwd_kernel<1>, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
+                     (const bf16*)wpack, bias, (bf16*)nullptr, 0LL, nseg, part, StemBn{});
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// y = relu(scale * z + shift) with z = conv(img) + bias recomputed (bit-identical to
+// dg_stem_fwd + dg_bn_apply on the stored z).
+extern "C" int dg_stem_apply(const float* img, int N, int H, int W, const void* wpack, const float* bias,
+                             const float* scale, const float* shift, void* y, int64_t ldy, void* stream) {
+  DG_REQUIRE(img && wpack && scale && shift && y && N > 0 && H > 0 && W > 0 && ldy >= SCO);
+  DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldy % 8 == 0);
+  const long long nseg = (long long)N * H * (W / 64);
+  StemBn bn{scale, shift, nullptr, nullptr, nullptr, 0};
+  hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
+                     (const bf16*)wpack, bias, (bf16*)y, (long long)ldy, nseg, (float*)nullptr, bn);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// BN-backward partial sums of the stem (z recomputed): part[dg_stem_part_rows][3][64] of
+// (sum g', sum g' xhat, sum xhat), g' = g * relu'(scale z + shift); then bn_bwd_finalize.
+extern "C" int dg_stem_bwd_coef(const float* img, int N, int H, int W, const void* wpack, const float* bias,
+                                const void* g, int64_t ldg, const float* gamma, const float* save_mean,
+                                const float* save_invstd, const float* scale, const float* shift, float* coef,
+                                float* dgamma, float* dbeta, float* dbias, float* part, void* stream) {
+  DG_REQUIRE(img && wpack && g && save_mean && save_invstd && scale && shift && coef && part && N > 0 && H > 0 &&
+             W > 0 && ldg >= SCO);
+  DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldg % 8 == 0);
+  const long long nseg = (long long)N * H * (W / 64);
+  const int grid = stem_fwd_grid(nseg);
+  StemBn bn{scale, shift, save_mean, save_invstd, (const bf16*)g, (long long)ldg};
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(stem_fwd_kernel<3>, dim3(grid), dim3(SNT), 0, st, img, H, W, (const bf16*)wpack, bias,
+                     (bf16*)nullptr, 0LL, nseg, part, bn);
+  DG_CHECK_LAUNCH();
+  return dg_bn_bwd_finalize_part(part, grid, (int)(N * (long long)H * W), SCO, gamma, save_invstd, dgamma, dbeta,
+                                 dbias, coef, stream);
 }
 
 extern "C" int64_t dg_bn_part_workspace(int nblk, int C) {
@@ -504,13 +691,15 @@ extern "C" int64_t dg_stem_bwd_workspace(int N, int H, int W) {
   return ((int64_t)grid + dg_cdiv(grid, STEM_RPB)) * SCO * SK * 4;
 }
 
+// z == NULL: z is recomputed from img with the packed filters wpack (+ bias), as dg_stem_stats
+// / dg_stem_apply do, instead of read from HBM.
 extern "C" int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
                            int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
                            const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,
-                           int accumulate, void* stream) {
-  DG_REQUIRE(img && g && z && save_mean && save_invstd && scale && shift && coef && dw && workspace);
-  DG_REQUIRE(N > 0 && H > 0 && W > 0 && ldg >= SCO && ldz >= SCO);
-  DG_SUPPORTED(W % 32 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldg % 8 == 0 && ldz % 8 == 0);
+                           int accumulate, const void* wpack, const float* bias, void* stream) {
+  DG_REQUIRE(img && g && save_mean && save_invstd && scale && shift && coef && dw && workspace && (z || wpack));
+  DG_REQUIRE(N > 0 && H > 0 && W > 0 && ldg >= SCO && (!z || ldz >= SCO));
+  DG_SUPPORTED(W % 32 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldg % 8 == 0 && (!z || ldz % 8 == 0));
   const long long nseg = (long long)N * H * (W / 32);
   const int grid = stem_bwd_grid(nseg);
   const int nred = dg_cdiv(grid, STEM_RPB);
@@ -518,8 +707,14 @@ extern "C" int dg_stem_bwd(const float* img, int N, int H, int W, const void* g,
   hipStream_t st = (hipStream_t)stream;
   float* slab = (float*)workspace;
   float* slab2 = slab + (long long)grid * SCO * SK;
-  hipLaunchKernelGGL(stem_bwd_kernel, dim3(grid), dim3(SNT), 0, st, img, H, W, (const bf16*)g, (long long)ldg,
-                     (const bf16*)z, (long long)ldz, save_mean, save_invstd, scale, shift, coef, nseg, slab);
+  if (z)
+    hipLaunchKernelGGL(stem_bwd_kernel<0>, dim3(grid), dim3(SNT), 0, st, img, H, W, (const bf16*)g, (long long)ldg,
+                       (const bf16*)z, (long long)ldz, save_mean, save_invstd, scale, shift, coef, nseg, slab,
+                       (const bf16*)nullptr, (const float*)nullptr);
+  else
+    hipLaunchKernelGGL(stem_bwd_kernel<1>, dim3(grid), dim3(SNT), 0, st, img, H, W, (const bf16*)g, (long long)ldg,
+                       (const bf16*)nullptr, 0LL, save_mean, save_invstd, scale, shift, coef, nseg, slab,
+                       (const bf16*)wpack, bias);
   DG_CHECK_LAUNCH();
   hipLaunchKernelGGL(colsum_rows_kernel, dim3(SCO * SK / SNT, nred), dim3(SNT), 0, st, (const float*)slab, grid,
                      SCO * SK, STEM_RPB, slab2);

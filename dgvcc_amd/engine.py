@@ -27,6 +27,7 @@ ACT_NONE, ACT_RELU = 0, 1
 
 _FROZEN_GEN = [0]
 _EVAL_FUSE = __import__("os").environ.get("DGVCC_EVAL_FUSE", "1") != "0"
+_STEM_RECOMP = __import__("os").environ.get("DGVCC_STEM_RECOMP", "1") != "0"
 
 
 def invalidate_frozen():
@@ -114,6 +115,20 @@ class ConvLayer:
             N, _, H, W = x.shape
             build = lambda: K.pack_weight(self.conv.weight.detach(), dt, cpad=3, row_len=32)  # noqa: E731
             wp = build() if training else frozen(self, ("stem", dt), (self.conv.weight,), build)
+            if _STEM_RECOMP and pool is None and drop is None and out is not None:
+                # z-free stem: statistics pass, then conv recomputed with BN+ReLU applied; the
+                # backward recomputes z again (27 MACs per output vs 128 B/px per HBM pass)
+                if training:
+                    part, nblk = K.stem_stats(x, wp, bias)
+                    bn.num_batches_tracked.add_(1)
+                    stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
+                                               bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+                else:
+                    stats = bn_eval_cached(self, bn)
+                K.stem_apply(x, wp, bias, stats, out)
+                if tape is not None:
+                    tape[self] = (x, None, stats, wp, drop, training)
+                return
             z = Act(K.nhwc(N, H, W, self.Cout, dt, x.device))
             part, nblk = K.stem_fwd(x, wp, bias, z)
             if training:
@@ -175,17 +190,22 @@ class ConvLayer:
         pre = tape.pop(("bnpart", self), None)
         if self.bn is not None and not training:
             raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
-        dev = z.buf.device
-        dz = Act(torch.empty_like(z.buf))
+        dev = stats.device
+        dz = Act(torch.empty_like(z.buf)) if z is not None else None
         dgamma = torch.empty(self.Cout, dtype=torch.float32, device=dev)
         dbeta = torch.empty(self.Cout, dtype=torch.float32, device=dev)
         dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) \
             if self.conv.bias is not None else None
         gamma = self.bn.weight.detach() if self.bn is not None else None
         if isinstance(x, torch.Tensor):  # fused bf16 stem: coefficients, then BN-backward + wgrad in one pass
-            coef = K.bn_bwd_coef(g, z, gamma, stats, self.act, dgamma, dbeta, dbias, drop)
             dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
-            K.stem_bwd(x, g, z, stats, coef, dw)
+            bias = self.conv.bias.detach() if self.conv.bias is not None else None
+            if z is None:  # z-free stem: z recomputed from the image in both passes
+                coef = K.stem_bwd_coef(x, wp, bias, g, gamma, stats, dgamma, dbeta, dbias)
+                K.stem_bwd(x, g, None, stats, coef, dw, wp=wp, bias=bias)
+            else:
+                coef = K.bn_bwd_coef(g, z, gamma, stats, self.act, dgamma, dbeta, dbias, drop)
+                K.stem_bwd(x, g, z, stats, coef, dw)
             grads = {self.conv.weight: dw, self.bn.weight: dgamma, self.bn.bias: dbeta}
             if self.conv.bias is not None:
                 grads[self.conv.bias] = dbias

@@ -271,16 +271,52 @@ def bn_bwd_coef(g: Act, z: Act, gamma, stats, act: int, dgamma, dbeta, dbias=Non
     return coef
 
 
-def stem_bwd(img: torch.Tensor, g: Act, z: Act, stats, coef, dw: torch.Tensor, accumulate=False):
+def stem_bwd(img: torch.Tensor, g: Act, z: Act | None, stats, coef, dw: torch.Tensor, accumulate=False,
+             wp: torch.Tensor | None = None, bias: torch.Tensor | None = None):
+    """z = None: z recomputed from img with the packed filters wp (+ bias)."""
     N, _, H, W = img.shape
     ws = query("dg_stem_bwd_workspace", N, H, W)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=img.device)
     flops = 2.0 * N * H * W * 27 * 64
-    nbytes = 2.0 * (g.M * g.C + z.M * z.C) + 4.0 * img.numel()
-    _timed("stem_wgrad", flops, lambda: call("dg_stem_bwd", ptr(img), N, H, W, g.ptr, g.ld, z.ptr, z.ld,
+    nbytes = 2.0 * g.M * g.C * (2 if z is not None else 1) + 4.0 * img.numel()
+    _timed("stem_wgrad", flops, lambda: call("dg_stem_bwd", ptr(img), N, H, W, g.ptr, g.ld,
+                                             z.ptr if z is not None else None, z.ld if z is not None else 0,
                                              ptr(stats[0]), ptr(stats[1]), ptr(stats[2]), ptr(stats[3]),
-                                             ptr(coef), ptr(dw), ptr(work), ws, int(accumulate),
+                                             ptr(coef), ptr(dw), ptr(work), ws, int(accumulate), ptr(wp), ptr(bias),
                                              stream()), nbytes)
+
+
+def stem_stats(img: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor | None) -> tuple:
+    """BN statistics partials of z = conv(img) + bias without storing z."""
+    N, _, H, W = img.shape
+    rows = query("dg_stem_part_rows", N, H, W)
+    part = torch.empty((rows, 3, 64), dtype=torch.float32, device=img.device)
+    _timed("stem", 2.0 * N * H * W * 27 * 64,
+           lambda: call("dg_stem_stats", ptr(img), N, H, W, ptr(wp), ptr(bias), ptr(part), stream()),
+           4.0 * img.numel())
+    return part, rows
+
+
+def stem_apply(img: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor | None, stats, y: Act):
+    """y = relu(BN(conv(img) + bias)) with z recomputed (stem_fwd + bn_apply, bit for bit)."""
+    N, _, H, W = img.shape
+    _timed("stem", 2.0 * N * H * W * 27 * 64,
+           lambda: call("dg_stem_apply", ptr(img), N, H, W, ptr(wp), ptr(bias), ptr(stats[2]), ptr(stats[3]),
+                        y.ptr, y.ld, stream()),
+           4.0 * img.numel() + 2.0 * N * H * W * 64)
+
+
+def stem_bwd_coef(img: torch.Tensor, wp: torch.Tensor, bias, g: Act, gamma, stats, dgamma, dbeta,
+                  dbias=None) -> torch.Tensor:
+    """bn_bwd_coef of the stem with z recomputed from the image."""
+    N, _, H, W = img.shape
+    rows = query("dg_stem_part_rows", N, H, W)
+    part = torch.empty((rows, 3, 64), dtype=torch.float32, device=img.device)
+    coef = torch.empty((3, 64), dtype=torch.float32, device=img.device)
+    call("dg_stem_bwd_coef", ptr(img), N, H, W, ptr(wp), ptr(bias), g.ptr, g.ld, ptr(gamma), ptr(stats[0]),
+         ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), ptr(coef), ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(part),
+         stream())
+    return coef
 
 
 # ---------------------------------------------------------------- BN -------

@@ -162,6 +162,11 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               const float* scale, const float* shift, int act, const float* drop, int HW,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
               void* workspace, void* stream);
+/* BN-backward finalize on caller-made partial sums part[nblk][3][C] = (sum g', sum g' xhat,
+ * sum xhat): coef[3][C] (dz = k1 g' - k2 xhat - k3) and dgamma/dbeta/dbias (may be NULL). */
+int dg_bn_bwd_finalize_part(const float* part, int nblk, int M, int C, const float* gamma,
+                            const float* save_invstd, float* dgamma, float* dbeta, float* dbias,
+                            float* coef, void* stream);
 /* dg_bn_bwd from precomputed partial sums part[nblk][3][C] (dg_conv_fwd_bnbwd): finalize +
  * apply; coef: caller workspace of 3*C floats. */
 int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const void* g, int64_t ldg, const void* z,
@@ -217,7 +222,21 @@ int64_t dg_stem_bwd_workspace(int N, int H, int W);
 int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
                 int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
                 const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,
-                int accumulate, void* stream);
+                int accumulate, const void* wpack, const float* bias, void* stream);
+/* z-free stem (z = conv(img) + bias is recomputed where needed instead of stored; 27 MACs
+ * per output against 128 B of HBM traffic per pixel per pass): dg_stem_stats (BN statistics
+ * partials only, rows = dg_stem_part_rows), dg_stem_apply (y = relu(scale z + shift), equal
+ * bit for bit to dg_stem_fwd + dg_bn_apply), dg_stem_bwd_coef (BN-backward coefficients
+ * from g with z recomputed; part: dg_stem_part_rows x 3 x 64 floats), and dg_stem_bwd with
+ * z = NULL (wpack/bias given). */
+int dg_stem_stats(const float* img, int N, int H, int W, const void* wpack, const float* bias, float* part,
+                  void* stream);
+int dg_stem_apply(const float* img, int N, int H, int W, const void* wpack, const float* bias,
+                  const float* scale, const float* shift, void* y, int64_t ldy, void* stream);
+int dg_stem_bwd_coef(const float* img, int N, int H, int W, const void* wpack, const float* bias,
+                     const void* g, int64_t ldg, const float* gamma, const float* save_mean,
+                     const float* save_invstd, const float* scale, const float* shift, float* coef,
+                     float* dgamma, float* dbeta, float* dbias, float* part, void* stream);
 
 /* ---- ResNet bottleneck joins and InstanceNorm (IBN-b / ISW / SW trunks) --------
  * Residual join out = act(bn3(z1) + bn_ds(z2) | z2) of Bottleneck.forward

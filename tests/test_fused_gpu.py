@@ -85,6 +85,24 @@ def test_stem_fwd_bwd(dev, N, H, W):
     assert relerr(dw, wref) < 1e-4
     assert relerr(dw, dw0) < 1e-4
 
+    # z-free route: statistics-only pass, recomputed z in the apply / coefficient / wgrad passes
+    part1, nblk1 = K.stem_stats(imgd, wp, bd)
+    rm1, rv1 = torch.zeros(64, device=dev), torch.ones(64, device=dev)
+    stats1 = K.bn_part_finalize(part1, nblk1, 64, gam.to(dev), bet.to(dev), rm1, rv1, 0.1, 1e-5)
+    y1 = K.Act(K.nhwc(N, H, W, 64, bf, dev))
+    K.stem_apply(imgd, wp, bd, stats1, y1)
+    y0 = K.Act(K.nhwc(N, H, W, 64, bf, dev))
+    K.bn_apply(z, stats, 1, y0)
+    dgam1, dbet1, dbias1 = (torch.empty(64, device=dev) for _ in range(3))
+    coef1 = K.stem_bwd_coef(imgd, wp, bd, g_act, gam.to(dev), stats1, dgam1, dbet1, dbias1)
+    dw1 = torch.empty(64, 3, 3, 3, device=dev)
+    K.stem_bwd(imgd, g_act, None, stats1, coef1, dw1, wp=wp, bias=bd)
+    torch.cuda.synchronize()
+    assert torch.equal(part1, part) and torch.equal(stats1, stats)
+    assert torch.equal(y1.buf, y0.buf)  # bit for bit: same z bits, same BN-apply arithmetic
+    assert relerr(coef1, coef) < 1e-5 and relerr(dgam1, dgam) < 1e-5 and relerr(dbet1, dbet) < 1e-5
+    assert relerr(dw1, dw) < 1e-4
+
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("with_y,with_gd", [(False, False), (True, True)])
