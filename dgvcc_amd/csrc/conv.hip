@@ -544,7 +544,10 @@ __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, const char* 
 }
 constexpr int PSTAGES = 3;
 
-template <int BN, int STG, int VAR = 0>
+// EPI selects the epilogue at compile time (each variant's registers stay out of the
+// others'; runtime branches on all four spilled the 256-wide kernel): 0 = bias / accumulate /
+// statistics, 1 = split-K f32 partials, 2 = BN-backward partials (dgrad), 3 = eval BN+ReLU.
+template <int BN, int STG, int VAR = 0, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   using T = bf16;
   constexpr int BK = 64;                    // bf16 channels per K-step (128-B rows)
@@ -663,7 +666,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   }
 #undef PIPE_ISSUE
 
-  if (a.ksplit > 1) {  // raw f32 partial sums of this K-slice
+  if constexpr (EPI == 1) {  // raw f32 partial sums of this K-slice
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = px0 + wpx + 16 * j + fr;
@@ -695,17 +698,191 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
         ld4(yrow + co, o);
         v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
-      epi_affine(v, a, co);
+      if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
     }
   }
-  if (a.part)
-    epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / PBM) * 3 * a.Cout, a.Cout,
-                             co0, tid, fr, fc);
-  else if (a.bpart)
-    epi_bnbwd<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, wpx, smem, a, px0, co0, tid, fr, fc);
+  if constexpr (EPI == 0) {
+    if (a.part)
+      epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / PBM) * 3 * a.Cout, a.Cout,
+                               co0, tid, fr, fc);
+  }
+  if constexpr (EPI == 2) epi_bnbwd<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, wpx, smem, a, px0, co0, tid, fr, fc);
+}
+
+// Persistent form of conv_fwd_pipe_kernel (VAR 2 schedule): one block per CU walks its
+// tiles (block b, tiles b, b + G, ... through the same XCD remap) and keeps the LDS-DMA
+// ring running across tile boundaries: the next tile's first K-steps are issued during
+// the current tile's last ones, so its prologue latency hides under the current tile's
+// MFMAs and epilogue stores.  The epilogue-statistics scratch gets its own LDS so the
+// in-flight ring stages are never touched.  Requires KT > PF (K-steps per tile).
+template <int BN, int STG, int EPI = 0>
+__global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
+  using T = bf16;
+  constexpr int BK = 64;
+  constexpr int AI = BN / 64;
+  constexpr int BI = PBM / 64;
+  constexpr int TI = BN / 32, TJ = 4;
+  constexpr int STAGE = (BN + PBM) * 128;
+  constexpr int PF = STG - 1;
+  constexpr int EPI_B = 4 * 3 * BN * 4;  // epi_stats scratch [4][3][BN] f32
+  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B];
+  char* epi_lds = smem + STG * STAGE;
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BN;
+  const int ntile = (M + PBM - 1) / PBM * nco;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lrow = lane >> 3;
+  const int gchunk = (lane & 7) ^ lrow;
+  const long long ldw = (long long)a.R * a.S * a.C;
+  const int CB = a.C / BK;
+  const int KT = a.R * a.S * CB;
+  const unsigned cbytes = (unsigned)(gchunk * 16);
+  unsigned aoff[AI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) aoff[i] = (unsigned)((((wid * AI + i) * 8 + lrow) * ldw + gchunk * 8) * 2);
+
+  struct Ctx {
+    int px0, co0;
+    __amdgpu_buffer_rsrc_t xr, wr;
+    int pp[BI], pq[BI], prow[BI];
+  };
+  auto setup = [&](int lin, Ctx& c) {
+    const int t = xcd_remap(lin, ntile);
+    c.co0 = (t % nco) * BN;
+    c.px0 = (t / nco) * PBM;
+    const int halo = a.pad * (a.W + 1);
+    const int plo = max(0, c.px0 - halo);
+    const int phi = min(M, c.px0 + PBM + halo);
+    const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 2);
+    c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 2), 0, win_bytes, 0x00020000);
+    c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.w + (long long)c.co0 * ldw * 2), 0, (unsigned)(BN * ldw * 2),
+                                             0x00020000);
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int m = c.px0 + (wid * BI + i) * 8 + lrow;
+      const int rem = m % HW;
+      c.prow[i] = m - plo;
+      c.pp[i] = (m < M) ? rem / a.W : -100000;
+      c.pq[i] = rem % a.W;
+    }
+  };
+  auto issue = [&](const Ctx& c, int kt, int stage) {
+    const int rs = kt / CB, cb = kt - rs * CB;
+    const int r = rs / a.S, s2 = rs - r * a.S;
+    char* As = smem + stage * STAGE;
+    char* Bs = As + BN * 128;
+    const unsigned kofs = (unsigned)((rs * a.C + cb * BK) * 2);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) lds_dma16(c.wr, As + (wid * AI + i) * 1024, aoff[i] + kofs);
+    const int dh = r - a.pad, dw = s2 - a.pad;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int hh = c.pp[i] + dh, ww = c.pq[i] + dw;
+      const bool ok = (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const unsigned off =
+          ok ? (unsigned)(((long long)(c.prow[i] + dh * a.W + dw) * a.ldx + cb * BK) * 2) + cbytes : 0xFFFFFFF0u;
+      lds_dma16(c.xr, Bs + (wid * BI + i) * 1024, off);
+    }
+  };
+
+  int lin = blockIdx.x;
+  if (lin >= ntile) return;
+  Ctx cur, nxt;
+  setup(lin, cur);
+  bool has_next = lin + G < ntile;
+  if (has_next) setup(lin + G, nxt);
+  const int wpx = (wid & 3) * 64, wco = (wid >> 2) * (BN / 2);
+  const int fr = lane & 15, fc = lane >> 4;
+  int gs = 0;  // K-steps issued/consumed across all tiles of this block
+  issue(cur, 0, 0);
+  if (PF > 1) issue(cur, 1, 1);
+  bool first_tile = true;
+  while (true) {
+    f4v acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < KT; ++t, ++gs) {
+      const bool more = t + 1 < KT || has_next;
+      if (PF > 1 && more && (t > 0 || first_tile)) {  // leave the next step's DMA in flight
+        if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else if constexpr (AI + BI == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {  // (after an epilogue its stores are the youngest operations: drain everything)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* As = smem + (gs % STG) * STAGE;
+      const char* Bs = As + BN * 128;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = 4 * ks + fc;
+        u4v af[TI], bfr[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
+#pragma unroll
+        for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+        __builtin_amdgcn_s_setprio(0);
+        if (ks == 0) {  // the step PF ahead, possibly the next tile's
+          const int u = t + PF;
+          if (u < KT) issue(cur, u, (gs + PF) % STG);
+          else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+        }
+      }
+    }
+    first_tile = false;
+    // epilogue of the current tile (the next tile's first DMAs are in flight)
+    T* y = (T*)a.y;
+    bool valid[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = cur.px0 + wpx + 16 * j + fr;
+      valid[j] = px < M;
+      if (px >= M) continue;
+      T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = cur.co0 + wco + 16 * i + 4 * fc;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (a.bias) {
+          const f4v b = *(const f4v*)(a.bias + co);
+          v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+        }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
+          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+        }
+        if constexpr (EPI == 3) epi_affine(v, a, co);
+        st4(yrow + co, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
+      }
+    }
+    if (EPI == 0 && a.part)
+      epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, epi_lds, a.part + (long long)(cur.px0 / PBM) * 3 * a.Cout,
+                               a.Cout, cur.co0, tid, fr, fc);
+    if (!has_next) break;
+    cur = nxt;
+    lin += G;
+    has_next = lin + G < ntile;
+    if (has_next) setup(lin + G, nxt);
+  }
 }
 
 // Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored
@@ -836,6 +1013,26 @@ static int fwd_ksplit(long long M, int Cout, int C, int R, int S) {
     if (t < tbest) { tbest = t; best = ks; }
   }
   return best;
+}
+
+static int g_persist_override = -1;  // dg_set_persist (tests): -1 = environment / default
+static bool use_persist() {
+  if (g_persist_override >= 0) return g_persist_override == 1;
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_PERSIST");
+    v = (e && e[0] == '0') ? 0 : 1;  // default on: +1.0% on the 768x1024 step (A/B in one call)
+  }
+  return v == 1;
+}
+
+static int persist_grid() {  // one block per CU (the ring takes most of the LDS)
+  static int g = -1;
+  if (g < 0) {
+    const char* e = getenv("DGVCC_PERSIST_GRID");
+    g = e ? std::max(8, atoi(e)) : 256;
+  }
+  return g;
 }
 
 static int pipe_var() {
@@ -1032,9 +1229,13 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31)) {
       const int np = dg_cdiv(M, PBM);
       const int var = pipe_var();
+      const int epi = a.ksplit > 1 ? 1 : a.bpart ? 2 : a.escale ? 3 : 0;
 #define PIPE_LAUNCH(BN_, STG_, G_) \
       do { \
-        if (var == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 1>), dim3(G_), dim3(512), 0, st, a); \
+        if (epi == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 1>), dim3(G_), dim3(512), 0, st, a); \
+        else if (epi == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 2>), dim3(G_), dim3(512), 0, st, a); \
+        else if (epi == 3) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 3>), dim3(G_), dim3(512), 0, st, a); \
+        else if (var == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 1>), dim3(G_), dim3(512), 0, st, a); \
         else if (var == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2>), dim3(G_), dim3(512), 0, st, a); \
         else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 0>), dim3(G_), dim3(512), 0, st, a); \
       } while (0)
@@ -1051,6 +1252,21 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && !a.part && tap3_pad_ok(a)) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
         hipLaunchKernelGGL(conv_fwd_tap3_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
+      } else if (use_persist() && !a.bpart && var == 2 && a.R * a.S * (a.C / 64) > 2 &&
+                 (long long)np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64))) >
+                     2 * 256) {
+        const int bn = a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64);
+        const long long tiles = (long long)np * (a.Cout / bn);
+        const unsigned g = (unsigned)std::min<long long>(tiles, persist_grid());
+        if (epi == 3) {
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3>), dim3(g), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3>), dim3(g), dim3(512), 0, st, a);
+        } else {
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3>), dim3(g), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3>), dim3(g), dim3(512), 0, st, a);
+        }
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
       else PIPE_LAUNCH(64, 3, np * (a.Cout / 64));
@@ -1920,6 +2136,14 @@ inline int grid_for(long long n, int bs = 256, int cap = 65536) {
 // C-ABI
 // ===========================================================================
 extern "C" int dg_version(void) { return DGVCC_ABI_VERSION; }
+
+// Test hook: force the persistent pipelined forward on (1) / off (0), or back to the
+// DGVCC_PERSIST environment default (-1).
+extern "C" int dg_set_persist(int mode) {
+  DG_REQUIRE(mode >= -1 && mode <= 1);
+  g_persist_override = mode;
+  return DG_OK;
+}
 
 extern "C" int dg_conv_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                            int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,

@@ -32,6 +32,8 @@ extern "C" {
 
 /* ---- library ----------------------------------------------------------- */
 int dg_version(void); /* returns DGVCC_ABI_VERSION */
+/* test hook: 1/0 force the persistent pipelined conv forward on/off, -1 = DGVCC_PERSIST default */
+int dg_set_persist(int mode);
 #define DGVCC_ABI_VERSION 1
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------

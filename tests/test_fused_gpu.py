@@ -391,3 +391,34 @@ def test_tap3_padded_index(dev, monkeypatch, N, H, W, C, acc):
         ref = ref + y0.double()
     assert relerr(outs[0], ref) < 1e-2
     assert relerr(outs[0], outs[1]) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,stats", [(5, 128, 256, 64, 256, True), (3, 96, 320, 128, 128, True),
+                                                (5, 128, 256, 128, 256, False)])
+def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
+    """The persistent pipelined forward (tiles walked by one block per CU, DMA ring running
+    across tile boundaries) against the one-tile-per-block kernel: bit-identical outputs and
+    statistics partials (same K order per tile)."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    w = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    wp = K.pack_weight(w, bf)
+    outs = []
+    for pers in ("0", "1"):
+        monkeypatch.setenv("DGVCC_PERSIST", pers)
+        K.call("dg_set_persist", int(pers))
+        z = K.Act(K.nhwc(N, H, W, Cout, bf, dev))
+        if stats:
+            res = K.conv_fwd_stats(K.Act(x), wp, Cout, 3, 1, z, bias=b)
+            outs.append((z.buf.clone(), res[0].clone()))
+        else:
+            K.conv_fwd(K.Act(x), wp, Cout, 3, 1, z, bias=b)
+            outs.append((z.buf.clone(), None))
+    K.call("dg_set_persist", -1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    if stats:
+        assert torch.equal(outs[0][1], outs[1][1])
