@@ -605,19 +605,23 @@ __global__ __launch_bounds__(256) void sw_bwd_apply(const T* __restrict__ gy, lo
     }
 #pragma unroll
     for (int a = 0; a < 16; ++a) xc[a] -= mv[a];
-    if (accumulate) {
+    // one V-wide output chunk at a time, loop kept rolled: only V outputs and one chunk's
+    // K/L rows live (fully unrolled, the hoisted LDS reads spilled ~50 VGPRs)
+#pragma unroll 1
+    for (int q = 0; q < 16; q += V) {
+      float oc[V];
+      if (accumulate) ldv(dx + pp * lddx + g * 16 + q, oc);
 #pragma unroll
-      for (int q = 0; q < 16; q += V) ldv(dx + pp * lddx + g * 16 + q, o + q);
+      for (int e = 0; e < V; ++e) {
+        const int a = q + e;
+        float s = cv[a];
+#pragma unroll
+        for (int b = 0; b < 16; ++b) s = fmaf(Km[a * 16 + b], ge[b], fmaf(Lm[a * 16 + b], xc[b], s));
+        oc[e] = accumulate ? oc[e] + s : s;
+      }
+      stv(dx + pp * lddx + g * 16 + q, oc);
     }
-#pragma unroll
-    for (int a = 0; a < 16; ++a) {
-      float s = cv[a];
-#pragma unroll
-      for (int b = 0; b < 16; ++b) s = fmaf(Km[a * 16 + b], ge[b], fmaf(Lm[a * 16 + b], xc[b], s));
-      o[a] = accumulate ? o[a] + s : s;
-    }
-#pragma unroll
-    for (int q = 0; q < 16; q += V) stv(dx + pp * lddx + g * 16 + q, o + q);
+    (void)o;
   }
 }
 
