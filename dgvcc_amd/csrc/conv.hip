@@ -1683,12 +1683,21 @@ constexpr int W9_XROWS = 72;
 
 // WT = 1 (BCO 128): wave tile 64 co x 16 c (TI 4, TJ 1) instead of 32 x 32: the 9 taps' B
 // fragments are read once per 4 A fragments (fewer transposed LDS reads per MFMA).
+// WT = 2 (BCO 64): wave tile 64 co x 16 c, the 8 waves split as 4 channel groups x 2 k-halves
+// (wave group kh takes the 32-px k-substep kh of every K-step) and each k-half writes its own
+// f32 slab split (the reduce sums 2x the splits).  The 32 co x 16 c tile of WT = 0 read 22
+// transposed fragments per 18 MFMAs and left the 64-channel layer LDS-bound.
 // PADK = 1 (W % 64 != 0, the 40/20-wide deep layers of 320-px crops): the K index runs over
 // the zero-padded image, u = (n, p+1, q+1) in N x (H+2) x (W+2), so a K-step of 64 u may
 // span rows and every shifted strip read lands on a zero pad cell exactly where the conv's
 // padding is: dy rows of pad cells are zero, x rows outside the image are zero.  Costs
 // (H+2)(W+2)/HW more K (10% at 40x40) instead of falling back to the per-tap kernel.
-template <int BCO, int WT = 0, int PADK = 0>
+// SCH (DMA issue point of the K-step after next): 0 = right after the barrier; 2 (default) =
+// after the first 32-px k-substep's MFMAs, MFMA blocks under s_setprio(1), as
+// conv_fwd_pipe_kernel (A/B in one call: wgrad 881 -> 949 TF/s, 15.1 -> 14.0 ms per step).
+// Measured and dropped: setprio alone (no change), priority without the moved issue (-0.7%),
+// the issue split over two points of the substep loop (777 TF/s).
+template <int BCO, int WT = 0, int PADK = 0, int SCH = 0>
 __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int BKP = 64, BC = 64;
   constexpr int RA = BCO * 2, RX = BC * 2;                    // bytes per LDS row
@@ -1700,7 +1709,8 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int A_BYTES = BKP * RA, X_BYTES = W9_XROWS * RX;
   constexpr int STAGE = A_BYTES + 3 * X_BYTES;
   constexpr bool WIDE = BCO == 128 && WT == 1;
-  constexpr int TI = WIDE ? 4 : 2, TJ = (BCO == 128 && !WIDE) ? 2 : 1;  // wave tile: 16*TI co x 16*TJ c, 9 taps
+  constexpr bool KH = BCO == 64 && WT == 2;
+  constexpr int TI = (WIDE || KH) ? 4 : 2, TJ = (BCO == 128 && !WIDE) ? 2 : 1;  // wave tile: 16*TI co x 16*TJ c, 9 taps
   __shared__ __attribute__((aligned(1024))) char smem[PSTAGES * STAGE];
 
   const int HW = a.H * a.W;
@@ -1794,8 +1804,9 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[tp][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-  const int wco = WIDE ? (wid & 1) * 64 : (BCO == 128 ? (wid & 3) * 32 : (wid & 1) * 32);
-  const int wc = WIDE ? (wid >> 1) * 16 : (BCO == 128 ? (wid >> 2) * 32 : (wid >> 1) * 16);
+  const int wco = KH ? 0 : WIDE ? (wid & 1) * 64 : (BCO == 128 ? (wid & 3) * 32 : (wid & 1) * 32);
+  const int wc = KH ? (wid & 3) * 16 : WIDE ? (wid >> 1) * 16 : (BCO == 128 ? (wid >> 2) * 32 : (wid >> 1) * 16);
+  const int kh = KH ? (wid >> 2) : 0;
   const int g = lane >> 4, qq = (lane & 15) >> 2, p4 = lane & 3;
   const int hb = (p4 & 1) * 8;
 
@@ -1813,11 +1824,13 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 2 < nkt) W9_ISSUE(kt + 2, (kt + 2) % PSTAGES);
+    if (SCH == 0 && kt + 2 < nkt) W9_ISSUE(kt + 2, (kt + 2) % PSTAGES);
     const char* As = smem + (kt % PSTAGES) * STAGE;
     const char* Xs = As + A_BYTES;
 #pragma unroll
     for (int ks = 0; ks < BKP / 32; ++ks) {
+      if (!KH || ks == kh) {
+      if constexpr (SCH == 2) __builtin_amdgcn_s_setprio(1);
       const int r1 = 32 * ks + 4 * g + qq, r2 = r1 + 16;
       s8v af[TI];
 #pragma unroll
@@ -1853,13 +1866,18 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
                   __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[dhi * 3 + sw][i][j], 0, 0, 0);
         }
       }
+      if constexpr (SCH == 2) __builtin_amdgcn_s_setprio(0);
+      }
+      if constexpr (SCH == 2) {
+        if (ks == 0 && kt + 2 < nkt) W9_ISSUE(kt + 2, (kt + 2) % PSTAGES);
+      }
     }
   }
 #undef W9_ISSUE
 #undef W9_ISSUE_PAD
 
   const long long ldk = 9ll * a.C;
-  float* out = a.slab + (long long)split * a.Cout * ldk;
+  float* out = a.slab + ((long long)split * (KH ? 2 : 1) + kh) * a.Cout * ldk;
 #pragma unroll
   for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
@@ -1873,6 +1891,24 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
           out[co * ldk + tp * a.C + c] = acc[tp][i][j][rr];
         }
       }
+}
+
+static int wg9_sched() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_WG9_SCH");
+    v = (e && e[0] == '0') ? 0 : 2;
+  }
+  return v;
+}
+
+static bool wg9_khalf() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_WG9_KH");
+    v = (e && e[0] == '0') ? 0 : 1;
+  }
+  return v == 1;
 }
 
 static bool wg9_wide() {
@@ -1959,6 +1995,7 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   const int tiles = (a.Cout / bco) * (a.C / bc) * a.R * a.S;
   const dim3 grid(tiles * a.splits);
   bool done = false;
+  int slab_splits = a.splits;
   if constexpr (std::is_same<T, bf16>::value) {
     const bool w9 = a.stride == 1 && !a.whole_x && wg9_ok(a.C, a.Cout, a.R, a.S, a.W, a.pad);
     const bool w9p = a.stride == 1 && !a.whole_x && !w9 && a.pad_ok &&
@@ -1966,13 +2003,22 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
     if (w9 || w9p) {
       const int b9 = a.Cout % 128 == 0 ? 128 : 64;
       const dim3 g9((a.Cout / b9) * (a.C / 64) * a.splits);
+      const int sch = wg9_sched();
+      const bool kh2 = b9 == 64 && sch == 2 && wg9_khalf();
+      if (kh2) slab_splits = 2 * a.splits;  // one slab split per k-half
       if (w9) {
-        if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1>), g9, dim3(512), 0, st, a);
+        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1>), g9, dim3(512), 0, st, a);
         else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
+        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 0, 2>), g9, dim3(512), 0, st, a);
+        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 2>), g9, dim3(512), 0, st, a);
         else hipLaunchKernelGGL((conv_wgrad9_kernel<64>), g9, dim3(512), 0, st, a);
       } else {
-        if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1>), g9, dim3(512), 0, st, a);
+        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1, 2>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1>), g9, dim3(512), 0, st, a);
         else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 1>), g9, dim3(512), 0, st, a);
+        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 1, 2>), g9, dim3(512), 0, st, a);
+        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1, 2>), g9, dim3(512), 0, st, a);
         else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1>), g9, dim3(512), 0, st, a);
       }
       done = true;
@@ -2001,7 +2047,7 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   DG_CHECK_LAUNCH();
   const long long total = (long long)a.Cout * a.C * a.R * a.S;
   const int blocks = (int)std::min<long long>((total + 255) / 256, 4096);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.slab, a.splits, a.Cout, a.C,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, a.slab, slab_splits, a.Cout, a.C,
                      a.R * a.S, dw, accumulate);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -2328,7 +2374,8 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
   // the padded 9-tap plan may be refused at launch (pixel strides too large): cover the
   // fallback plan too
   WgPlan q = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
-  return (int64_t)std::max(p.splits, q.splits) * Cout * C * R * S * 4;
+  const int kh = (dtype == DG_BF16 && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
+  return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
 }
 
 extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,

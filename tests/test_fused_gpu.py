@@ -271,6 +271,7 @@ def test_conv_splitk_matches_unsplit(dev, monkeypatch, N, H, W, C, Cout, acc):
     (16, 40, 40, 256, 512),   # conv4 of a 320-px crop
     (16, 20, 20, 512, 512),   # conv5 of a 320-px crop
     (3, 7, 24, 64, 128),      # ragged: K-steps span rows and images, last step partial
+    (2, 9, 40, 64, 64),       # Cout 64: the k-half wave split (two slab splits per block)
 ])
 def test_wgrad9_padded_k(dev, monkeypatch, N, H, W, C, Cout):
     """Fused 9-tap bf16 wgrad over the zero-padded K index (W % 64 != 0) against float64

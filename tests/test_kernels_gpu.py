@@ -38,6 +38,7 @@ CONV_CASES = [
     (1, 12, 8, 256, 128, 1),
     (1, 8, 8, 896, 256, 1),
     (1, 4, 256, 64, 64, 3),     # Cout 64, W % 256 == 0: fused 3-tap forward (+ its dgrad)
+    (2, 6, 128, 64, 64, 3),     # Cout 64 9-tap wgrad: k-half wave split over several splits
     (2, 3, 512, 128, 64, 3),    # fused 3-tap forward with 2 channel blocks
     (2, 3, 512, 64, 128, 3),    # dgrad into 64 channels on the fused 3-tap kernel
 ]
