@@ -1082,6 +1082,44 @@ static bool use_pipe() {
 // ---------------------------------------------------------------------------
 constexpr int T3_XROWS = 264;
 
+// Epilogue of the 3-tap kernels: bias / accumulate / eval-BN affine, bf16 store, and the
+// per-256-pixel BN statistics row of the stored values.
+template <int PADK, int TI, int TJ, int BN, int BM, typename Unpad>
+__device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs& a, int px0, int wpx, int fr, int fc,
+                                              int wid, int tid, char* smem, Unpad unpad) {
+  using T = bf16;
+  T* y = (T*)a.y;
+  bool valid[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = PADK ? unpad(px0 + wpx + 16 * j + fr) : px0 + wpx + 16 * j + fr;
+    valid[j] = px >= 0;  // unpadded path: M % 256 == 0
+    if (px < 0) continue;
+    T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      epi_affine(v, a, co);
+      st4(yrow + co, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
+    }
+  }
+  if (a.part)
+    epi_stats<TI, TJ, 4, BN>(acc, valid, wid, 0, smem, a.part + (long long)(px0 / BM) * 3 * a.Cout, a.Cout, 0, tid,
+                             fr, fc);
+}
+
 // PADK = 1 (W % 256 != 0: 320-px crops, evaluation frames): the 256-wide tile runs over the
 // zero-padded pixel index u = (n, p+1, q+1) in N x (H+2) x (W+2) instead of one image row, so
 // a tile may span rows and images; each kernel row's X strip is contiguous in u and the taps'
@@ -1180,36 +1218,120 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
     asm volatile("" ::: "memory");
   }
 
-  T* y = (T*)a.y;
-  bool valid[TJ];
+  tap3_epilogue<PADK, TI, TJ, BN, BM>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
+}
+
+// Narrow-K 3-tap forward/dgrad (same tiles and outputs as conv_fwd_tap3_kernel): a K-step is
+// one kernel row and 32 input channels, so LDS rows are 64 B and a block's single stage is
+// 29 KB (filters 12 KB + a 272-pixel X strip 17 KB).  Five blocks per CU then keep five
+// stages in flight where the 57 KB stage allowed two (the 64-wide kernel runs at ~28% MFMA
+// busy, latency-bound).  Measured gain is small (~8% on these launches): the layer stages
+// 110 FLOP per byte, so the bytes a CU must keep in flight exceed what its LDS can hold.  64-B rows are swizzled as chunk ^ 2*((row >> 2) & 1): for any row offset
+// the 16 lanes of each ds_read_b128 group hit 16 distinct (row & 3, chunk) bank groups.
+constexpr int T3N_XROWS = 272;
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
+
+template <int PADK = 0>
+__global__ __launch_bounds__(256, 5) void conv_fwd_tap3n_kernel(FwdArgs a) {
+  constexpr int BN = 64, BM = 256, BKC = 32;
+  constexpr int A_BYTES = 3 * BN * 64, X_BYTES = T3N_XROWS * 64;
+  constexpr int A_INST = A_BYTES / 1024, X_INST = X_BYTES / 1024;   // 12 + 17
+  constexpr int N_INST = A_INST + X_INST;
+  constexpr int TI = 4, TJ = 4;                                      // wave tile 64 px x 64 co
+  __shared__ __attribute__((aligned(1024))) char smem[A_BYTES + X_BYTES];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int PW = a.W + 2, PHW = (a.H + 2) * PW;
+  const int U = PADK ? a.N * PHW : M;
+  const int px0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+  const int n = px0 / HW, rem = px0 - n * HW;
+  const int pr = rem / a.W, q0 = rem - pr * a.W;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lrow = lane >> 2;
+  const int xlo = PADK ? 0 : max(0, px0 - a.W - 8), xhi = PADK ? M : min(M, px0 + BM + a.W + 8);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * 2), 0, (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 2),
+      0x00020000);
+  auto unpad = [&](int u) -> int {
+    if (u < 0 || u >= U) return -1;
+    const int nn = u / PHW, r = u - nn * PHW;
+    const int pp = r / PW, qq = r - pp * PW;
+    if (pp < 1 || pp > a.H || qq < 1 || qq > a.W) return -1;
+    return nn * HW + (pp - 1) * a.W + (qq - 1);
+  };
+  const long long ldw = 9ll * a.C;
+  __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, (unsigned)(BN * ldw * 2), 0x00020000);
+  const int KT = 3 * (a.C / BKC);
+
+  f4v acc[TI][TJ];
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int px = PADK ? unpad(px0 + wpx + 16 * j + fr) : px0 + wpx + 16 * j + fr;
-    valid[j] = px >= 0;  // unpadded path: M % 256 == 0
-    if (px < 0) continue;
-    T* yrow = y + (long long)px * a.ldy;
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int co = 16 * i + 4 * fc;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
-        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wpx = wid * 64;
+  const int fr = lane & 15, fc = lane >> 4;
+  const char* As = smem;
+  const char* Xs = smem + A_BYTES;
+
+  for (int t = 0; t < KT; ++t) {
+    const int dh = t % 3, cb = t / 3;
+    for (int ii = wid; ii < N_INST; ii += 4) {
+      if (ii < A_INST) {  // filter rows: tap s = ii / 4, co rows (ii % 4) * 16 + lrow
+        const int sw = ii >> 2, row = (ii & 3) * 16 + lrow;
+        const int ch = (lane & 3) ^ (((row >> 2) & 1) << 1);
+        lds_dma16(wr, smem + ii * 1024,
+                  (unsigned)(((long long)row * ldw + (dh * 3 + sw) * a.C + cb * BKC + ch * 8) * 2));
+      } else {
+        const int jj = ii - A_INST, row = jj * 16 + lrow;
+        const int ch = (lane & 3) ^ (((row >> 2) & 1) << 1);
+        if (PADK) {
+          const int pin = unpad(px0 - 4 + row + (dh - 1) * PW);
+          lds_dma16(xr, smem + A_BYTES + jj * 1024,
+                    pin >= 0 ? (unsigned)(((long long)pin * a.ldx + cb * BKC + ch * 8) * 2) : 0xFFFFFFF0u);
+        } else {
+          const int h = pr + dh - 1, w = q0 - 4 + row;
+          const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+          const long long pin = (long long)n * HW + (long long)h * a.W + w - xlo;
+          lds_dma16(xr, smem + A_BYTES + jj * 1024,
+                    ok ? (unsigned)((pin * a.ldx + cb * BKC + ch * 8) * 2) : 0xFFFFFFF0u);
+        }
       }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-      }
-      epi_affine(v, a, co);
-      st4(yrow + co, v);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int sw = 0; sw < 3; ++sw) {
+      u4v af[TI], bfr[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Xs + swz64(wpx + 16 * j + fr + sw + 3, fc));
+#pragma unroll
+      for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + sw * BN * 64 + swz64(16 * i + fr, fc));
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) mfma_frag<bf16>(acc[i][j], af[i], bfr[j]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
   }
-  if (a.part)
-    epi_stats<TI, TJ, 4, BN>(acc, valid, wid, 0, smem, a.part + (long long)(px0 / BM) * 3 * a.Cout, a.Cout, 0, tid,
-                             fr, fc);
+  tap3_epilogue<PADK, TI, TJ, BN, BM>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
+}
+
+// K-step width of the 3-tap kernels: 64 channels on row-aligned tiles (768x1024: the 32-ch
+// kernel's forwards were 0.27 ms/step faster but the step 0.07 ms slower, same-box A/B), 32 on
+// the padded index (320-px final-mode training: +1%, conv 9.74 -> 9.51 ms/step).
+// DGVCC_TAP3_BK=32|64 forces one.
+static int tap3_bk(bool padk) {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("DGVCC_TAP3_BK");
+    v = e ? atoi(e) : 0;
+  }
+  return v == 32 || v == 64 ? v : (padk ? 32 : 64);
 }
 
 // the padded 3-tap variant: whole-tensor x descriptor (32-bit byte offsets), no split-K
@@ -1248,10 +1370,12 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
                            (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (bf16*)a.y, a.ldy, a.accumulate,
                            a.part, a.escale, a.eshift, a.eact);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
-        hipLaunchKernelGGL(conv_fwd_tap3_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+        if (tap3_bk(false) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(conv_fwd_tap3_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && !a.part && tap3_pad_ok(a)) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
-        hipLaunchKernelGGL(conv_fwd_tap3_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
+        if (tap3_bk(true) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL(conv_fwd_tap3_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
       } else if (use_persist() && !a.bpart && var == 2 && a.R * a.S * (a.C / 64) > 2 &&
                  (long long)np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64))) >
                      2 * 256) {
