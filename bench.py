@@ -149,10 +149,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DGVCC_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing one
+    # GPU (local rank modulo the visible devices); the driver's runs use RCCL ("nccl").
+    backend = os.environ.get("DGVCC_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -219,6 +227,12 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
+        # data-parallel sanity check outside the timed region: identical parameters on every rank
+        chk = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum().reshape(1)
+        hi, lo = chk.clone(), chk.clone()
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        params_in_sync = bool(hi.item() == lo.item())
 
     views = 2 if (args.mode == "final" and not args.trunk) else 1
     frames = B * views * world * args.steps
@@ -266,6 +280,8 @@ def main():
                      "model_conv_tflops_per_step_algorithmic": round(step_flops / 1e12, 4),
                      "whole_step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / peak, 4)},
     }
+    if world > 1:
+        out["params_in_sync"] = params_in_sync
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:
