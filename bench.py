@@ -14,7 +14,8 @@ fp32 gradient per step inside the fused optimizer.
 Prints ONE JSON line on rank 0 with roofline (dominant kernel = the implicit-GEMM
 conv, timed per launch with HIP events on the launch stream during the timed
 region) and cpu_baseline (the oracle's CPU restatement of the same step, timed
-on this host on a bounded sample).
+on this host on a bounded sample, plus the fp32 density-map parity of the HIP
+path against it on the same 768x1024 frame).
 """
 from __future__ import annotations
 
@@ -130,7 +131,8 @@ def cpu_baseline(args, seconds):
     sd = O.seeded_state_dict(tmpl)
     batch = O.synthetic_batch(1, args.height, args.width, seed=7)
     mode = "simple" if args.mode == "simple" else "final"
-    O.train_step(sd, batch, mode)  # warm-up
+    loss_ref, outs, _, _ = O.train_step(sd, batch, mode)  # warm-up (and the parity reference below)
+    parity = density_parity(sd, batch, loss_ref, outs[0]) if mode == "simple" else None
     n, t0 = 0, time.perf_counter()
     while True:
         O.train_step(sd, batch, mode)
@@ -139,9 +141,35 @@ def cpu_baseline(args, seconds):
             break
     dt = time.perf_counter() - t0
     frames = n * (2 if mode == "final" else 1)
-    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "sample": f"{n} oracle train steps ({mode} mode, batch 1, {args.height}x{args.width}, fp32, "
-                      f"torch CPU {threads} threads) after 1 warm-up"}
+    out = {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+           "sample": f"{n} oracle train steps ({mode} mode, batch 1, {args.height}x{args.width}, fp32, "
+                     f"torch CPU {threads} threads) after 1 warm-up"}
+    if parity is not None:
+        out["parity"] = parity
+    return out
+
+
+def density_parity(sd, batch, loss_ref, d_ref):
+    """The metric's "MAE vs reference" on the warm-up frame: the HIP path (fp32 mode, the
+    parity precision of BASELINE.json's north_star) against the oracle's density map and
+    MSE loss for the same weights and frame.  The oracle is only the checker here."""
+    from dgvcc_amd.models.models import DGModel_base
+    from dgvcc_amd.losses import mse_loss
+    dev = torch.device("cuda", torch.cuda.current_device())
+    model = DGModel_base(pretrained=False, den_dropout=0.0)
+    model.load_state_dict(sd)
+    model = model.to(dev).set_precision("fp32").train()
+    d = model(batch[0].to(dev))
+    loss = mse_loss(d, batch[2][1].to(dev), 1000.0)
+    loss.backward()
+    torch.cuda.synchronize()
+    d = d.detach().double().cpu()
+    r = d_ref.detach().double()
+    return {"precision": "fp32", "frame": "1x3x%dx%d" % tuple(r.shape[-2:]), "tolerance_rel": 1e-4,
+            "density_map_mae": float((d - r).abs().mean()),
+            "density_map_max_rel": float((d - r).abs().max() / r.abs().max()),
+            "count_abs_err": float(abs(d.sum() - r.sum()) / 1000.0),
+            "loss_rel": float(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))}
 
 
 def main():
