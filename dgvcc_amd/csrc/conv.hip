@@ -1321,6 +1321,190 @@ __global__ __launch_bounds__(256, 5) void conv_fwd_tap3n_kernel(FwdArgs a) {
   tap3_epilogue<PADK, TI, TJ, BN, BM>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
 }
 
+// Persistent 3-tap forward/dgrad for C = Cout = 64 on row-aligned tiles (the full-resolution
+// layer enc1.3 and its dgrad, models/models.py:35-38).  conv_fwd_tap3_kernel stages 57 KB per
+// K-step with one stage per block and waits on it (rocprofv3: waves wait 40% of their time,
+// 28% MFMA-busy).  Here the whole 72-KB filter bank (3 kernel rows x 3 taps x 64 co) is
+// staged once per block and stays resident, and a K-step streams only its 33-KB X strip
+// through a two-slot ring that runs across tile boundaries: the next strip (possibly the next
+// tile's first) is in flight during the current step's MFMAs and the epilogue's stores.
+// One block of 8 waves per CU (2 per SIMD), wave tile 64 px x 32 co.  Per tile the K order
+// (dh, tap, k-half) and the statistics merge are those of conv_fwd_tap3_kernel<0>, so
+// outputs and BN partials are bit-identical to it.  (A four-slot ring of 32-channel
+// half-strips, three steps ahead, measured slower: 1.41 vs 1.35 ms on 16x768x1024: twice the
+// barriers per tile cost more than the deeper lookahead gained.)
+constexpr int T3P_FILT = 9 * 64 * 128;    // resident filters, 72 KB
+constexpr int T3P_XS = T3_XROWS * 128;    // one X strip, 33 KB
+template <int ROWS>
+__global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
+  using T = bf16;
+  constexpr int BN = 64, BM = 256, TI = 2, TJ = 4;
+  constexpr int X_INST = T3P_XS / 1024;   // 33 DMA instructions per strip
+  constexpr int EPI_B = 4 * 3 * BN * 4;   // epi_stats scratch [4][3][BN] f32
+  __shared__ __attribute__((aligned(1024))) char smem[T3P_FILT + 2 * T3P_XS + EPI_B];
+  char* Ws = smem;
+  char* Xring = smem + T3P_FILT;
+  char* epi_lds = Xring + 2 * T3P_XS;
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int TPR = a.W / BM;                // W % 256 == 0 (and H % ROWS == 0)
+  const int ntile = M / (BM * ROWS);
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lrow = lane >> 3;
+  int lin = blockIdx.x;
+  if (lin >= ntile) return;
+
+  // resident filters: tap k = dh * 3 + sw at Ws + k * 8 KB, co rows swizzled as swz(row, chunk)
+  {
+    const long long ldw = 9ll * 64;
+    __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, (unsigned)(BN * ldw * 2), 0x00020000);
+    for (int ii = wid; ii < 72; ii += 8) {
+      const int k = ii >> 3, row = (ii & 7) * 8 + lrow;
+      const int ch = (lane & 7) ^ (row & 7);
+      lds_dma16(wr, Ws + ii * 1024, (unsigned)((row * ldw + k * 64 + ch * 8) * 2));
+    }
+  }
+
+  struct Ctx {
+    int px0, n, pr, q0, xlo;
+    __amdgpu_buffer_rsrc_t xr;
+  };
+  auto setup = [&](int l, Ctx& c) {
+    const int t = xcd_remap(l, ntile);
+    const int rp = t / TPR;                  // row group: image rows pr .. pr + ROWS - 1
+    c.q0 = (t - rp * TPR) * BM;
+    c.n = rp / (a.H / ROWS);
+    c.pr = (rp - c.n * (a.H / ROWS)) * ROWS;
+    c.px0 = c.n * HW + c.pr * a.W + c.q0;
+    c.xlo = max(0, c.px0 - a.W - 8);
+    const int xhi = min(M, c.px0 + (ROWS - 1) * a.W + BM + a.W + 8);
+    c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)c.xlo * a.ldx * 2), 0,
+                                             (unsigned)(((long long)(xhi - c.xlo - 1) * a.ldx + a.C) * 2), 0x00020000);
+  };
+  // X strip s: pixels q0 - 4 + row (row < 264) of image row pr + s - 1 (kernel row s of
+  // output row pr, kernel row s - 1 of output row pr + 1)
+  auto issue = [&](const Ctx& c, int dh, int slot) {
+    char* Xs = Xring + slot * T3P_XS;
+    const int h = c.pr + dh - 1;
+    for (int jj = wid; jj < X_INST; jj += 8) {
+      const int row = jj * 8 + lrow;
+      const int ch = (lane & 7) ^ (row & 7);
+      const int w = c.q0 - 4 + row;
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)w < (unsigned)a.W;
+      const long long pin = (long long)c.n * HW + (long long)h * a.W + w - c.xlo;
+      lds_dma16(c.xr, Xs + jj * 1024, ok ? (unsigned)((pin * a.ldx + ch * 8) * 2) : 0xFFFFFFF0u);
+    }
+  };
+
+  Ctx cur, nxt;
+  setup(lin, cur);
+  bool has_next = lin + G < ntile;
+  if (has_next) setup(lin + G, nxt);
+  const int wpx = (wid & 3) * 64, wco = (wid >> 2) * 32;
+  const int fr = lane & 15, fc = lane >> 4;
+  int gs = 0;  // K-steps consumed across all tiles of this block (ring slot = gs & 1)
+  issue(cur, 0, 0);
+  while (true) {
+    constexpr int NS = ROWS + 2;  // strips per tile
+    f4v acc[ROWS][TI][TJ];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) acc[r][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dh = 0; dh < NS; ++dh, ++gs) {
+      // this step's strip (and, first time, the filters) have landed; every wave is done
+      // reading the other slot (previous step)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (dh < NS - 1) issue(cur, dh + 1, (gs + 1) & 1);
+      else if (has_next) issue(nxt, 0, (gs + 1) & 1);
+      const char* Xs = Xring + (gs & 1) * T3P_XS;
+#pragma unroll
+      for (int sw = 0; sw < 3; ++sw) {
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int ch = 4 * ks + fc;
+          u4v bfr[TJ];
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Xs + swz(wpx + 16 * j + fr + sw + 3, ch));
+#pragma unroll
+          for (int r = 0; r < ROWS; ++r) {  // output row pr + r takes this strip as kernel row dh - r
+            const int kr = dh - r;
+            if (kr < 0 || kr > 2) continue;
+            const char* As = Ws + (kr * 3 + sw) * (BN * 128);
+            u4v af[TI];
+#pragma unroll
+            for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < TI; ++i)
+#pragma unroll
+              for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[r][i][j], af[i], bfr[j]);
+            __builtin_amdgcn_s_setprio(0);
+          }
+        }
+      }
+    }
+    // epilogue (the next strip's DMA is in flight)
+    T* y = (T*)a.y;
+    bool valid[TJ];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+    const int opx0 = cur.px0 + r * a.W;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      valid[j] = true;
+      T* yrow = y + (long long)(opx0 + wpx + 16 * j + fr) * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = wco + 16 * i + 4 * fc;
+        float v[4] = {acc[r][i][j][0], acc[r][i][j][1], acc[r][i][j][2], acc[r][i][j][3]};
+        if (a.bias) {
+          const f4v b = *(const f4v*)(a.bias + co);
+          v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+        }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
+          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+        }
+        epi_affine(v, a, co);
+        st4(yrow + co, v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[r][i][j][e] = bf2f(f2bf(v[e]));  // the stored value, for the statistics
+      }
+    }
+    if (a.part)
+      epi_stats<TI, TJ, 4, BN>(acc[r], valid, wid & 3, wco, epi_lds, a.part + (long long)(opx0 / BM) * 3 * a.Cout,
+                               a.Cout, 0, tid, fr, fc);
+    }
+    if (!has_next) break;
+    cur = nxt;
+    lin += G;
+    has_next = lin + G < ntile;
+    if (has_next) setup(lin + G, nxt);
+  }
+}
+
+// output rows per persistent 3-tap tile (DGVCC_TAP3P_ROWS=1|2; 2 needs H even)
+static int tap3p_rows() {
+  const char* e = getenv("DGVCC_TAP3P_ROWS");
+  return (e && e[0] == '1') ? 1 : 2;
+}
+
+static bool use_tap3p() {
+  const char* e = getenv("DGVCC_TAP3P");
+  return !(e && e[0] == '0');
+}
+
 // K-step width of the 3-tap kernels: 64 channels on row-aligned tiles (768x1024: the 32-ch
 // kernel's forwards were 0.27 ms/step faster but the step 0.07 ms slower, same-box A/B), 32 on
 // the padded index (320-px final-mode training: +1%, conv 9.74 -> 9.51 ms/step).
@@ -1370,7 +1554,13 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
                            (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (bf16*)a.y, a.ldy, a.accumulate,
                            a.part, a.escale, a.eshift, a.eact);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
-        if (tap3_bk(false) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+        if (a.C == 64 && !a.bpart && use_tap3p()) {
+          const unsigned g = (unsigned)std::min<long long>(M / 256, persist_grid());
+          if (a.H % 2 == 0 && tap3p_rows() == 2)
+            hipLaunchKernelGGL(conv_fwd_tap3p_kernel<2>, dim3((unsigned)std::min<long long>(M / 512, g)), dim3(512), 0, st, a);
+          else
+            hipLaunchKernelGGL(conv_fwd_tap3p_kernel<1>, dim3(g), dim3(512), 0, st, a);
+        } else if (tap3_bk(false) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
         else hipLaunchKernelGGL(conv_fwd_tap3_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && !a.part && tap3_pad_ok(a)) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);

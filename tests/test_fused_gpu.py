@@ -423,3 +423,47 @@ def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
     assert torch.equal(outs[0][0], outs[1][0])
     if stats:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("N,H,W,acc", [(2, 16, 256, False), (5, 128, 256, True), (3, 40, 512, False),
+                                       (1, 15, 256, True)])
+def test_tap3_persistent_matches(dev, monkeypatch, N, H, W, acc):
+    """C = Cout = 64 row-aligned 3x3 (enc1.3 and its dgrad): the persistent resident-filter
+    kernel (conv_fwd_tap3p_kernel; grids below and above one block per CU) against the
+    one-tile-per-block 3-tap kernel: bit-identical forward (+accumulate), BN statistics
+    partials, eval-BN epilogue and dgrad (same K order per output row) with one or two output
+    rows per tile, and within bf16 rounding of float64."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(N, H, W, 64, generator=g).to(dev, bf)
+    gy = torch.randn(N, H, W, 64, generator=g).to(dev, bf)
+    w = (torch.randn(64, 64, 3, 3, generator=g) / 24.0).to(dev)
+    b = torch.randn(64, generator=g).to(dev)
+    y0 = torch.randn(N, H, W, 64, generator=g).to(dev, bf)
+    gam, bet = torch.rand(64, device=dev) + 0.5, torch.randn(64, device=dev)
+    st = K.bn_eval_stats(gam, bet, torch.randn(64, device=dev) * 0.1, torch.rand(64, device=dev) + 0.5, 1e-5)
+    wp = K.pack_weight(w, bf)
+    outs = []
+    for p, rows in (("0", "2"), ("1", "1"), ("1", "2")):  # 2 output rows per tile need H even
+        monkeypatch.setenv("DGVCC_TAP3P", p)
+        monkeypatch.setenv("DGVCC_TAP3P_ROWS", rows)
+        y = K.Act(y0.clone())
+        K.conv_fwd(K.Act(x), wp, 64, 3, 1, y, bias=b, accumulate=acc)
+        z = K.Act(K.nhwc(N, H, W, 64, bf, dev))
+        res = K.conv_fwd_stats(K.Act(x), wp, 64, 3, 1, z, bias=b)
+        ye = K.Act(K.nhwc(N, H, W, 64, bf, dev))
+        K.conv_fwd_bn_eval(K.Act(x), wp, 64, 3, 1, ye, b, st, 1)
+        dx = K.Act(K.nhwc(N, H, W, 64, bf, dev))
+        K.conv_dgrad(K.Act(gy), wp, 64, 3, 1, dx)
+        torch.cuda.synchronize()
+        outs.append((y.buf.clone(), z.buf.clone(), res[0].clone(), ye.buf.clone(), dx.buf.clone()))
+    for o in outs[1:]:
+        for u, v in zip(outs[0], o):
+            assert torch.equal(u, v)
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + y0.double()
+    assert relerr(outs[1][0], ref) < 1e-2
+    refd = F.conv_transpose2d(gy.double().permute(0, 3, 1, 2), w.double(), padding=1).permute(0, 2, 3, 1)
+    assert relerr(outs[1][4], refd) < 1e-2
