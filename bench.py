@@ -295,7 +295,7 @@ def main():
                     if args.mode == "simple" else "DGModel_final final-mode DGTrainer.train_step (configs/sta_final.yml)"),
                    "global_batch": B * world, "frames_per_gpu_step": B * views,
                    "resolution": f"{H}x{W}", "parallelism": f"dp{world}", "last_loss": last},
-        "roofline": {"bound": "mfma", "kernel": "conv_fwd_pers_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel (implicit-GEMM conv: forward + dgrad launches)",
+        "roofline": {"bound": "mfma", "kernel": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel (implicit-GEMM conv: forward + dgrad launches)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                      "frac": round(achieved / peak, 4), "traffic": traffic,
                      "algorithmic_bytes_per_launch": round(conv_alg_bytes),

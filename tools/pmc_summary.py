@@ -35,12 +35,12 @@ for k in sorted(set(fetch) | set(write), key=lambda k: -fetch.get(k, [0, 1])[0])
               "write_bytes_per_dispatch": w * 1024 / max(nw, 1)}
 json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
 # the launches bench.py's roofline times (kinds fwd + dgrad): every forward-GEMM kernel variant
-FWD_KERNELS = ("conv_fwd_pers_kernel", "conv_fwd_pipe_kernel", "conv_fwd_tap3_kernel", "conv_fwd_kernel")
+FWD_KERNELS = ("conv_fwd_pers_kernel", "conv_fwd_pipe_kernel", "conv_fwd_tap3_kernel", "conv_fwd_tap3p_kernel", "conv_fwd_kernel")
 conv = [v for k, v in out.items() if any(f in k for f in FWD_KERNELS)]
 if conv:
     n = sum(v["dispatches"] for v in conv)
     tot = sum((v["fetch_bytes_per_dispatch_corrected"] + v["write_bytes_per_dispatch"]) * v["dispatches"] for v in conv)
-    json.dump({"kernel": "implicit-GEMM conv forward/dgrad (conv_fwd_pers_kernel, conv_fwd_pipe_kernel, conv_fwd_tap3_kernel)",
+    json.dump({"kernel": "implicit-GEMM conv forward/dgrad (conv_fwd_pers_kernel, conv_fwd_pipe_kernel, conv_fwd_tap3_kernel, conv_fwd_tap3p_kernel)",
                "dispatches": n,
                "hbm_bytes_per_launch": tot / n,
                "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB->bytes, averaged over dispatches of a 2-step bench run"},
