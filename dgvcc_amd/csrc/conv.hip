@@ -679,6 +679,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
   }
   T* y = (T*)a.y;
   bool valid[TJ];
+  // bias read once, ahead of the stores: a load between stores makes the compiler drain vmcnt
+  // to 0 per use (the stores may alias it), serialising the tile's stores
+  f4v bv[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+    bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
+        const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
       if (a.accumulate) {
@@ -718,6 +724,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 // the current tile's last ones, so its prologue latency hides under the current tile's
 // MFMAs and epilogue stores.  The epilogue-statistics scratch gets its own LDS so the
 // in-flight ring stages are never touched.  Requires KT > PF (K-steps per tile).
+constexpr int PERS_BIAS_MAX = 1024;  // Cout limit of the persistent forward (LDS bias)
 template <int BN, int STG, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   using T = bf16;
@@ -728,8 +735,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   constexpr int STAGE = (BN + PBM) * 128;
   constexpr int PF = STG - 1;
   constexpr int EPI_B = 4 * 3 * BN * 4;  // epi_stats scratch [4][3][BN] f32
-  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B];
+  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B + PERS_BIAS_MAX * 4];
   char* epi_lds = smem + STG * STAGE;
+  // bias staged in LDS once per block: a global load per use in the epilogue makes the
+  // compiler drain vmcnt to 0, i.e. wait for the next tile's in-flight DMA steps and every
+  // earlier store of the tile (vector-memory operations retire in issue order)
+  float* bbuf = (float*)(epi_lds + EPI_B);
 
   const int HW = a.H * a.W;
   const int M = a.N * HW;
@@ -794,6 +805,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
 
   int lin = blockIdx.x;
   if (lin >= ntile) return;
+  if (a.bias)
+    for (int c = tid; c < a.Cout; c += 512) bbuf[c] = a.bias[c];
   Ctx cur, nxt;
   setup(lin, cur);
   bool has_next = lin + G < ntile;
@@ -860,7 +873,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
         const int co = cur.co0 + wco + 16 * i + 4 * fc;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (a.bias) {
-          const f4v b = *(const f4v*)(a.bias + co);
+          const f4v b = *(const f4v*)(bbuf + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         }
         if (a.accumulate) {
@@ -1090,6 +1103,12 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
   using T = bf16;
   T* y = (T*)a.y;
   bool valid[TJ];
+  // bias read once, ahead of the stores (see conv_fwd_pipe_kernel); on the padded index the
+  // extra 16 VGPRs spill the narrow kernel, so it keeps the per-use load there
+  f4v bv[TI];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+    bv[i] = (!PADK && a.bias) ? *(const f4v*)(a.bias + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = PADK ? unpad(px0 + wpx + 16 * j + fr) : px0 + wpx + 16 * j + fr;
@@ -1101,7 +1120,7 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
       const int co = 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
+        const f4v b = PADK ? *(const f4v*)(a.bias + co) : bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
       if (a.accumulate) {
@@ -1341,10 +1360,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
   constexpr int BN = 64, BM = 256, TI = 2, TJ = 4;
   constexpr int X_INST = T3P_XS / 1024;   // 33 DMA instructions per strip
   constexpr int EPI_B = 4 * 3 * BN * 4;   // epi_stats scratch [4][3][BN] f32
-  __shared__ __attribute__((aligned(1024))) char smem[T3P_FILT + 2 * T3P_XS + EPI_B];
+  __shared__ __attribute__((aligned(1024))) char smem[T3P_FILT + 2 * T3P_XS + EPI_B + 3 * BN * 4];
   char* Ws = smem;
   char* Xring = smem + T3P_FILT;
   char* epi_lds = Xring + 2 * T3P_XS;
+  // bias / eval-BN scale / shift staged in LDS once: a global load in the epilogue would make
+  // the compiler drain vmcnt to 0 per use, i.e. wait for the in-flight strip DMA and every
+  // earlier store of the tile (vector-memory operations retire in issue order)
+  float* ebuf = (float*)(epi_lds + EPI_B);
 
   const int HW = a.H * a.W;
   const int M = a.N * HW;
@@ -1356,6 +1379,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
   const int lrow = lane >> 3;
   int lin = blockIdx.x;
   if (lin >= ntile) return;
+  if (tid < BN) {
+    ebuf[tid] = a.bias ? a.bias[tid] : 0.f;
+    ebuf[BN + tid] = a.escale ? a.escale[tid] : 1.f;
+    ebuf[2 * BN + tid] = a.escale ? a.eshift[tid] : 0.f;
+  }
 
   // resident filters: tap k = dh * 3 + sw at Ws + k * 8 KB, co rows swizzled as swz(row, chunk)
   {
@@ -1468,7 +1496,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
         const int co = wco + 16 * i + 4 * fc;
         float v[4] = {acc[r][i][j][0], acc[r][i][j][1], acc[r][i][j][2], acc[r][i][j][3]};
         if (a.bias) {
-          const f4v b = *(const f4v*)(a.bias + co);
+          const f4v b = *(const f4v*)(ebuf + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         }
         if (a.accumulate) {
@@ -1476,7 +1504,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
           ld4(yrow + co, o);
           v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
         }
-        epi_affine(v, a, co);
+        if (a.escale) {  // as epi_affine
+          const f4v sc = *(const f4v*)(ebuf + BN + co), sf = *(const f4v*)(ebuf + 2 * BN + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float t = fmaf(v[e], sc[e], sf[e]);
+            if (a.eact == 1) t = t > 0.f ? t : 0.f;
+            v[e] = t;
+          }
+        }
         st4(yrow + co, v);
 #pragma unroll
         for (int e = 0; e < 4; ++e) acc[r][i][j][e] = bf2f(f2bf(v[e]));  // the stored value, for the statistics
@@ -1566,7 +1602,7 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
         if (tap3_bk(true) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
         else hipLaunchKernelGGL(conv_fwd_tap3_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
-      } else if (use_persist() && !a.bpart && var == 2 && a.R * a.S * (a.C / 64) > 2 &&
+      } else if (use_persist() && !a.bpart && var == 2 && a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX &&
                  (long long)np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64))) >
                      2 * 256) {
         const int bn = a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64);
