@@ -1,27 +1,38 @@
 """DGVCC MI355X benchmark: train-step frames/s at 768x1024 (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--mode simple|final]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--mode final|simple|base]
+                    [--precision fp32|bf16] [--no-bf16] [--trunk ibn|sw|isw]
 
-Workload (BASELINE.json configs[1], configs/stb_reg_base.yml): DGModel_base
-(VGG16-BN encoder + density decoder), DGTrainer 'simple' mode, MSE count loss
-(log_para 1000), fused AdamW, bf16 storage/MFMA with f32 accumulation, batch 16
-per GPU of synthetic 3x768x1024 frames resident in HBM (no dataset offline).
-A step = DGTrainer.train_step (forward + loss + backward + optimizer step +
-the reference's per-step `.item()` sync).  Multi-GPU: one process per GPU
-(torchrun), per-GPU batch fixed (weak scaling), one RCCL all-reduce of the flat
-fp32 gradient per step inside the fused optimizer.
+Default workload = the config BASELINE.json's metric is quoted on, configs/sta_final.yml
+(ShanghaiTech-A "final"): DGModel_final, DGTrainer 'final' mode (two photometric views,
+MSE count loss x log_para 1000 + 10 BCE class-map loss + 10 JSD-MSE consistency loss,
+fused AdamW), batch 16 per GPU of synthetic 3x768x1024 frames resident in HBM (no dataset
+offline), computed in fp32 like the reference (exact-f32 MFMA).  A step is
+DGTrainer.train_step: forward + loss + backward + optimizer step + the reference's per-step
+`.item()`; a frame is one 3x768x1024 view through forward and backward (final mode counts
+both views).  The same step in bf16 (bf16 storage/MFMA, f32 accumulation and
+statistics) is reported beside it as `perf_bf16`, with its own roofline.
 
-Prints ONE JSON line on rank 0 with roofline (dominant kernel = the implicit-GEMM
-conv, timed per launch with HIP events on the launch stream during the timed
-region) and cpu_baseline (the oracle's CPU restatement of the same step, timed
-on this host on a bounded sample, plus the fp32 density-map parity of the HIP
-path against it on the same 768x1024 frame).
+Multi-GPU: `--gpus N` without a torchrun environment starts
+`python -m torch.distributed.run --nproc-per-node N` as a child process (before any GPU
+call) and relays its rank-0 line; under torchrun one process per GPU, per-GPU batch fixed
+(weak scaling), one RCCL all-reduce of the flat fp32 gradient per step inside the fused
+optimizer, max-over-ranks timing.
+
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel = the implicit-GEMM conv
+forward/dgrad launches, each timed with HIP events on its launch stream over the timed
+region; `traffic` = PMC HBM bytes per launch of the same workload from profiles/traffic/,
+null when that workload has not been profiled) and `cpu_baseline` (the oracle's CPU
+restatement of the same step on a bounded sample on this host's cores, plus the full-frame
+fp32 parity of the HIP path against it).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,9 +41,13 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16
-F32_MFMA_PEAK_TFLOPS = 157.3
+BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
+F32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector peak
+PEAKS = {"fp32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_DENSE_PEAK_TFLOPS, "fp16": BF16_DENSE_PEAK_TFLOPS}
 H0, W0 = 768, 1024
+METRIC = "train-step frames/sec at 768×1024, ShanghaiTech-A; MAE vs reference"
+CONFIG_FILES = {"final": "configs/sta_final.yml", "simple": "configs/stb_reg_base.yml",
+                "base": "configs/ablation (mode base)"}
 
 
 def parse():
@@ -40,16 +55,35 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="frames per GPU")
-    ap.add_argument("--mode", default="simple", choices=["simple", "final"])
+    ap.add_argument("--batch", type=int, default=16, help="frames (samples) per GPU")
+    ap.add_argument("--mode", default="final", choices=["simple", "base", "final"])
+    ap.add_argument("--model", default=None,
+                    help="model class (default: DGModel_final for final mode, DGModel_base otherwise; "
+                         "DensityRegressorBase = models2 'dgnet')")
     ap.add_argument("--trunk", default=None, choices=["ibn", "sw", "isw"],
                     help="secondary workload: ResNet-50 DG counter (IBN-b / SW / ISW) train step")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
+    ap.add_argument("--no-bf16", action="store_true", help="skip the perf_bf16 leg")
     ap.add_argument("--height", type=int, default=H0)
     ap.add_argument("--width", type=int, default=W0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` outside torchrun: one process per GPU via torch.distributed.run, started as
+    a child (this process has not touched the GPU), whose rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+           *sys.argv[1:]]
+    return subprocess.call(cmd)
 
 
 def synthetic(B, H, W, device, seed):
@@ -68,149 +102,122 @@ def synthetic(B, H, W, device, seed):
     return img1.to(device), img2.to(device), (tuple(p.to(device) for p in pts), dmaps, bmaps)
 
 
-def conv_flops_per_step(B, H, W, mode):
-    """Algorithmic conv FLOPs of one train step (fwd + dgrad + wgrad), SURVEY.md §8d."""
-    views = 2 if mode == "final" else 1
-    layers = []
+def _vgg_layers(H, W):
+    """(h, w, cin, cout, k, has_dgrad) of the encoder + decoder convs of DGModel_base."""
+    layers, enc = [], []
     h, w, cin = H, W, 3
     for v in [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512]:
         if v == "M":
             h, w = h // 2, w // 2
             continue
-        layers.append((h, w, cin, v, 9, cin != 3))
+        enc.append((h, w, cin, v, 9, cin != 3))
         cin = v
     s = H // 16, W // 16
-    layers += [(s[0], s[1], 512, 1024, 9, True), (s[0], s[1], 1024, 512, 9, True),
-               (2 * s[0], 2 * s[1], 1024, 512, 9, True), (2 * s[0], 2 * s[1], 512, 256, 9, True),
-               (4 * s[0], 4 * s[1], 512, 256, 9, True), (4 * s[0], 4 * s[1], 256, 128, 9, True),
-               (4 * s[0], 4 * s[1], 896, 256, 1, True)]
-    tot = 0.0
-    for (h, w, ci, co, k, dgrad) in layers:
-        f = 2.0 * B * views * h * w * ci * co * k
-        tot += f * (3 if dgrad else 2)
-    return tot
+    dec = [(s[0], s[1], 512, 1024, 9, True), (s[0], s[1], 1024, 512, 9, True),
+           (2 * s[0], 2 * s[1], 1024, 512, 9, True), (2 * s[0], 2 * s[1], 512, 256, 9, True),
+           (4 * s[0], 4 * s[1], 512, 256, 9, True), (4 * s[0], 4 * s[1], 256, 128, 9, True),
+           (4 * s[0], 4 * s[1], 896, 256, 1, True)]
+    return enc, dec
+
+
+def step_flops(B, H, W, mode):
+    """Algorithmic GEMM FLOPs of one train step (fwd + dgrad + wgrad), SURVEY.md §8d: the
+    reference's op count (y_cat's 1x1 conv at H/4, the memory logits/readout bmm's)."""
+    enc, dec = _vgg_layers(H, W)
+    views = 2 if mode in ("final", "base") else 1
+    tot = enc_tot = 0.0
+    for i, (h, w, ci, co, k, dgrad) in enumerate(enc + dec):
+        f = 2.0 * B * views * h * w * ci * co * k * (3 if dgrad else 2)
+        tot += f
+        if i < len(enc):
+            enc_tot += f
+    if mode == "final":
+        hw = (H // 4) * (W // 4)
+        tot += 2 * 3 * 2.0 * B * hw * 256 * 1024 * 2             # memory logits + readout, fwd/dgrad/wgrad
+        tot += 2 * 3 * 2.0 * B * (H // 16) * (W // 16) * 512 * 256 * 9   # cls_head 3x3
+    return tot, enc_tot
 
 
 class ConvTimer:
-    """Per-launch HIP events around the implicit-GEMM conv launches, recorded on
-    torch's current stream — the stream the C-ABI launches on.  Kinds: 'fwd' and
-    'dgrad' run `conv_fwd_kernel`, 'wgrad' runs `conv_wgrad_kernel` (+ reduce)."""
+    """Per-launch HIP events around the implicit-GEMM conv launches, recorded on torch's
+    current stream — the stream the C-ABI launches on.  Kinds: 'fwd', 'dgrad' (forward GEMM
+    kernels), 'wgrad', 'stem', 'stem_wgrad'; scope: 'enc' / 'dec' / 'head' (engine.py)."""
 
     def __init__(self):
-        self.ev = {}
+        self.ev = []
 
-    def __call__(self, kind, flops, launch, nbytes=0.0):
+    def __call__(self, kind, flops, launch, nbytes=0.0, scope="other"):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         launch()
         e.record()
-        self.ev.setdefault(kind, []).append((s, e, flops, nbytes))
+        self.ev.append((kind, scope, s, e, flops, nbytes))
 
-    def summary(self, kinds):
+    def summary(self, kinds, scopes=None):
         torch.cuda.synchronize()
         ms = fl = nb = 0.0
         n = 0
-        for k in kinds:
-            for s, e, f, b in self.ev.get(k, []):
+        for k, sc, s, e, f, b in self.ev:
+            if k in kinds and (scopes is None or sc in scopes):
                 ms += s.elapsed_time(e)
                 fl += f
                 nb += b
                 n += 1
-        self.nbytes = nb
-        return ms, fl, n
+        return ms, fl, n, nb
 
 
-def cpu_baseline(args, seconds):
-    """The oracle's CPU restatement of the same train step (kind 'port'), batch 1."""
-    from oracle import dg_oracle as O
-    from dgvcc_amd.models.models import DGModel_base
-    threads = max(1, min(os.cpu_count() or 1, 16))
-    torch.set_num_threads(threads)
-    tmpl = DGModel_base(pretrained=False, den_dropout=0.0).state_dict()
-    sd = O.seeded_state_dict(tmpl)
-    batch = O.synthetic_batch(1, args.height, args.width, seed=7)
-    mode = "simple" if args.mode == "simple" else "final"
-    loss_ref, outs, _, _ = O.train_step(sd, batch, mode)  # warm-up (and the parity reference below)
-    parity = density_parity(sd, batch, loss_ref, outs[0]) if mode == "simple" else None
-    n, t0 = 0, time.perf_counter()
-    while True:
-        O.train_step(sd, batch, mode)
-        n += 1
-        if time.perf_counter() - t0 >= seconds or n >= 8:
-            break
-    dt = time.perf_counter() - t0
-    frames = n * (2 if mode == "final" else 1)
-    out = {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-           "sample": f"{n} oracle train steps ({mode} mode, batch 1, {args.height}x{args.width}, fp32, "
-                     f"torch CPU {threads} threads) after 1 warm-up"}
-    if parity is not None:
-        out["parity"] = parity
-    return out
-
-
-def density_parity(sd, batch, loss_ref, d_ref):
-    """The metric's "MAE vs reference" on the warm-up frame: the HIP path (fp32 mode, the
-    parity precision of BASELINE.json's north_star) against the oracle's density map and
-    MSE loss for the same weights and frame.  The oracle is only the checker here."""
-    from dgvcc_amd.models.models import DGModel_base
-    from dgvcc_amd.losses import mse_loss
-    dev = torch.device("cuda", torch.cuda.current_device())
-    model = DGModel_base(pretrained=False, den_dropout=0.0)
-    model.load_state_dict(sd)
-    model = model.to(dev).set_precision("fp32").train()
-    d = model(batch[0].to(dev))
-    loss = mse_loss(d, batch[2][1].to(dev), 1000.0)
-    loss.backward()
-    torch.cuda.synchronize()
-    d = d.detach().double().cpu()
-    r = d_ref.detach().double()
-    return {"precision": "fp32", "frame": "1x3x%dx%d" % tuple(r.shape[-2:]), "tolerance_rel": 1e-4,
-            "density_map_mae": float((d - r).abs().mean()),
-            "density_map_max_rel": float((d - r).abs().max() / r.abs().max()),
-            "count_abs_err": float(abs(d.sum() - r.sum()) / 1000.0),
-            "loss_rel": float(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))}
-
-
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # DGVCC_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing one
-    # GPU (local rank modulo the visible devices); the driver's runs use RCCL ("nccl").
-    backend = os.environ.get("DGVCC_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
-
-    from dgvcc_amd import kernels as K
+def build_model(args, precision, dev):
     from dgvcc_amd.models import models as MM
+    if args.trunk:
+        from dgvcc_amd.models import trunks as TM
+        cls = {"ibn": TM.IBNCounter_ResNet, "sw": TM.SWCounter_ResNet, "isw": TM.ISWCounter_ResNet}
+        return cls[args.trunk](pretrained=False).to(dev).set_precision(precision), \
+            ("isw" if args.trunk == "isw" else "simple")
+    name = args.model or ("DGModel_final" if args.mode == "final" else "DGModel_base")
+    if name == "DensityRegressorBase":
+        from dgvcc_amd.models import models2 as M2
+        model = M2.DensityRegressorBase(pretrained=False)
+    else:
+        model = getattr(MM, name)(pretrained=False)
+    return model.to(dev).set_precision(precision), args.mode
+
+
+def traffic_key(args, precision):
+    label = args.trunk or (args.model or args.mode)
+    return f"{label}_{precision}_b{args.batch}_{args.height}x{args.width}"
+
+
+def measured_traffic(args, precision):
+    """PMC HBM bytes per conv forward/dgrad launch of THIS workload (tools/pmc_summary.py over a
+    rocprofv3 FETCH_SIZE / WRITE_SIZE pass of the same bench command), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic", traffic_key(args, precision) + ".json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        return None, None
+
+
+FWD_KERNEL_NAMES = {
+    "fp32": "conv_fwd_kernel<float> (implicit-GEMM conv on v_mfma_f32_16x16x4_f32: forward + dgrad launches)",
+    "bf16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
+            "(implicit-GEMM conv on v_mfma_f32_16x16x32_bf16: forward + dgrad launches)",
+}
+
+
+def run_leg(args, precision, dev, world, rank):
+    """Build, warm up and time one precision of the workload; returns the measurements."""
+    from dgvcc_amd import kernels as K
     from dgvcc_amd.losses import MSELoss
     from dgvcc_amd.optim import AdamW
     from dgvcc_amd.trainers.dgtrainer import DGTrainer
 
     B, H, W = args.batch, args.height, args.width
     torch.manual_seed(2112)
-    mode = args.mode
-    if args.trunk:
-        from dgvcc_amd.models import trunks as TM
-        cls = {"ibn": TM.IBNCounter_ResNet, "sw": TM.SWCounter_ResNet, "isw": TM.ISWCounter_ResNet}
-        model = cls[args.trunk](pretrained=False)
-        mode = "isw" if args.trunk == "isw" else "simple"
-    elif args.mode == "simple":
-        model = MM.DGModel_base(pretrained=False, den_dropout=0.5)
-    else:
-        model = MM.DGModel_final(pretrained=False)
-    model = model.to(dev).set_precision(args.precision)
+    model, mode = build_model(args, precision, dev)
     if world > 1:  # identical init on every rank
         import torch.distributed as dist
         for t in model.state_dict().values():
@@ -240,6 +247,7 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    last = None
     for _ in range(args.steps):
         last = trainer.train_step(model, loss_fn, opt, batch, epoch)
     torch.cuda.synchronize()
@@ -247,70 +255,235 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     K.set_conv_timer(None)
-    conv_ms, conv_flops, conv_launches = timer.summary(("fwd", "dgrad"))
-    conv_alg_bytes = timer.nbytes / max(conv_launches, 1)
-    wg_ms, wg_flops, wg_launches = timer.summary(("wgrad",))
+    res = {"elapsed": elapsed, "last_loss": last, "mode": mode, "model": type(model).__name__}
+    conv_ms, conv_flops, conv_n, conv_bytes = timer.summary(("fwd", "dgrad"))
+    wg_ms, wg_flops, wg_n, _ = timer.summary(("wgrad",))
+    enc_kinds = ("fwd", "dgrad", "wgrad", "stem", "stem_wgrad")
+    enc_ms, enc_flops, _, _ = timer.summary(enc_kinds, scopes=("enc",))
+    enc_gemm_ms, enc_gemm_flops, _, _ = timer.summary(("fwd", "dgrad", "wgrad"), scopes=("enc",))
+    res.update(conv_ms=conv_ms, conv_flops=conv_flops, conv_n=conv_n, conv_bytes=conv_bytes,
+               wg_ms=wg_ms, wg_flops=wg_flops, enc_ms=enc_ms, enc_flops=enc_flops,
+               enc_gemm_ms=enc_gemm_ms, enc_gemm_flops=enc_gemm_flops)
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+        res["elapsed"] = t.item()
         # data-parallel sanity check outside the timed region: identical parameters on every rank
         chk = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum().reshape(1)
         hi, lo = chk.clone(), chk.clone()
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-        params_in_sync = bool(hi.item() == lo.item())
+        res["params_in_sync"] = bool(hi.item() == lo.item())
+    views = 2 if (mode in ("final", "base") and not args.trunk) else 1
+    res["frames"] = B * views * world * args.steps
+    del model, opt, trainer, batch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
-    views = 2 if (args.mode == "final" and not args.trunk) else 1
-    frames = B * views * world * args.steps
-    value = frames / elapsed
-    peak = BF16_DENSE_PEAK_TFLOPS if args.precision == "bf16" else F32_MFMA_PEAK_TFLOPS
-    achieved = conv_flops / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "conv_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    step_flops = conv_flops_per_step(B, H, W, args.mode) if not args.trunk else \
-        (conv_flops + wg_flops) / args.steps
+
+def roofline(args, precision, r):
+    peak = PEAKS[precision]
+    achieved = r["conv_flops"] / (r["conv_ms"] * 1e-3) / 1e12 if r["conv_ms"] > 0 else 0.0
+    traffic, tsrc = measured_traffic(args, precision)
+    steps = args.steps
+    tot, enc_tot = step_flops(args.batch, args.height, args.width, r["mode"]) if not args.trunk else \
+        ((r["conv_flops"] + r["wg_flops"]) / steps, None)
+    step_s = r["elapsed"] / steps
+    out = {"bound": "mfma", "kernel": FWD_KERNEL_NAMES.get(precision, "implicit-GEMM conv forward + dgrad"),
+           "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+           "traffic": traffic, "traffic_source": tsrc,
+           "algorithmic_bytes_per_launch": round(r["conv_bytes"] / max(r["conv_n"], 1)),
+           "algorithmic_flop_per_launch": round(r["conv_flops"] / max(r["conv_n"], 1)),
+           "launches_per_step": r["conv_n"] // steps,
+           "avg_launch_us": round(r["conv_ms"] * 1e3 / max(r["conv_n"], 1), 2),
+           "kernel_ms_per_step": round(r["conv_ms"] / steps, 3),
+           "wgrad_achieved": round(r["wg_flops"] / (r["wg_ms"] * 1e-3) / 1e12, 2) if r["wg_ms"] > 0 else None,
+           "wgrad_frac": round(r["wg_flops"] / (r["wg_ms"] * 1e-3) / 1e12 / peak, 4) if r["wg_ms"] > 0 else None,
+           "wgrad_ms_per_step": round(r["wg_ms"] / steps, 3),
+           "step_gemm_tflop_algorithmic": round(tot / 1e12, 4),
+           "whole_step_mfma_frac": round(tot / step_s / 1e12 / peak, 4)}
+    if r["enc_ms"] > 0:
+        # encoder only (enc1-enc3 of vgg16_bn.features: fwd + dgrad + wgrad launches, measured
+        # per launch; the fused bf16 stem's launches included in the first figure)
+        out["encoder_achieved"] = round(r["enc_flops"] / (r["enc_ms"] * 1e-3) / 1e12, 2)
+        out["encoder_frac"] = round(out["encoder_achieved"] / peak, 4)
+        out["encoder_ms_per_step"] = round(r["enc_ms"] / steps, 3)
+        if r["enc_gemm_ms"] > 0:
+            out["encoder_gemm_frac"] = round(r["enc_gemm_flops"] / (r["enc_gemm_ms"] * 1e-3) / 1e12 / peak, 4)
+    if enc_tot is not None:
+        out["encoder_tflop_per_step_algorithmic"] = round(enc_tot / 1e12, 4)
+    return out
+
+
+def cpu_baseline(args, seconds):
+    """The oracle's CPU restatement of the same train step (kind 'port'), batch 1, fp32, on
+    this host's cores, plus the full-frame fp32 parity of the HIP path on the warm-up frame."""
+    from oracle import dg_oracle as O
+    from dgvcc_amd.models.models import DGModel_base, DGModel_final
+    nproc = os.cpu_count() or 1
+    threads = max(1, min(nproc, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    torch.set_num_threads(threads)
+    mode = args.mode if args.mode in ("simple", "final") else "simple"
+    tmpl = (DGModel_final(pretrained=False) if mode == "final" else DGModel_base(pretrained=False)).state_dict()
+    sd = O.seeded_state_dict(tmpl)
+    batch = O.synthetic_batch(1, args.height, args.width, seed=7)
+    t0 = time.perf_counter()
+    loss_ref, outs, _, _ = O.train_step(sd, batch, mode)  # warm-up, and the parity reference below
+    t_warm = time.perf_counter() - t0
+    parity = density_parity(sd, batch, loss_ref, outs, mode)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        O.train_step(sd, batch, mode)
+        n += 1
+        if time.perf_counter() - t0 + t_warm / 2 >= seconds or n >= 8:
+            break
+    dt = time.perf_counter() - t0
+    frames = n * (2 if mode == "final" else 1)
+    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "host_nproc": nproc, "cpu_model": _cpu_model(),
+            "sample": f"{n} oracle train steps ({mode} mode, batch 1 = {2 if mode == 'final' else 1} frame(s) "
+                      f"of {args.height}x{args.width}, fp32, torch CPU {threads} threads) after 1 warm-up step",
+            "parity": parity}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def density_parity(sd, batch, loss_ref, outs_ref, mode):
+    """The metric's "MAE vs reference" on the warm-up frame: the HIP path in fp32 (north_star's
+    parity precision) against the oracle for the same weights and frame.  Final mode: the
+    oracle is re-run on the HIP path's own threshold decisions (e_mask, class maps) and the
+    number of decisions that differ is reported; the loss is compared as is."""
+    from oracle import dg_oracle as O
+    from dgvcc_amd.models.models import DGModel_base, DGModel_final
+    from dgvcc_amd.losses import mse_loss
+    from dgvcc_amd.losses.bce import binary_cross_entropy
+    dev = torch.device("cuda", torch.cuda.current_device())
+    img1, img2, (pts, dmaps, bmaps) = batch
+    if mode == "final":
+        model = DGModel_final(pretrained=False, den_dropout=0.0, cls_dropout=0.0)
+    else:
+        model = DGModel_base(pretrained=False, den_dropout=0.0)
+    model.load_state_dict(sd)
+    model = model.to(dev).set_precision("fp32").train()
+    res = {"precision": "fp32", "frame": "1x3x%dx%d" % tuple(img1.shape[-2:]), "tolerance_rel": 1e-4}
+    with torch.no_grad():
+        if mode == "final":
+            plan = model._get_plans()["pair"]
+            plan.capture = {}
+            gb = bmaps.to(dev)
+            dc1, dc2, c1, c2, _, loss_con, _ = model.forward_train(img1.to(dev), img2.to(dev), gb)
+            gt = dmaps.to(dev)
+            loss = (mse_loss(dc1, gt, 1000.0) + mse_loss(dc2, gt, 1000.0)
+                    + 10 * (binary_cross_entropy(c1, gb) + binary_cross_entropy(c2, gb)) + 10 * loss_con)
+            cap = plan.capture
+            plan.capture = None
+            em = cap["emask"].permute(0, 3, 1, 2).bool().cpu()
+            cp = tuple(c.cpu() for c in cap["c_pred"])
+            info = {}
+            sd2 = {k: v.clone() for k, v in sd.items()}
+            r1, r2, *_ = O.final_forward(sd2, img1, img2, bmaps, e_mask_in=em, c_pred_in=cp, info=info)
+            pairs = [(dc1, r1), (dc2, r2)]
+            res.update({k: v for k, v in info.items()})
+            res["note"] = ("oracle re-run on the HIP path's e_mask / class-map decisions; flips = decisions "
+                           "within fp32 rounding of the threshold")
+            res["loss_rel_uninjected"] = float(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))
+        else:
+            d = model(img1.to(dev))
+            loss = mse_loss(d, dmaps.to(dev), 1000.0)
+            pairs = [(d, outs_ref[0])]
+            res["loss_rel"] = float(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))
+    torch.cuda.synchronize()
+    mae = mx = cnt = 0.0
+    for d, r in pairs:
+        d = d.detach().double().cpu()
+        r = r.detach().double()
+        mae = max(mae, float((d - r).abs().mean()))
+        mx = max(mx, float((d - r).abs().max() / r.abs().max()))
+        cnt = max(cnt, float(abs(d.sum() - r.sum()) / 1000.0))
+    res.update(density_map_mae=mae, density_map_max_rel=mx, count_abs_err=cnt)
+    del model
+    torch.cuda.empty_cache()
+    return res
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    # DGVCC_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing one
+    # GPU (local rank modulo the visible devices); the driver's runs use RCCL ("nccl").
+    backend = os.environ.get("DGVCC_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
+    dist_world = 1
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        dist_world = dist.get_world_size()
+        assert dist_world == args.gpus, (dist_world, args.gpus)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    prec = args.precision
+    r = run_leg(args, prec, dev, world, rank)
+    value = r["frames"] / r["elapsed"]
+    workload = (f"{r['model']} {r['mode']}-mode DGTrainer.train_step (configs/baselines/sta_{args.trunk}.yml)"
+                if args.trunk else
+                f"{r['model']} {r['mode']}-mode DGTrainer.train_step ({CONFIG_FILES.get(args.mode, '')}: "
+                + ("two views, MSE x log_para 1000 + 10 BCE(class maps) + 10 JSD-MSE, AdamW"
+                   if r["mode"] == "final" else "MSE x log_para 1000, AdamW") + ")")
     out = {
-        "metric": "train-step frames/sec at 768×1024, ShanghaiTech-A; MAE vs reference",
+        "metric": METRIC,
         "value": round(value, 3),
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.precision,
-        "data": "synthetic 3x768x1024 frames + Poisson(500) point sets (dmap via HIP scatter), HBM-resident",
-        "config": {"workload": (f"{type(model).__name__} {mode}-mode DGTrainer.train_step "
-                                f"(configs/baselines/sta_{args.trunk}.yml)") if args.trunk else
-                   (f"DGModel_base {args.mode}-mode DGTrainer.train_step (configs/stb_reg_base.yml)"
-                    if args.mode == "simple" else "DGModel_final final-mode DGTrainer.train_step (configs/sta_final.yml)"),
-                   "global_batch": B * world, "frames_per_gpu_step": B * views,
-                   "resolution": f"{H}x{W}", "parallelism": f"dp{world}", "last_loss": last},
-        "roofline": {"bound": "mfma", "kernel": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel (implicit-GEMM conv: forward + dgrad launches)",
-                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4), "traffic": traffic,
-                     "algorithmic_bytes_per_launch": round(conv_alg_bytes),
-                     "algorithmic_flop_per_launch": round(conv_flops / max(conv_launches, 1)),
-                     "launches_per_step": conv_launches // args.steps,
-                     "avg_launch_us": round(conv_ms * 1e3 / max(conv_launches, 1), 2),
-                     "kernel_ms_per_step": round(conv_ms / args.steps, 3),
-                     "wgrad_achieved": round(wg_flops / (wg_ms * 1e-3) / 1e12, 2) if wg_ms > 0 else None,
-                     "wgrad_ms_per_step": round(wg_ms / args.steps, 3),
-                     "model_conv_tflops_per_step_algorithmic": round(step_flops / 1e12, 4),
-                     "whole_step_mfma_frac": round(step_flops / (elapsed / args.steps) / 1e12 / peak, 4)},
+        "dtype": prec,
+        "data": f"synthetic 3x{args.height}x{args.width} frames (view 2 = view 1 + 0.1 N(0,1)) + Poisson(500) "
+                "point sets, dmap via the HIP scatter, HBM-resident; random-init weights",
+        "config": {"workload": workload, "global_batch": args.batch * world,
+                   "frames_per_gpu_step": r["frames"] // (world * args.steps),
+                   "resolution": f"{args.height}x{args.width}", "parallelism": f"dp{world}",
+                   "rccl_world_size": dist_world, "backend": backend if world > 1 else None,
+                   "last_loss": r["last_loss"]},
+        "roofline": roofline(args, prec, r),
     }
-    if world > 1:
-        out["params_in_sync"] = params_in_sync
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if "params_in_sync" in r:
+        out["params_in_sync"] = r["params_in_sync"]
+    if prec == "fp32" and not args.no_bf16:
+        rb = run_leg(args, "bf16", dev, world, rank)
+        out["perf_bf16"] = {"value": round(rb["frames"] / rb["elapsed"], 3), "unit": "frames/s", "dtype": "bf16",
+                            "ms_per_step": round(rb["elapsed"] / args.steps * 1e3, 3),
+                            "note": "same workload in bf16 storage/MFMA with f32 accumulation, statistics and "
+                                    "losses (a perf mode; not the headline value)",
+                            "last_loss": rb["last_loss"], "roofline": roofline(args, "bf16", rb)}
+        if "params_in_sync" in rb:
+            out["perf_bf16"]["params_in_sync"] = rb["params_in_sync"]
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.trunk:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

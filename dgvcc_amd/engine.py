@@ -75,6 +75,7 @@ class ConvLayer:
                  first: bool = False):
         assert conv.stride == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
         self.conv, self.bn, self.act, self.first = conv, bn, act, first
+        self.scope = "head"  # FeaturePlan relabels its encoder / decoder layers (bench timing)
         self.R = conv.kernel_size[0]
         self.pad = conv.padding[0]
         self.Cin, self.Cout = conv.in_channels, conv.out_channels
@@ -107,6 +108,7 @@ class ConvLayer:
         """x: NHWC Act, or for the fused bf16 stem the NCHW f32 image itself.
         pool: also apply the following MaxPool2d(2,2) into `pool` (BN/ReLU/pool in one pass);
         `out` (the un-pooled activation) may then be None when nothing else reads it."""
+        K.set_scope(self.scope)
         stem = isinstance(x, torch.Tensor)
         dt = (out if out is not None else pool).buf.dtype
         bias = self.conv.bias.detach() if self.conv.bias is not None else None
@@ -186,6 +188,7 @@ class ConvLayer:
         g_pool: gradient of the pooled output when the forward ran with `pool`;
         gx_bn: the layer whose whole output gradient gx is (its BN-backward partial sums
         then come from this layer's dgrad epilogue)."""
+        K.set_scope(self.scope)
         x, z, stats, wp, drop, training = tape.pop(self)
         pre = tape.pop(("bnpart", self), None)
         if self.bn is not None and not training:
@@ -310,8 +313,8 @@ class CatConvLayer(ConvLayer):
     def forward(self, x, out, training, tape, drop=None, pool=None):
         if not isinstance(x, CatParts):
             return super().forward(x, out, training, tape, drop=drop, pool=pool)
-        if self.R != 1 or self.bn is None or pool is not None or x.C != self.Cin:
-            raise ValueError("CatConvLayer: decomposed path needs a 1x1 conv with BatchNorm")
+        if self.R != 1 or pool is not None or x.C != self.Cin:
+            raise ValueError("CatConvLayer: decomposed path needs an unpooled 1x1 conv")
         dt = out.buf.dtype
         dev = out.buf.device
         w = self.conv.weight.detach()
@@ -331,7 +334,9 @@ class CatConvLayer(ConvLayer):
         K.call("dg_cat_combine", z.dt, z.ptr, z.ld, zs[1].ptr, zs[1].ld, zs[2].ptr, zs[2].ld, z.N, z.H, z.W,
                self.Cout, K.ptr(bias), z.ptr, z.ld, K.ptr(part), K.stream())
         bn = self.bn
-        if training:
+        if bn is None:  # models2 den_dec: ConvBlock without BatchNorm (bias-free conv + ReLU)
+            stats = frozen(self, ("ident", dev), (), lambda: _ident_stats(self.Cout, dev))
+        elif training:
             bn.num_batches_tracked.add_(1)
             stats = K.bn_part_finalize(part, rows, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                        bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
@@ -345,14 +350,16 @@ class CatConvLayer(ConvLayer):
         if not isinstance(tape[self][0], CatParts):
             return super().backward(tape, g, gx, accumulate_gx=accumulate_gx, g_pool=g_pool)
         x, z, stats, wps, drop, training = tape.pop(self)
-        if not training:
+        if not training and self.bn is not None:
             raise RuntimeError("backward through an eval-mode BatchNorm is not supported")
         dev = z.buf.device
         dz = Act(torch.empty_like(z.buf))
         dgamma = torch.empty(self.Cout, dtype=torch.float32, device=dev)
         dbeta = torch.empty(self.Cout, dtype=torch.float32, device=dev)
-        dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) if self.conv.bias is not None else None
-        K.bn_bwd(g, z, self.bn.weight.detach(), stats, self.act, dz, dgamma, dbeta, dbias, drop)
+        dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) \
+            if (self.conv.bias is not None and self.bn is not None) else None
+        gamma = self.bn.weight.detach() if self.bn is not None else None
+        K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta, dbias, drop)
         gzs = [dz]
         for part, sc in zip(x.parts[1:], CatParts.SCALES[1:]):  # U^T dz at the part's resolution
             gk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dz.buf.dtype, dev))
@@ -367,9 +374,11 @@ class CatConvLayer(ConvLayer):
             if gx is not None:
                 K.conv_dgrad(gzs[k], wps[k], part.C, 1, 0, gx.parts[k], accumulate=accumulate_gx)
             lo += part.C
-        grads = {self.conv.weight: dw, self.bn.weight: dgamma, self.bn.bias: dbeta}
+        grads = {self.conv.weight: dw}
+        if self.bn is not None:
+            grads.update({self.bn.weight: dgamma, self.bn.bias: dbeta})
         if self.conv.bias is not None:
-            grads[self.conv.bias] = dbias
+            grads[self.conv.bias] = dbias if self.bn is not None else dbeta
         return grads
 
 
@@ -382,13 +391,19 @@ class FeaturePlan:
     CatConvLayer (never materialised on the hot path)."""
 
     def __init__(self, model):
-        feats = list(model.enc1) + list(model.enc2) + list(model.enc3)
+        # DGModel_* name the VGG16-BN stages enc1/2/3, models2's DensityRegressor* stage1/2/3
+        names = getattr(model, "_ENC_NAMES", ("enc1", "enc2", "enc3"))
+        feats = [m for n in names for m in getattr(model, n)]
         conv_idx = [i for i, m in enumerate(feats) if isinstance(m, nn.Conv2d)]
         assert conv_idx == [0, 3, 7, 10, 14, 17, 20, 24, 27, 30, 34, 37, 40], conv_idx
         self.enc = [ConvLayer(feats[i], feats[i + 1], ACT_RELU, first=(i == 0)) for i in conv_idx]
         self.dec = [ConvLayer(cb.conv, cb.bn, ACT_RELU if cb.relu is not None else ACT_NONE)
                     for d in (model.dec3, model.dec2, model.dec1) for cb in d]
         self.layers = self.enc + self.dec
+        for l in self.enc:
+            l.scope = "enc"
+        for l in self.dec:
+            l.scope = "dec"
 
     def params(self):
         return [p for l in self.layers for p in l.params()]
@@ -828,6 +843,10 @@ class PairPlan(_Heads):
         super().__init__(model, mem=True, cls=cls)
         # final: (dc1, dc2, c1, c2, c_err, loss_con); memadd: (d1, d2, loss_con)
         self.nondiff = (4,) if cls else ()
+        # parity instrumentation: a dict here receives the threshold decisions of the next
+        # forward (e_mask as uint8 NHWC [N,h,w,C]; the thresholded class maps), so a checker
+        # can be run on the same decisions (bench.py's full-frame final-mode parity)
+        self.capture = None
 
     def forward(self, ycat1, ycat2, x3_1, x3_2, c_gt, p_drop, err_thrs, tape=None):
         """ycat1/2: (y1, y2, y3) NHWC parts or materialised NHWC y_cat tensors."""
@@ -891,6 +910,12 @@ class PairPlan(_Heads):
             st.update(cres=cres, sub=sub)
             outs = (_up4(p1, N, h, w), _up4(p2, N, h, w), c1.view(N, 1, h // 4, w // 4),
                     c2.view(N, 1, h // 4, w // 4), _up4(cerr, N, h, w), loss_con)
+            if self.capture is not None:
+                thr = float(self.model.cls_thrs)
+                self.capture.update(c_pred=((c1 >= thr).float().view(N, 1, h // 4, w // 4),
+                                            (c2 >= thr).float().view(N, 1, h // 4, w // 4)))
+        if self.capture is not None:
+            self.capture["emask"] = mask.view(N, h, w, C)
         if tape is not None:
             tape[self] = st
         return outs

@@ -67,20 +67,26 @@ def nhwc(N, H, W, C, dtype, device="cuda", zero=False) -> torch.Tensor:
 
 # ---------------------------------------------------------------- conv -----
 _CONV_TIMER = None
+_SCOPE = ["other"]
 
 
 def set_conv_timer(timer):
-    """Install a callable timer(kind, flops, launch_fn) around conv GEMM launches
-    (bench.py roofline measurement); None disables."""
+    """Install a callable timer(kind, flops, launch_fn, nbytes, scope) around conv GEMM
+    launches (bench.py roofline measurement); None disables."""
     global _CONV_TIMER
     _CONV_TIMER = timer
+
+
+def set_scope(scope: str):
+    """Label the following conv launches ('enc' / 'dec' / 'head') for the timer."""
+    _SCOPE[0] = scope
 
 
 def _timed(kind, flops, fn, nbytes=0.0):
     if _CONV_TIMER is None:
         fn()
     else:
-        _CONV_TIMER(kind, flops, fn, nbytes)
+        _CONV_TIMER(kind, flops, fn, nbytes, _SCOPE[0])
 
 def pack_weight(w: torch.Tensor, dtype: torch.dtype, cpad: int | None = None,
                 row_len: int | None = None) -> torch.Tensor:

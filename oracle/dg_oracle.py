@@ -114,15 +114,29 @@ def cls_pred_map(c, thrs=0.5):
 
 
 def final_forward(sd, img1, img2, c_gt, training=True, err_thrs=0.5, cls_thrs=0.5,
-                  drop1=None, drop2=None):
-    """DGModel_final.forward_train (models/models.py:298-335); drop* = dropout2d masks."""
+                  drop1=None, drop2=None, e_mask_in=None, c_pred_in=None, info=None):
+    """DGModel_final.forward_train (models/models.py:298-335); drop* = dropout2d masks.
+
+    Threshold injection for full-frame parity (SURVEY.md §7 "threshold discontinuities"):
+    e_mask_in (bool [B,C,h,w]) replaces the |IN1-IN2| < err_thrs mask and c_pred_in
+    ((c_r1, c_r2) 0/1 maps [B,1,h/4,w/4]) the thresholded class maps, so that a checked
+    path whose fp32 rounding flips a few near-threshold decisions is compared on the same
+    decisions; `info` (a dict) receives how many decisions the injection changed."""
     y_cat1, x3_1 = forward_fe(sd, img1, training)
     y_cat2, x3_2 = forward_fe(sd, img2, training)
     y_den1 = _conv_bn_relu(y_cat1, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
     y_den2 = _conv_bn_relu(y_cat2, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
     y_in1 = F.instance_norm(y_den1, eps=1e-5)
     y_in2 = F.instance_norm(y_den2, eps=1e-5)
-    e_mask = (torch.abs(y_in1 - y_in2) < err_thrs).clone().detach()
+    e_y = torch.abs(y_in1 - y_in2)
+    e_mask = (e_y < err_thrs).clone().detach()
+    if e_mask_in is not None:
+        flip = e_mask_in.bool() != e_mask
+        if info is not None:
+            info["emask_elements"] = int(e_mask.numel())
+            info["emask_flips"] = int(flip.sum())
+            info["emask_flip_max_margin"] = float((e_y[flip] - err_thrs).abs().max()) if flip.any() else 0.0
+        e_mask = e_mask_in.bool()
     m1 = y_den1 * e_mask
     m2 = y_den2 * e_mask
     if drop1 is not None:
@@ -137,6 +151,13 @@ def final_forward(sd, img1, img2, c_gt, training=True, err_thrs=0.5, cls_thrs=0.
     c_resized_gt = _up(c_gt, 4, "nearest")
     c_r1 = cls_pred_map(c1, cls_thrs)
     c_r2 = cls_pred_map(c2, cls_thrs)
+    if c_pred_in is not None:
+        r1, r2 = (_up(c.float(), 4, "nearest") for c in c_pred_in)
+        if info is not None:
+            info["cls_elements"] = int(c1.numel() + c2.numel())
+            info["cls_flips"] = int(((c1 >= cls_thrs).float() != c_pred_in[0].float()).sum()
+                                    + ((c2 >= cls_thrs).float() != c_pred_in[1].float()).sum())
+        c_r1, c_r2 = r1, r2
     c_err = torch.abs(c_r1 - c_r2)
     c_resized = torch.clamp(c_resized_gt + c_err, 0, 1)
     d1 = F.relu(F.conv2d(y_new1, sd["den_head.0.conv.weight"]))

@@ -25,6 +25,47 @@ def available() -> bool:
     return os.path.isdir(os.path.join(REF, "models"))
 
 
+# torchvision's published VGG "D" configuration (Simonyan & Zisserman 2014, table 1,
+# column D); vgg16_bn inserts BatchNorm2d after every conv (torchvision/models/vgg.py
+# `make_layers(cfgs["D"], batch_norm=True)`).  Restated here so the oracle's placeholder
+# is independent of the product package.
+_CFG_D = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
+
+
+def _vgg16_bn_features():
+    """torchvision vgg16_bn().features: 44 children (13 x Conv3x3(pad 1)/BN/ReLU + 5 pools)
+    with torchvision's initialisation (kaiming_normal fan_out on convs, zero bias, BN 1/0).
+    Fixtures overwrite every weight with oracle.dg_oracle.seeded_state_dict, so only the
+    layout matters for parity."""
+    import torch.nn as nn
+    layers, cin = [], 3
+    for v in _CFG_D:
+        if v == "M":
+            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            continue
+        conv = nn.Conv2d(cin, v, kernel_size=3, padding=1)
+        nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+        nn.init.zeros_(conv.bias)
+        layers += [conv, nn.BatchNorm2d(v), nn.ReLU(inplace=True)]
+        cin = v
+    return nn.Sequential(*layers)
+
+
+def _vgg19_features():
+    """torchvision vgg19().features (cfg "E", no BN) for models2.Generator."""
+    import torch.nn as nn
+    cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M",
+           512, 512, 512, 512, "M"]
+    layers, cin = [], 3
+    for v in cfg:
+        if v == "M":
+            layers.append(nn.MaxPool2d(kernel_size=2, stride=2))
+            continue
+        layers += [nn.Conv2d(cin, v, kernel_size=3, padding=1), nn.ReLU(inplace=True)]
+        cin = v
+    return nn.Sequential(*layers)
+
+
 def _install_placeholders():
     import torch.nn as nn
 
@@ -42,8 +83,7 @@ def _install_placeholders():
         def vgg16_bn(weights=None, **kw):
             if weights is not None:
                 raise RuntimeError("no pretrained weights offline")
-            from dgvcc_amd.models.models import vgg16_bn_features  # same cfg-D layout/init
-            return _VGG(vgg16_bn_features())
+            return _VGG(_vgg16_bn_features())
 
         class VGG16_BN_Weights:
             DEFAULT = "DEFAULT"
