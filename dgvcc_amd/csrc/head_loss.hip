@@ -341,6 +341,20 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
   }
 }
 
+__global__ void tanh_fwd_kernel(const float* __restrict__ x, long long n, float* __restrict__ y) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    y[i] = tanhf(x[i]);
+}
+
+__global__ void tanh_bwd_kernel(const float* __restrict__ y, const float* __restrict__ gy, long long n,
+                                float* __restrict__ gx, int acc) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float t = y[i];
+    const float g = gy[i] * (1.f - t * t);
+    gx[i] = acc ? gx[i] + g : g;
+  }
+}
+
 }  // namespace
 
 extern "C" int dg_dmap_adaptive(const float* points, const int64_t* offsets, int N, int H, int W, double* sigma_ws,
@@ -464,6 +478,23 @@ extern "C" int dg_dmap_fixed(const float* points, const int64_t* offsets, int N,
   if (hipMemsetAsync(dmap, 0, (size_t)N * H * W * 4, st) != hipSuccess) return DG_ERR_HIP;
   if (!points) return DG_OK;
   hipLaunchKernelGGL(dmap_fixed_kernel, dim3(1024), dim3(NT), 0, st, points, offsets, N, H, W, sigma, radius, dmap);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_tanh_fwd(const float* x, int64_t n, float* y, void* stream) {
+  DG_REQUIRE(x && y && n > 0);
+  const int grid = (int)std::min<long long>(16384, (n + 255) / 256);
+  hipLaunchKernelGGL(tanh_fwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, x, (long long)n, y);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx, int accumulate, void* stream) {
+  DG_REQUIRE(y && gy && gx && n > 0);
+  const int grid = (int)std::min<long long>(16384, (n + 255) / 256);
+  hipLaunchKernelGGL(tanh_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, y, gy, (long long)n, gx,
+                     accumulate);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -225,6 +225,162 @@ __global__ __launch_bounds__(NT) void softmax_pair_bwd(const T* __restrict__ P1,
   }
 }
 
+// JSD of the two slot posteriors as models2.DensityRegressorM.forward_train computes it
+// (models/models2.py:339-346): pm = (p1 + p2)/2,
+//   loss_kl = 0.5/HW * (kl_div(log p1, pm, batchmean) + kl_div(log p2, pm, batchmean))
+//           = sum_{rows, slots} pm (2 log pm - log p1 - log p2) / (2 M),  M = B*HW rows.
+// log p is the log-softmax of the row (l - max - log sum); pm = 0 terms are 0 (xlogy).
+template <typename T, int EPL>
+__global__ __launch_bounds__(NT) void softmax_jsd_fwd(const T* __restrict__ L1, const T* __restrict__ L2, int M, int C,
+                                                      T* __restrict__ P1, T* __restrict__ P2,
+                                                      float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float a[EPL], b[EPL], la[EPL], lb[EPL];
+    load_row(L1 + r * C, lane, C, a, EPL);
+    load_row(L2 + r * C, lane, C, b, EPL);
+    float ma = -INFINITY, mb = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) { ma = fmaxf(ma, a[j]); mb = fmaxf(mb, b[j]); }
+    ma = wave_max(ma); mb = wave_max(mb);
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      la[j] = a[j] - ma; lb[j] = b[j] - mb;
+      a[j] = expf(la[j]); sa += a[j]; b[j] = expf(lb[j]); sb += b[j];
+    }
+    sa = wave_sum(sa); sb = wave_sum(sb);
+    const float ra = 1.f / sa, rb = 1.f / sb, dls = logf(sa) - logf(sb);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      a[j] *= ra; b[j] *= rb;
+      const float pm = 0.5f * (a[j] + b[j]);
+      // 2 log pm - log p1 - log p2 = log1p((p1 - p2)^2 / (4 p1 p2)) = log1p(e^2 / (4 (1 + e))),
+      // e = expm1(log p1 - log p2): no cancellation between the three O(log C) logs
+      const float e = expm1f((la[j] - lb[j]) - dls);
+      if (pm > 0.f) acc += pm * log1pf(e * e / (4.f * (1.f + e)));
+    }
+    store_row(P1 + r * C, lane, a, EPL);
+    store_row(P2 + r * C, lane, b, EPL);
+  }
+  acc = wave_sum(acc);
+  __shared__ float sh[4];
+  if (lane == 0) sh[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// d loss_kl / d l1_j = k (p1_j (A_j - S1 + 1) - pm_j),  A = log pm - (log p1 + log p2)/2,
+// S1 = sum_j p1_j A_j, k = coef / (2 M); plus the readout's p1 (gP1 - <p1, gP1>).
+template <typename T, int EPL>
+__global__ __launch_bounds__(NT) void softmax_jsd_bwd(const T* __restrict__ P1, const T* __restrict__ P2,
+                                                      const T* __restrict__ G1, const T* __restrict__ G2, int M,
+                                                      int C, const float* __restrict__ coef, T* __restrict__ GL1,
+                                                      T* __restrict__ GL2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float k = coef ? coef[0] / (2.f * (float)M) : 0.f;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float p1[EPL], p2[EPL], g1[EPL], g2[EPL], A[EPL];
+    load_row(P1 + r * C, lane, C, p1, EPL);
+    load_row(P2 + r * C, lane, C, p2, EPL);
+    if (G1) load_row(G1 + r * C, lane, C, g1, EPL);
+    else for (int j = 0; j < EPL; ++j) g1[j] = 0.f;
+    if (G2) load_row(G2 + r * C, lane, C, g2, EPL);
+    else for (int j = 0; j < EPL; ++j) g2[j] = 0.f;
+    float s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      const float pm = 0.5f * (p1[j] + p2[j]);
+      // A = log pm - (log p1 + log p2)/2 = log1p((p1-p2)^2 / (4 p1 p2)) / 2 (cancellation-free)
+      const float d = p1[j] - p2[j];
+      A[j] = (p1[j] > 0.f && p2[j] > 0.f) ? 0.5f * log1pf(d * d / (4.f * p1[j] * p2[j]))
+                                          : (pm > 0.f ? logf(pm) - 0.5f * (logf(p1[j]) + logf(p2[j])) : 0.f);
+      s1 = fmaf(p1[j], g1[j], s1);
+      s2 = fmaf(p2[j], g2[j], s2);
+      t1 += p1[j] > 0.f ? p1[j] * A[j] : 0.f;
+      t2 += p2[j] > 0.f ? p2[j] * A[j] : 0.f;
+    }
+    s1 = wave_sum(s1); s2 = wave_sum(s2); t1 = wave_sum(t1); t2 = wave_sum(t2);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      const float pm = 0.5f * (p1[j] + p2[j]);
+      const float a1 = p1[j] > 0.f ? p1[j] * (A[j] - t1 + 1.f) : 0.f;
+      const float a2 = p2[j] > 0.f ? p2[j] * (A[j] - t2 + 1.f) : 0.f;
+      g1[j] = p1[j] * (g1[j] - s1) + k * (a1 - pm);
+      g2[j] = p2[j] * (g2[j] - s2) + k * (a2 - pm);
+    }
+    store_row(GL1 + r * C, lane, g1, EPL);
+    store_row(GL2 + r * C, lane, g2, EPL);
+  }
+}
+
+// loss_err = F.l1_loss(IN(y1), IN(y2)) (models/models2.py:334): block partial sums of
+// |(y1-mu1)*is1 - (y2-mu2)*is2| over dense [N*HW][C] rows with pixel stride ld
+template <typename T>
+__global__ __launch_bounds__(NT) void in_l1_fwd_kernel(const T* __restrict__ y1, const T* __restrict__ y2,
+                                                       long long ld, int N, int HW, int C, const float* mu1,
+                                                       const float* is1, const float* mu2, const float* is2,
+                                                       float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * HW * tpp;
+  float acc = 0.f;
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    const int n = (int)(p / HW);
+    float a[V], b[V];
+    ldv(y1 + p * ld + c0, a);
+    ldv(y2 + p * ld + c0, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int nc = n * C + c0 + e;
+      acc += fabsf((a[e] - mu1[nc]) * is1[nc] - (b[e] - mu2[nc]) * is2[nc]);
+    }
+  }
+  acc = wave_sum(acc);
+  __shared__ float sh[NT / 64];
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < NT / 64; ++k) t += sh[k];
+    part[blockIdx.x] = t;
+  }
+}
+
+// g_in1 = coef[0] * sgn(IN(y1) - IN(y2)) / (N*HW*C), g_in2 = -g_in1 (dense [N*HW][C])
+template <typename T>
+__global__ __launch_bounds__(NT) void in_l1_bwd_kernel(const T* __restrict__ y1, const T* __restrict__ y2,
+                                                       long long ld, int N, int HW, int C, const float* mu1,
+                                                       const float* is1, const float* mu2, const float* is2,
+                                                       const float* __restrict__ coef, T* __restrict__ g1,
+                                                       T* __restrict__ g2) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int tpp = C / V;
+  const long long total = (long long)N * HW * tpp;
+  const float k = coef[0] / ((float)N * (float)HW * (float)C);
+  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
+    const long long p = i / tpp;
+    const int c0 = (int)(i % tpp) * V;
+    const int n = (int)(p / HW);
+    float a[V], b[V];
+    ldv(y1 + p * ld + c0, a);
+    ldv(y2 + p * ld + c0, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const int nc = n * C + c0 + e;
+      const float d = (a[e] - mu1[nc]) * is1[nc] - (b[e] - mu2[nc]) * is2[nc];
+      const float sg = d > 0.f ? k : (d < 0.f ? -k : 0.f);
+      a[e] = sg;
+      b[e] = -sg;
+    }
+    stv(g1 + p * C + c0, a);
+    stv(g2 + p * C + c0, b);
+  }
+}
+
 // single-view softmax (DGModel_mem.forward / memcls.forward)
 template <typename T, int EPL>
 __global__ __launch_bounds__(NT) void softmax_fwd(const T* __restrict__ L, int M, int C, T* __restrict__ P) {
@@ -414,6 +570,86 @@ extern "C" int dg_softmax_pair_bwd(int dtype, const void* P1, const void* P2, co
   else
     SOFTMAX_DISPATCH(softmax_pair_bwd, float, C, (const float*)P1, (const float*)P2, (const float*)G1,
                      (const float*)G2, M, C, coef, (float*)GL1, (float*)GL2);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_jsd_fwd(int dtype, const void* L1, const void* L2, int M, int C, void* P1, void* P2,
+                                  float* loss_kl, void* workspace, void* stream) {
+  DG_REQUIRE(L1 && L2 && P1 && P2 && loss_kl && workspace && M > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = std::min(4096, dg_cdiv(M, 4));
+  if (dtype == DG_BF16)
+    SOFTMAX_DISPATCH(softmax_jsd_fwd, bf16, C, (const bf16*)L1, (const bf16*)L2, M, C, (bf16*)P1, (bf16*)P2,
+                     (float*)workspace);
+  else
+    SOFTMAX_DISPATCH(softmax_jsd_fwd, float, C, (const float*)L1, (const float*)L2, M, C, (float*)P1, (float*)P2,
+                     (float*)workspace);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_final, dim3(1), dim3(64), 0, st, (const float*)workspace, grid, 2.0 * (double)M, loss_kl);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_jsd_bwd(int dtype, const void* P1, const void* P2, const void* G1, const void* G2, int M,
+                                  int C, const float* coef, void* GL1, void* GL2, void* stream) {
+  DG_REQUIRE(P1 && P2 && GL1 && GL2 && M > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = std::min(4096, dg_cdiv(M, 4));
+  if (dtype == DG_BF16)
+    SOFTMAX_DISPATCH(softmax_jsd_bwd, bf16, C, (const bf16*)P1, (const bf16*)P2, (const bf16*)G1, (const bf16*)G2,
+                     M, C, coef, (bf16*)GL1, (bf16*)GL2);
+  else
+    SOFTMAX_DISPATCH(softmax_jsd_bwd, float, C, (const float*)P1, (const float*)P2, (const float*)G1,
+                     (const float*)G2, M, C, coef, (float*)GL1, (float*)GL2);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int64_t dg_in_l1_workspace(int N, int HW, int C) {
+  if (N <= 0 || HW <= 0 || C <= 0) return DG_ERR_INVALID;
+  return (int64_t)ew_grid((long long)N * HW * C / 4, 4096) * 4;
+}
+
+extern "C" int dg_in_l1_fwd(int dtype, const void* y1, const void* y2, int64_t ld, int N, int HW, int C,
+                            const float* mu1, const float* is1, const float* mu2, const float* is2, float* loss,
+                            void* workspace, void* stream) {
+  DG_REQUIRE(y1 && y2 && mu1 && is1 && mu2 && is2 && loss && workspace && N > 0 && HW > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ld % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * HW * (C / V);
+  const int grid = ew_grid(total, 4096);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(in_l1_fwd_kernel<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)y1, (const bf16*)y2, ld, N,
+                       HW, C, mu1, is1, mu2, is2, (float*)workspace);
+  else
+    hipLaunchKernelGGL(in_l1_fwd_kernel<float>, dim3(grid), dim3(NT), 0, st, (const float*)y1, (const float*)y2, ld,
+                       N, HW, C, mu1, is1, mu2, is2, (float*)workspace);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(sum_final, dim3(1), dim3(64), 0, st, (const float*)workspace, grid, (double)N * HW * C, loss);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_in_l1_bwd(int dtype, const void* y1, const void* y2, int64_t ld, int N, int HW, int C,
+                            const float* mu1, const float* is1, const float* mu2, const float* is2, const float* coef,
+                            void* g1, void* g2, void* stream) {
+  DG_REQUIRE(y1 && y2 && mu1 && is1 && mu2 && is2 && coef && g1 && g2 && N > 0 && HW > 0 && C > 0);
+  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_SUPPORTED(C % V == 0 && ld % V == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)N * HW * (C / V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(in_l1_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)y1,
+                       (const bf16*)y2, ld, N, HW, C, mu1, is1, mu2, is2, coef, (bf16*)g1, (bf16*)g2);
+  else
+    hipLaunchKernelGGL(in_l1_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)y1,
+                       (const float*)y2, ld, N, HW, C, mu1, is1, mu2, is2, coef, (float*)g1, (float*)g2);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -111,6 +111,12 @@ class ConvLayer:
         K.set_scope(self.scope)
         stem = isinstance(x, torch.Tensor)
         dt = (out if out is not None else pool).buf.dtype
+        # host-side shape guard: the kernels size their grids from x and write `out` blindly
+        xs = (x.shape[0], x.shape[2], x.shape[3]) if stem else (x.N, x.H, x.W)
+        if out is not None and ((out.N, out.H, out.W) != xs or out.C != self.Cout):
+            raise ValueError(f"ConvLayer: output {(out.N, out.H, out.W, out.C)} != input {xs} x Cout {self.Cout}")
+        if pool is not None and ((pool.N, pool.H * 2, pool.W * 2) != xs or pool.C != self.Cout):
+            raise ValueError("ConvLayer: pooled output shape mismatch")
         bias = self.conv.bias.detach() if self.conv.bias is not None else None
         bn = self.bn
         if stem:
@@ -390,7 +396,10 @@ class FeaturePlan:
     reference's y_cat = cat[y1, up2(y2), up4(y3)] (models/models.py:84) is left to the heads'
     CatConvLayer (never materialised on the hot path)."""
 
-    def __init__(self, model):
+    def __init__(self, model, inorm: bool = False):
+        # inorm: F.instance_norm (affine-free) on every stage output x1, x2, x3 before the next
+        # stage and the decoder read it (models2.DensityRegressor, models/models2.py:149-155)
+        self.inorm = inorm
         # DGModel_* name the VGG16-BN stages enc1/2/3, models2's DensityRegressor* stage1/2/3
         names = getattr(model, "_ENC_NAMES", ("enc1", "enc2", "enc3"))
         feats = [m for n in names for m in getattr(model, n)]
@@ -430,15 +439,28 @@ class FeaturePlan:
         a5 = nh(H // 4, W // 4, 256); E[5].forward(a4, a5, training, tape)
         dec1in = K.nhwc(N, H // 4, W // 4, 512, dt, dev)
         x1 = Act(dec1in, 256, 256)
-        p3 = nh(H // 8, W // 8, 256); E[6].forward(a5, x1, training, tape, pool=p3)
+        p3 = nh(H // 8, W // 8, 256)
+        inst = {}
+        if self.inorm:
+            inst["x1"] = self._inorm_stage(E[6], a5, x1, p3, training, tape)
+        else:
+            E[6].forward(a5, x1, training, tape, pool=p3)
         a7 = nh(H // 8, W // 8, 512); E[7].forward(p3, a7, training, tape)
         a8 = nh(H // 8, W // 8, 512); E[8].forward(a7, a8, training, tape)
         dec2in = K.nhwc(N, H // 8, W // 8, 1024, dt, dev)
         x2 = Act(dec2in, 512, 512)
-        p4 = nh(H // 16, W // 16, 512); E[9].forward(a8, x2, training, tape, pool=p4)
+        p4 = nh(H // 16, W // 16, 512)
+        if self.inorm:
+            inst["x2"] = self._inorm_stage(E[9], a8, x2, p4, training, tape)
+        else:
+            E[9].forward(a8, x2, training, tape, pool=p4)
         a10 = nh(H // 16, W // 16, 512); E[10].forward(p4, a10, training, tape)
         a11 = nh(H // 16, W // 16, 512); E[11].forward(a10, a11, training, tape)
-        x3 = nh(H // 16, W // 16, 512); E[12].forward(a11, x3, training, tape)
+        x3 = nh(H // 16, W // 16, 512)
+        if self.inorm:
+            inst["x3"] = self._inorm_stage(E[12], a11, x3, None, training, tape)
+        else:
+            E[12].forward(a11, x3, training, tape)
         # decoder
         a13 = nh(H // 16, W // 16, 1024); D[0].forward(x3, a13, training, tape)
         y3 = nh(H // 16, W // 16, 512); D[1].forward(a13, y3, training, tape)
@@ -449,8 +471,31 @@ class FeaturePlan:
         a17 = nh(H // 4, W // 4, 256); D[4].forward(Act(dec1in), a17, training, tape)
         y1 = nh(H // 4, W // 4, 128); D[5].forward(a17, y1, training, tape)
         if tape is not None:
-            tape[self] = dict(dec1in=dec1in, dec2in=dec2in, shape=(N, H, W), dt=dt)
+            tape[self] = dict(dec1in=dec1in, dec2in=dec2in, shape=(N, H, W), dt=dt, inst=inst, x1=x1, x2=x2, x3=x3)
         return y1.buf, y2.buf, y3.buf, x3.buf
+
+    @staticmethod
+    def _inorm_stage(layer, x, out: Act, pool: Act | None, training, tape):
+        """layer -> raw stage output, instance-normalised into `out`, then max-pooled into
+        `pool` (the next stage's input).  Returns (raw output, IN statistics)."""
+        raw = Act(K.nhwc(out.N, out.H, out.W, out.C, out.buf.dtype, out.buf.device))
+        layer.forward(x, raw, training, tape)
+        st = K.instnorm_stats(raw)
+        K.instnorm_apply(raw, st, None, None, K.ACT_NONE, out)
+        if pool is not None:
+            K.maxpool_fwd(out, pool)
+        return raw, st
+
+    @staticmethod
+    def _inorm_stage_bwd(layer, tape, g_out: Act, out: Act, g_pool: Act | None, inst, gx: Act, gx_bn=None):
+        """Backward of _inorm_stage: g_out (the normalised output's direct gradient, written in
+        place) += maxpool backward of g_pool; IN backward; the layer's backward."""
+        raw, st = inst
+        if g_pool is not None:
+            K.maxpool_bwd(out, g_pool, g_out, accumulate=True)
+        g_raw = Act(torch.empty_like(raw.buf))
+        K.instnorm_bwd(g_out, raw, st, None, g_raw)
+        return layer.backward(tape, g_raw, gx, gx_bn=gx_bn)
 
     def backward(self, tape: dict, g_y1, g_y2, g_y3, g_x3) -> dict:
         """Gradients of (y1, y2, y3, x3) from the heads (None = unused)."""
@@ -482,24 +527,35 @@ class FeaturePlan:
         K.upsample_bwd(Act(g_dec2in, 0, 512), 2, K.UP_BILINEAR, g_y3, accumulate=True)
         g_a13 = nh(H // 16, W // 16, 1024)
         grads.update(D[1].backward(tape, g_y3, g_a13, gx_bn=D[0]))
+        inst = s["inst"]
         if g_x3 is not None:
             gx3 = Act(g_x3.to(dt).contiguous().clone())
             grads.update(D[0].backward(tape, g_a13, gx3, accumulate_gx=True))
         else:
             gx3 = nh(H // 16, W // 16, 512)
-            grads.update(D[0].backward(tape, g_a13, gx3, gx_bn=E[12]))
+            grads.update(D[0].backward(tape, g_a13, gx3, gx_bn=None if inst else E[12]))
         # enc3
-        g_a11 = nh(H // 16, W // 16, 512); grads.update(E[12].backward(tape, gx3, g_a11, gx_bn=E[11]))
+        g_a11 = nh(H // 16, W // 16, 512)
+        if inst:
+            grads.update(self._inorm_stage_bwd(E[12], tape, gx3, s["x3"], None, inst["x3"], g_a11, gx_bn=E[11]))
+        else:
+            grads.update(E[12].backward(tape, gx3, g_a11, gx_bn=E[11]))
         g_a10 = nh(H // 16, W // 16, 512); grads.update(E[11].backward(tape, g_a11, g_a10, gx_bn=E[10]))
         g_p4 = nh(H // 16, W // 16, 512); grads.update(E[10].backward(tape, g_a10, g_p4))
         # enc2 (the pooled gradients are routed inside the BN backward of the pooled layers)
         g_a8 = nh(H // 8, W // 8, 512)
-        grads.update(E[9].backward(tape, Act(g_dec2in, 512, 512), g_a8, g_pool=g_p4))
+        if inst:
+            grads.update(self._inorm_stage_bwd(E[9], tape, Act(g_dec2in, 512, 512), s["x2"], g_p4, inst["x2"], g_a8))
+        else:
+            grads.update(E[9].backward(tape, Act(g_dec2in, 512, 512), g_a8, g_pool=g_p4))
         g_a7 = nh(H // 8, W // 8, 512); grads.update(E[8].backward(tape, g_a8, g_a7, gx_bn=E[7]))
         g_p3 = nh(H // 8, W // 8, 256); grads.update(E[7].backward(tape, g_a7, g_p3))
         # enc1
         g_a5 = nh(H // 4, W // 4, 256)
-        grads.update(E[6].backward(tape, Act(g_dec1in, 256, 256), g_a5, g_pool=g_p3))
+        if inst:
+            grads.update(self._inorm_stage_bwd(E[6], tape, Act(g_dec1in, 256, 256), s["x1"], g_p3, inst["x1"], g_a5))
+        else:
+            grads.update(E[6].backward(tape, Act(g_dec1in, 256, 256), g_a5, g_pool=g_p3))
         g_a4 = nh(H // 4, W // 4, 256); grads.update(E[5].backward(tape, g_a5, g_a4, gx_bn=E[4]))
         g_p2 = nh(H // 4, W // 4, 128); grads.update(E[4].backward(tape, g_a4, g_p2))
         g_a2 = nh(H // 2, W // 2, 128); grads.update(E[3].backward(tape, None, g_a2, g_pool=g_p2, gx_bn=E[2]))
@@ -676,9 +732,12 @@ class _Heads:
         dd = model.den_dec[0]
         self.den = CatConvLayer(dd.conv, dd.bn, ACT_RELU)
         self.den_drop_module = next((m for m in model.den_dec if isinstance(m, nn.Dropout2d)), None)
-        hc = model.den_head[0].conv
+        # DGModel_*: den_head = Sequential(ConvBlock); models2.DensityRegressorM: a bare ConvBlock
+        hb = model.den_head[0] if isinstance(model.den_head, nn.Sequential) else model.den_head
+        hc = hb.conv
         self.head_w, self.head_b = hc.weight, hc.bias
-        self.head_act = K.ACT_RELU if model.den_head[0].relu is not None else K.ACT_NONE
+        self.head_act = K.ACT_RELU if hb.relu is not None else K.ACT_NONE
+        self.raw = True  # models2.DensityRegressorM.forward(raw=False): memory read under no_grad
         self.memr = MemRead(model.mem) if mem else None
         self.cls = None
         if cls:
@@ -774,7 +833,7 @@ class SinglePlan(_Heads):
         sub = {} if tape is not None else None
         yden = Act(K.nhwc(N, h, w, self.den.Cout, dt, dev))
         self.den.forward(cat, yden, training, sub, drop=drop)
-        st = {"sub": sub, "yden": yden, "cat": cat}
+        st = {"sub": sub, "yden": yden, "cat": cat, "raw": self.raw}
         y = yden
         if self.memr is not None:
             memT_s, mem_p, scale = self.memr.packs(dt, training)
@@ -810,7 +869,7 @@ class SinglePlan(_Heads):
         grads = {}
         g_d = gouts[0]
         g_x3 = None
-        if g_d is not None:
+        if g_d is not None and not (self.memr is not None and not st["raw"]):
             g_h = _up4_bwd(g_d, N, h, w)
             if self.cls is not None:
                 K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
@@ -829,6 +888,11 @@ class SinglePlan(_Heads):
             g_cat = cat_grads(g_cat)
         else:
             g_cat = (None,) * (3 if isinstance(cat, CatParts) else 1)
+            if g_d is not None:  # raw=False: only the density head sees the (constant) memory readout
+                g_h = _up4_bwd(g_d, N, h, w)
+                if self.cls is not None:
+                    K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
+                self.head_bwd(st["ynew"], st["yh"], g_h, grads)
         if self.cls is not None and len(gouts) > 1 and gouts[1] is not None:
             g_x3 = self.cls_bwd(sub, "cls", gouts[1], grads)
         return (*g_cat, g_x3), grads
@@ -839,10 +903,14 @@ class PairPlan(_Heads):
     (models/models.py:147-184, 298-335): two views, e_mask from instance norms,
     functional Dropout2d (always on), memory read, JSD-MSE consistency loss."""
 
-    def __init__(self, model, cls: bool):
+    def __init__(self, model, cls: bool, variant: str = "final"):
         super().__init__(model, mem=True, cls=cls)
+        # variant "M" = models2.DensityRegressorM.forward_train (models/models2.py:321-373): KL-JSD
+        # instead of the softmax MSE, per-view class maps (no c_err), plus loss_err =
+        # L1(IN(y1), IN(y2)); outputs (dc1, dc2, c1, c2, loss_kl, loss_err)
+        self.variant = variant
         # final: (dc1, dc2, c1, c2, c_err, loss_con); memadd: (d1, d2, loss_con)
-        self.nondiff = (4,) if cls else ()
+        self.nondiff = (4,) if (cls and variant == "final") else ()
         # parity instrumentation: a dict here receives the threshold decisions of the next
         # forward (e_mask as uint8 NHWC [N,h,w,C]; the thresholded class maps), so a checker
         # can be run on the same decisions (bench.py's full-frame final-mode parity)
@@ -887,8 +955,8 @@ class PairPlan(_Heads):
         loss_con = torch.empty((), dtype=torch.float32, device=dev)
         ws = K.query("dg_softmax_workspace", L1.M)
         work2 = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
-        K.call("dg_softmax_pair_fwd", L1.dt, L1.ptr, L2.ptr, L1.M, L1.C, P1.ptr, P2.ptr, K.ptr(loss_con),
-               K.ptr(work2), K.stream())
+        fn = "dg_softmax_jsd_fwd" if self.variant == "M" else "dg_softmax_pair_fwd"
+        K.call(fn, L1.dt, L1.ptr, L2.ptr, L1.M, L1.C, P1.ptr, P2.ptr, K.ptr(loss_con), K.ptr(work2), K.stream())
         yn1 = self.memr.readout(P1, mem_p, dt)
         yn2 = self.memr.readout(P2, mem_p, dt)
         yh1, yh2 = self.head(yn1), self.head(yn2)
@@ -896,6 +964,28 @@ class PairPlan(_Heads):
                   P2=P2, yn1=yn1, yn2=yn2, yh1=yh1, yh2=yh2, mem_p=mem_p, scale=scale)
         if self.cls is None:
             outs = (_up4(yh1, N, h, w), _up4(yh2, N, h, w), loss_con)
+        elif self.variant == "M":
+            c1 = self.cls_fwd(x3_1, training, sub, "c1")
+            c2 = self.cls_fwd(x3_2, training, sub, "c2")
+            cg = c_gt.float().contiguous() if c_gt is not None else None
+            thr = float(self.model.cls_thrs)
+            cres1 = torch.empty((N, h, w), dtype=torch.float32, device=dev)
+            cres2 = torch.empty((N, h, w), dtype=torch.float32, device=dev)
+            K.call("dg_cls_combine", K.ptr(c1), None, K.ptr(cg), N, h // 4, w // 4, 4, thr, K.ptr(cres1), None,
+                   K.stream())
+            K.call("dg_cls_combine", K.ptr(c2), None, K.ptr(cg), N, h // 4, w // 4, 4, thr, K.ptr(cres2), None,
+                   K.stream())
+            p1, p2 = torch.empty_like(yh1), torch.empty_like(yh2)
+            K.call("dg_mul_f32", K.ptr(yh1), K.ptr(cres1), yh1.numel(), K.ptr(p1), K.stream())
+            K.call("dg_mul_f32", K.ptr(yh2), K.ptr(cres2), yh2.numel(), K.ptr(p2), K.stream())
+            loss_err = torch.empty((), dtype=torch.float32, device=dev)
+            ws = K.query("dg_in_l1_workspace", N, HW, C)
+            work3 = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
+            K.call("dg_in_l1_fwd", y1.dt, y1.ptr, y2.ptr, y1.ld, N, HW, C, K.ptr(stats[0]), K.ptr(stats[1]),
+                   K.ptr(stats[2]), K.ptr(stats[3]), K.ptr(loss_err), K.ptr(work3), K.stream())
+            st.update(cres1=cres1, cres2=cres2, sub=sub, stats=stats, y1=y1, y2=y2)
+            outs = (_up4(p1, N, h, w), _up4(p2, N, h, w), c1.view(N, 1, h // 4, w // 4),
+                    c2.view(N, 1, h // 4, w // 4), loss_con, loss_err)
         else:
             c1 = self.cls_fwd(x3_1, training, sub, "c1")
             c2 = self.cls_fwd(x3_2, training, sub, "c2")
@@ -925,25 +1015,28 @@ class PairPlan(_Heads):
         N, h, w = st["cat1"].N, st["cat1"].H, st["cat1"].W
         HW = h * w
         grads = {}
+        g_err = None
         if self.cls is None:
             g_d1, g_d2, g_con = gouts
             g_c1 = g_c2 = None
+        elif self.variant == "M":
+            g_d1, g_d2, g_c1, g_c2, g_con, g_err = gouts
         else:
             g_d1, g_d2, g_c1, g_c2, _g_cerr, g_con = gouts
         dt = st["m1"].buf.dtype
         dev = st["m1"].buf.device
         C = self.den.Cout
 
-        def head_path(g_d, yh, yn):
+        def head_path(g_d, yh, yn, cres):
             if g_d is None:
                 return None
             g_h = _up4_bwd(g_d, N, h, w)
-            if self.cls is not None:
-                K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
+            if cres is not None:
+                K.call("dg_mul_f32", K.ptr(g_h), K.ptr(cres), g_h.numel(), K.ptr(g_h), K.stream())
             return self.head_bwd(yn, yh, g_h, grads)
 
-        g_yn1 = head_path(g_d1, st["yh1"], st["yn1"])
-        g_yn2 = head_path(g_d2, st["yh2"], st["yn2"])
+        g_yn1 = head_path(g_d1, st["yh1"], st["yn1"], st.get("cres1", st.get("cres")))
+        g_yn2 = head_path(g_d2, st["yh2"], st["yn2"], st.get("cres2", st.get("cres")))
         gP1 = gP2 = None
         dmem = torch.zeros((C, self.memr.mem.shape[2]), dtype=torch.float32, device=dev)
         if g_yn1 is not None:
@@ -955,7 +1048,8 @@ class PairPlan(_Heads):
         P1, P2 = st["P1"], st["P2"]
         gL1, gL2 = Act(torch.empty_like(P1.buf)), Act(torch.empty_like(P2.buf))
         coef = g_con.float().reshape(1).contiguous() if g_con is not None else None
-        K.call("dg_softmax_pair_bwd", P1.dt, P1.ptr, P2.ptr, gP1.ptr if gP1 is not None else None,
+        fn = "dg_softmax_jsd_bwd" if self.variant == "M" else "dg_softmax_pair_bwd"
+        K.call(fn, P1.dt, P1.ptr, P2.ptr, gP1.ptr if gP1 is not None else None,
                gP2.ptr if gP2 is not None else None, P1.M, P1.C, K.ptr(coef), gL1.ptr, gL2.ptr, K.stream())
         g_m1, db1 = self.memr.bwd_logits(gL1, st["m1"], st["mem_p"], st["scale"], dt)
         g_m2, db2 = self.memr.bwd_logits(gL2, st["m2"], st["mem_p"], st["scale"], dt)
@@ -965,6 +1059,14 @@ class PairPlan(_Heads):
         g_y2 = Act(K.nhwc(N, h, w, C, dt, dev))
         K.call("dg_emask_bwd", g_m1.dt, g_m1.ptr, g_m2.ptr, N, HW, C, K.ptr(st["mask"]), K.ptr(st["d1"]),
                K.ptr(st["d2"]), g_y1.ptr, g_y2.ptr, g_y1.ld, K.stream())
+        if g_err is not None:  # loss_err = L1(IN(y1), IN(y2)) back through both instance norms
+            stats, y1, y2 = st["stats"], st["y1"], st["y2"]
+            gi1, gi2 = Act(torch.empty_like(y1.buf)), Act(torch.empty_like(y2.buf))
+            ce = g_err.float().reshape(1).contiguous()
+            K.call("dg_in_l1_bwd", y1.dt, y1.ptr, y2.ptr, y1.ld, N, HW, C, K.ptr(stats[0]), K.ptr(stats[1]),
+                   K.ptr(stats[2]), K.ptr(stats[3]), K.ptr(ce), gi1.ptr, gi2.ptr, K.stream())
+            K.instnorm_bwd(gi1, y1, stats[0:2], None, g_y1, accumulate=True)
+            K.instnorm_bwd(gi2, y2, stats[2:4], None, g_y2, accumulate=True)
         g_cat1, g_cat2 = cat_empty_like(st["cat1"]), cat_empty_like(st["cat2"])
         for p, g in self.den.backward(st["s1"], g_y1, g_cat1).items():
             _acc(grads, p, g)

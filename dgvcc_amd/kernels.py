@@ -380,11 +380,19 @@ def bn_bwd_pool(gp: Act, gd: Act | None, z: Act, gamma, stats, act: int, dz: Act
 
 
 # ---------------------------------------------------------------- resample -
+def _expect(y: Act, N, H, W, C, what):
+    if (y.N, y.H, y.W, y.C) != (N, H, W, C):
+        raise DGError(f"{what}: output {(y.N, y.H, y.W, y.C)} != expected {(N, H, W, C)}")
+
+
 def maxpool_fwd(x: Act, y: Act):
+    _expect(y, x.N, x.H // 2, x.W // 2, x.C, "maxpool_fwd")
     call("dg_maxpool2_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, y.ptr, y.ld, stream())
 
 
 def maxpool_bwd(x: Act, gy: Act, gx: Act, accumulate=False):
+    _expect(gy, x.N, x.H // 2, x.W // 2, x.C, "maxpool_bwd")
+    _expect(gx, x.N, x.H, x.W, x.C, "maxpool_bwd")
     call("dg_maxpool2_bwd", x.dt, x.ptr, x.ld, gy.ptr, gy.ld, x.N, x.H, x.W, x.C, gx.ptr, gx.ld,
          int(accumulate), stream())
 
@@ -393,10 +401,12 @@ UP_BILINEAR, UP_BILINEAR_AC, UP_NEAREST = 0, 1, 2
 
 
 def upsample_fwd(x: Act, scale: int, mode: int, y: Act):
+    _expect(y, x.N, x.H * scale, x.W * scale, x.C, "upsample_fwd")
     call("dg_upsample_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, scale, mode, y.ptr, y.ld, stream())
 
 
 def upsample_bwd(gy: Act, scale: int, mode: int, gx: Act, gy2: Act | None = None, accumulate=False):
+    _expect(gy, gx.N, gx.H * scale, gx.W * scale, gx.C, "upsample_bwd")
     call("dg_upsample_bwd", gx.dt, gy.ptr, gy.ld, gy2.ptr if gy2 is not None else None,
          gy2.ld if gy2 is not None else 0, gx.N, gx.H, gx.W, gx.C, scale, mode, gx.ptr, gx.ld,
          int(accumulate), stream())

@@ -3,7 +3,12 @@ same YAML schema, the same factories (`get_model`, `get_loss`, `get_dataset`,
 `get_optimizer`, `get_scheduler`, `load_config`) and the same tasks, with the HIP
 implementations behind them:
 
-* models: DGModel_* and the ResNet counters of `dgvcc_amd.models`;
+* models: DGModel_*, models2's DensityRegressorBase ('dgnet') and the ResNet counters of
+  `dgvcc_amd.models`;
+* data parallel under torchrun (`torchrun --nproc-per-node N -m dgvcc_amd.main ...`): RCCL
+  process group, one GPU per rank, DistributedSampler over the train set, identical initial
+  weights (broadcast from rank 0), the flat-gradient all-reduce inside the fused AdamW, and
+  logs / checkpoints written by rank 0 only;
 * losses: 'mse' -> the fused HIP MSELoss, 'bl' -> the fused Bayesian loss;
 * datasets: 'den_cls' and 'jhu_domain_cls' (every shipped config's train/val/test set)
   with the pixel augmentation on the GPU; the other reference datasets ('den', 'bay',
@@ -30,13 +35,23 @@ from .utils.misc import get_seeded_generator, seed_everything, seed_worker
 
 def get_model(name, params):
     from .models import models as M
+    from .models import models2 as M2
     from .models import trunks as T
     table = {"base": M.DGModel_base, "mem": M.DGModel_mem, "memadd": M.DGModel_memadd, "cls": M.DGModel_cls,
              "memcls": M.DGModel_memcls, "final": M.DGModel_final, "sw": T.SWCounter_ResNet,
-             "ibn": T.IBNCounter_ResNet, "isw": T.ISWCounter_ResNet}
+             "ibn": T.IBNCounter_ResNet, "isw": T.ISWCounter_ResNet,
+             # main_base.py:35-37: 'dgnet' -> models2.get_basemodel() = DensityRegressorBase
+             # (pretrained=True; the config's params carry the same flag)
+             "dgnet": M2.DensityRegressorBase}
     if name not in table:
-        return None  # main.py:30-48 returns None for unknown names (e.g. 'dgnet')
+        return None  # main.py:30-48 returns None for unknown names
     return table[name](**params)
+
+
+# The 'dgnet' configs (stb_reg_base, mall_base, qnrf_final) belong to main_base.py, whose
+# BaseTrainer runs `model(img)` + the count loss whatever their `mode` says and has no
+# `patch_size` (main_base.py:111-116); here they run as DGTrainer 'simple' mode.
+_BASE_MODELS = ("dgnet",)
 
 
 def get_loss(name, params):
@@ -84,15 +99,29 @@ def load_config(config_path, task):
     """(init_params, task_params) exactly as main.py:102-136."""
     with open(config_path) as f:
         cfg = yaml.load(f, Loader=yaml.SafeLoader)
+    if cfg["model"]["name"] in _BASE_MODELS:
+        cfg = dict(cfg, mode="simple", patch_size=cfg.get("patch_size", 10000))
     init_params = {k: cfg[k] for k in ("seed", "version", "device", "log_para", "patch_size", "mode")}
     seed_everything(cfg["seed"])
+    from . import dist as D
+    if D.world() > 1:  # one process per GPU under torchrun: this rank's device
+        init_params["device"] = (f"cuda:{torch.cuda.current_device()}" if torch.cuda.is_available()
+                                 else "cpu")
     task_params = {"model": get_model(cfg["model"]["name"], cfg["model"]["params"]),
                    "checkpoint": cfg["checkpoint"]}
     generator = get_seeded_generator(cfg["seed"])
     if task in ("train", "train_test"):
         task_params["loss"] = get_loss(cfg["loss"]["name"], cfg["loss"]["params"])
         train_set, collate = get_dataset(cfg["train_dataset"]["name"], cfg["train_dataset"]["params"], "train")
-        task_params["train_dataloader"] = DataLoader(train_set, collate_fn=collate, **cfg["train_loader"],
+        loader_kw = dict(cfg["train_loader"])
+        if D.world() > 1:
+            # frames shard over ranks (SURVEY.md §8e): each rank reads its 1/world of every
+            # epoch; the config's batch size is per rank (weak scaling, as bench.py)
+            from torch.utils.data.distributed import DistributedSampler
+            loader_kw["sampler"] = DistributedSampler(train_set, num_replicas=D.world(), rank=D.rank(),
+                                                      shuffle=bool(loader_kw.pop("shuffle", False)),
+                                                      seed=cfg["seed"], drop_last=True)
+        task_params["train_dataloader"] = DataLoader(train_set, collate_fn=collate, **loader_kw,
                                                      worker_init_fn=seed_worker, generator=generator)
         val_set, _ = get_dataset(cfg["val_dataset"]["name"], cfg["val_dataset"]["params"], "val")
         task_params["val_dataloader"] = DataLoader(val_set, **cfg["val_loader"])
@@ -113,9 +142,12 @@ def main(argv=None):
     ap.add_argument("--config", type=str, default="configs/dg.yaml", help="path to config file")
     ap.add_argument("--task", type=str, default="train", choices=["train", "test", "vis", "train_test"])
     args = ap.parse_args(argv)
+    from . import dist as D
+    D.init_from_env()  # torchrun: one process per GPU, RCCL; a no-op for a single process
     init_params, task_params = load_config(args.config, args.task)
     trainer = DGTrainer(**init_params)
-    shutil.copy(args.config, trainer.log_dir)
+    if D.rank() == 0:
+        shutil.copy(args.config, trainer.log_dir)
     getattr(trainer, {"train": "train", "test": "test", "vis": "vis", "train_test": "train_and_test"}[args.task])(
         **task_params)
 

@@ -64,7 +64,10 @@ class AdamW(torch.optim.Optimizer):
         group["_m"] = group["_m"].to(dev) if "_m" in group else torch.zeros_like(flat)
         group["_v"] = group["_v"].to(dev) if "_v" in group else torch.zeros_like(flat)
         group["_g"] = torch.empty_like(flat)
-        group.setdefault("_step", 0)
+        # per-parameter step counts, as torch.optim.AdamW's per-parameter state["step"]: a
+        # parameter whose .grad is None on a step is skipped and its count does not advance
+        steps = group.get("_steps")
+        group["_steps"] = list(steps) if steps is not None and len(steps) == len(ps) else [0] * len(ps)
         group.pop("_live_cache", None)
 
     def _gather(self, group):
@@ -118,13 +121,34 @@ class AdamW(torch.optim.Optimizer):
             g = group["_g"]
             if self.allreduce:
                 average_flat_(g)
-            group["_step"] += 1
             b1, b2 = group["betas"]
             flat, m, v = group["_flat"], group["_m"], group["_v"]
-            for a, b in runs:
+            for a, b, step in self._step_runs(group, runs):
                 K.adamw_step(flat[a:b], g[a:b], m[a:b], v[a:b], group["lr"], b1, b2,
-                             group["eps"], group["weight_decay"], group["_step"])
+                             group["eps"], group["weight_decay"], step)
         return loss
+
+    @staticmethod
+    def _step_runs(group, runs):
+        """Advance the step count of every live parameter and split the live runs into
+        maximal sub-runs of equal count: one launch per (run, bias-correction step); a
+        single launch when every parameter has always had a gradient."""
+        offs, steps = group["_offs"], group["_steps"]
+        out = []
+        for a, b in runs:
+            i = offs.index(a)
+            start = i
+            while i < len(steps) and offs[i] < b:
+                steps[i] += 1
+                i += 1
+            j = start
+            while j < i:
+                k = j
+                while k + 1 < i and steps[k + 1] == steps[j]:
+                    k += 1
+                out.append((offs[j], offs[k + 1], steps[j]))
+                j = k + 1
+        return out
 
     def zero_grad(self, set_to_none: bool = True):
         super().zero_grad(set_to_none=set_to_none)

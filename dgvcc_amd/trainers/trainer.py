@@ -26,7 +26,15 @@ class Trainer:
         self.log_dir = os.path.join("logs", self.version)
         os.makedirs(self.log_dir, exist_ok=True)
 
+    @staticmethod
+    def is_main() -> bool:
+        """Rank 0 (or a single process): the one that prints, logs and writes checkpoints."""
+        from ..dist import rank
+        return rank() == 0
+
     def log(self, msg, verbose=True, **kwargs):
+        if not self.is_main():
+            return
         if verbose:
             print(msg, **kwargs)
         with open(os.path.join(self.log_dir, "log.txt"), "a") as f:
@@ -39,7 +47,13 @@ class Trainer:
             model.load_state_dict(sd, strict=False)
 
     def save_ckpt(self, model, path):
-        torch.save(model.state_dict(), path)
+        if self.is_main():
+            torch.save(model.state_dict(), path)
+
+    def _remove(self, pattern):
+        if self.is_main():
+            for f in glob(os.path.join(self.log_dir, pattern)):
+                os.remove(f)
 
     @staticmethod
     def _each(model):
@@ -69,6 +83,9 @@ class Trainer:
                     best_criterion, best_epoch):
         t0 = time.time()
         self.set_model_train(model)
+        sampler = getattr(train_dataloader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):  # DistributedSampler: a new shard order per epoch
+            sampler.set_epoch(epoch)
         train_loss = float("nan")
         for batch in easy_track(train_dataloader, description=f"Epoch {epoch}: Training..."):
             train_loss = self.train_step(model, loss, optimizer, batch, epoch)
@@ -90,14 +107,12 @@ class Trainer:
             self.log(f"{k}: {v:.4f}", end=" ")
         self.log(f"best: {best_criterion:.4f}, time: {time.time() - t0:.4f}")
 
-        for f in glob(os.path.join(self.log_dir, "last*.pth")):
-            os.remove(f)
+        self._remove("last*.pth")
         self.save_ckpt(model, os.path.join(self.log_dir, "last.pth"))
         if cur < best_criterion:
             best_criterion, best_epoch = cur, epoch
             self.log(f"Epoch {epoch}: saving best model...")
-            for f in glob(os.path.join(self.log_dir, "best*.pth")):
-                os.remove(f)
+            self._remove("best*.pth")
             self.save_ckpt(model, os.path.join(self.log_dir, f"best_{best_epoch}_{best_criterion:.4f}.pth"))
         return best_criterion, best_epoch
 
@@ -106,6 +121,9 @@ class Trainer:
         self.log(f"Start training at {get_current_datetime()}")
         self.load_ckpt(model, checkpoint)
         model = model.to(self.device) if isinstance(model, nn.Module) else [m.to(self.device) for m in model]
+        from ..dist import broadcast_module_
+        for m in self._each(model):
+            broadcast_module_(m)  # identical initial weights on every rank (no-op for one process)
         loss = loss.to(self.device)
         best_criterion, best_epoch = 1e10, -1
         for epoch in range(num_epochs):

@@ -418,6 +418,28 @@ int dg_softmax_bwd(int dtype, const void* P, const void* G, int M, int C, void* 
 int dg_cls_combine(const float* c1, const float* c2, const float* cgt, int N, int h, int w, int scale,
                    float thr, float* c_resized, float* c_err, void* stream);
 int dg_mul_f32(const float* a, const float* b, int64_t n, float* out, void* stream);
+/* models2.DensityRegressorM.forward_train (models/models2.py:326-346): the two slot
+ * softmaxes plus loss_kl = 0.5/HW (KL(p1||pm) + KL(p2||pm)) batchmean, pm = (p1+p2)/2;
+ * backward adds k (p_v (A - <p_v, A> + 1) - pm), A = log pm - (log p1 + log p2)/2,
+ * k = coef[0] / (2M), to the readout's softmax backward. */
+int dg_softmax_jsd_fwd(int dtype, const void* L1, const void* L2, int M, int C, void* P1, void* P2,
+                       float* loss_kl, void* workspace, void* stream);
+int dg_softmax_jsd_bwd(int dtype, const void* P1, const void* P2, const void* G1, const void* G2,
+                       int M, int C, const float* coef, void* GL1, void* GL2, void* stream);
+/* loss_err = F.l1_loss(IN(y1), IN(y2)) (models/models2.py:334) from the instance-norm
+ * statistics; backward writes g_IN1 = coef[0] sgn(IN1 - IN2)/(N HW C) and g_IN2 = -g_IN1
+ * (dense [N*HW][C]) for dg_instnorm_bwd. */
+int64_t dg_in_l1_workspace(int N, int HW, int C);
+int dg_in_l1_fwd(int dtype, const void* y1, const void* y2, int64_t ld, int N, int HW, int C,
+                 const float* mu1, const float* is1, const float* mu2, const float* is2, float* loss,
+                 void* workspace, void* stream);
+int dg_in_l1_bwd(int dtype, const void* y1, const void* y2, int64_t ld, int N, int HW, int C,
+                 const float* mu1, const float* is1, const float* mu2, const float* is2,
+                 const float* coef, void* g1, void* g2, void* stream);
+/* nn.Tanh of models2.Generator/Generator0 (models/models2.py:50,85): y = tanh(x);
+ * backward gx (+)= gy (1 - y^2) from the saved output. */
+int dg_tanh_fwd(const float* x, int64_t n, float* y, void* stream);
+int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx, int accumulate, void* stream);
 
 /* ---- losses ------------------------------------------------------------------
  * nn.MSELoss()(pred, gt*log_para) (trainers/dgtrainer.py:57): loss (f32 scalar

@@ -88,8 +88,19 @@ def _install_placeholders():
         class VGG16_BN_Weights:
             DEFAULT = "DEFAULT"
 
+        def vgg19(weights=None, **kw):
+            # models2.Generator/Generator0 always ask for VGG19_Weights.DEFAULT (a remote
+            # download); the fixtures overwrite every weight with seeded values, so the
+            # placeholder returns the cfg-E layout with random init whatever `weights` says.
+            return _VGG(_vgg19_features())
+
+        class VGG19_Weights:
+            DEFAULT = "DEFAULT"
+
         tvm.vgg16_bn = vgg16_bn
         tvm.VGG16_BN_Weights = VGG16_BN_Weights
+        tvm.vgg19 = vgg19
+        tvm.VGG19_Weights = VGG19_Weights
         tv.models = tvm
         tv.transforms = tvt
         tvt.functional = tvtf

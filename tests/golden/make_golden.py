@@ -109,6 +109,84 @@ def gen_train(name, model_cls, kwargs, mode, B=2, H=64, W=64):
 
 
 
+# ---------------------------------------------------------------------------
+# models/models2.py classes: outputs and parameter gradients of a fixed scalar objective
+# ---------------------------------------------------------------------------
+M2_CASES = {  # name -> (ctor kwargs, [(method, input names)])
+    "DensityRegressorBase": ({"pretrained": False}, [("forward", ("img1",))]),
+    "DensityRegressor": ({"pretrained": False}, [("forward", ("img1", "bmaps"))]),
+    "DensityRegressorBaseCls": ({"pretrained": False}, [("forward", ("img1", "bmaps"))]),
+    "DensityRegressorM": ({"pretrained": False}, [("forward", ("img1", "bmaps")),
+                                                  ("forward_train", ("img1", "img2", "bmaps"))]),
+    "Generator": ({}, [("forward", ("img1",))]),
+    "Generator0": ({}, [("forward", ("img1",))]),
+}
+
+
+def _flat_outputs(o):
+    if isinstance(o, (tuple, list)):
+        return [t for x in o for t in _flat_outputs(x)]
+    return [o] if isinstance(o, torch.Tensor) else []
+
+
+def m2_run(name, method, dtype, B=2, H=64, W=64):
+    """Run reference models2.<name>.<method> on the seeded batch with every dropout off
+    (module p = 0; forward_train's functional F.dropout2d(., 0.5) patched to identity) and
+    back-propagate sum_k <out_k, r_k> for fixed r_k.  Returns (outputs, grads, sd0)."""
+    m2 = import_ref("models.models2")
+    m2.F.dropout2d = lambda x, p=0.5, training=True, inplace=False: x
+    kw, _ = M2_CASES[name]
+    model = getattr(m2, name)(**kw)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    for mod in model.modules():
+        if isinstance(mod, torch.nn.Dropout2d):
+            mod.p = 0.0
+    model.to(dtype).train()
+    img1, img2, (pts, dmaps, bmaps) = O.synthetic_batch(B, H, W, seed=2112)
+    inp = {"img1": img1.to(dtype), "img2": img2.to(dtype), "bmaps": bmaps.to(dtype)}
+    args = [inp[a] for a in dict(M2_CASES[name][1])[method]]
+    outs = _flat_outputs(getattr(model, method)(*args))
+    g = torch.Generator().manual_seed(99)
+    obj = 0
+    for o in outs:
+        r = torch.randn(o.shape, generator=g, dtype=torch.float64).to(dtype)
+        obj = obj + (o * r).sum()
+    obj.backward()
+    grads = {k: (p.grad if p.grad is not None else torch.zeros_like(p)) for k, p in model.named_parameters()}
+    return outs, grads, sd0
+
+
+def gen_models2():
+    """models2 fixtures: the float64 run is the exact math; the fp32 run measures the
+    reference's own fp32 error, which sets the test tolerance."""
+    for name, (_, methods) in M2_CASES.items():
+        out = {}
+        for method, _ in methods:
+            o64, g64, _ = m2_run(name, method, torch.float64)
+            o32, g32, _ = m2_run(name, method, torch.float32)
+            for i, (a, b) in enumerate(zip(o64, o32)):
+                out[f"{method}__out{i}"] = a.detach().numpy()
+                err = (b.double() - a).abs().max().item() / max(a.abs().max().item(), 1e-30)
+                out[f"{method}__out{i}__ref32_err"] = np.array([err])
+            num = sum(float((g32[k].double() - g64[k]).norm() ** 2) for k in g64)
+            den = sum(float(g64[k].norm() ** 2) for k in g64)
+            out[f"{method}__grad_ref32_err"] = np.array([(num / max(den, 1e-300)) ** 0.5])
+            summarize(f"{method}__grad__", {k: v.double() for k, v in g64.items()}, out)
+            out[f"{method}__gradnorm"] = np.array([den ** 0.5])
+        np.savez_compressed(os.path.join(HERE, f"models2_{name}.npz"), **out)
+        print(name, {k: float(v[0]) for k, v in out.items() if "ref32" in k})
+
+
+def gen_models2_keys():
+    import json
+    m2 = import_ref("models.models2")
+    out = {}
+    for name, (kw, _) in M2_CASES.items():
+        out[name] = [[k, list(v.shape)] for k, v in getattr(m2, name)(**kw).state_dict().items()]
+    json.dump(out, open(os.path.join(HERE, "models2_state_dict_keys.json"), "w"))
+
+
 def gen_state_dict_keys():
     """Key order + shapes of every DGModel_* state_dict (checkpoint interchange)."""
     import json
@@ -333,6 +411,10 @@ if __name__ == "__main__":
     for kind in ("ibn", "sw", "isw"):
         if "trunk_" + kind in which:
             gen_trunk(kind, dtype=torch.float64 if kind == "sw" else torch.float32)
+    if "models2" in which:
+        gen_models2()
+    if "models2_keys" in which:
+        gen_models2_keys()
     if "trunk_keys" in which:
         gen_trunk_keys()
     print("fixtures written to", HERE)

@@ -111,7 +111,9 @@ def test_load_config_builds_the_reference_objects(tmp_path):
     assert "test_dataloader" not in task_t
     _, task_e = Mn.load_config(str(cfg), "test")
     assert "optimizer" not in task_e and "test_dataloader" in task_e
-    assert Mn.get_model("dgnet", {}) is None  # as main.py's get_model
+    assert Mn.get_model("csrnet", {}) is None  # as main.py's get_model for unknown names
+    # 'dgnet' (stb_reg_base / mall_base / qnrf_final) is main_base.py's get_basemodel()
+    assert type(Mn.get_model("dgnet", {"pretrained": False})).__name__ == "DensityRegressorBase"
     with pytest.raises(NotImplementedError):
         Mn.get_dataset("bay", {}, "train")
     with pytest.raises(ValueError):

@@ -94,6 +94,33 @@ def test_fused_adamw_onecycle_matches_torch(dev):
     assert o1.param_groups[0]["betas"] == o2.param_groups[0]["betas"]
 
 
+def test_fused_adamw_late_gradient_matches_torch(dev):
+    """A parameter whose .grad is None on the first steps: torch skips it and does not advance
+    its step count, so its first update uses bias correction step 1 (per-parameter counts in
+    the fused optimizer; a middle parameter splits the flat update into runs)."""
+    from dgvcc_amd.optim import AdamW
+
+    def build(cls):
+        torch.manual_seed(0)
+        m = nn.Sequential(nn.Conv2d(3, 8, 3), nn.Conv2d(8, 8, 1), nn.Conv2d(8, 4, 1)).to(dev)
+        return m, cls(m.parameters(), lr=1e-2, weight_decay=1e-2)
+
+    m1, o1 = build(lambda p, **a: AdamW(p, allreduce=False, **a))
+    m2, o2 = build(torch.optim.AdamW)
+    g = torch.Generator().manual_seed(3)
+    for step in range(6):
+        grads = [torch.randn(p.shape, generator=g) for p in m1.parameters()]
+        for m, o in ((m1, o1), (m2, o2)):
+            o.zero_grad()
+            for i, (p, gr) in enumerate(zip(m.parameters(), grads)):
+                late = i in (2, 3) and step < 3   # conv #2 (weight, bias) joins at step 3
+                p.grad = None if late else gr.to(dev)
+            o.step()
+    torch.cuda.synchronize()
+    for p, q in zip(m1.parameters(), m2.parameters()):
+        assert ((p - q).abs().max() / q.abs().max()).item() < 1e-6
+
+
 def test_eval_weight_memo_follows_updates(dev):
     """Evaluation reuses packed filters / BN scale-shift across frames; they must follow a
     fused optimizer step (which writes parameters behind torch's version counters), a

@@ -467,3 +467,94 @@ def test_tap3_persistent_matches(dev, monkeypatch, N, H, W, acc):
     assert relerr(outs[1][0], ref) < 1e-2
     refd = F.conv_transpose2d(gy.double().permute(0, 3, 1, 2), w.double(), padding=1).permute(0, 2, 3, 1)
     assert relerr(outs[1][4], refd) < 1e-2
+
+
+# ---------------------------------------------------------------------------
+# models2.DensityRegressorM pieces: KL-JSD of the slot posteriors, L1 of the instance norms,
+# tanh (Generator heads) — against float64 torch autograd of the reference's formulas
+# (models/models2.py:326-346, :334, :50)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("C", [1024, 512])
+def test_softmax_jsd_matches_reference_formula(dev, C):
+    import torch.nn.functional as F
+    from dgvcc_amd import kernels as K
+    B, HW = 2, 96
+    g = torch.Generator().manual_seed(4)
+    l1 = torch.randn(B * HW, C, generator=g) * 2
+    l2 = l1 + 0.3 * torch.randn(B * HW, C, generator=g)
+    gp1 = torch.randn(B * HW, C, generator=g) * 1e-3
+    coef = 1.7
+    # reference: logits [B, C, HW], softmax / log_softmax over the slot dim
+    a = l1.double().view(B, HW, C).permute(0, 2, 1).requires_grad_(True)
+    b = l2.double().view(B, HW, C).permute(0, 2, 1).requires_grad_(True)
+    p1, p2 = F.softmax(a, 1), F.softmax(b, 1)
+    pm = (p1 + p2) / 2
+    loss = 0.5 / HW * (F.kl_div(F.log_softmax(a, 1), pm, reduction="batchmean")
+                       + F.kl_div(F.log_softmax(b, 1), pm, reduction="batchmean"))
+    (coef * loss + (p1 * gp1.double().view(B, HW, C).permute(0, 2, 1)).sum()).backward()
+    P1 = torch.empty(B * HW, C, device=dev)
+    P2 = torch.empty_like(P1)
+    lk = torch.empty((), device=dev)
+    ws = K.query("dg_softmax_workspace", B * HW)
+    work = torch.empty(ws // 4 + 1, device=dev)
+    L1, L2 = l1.to(dev), l2.to(dev)
+    K.call("dg_softmax_jsd_fwd", 0, K.ptr(L1), K.ptr(L2), B * HW, C, K.ptr(P1), K.ptr(P2), K.ptr(lk), K.ptr(work),
+           K.stream())
+    G1 = gp1.to(dev)
+    GL1, GL2 = torch.empty_like(P1), torch.empty_like(P1)
+    cf = torch.tensor([coef], device=dev)
+    K.call("dg_softmax_jsd_bwd", 0, K.ptr(P1), K.ptr(P2), K.ptr(G1), None, B * HW, C, K.ptr(cf), K.ptr(GL1),
+           K.ptr(GL2), K.stream())
+    torch.cuda.synchronize()
+    assert abs(lk.item() - loss.item()) <= 1e-5 * abs(loss.item()), (lk.item(), loss.item())
+    assert relerr(P1, p1.detach().permute(0, 2, 1).reshape(B * HW, C)) < 1e-5
+    ga = a.grad.permute(0, 2, 1).reshape(B * HW, C)
+    gb = b.grad.permute(0, 2, 1).reshape(B * HW, C)
+    assert ((GL1.double().cpu() - ga).norm() / ga.norm()).item() < 1e-4
+    assert ((GL2.double().cpu() - gb).norm() / gb.norm()).item() < 1e-4
+
+
+def test_instance_norm_l1_loss_and_grad(dev):
+    import torch.nn.functional as F
+    from dgvcc_amd import kernels as K
+    N, H, W, C = 2, 6, 5, 32
+    g = torch.Generator().manual_seed(8)
+    y1 = torch.randn(N, H, W, C, generator=g) * 1.5 + 0.3
+    y2 = y1 + 0.4 * torch.randn(N, H, W, C, generator=g)
+    a = y1.double().permute(0, 3, 1, 2).requires_grad_(True)
+    b = y2.double().permute(0, 3, 1, 2).requires_grad_(True)
+    loss = F.l1_loss(F.instance_norm(a, eps=1e-5), F.instance_norm(b, eps=1e-5))
+    (0.7 * loss).backward()
+    Y1, Y2 = K.Act(y1.to(dev)), K.Act(y2.to(dev))
+    s1, s2 = K.instnorm_stats(Y1), K.instnorm_stats(Y2)
+    out = torch.empty((), device=dev)
+    ws = K.query("dg_in_l1_workspace", N, H * W, C)
+    work = torch.empty(ws // 4 + 1, device=dev)
+    K.call("dg_in_l1_fwd", 0, Y1.ptr, Y2.ptr, C, N, H * W, C, K.ptr(s1[0]), K.ptr(s1[1]), K.ptr(s2[0]),
+           K.ptr(s2[1]), K.ptr(out), K.ptr(work), K.stream())
+    gi1, gi2 = K.Act(torch.empty_like(Y1.buf)), K.Act(torch.empty_like(Y2.buf))
+    cf = torch.tensor([0.7], device=dev)
+    K.call("dg_in_l1_bwd", 0, Y1.ptr, Y2.ptr, C, N, H * W, C, K.ptr(s1[0]), K.ptr(s1[1]), K.ptr(s2[0]),
+           K.ptr(s2[1]), K.ptr(cf), gi1.ptr, gi2.ptr, K.stream())
+    g1, g2 = K.Act(torch.empty_like(Y1.buf)), K.Act(torch.empty_like(Y2.buf))
+    K.instnorm_bwd(gi1, Y1, s1, None, g1)
+    K.instnorm_bwd(gi2, Y2, s2, None, g2)
+    torch.cuda.synchronize()
+    assert abs(out.item() - loss.item()) <= 1e-5 * loss.item()
+    assert relerr(g1.buf, a.grad.permute(0, 2, 3, 1)) < 1e-4
+    assert relerr(g2.buf, b.grad.permute(0, 2, 3, 1)) < 1e-4
+
+
+def test_tanh_fwd_bwd(dev):
+    from dgvcc_amd import kernels as K
+    x = torch.randn(3, 1000, generator=torch.Generator().manual_seed(2)) * 3
+    gy = torch.randn(3, 1000, generator=torch.Generator().manual_seed(3))
+    X, GY = x.to(dev), gy.to(dev)
+    Y, GX = torch.empty_like(X), torch.empty_like(X)
+    K.call("dg_tanh_fwd", K.ptr(X), X.numel(), K.ptr(Y), K.stream())
+    K.call("dg_tanh_bwd", K.ptr(Y), K.ptr(GY), X.numel(), K.ptr(GX), 0, K.stream())
+    torch.cuda.synchronize()
+    xd = x.double().requires_grad_(True)
+    torch.tanh(xd).backward(gy.double())
+    assert relerr(Y, torch.tanh(x.double())) < 1e-6
+    assert relerr(GX, xd.grad) < 1e-5
