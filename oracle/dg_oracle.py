@@ -5,7 +5,9 @@ leg as the checker.  Never imported by the product package (dgvcc_amd).
 Functional torch-CPU code over a state_dict (same keys as the reference):
   base_forward      models/models.py:64-96  (DGModel_base.forward_fe/forward)
   final_forward     models/models.py:298-335 (DGModel_final.forward_train)
-  train_step        trainers/dgtrainer.py:143-192 (modes simple/base/final)
+  single_forward    models/models.py:89-273 (DGModel_base/mem/cls/memcls .forward)
+  memadd_forward_train models/models.py:159-184
+  train_step        trainers/dgtrainer.py:143-192 (modes simple/base/add/cls/final)
   AdamW             torch.optim.AdamW (main.py:85-86)
 Pinned against fixtures produced by running the reference itself
 (tests/golden/make_golden.py -> tests/golden/*.npz).
@@ -167,6 +169,36 @@ def final_forward(sd, img1, img2, c_gt, training=True, err_thrs=0.5, cls_thrs=0.
     return dc1, dc2, c1, c2, _up(c_err, 4), loss_con, e_mask
 
 
+def single_forward(sd, x, training, c_gt=None, cls_thrs=0.5):
+    """`.forward` of DGModel_base / mem / cls / memcls (models/models.py:89-96, 127-136,
+    208-228, 262-273), chosen by the state_dict's keys (a 'mem' entry, cls_head.* entries)."""
+    y_cat, x3 = forward_fe(sd, x, training)
+    y = _conv_bn_relu(y_cat, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
+    if "mem" in sd:
+        y, _ = forward_mem(sd, y)
+    d = F.relu(F.conv2d(y, sd["den_head.0.conv.weight"], sd.get("den_head.0.conv.bias")))
+    if "cls_head.0.conv.weight" not in sd:
+        return _up(d, 4)
+    c = cls_head(sd, x3, training)
+    c_resized = _up(c_gt, 4, "nearest") if c_gt is not None else cls_pred_map(c, cls_thrs)
+    return _up(d * c_resized, 4), c
+
+
+def memadd_forward_train(sd, img1, img2, training=True, err_thrs=0.5):
+    """DGModel_memadd.forward_train (models/models.py:159-184) with dropout p = 0."""
+    y_cat1, _ = forward_fe(sd, img1, training)
+    y_cat2, _ = forward_fe(sd, img2, training)
+    y_den1 = _conv_bn_relu(y_cat1, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
+    y_den2 = _conv_bn_relu(y_cat2, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
+    e_mask = (torch.abs(F.instance_norm(y_den1, eps=1e-5) - F.instance_norm(y_den2, eps=1e-5)) < err_thrs).detach()
+    y_new1, logits1 = forward_mem(sd, y_den1 * e_mask)
+    y_new2, logits2 = forward_mem(sd, y_den2 * e_mask)
+    loss_con = F.mse_loss(F.softmax(logits1, dim=1), F.softmax(logits2, dim=1))
+    d1 = _up(F.relu(F.conv2d(y_new1, sd["den_head.0.conv.weight"])), 4)
+    d2 = _up(F.relu(F.conv2d(y_new2, sd["den_head.0.conv.weight"])), 4)
+    return d1, d2, loss_con
+
+
 def trainable_keys(sd):
     return [k for k in sd if not (k.endswith("running_mean") or k.endswith("running_var")
                                  or k.endswith("num_batches_tracked"))]
@@ -185,11 +217,21 @@ def train_step(sd, batch, mode="simple", log_para=1000.0, lr=1e-4, weight_decay=
         d1 = base_forward(sd, imgs1, True)
         loss = F.mse_loss(d1, gt)
         outs = (d1,)
-    elif mode == "base":
-        d1 = base_forward(sd, imgs1, True)
-        d2 = base_forward(sd, imgs2, True)
+    elif mode == "base":  # DGModel_base / DGModel_mem (configs/ablation/*_base.yml, *_mem.yml)
+        d1 = single_forward(sd, imgs1, True)
+        d2 = single_forward(sd, imgs2, True)
         loss = F.mse_loss(d1, gt) + F.mse_loss(d2, gt)
         outs = (d1, d2)
+    elif mode == "add":  # DGModel_memadd (trainers/dgtrainer.py:166-173)
+        d1, d2, loss_con = memadd_forward_train(sd, imgs1, imgs2)
+        loss = F.mse_loss(d1, gt) + F.mse_loss(d2, gt) + loss_con
+        outs = (d1, d2, loss_con)
+    elif mode == "cls":  # DGModel_cls / DGModel_memcls (trainers/dgtrainer.py:175-183)
+        d1, c1 = single_forward(sd, imgs1, True, c_gt=bmaps)
+        d2, c2 = single_forward(sd, imgs2, True, c_gt=bmaps)
+        loss = (F.mse_loss(d1, gt) + F.mse_loss(d2, gt)
+                + 10 * (F.binary_cross_entropy(c1, bmaps) + F.binary_cross_entropy(c2, bmaps)))
+        outs = (d1, d2, c1, c2)
     elif mode == "final":
         dc1, dc2, c1, c2, c_err, loss_con, _ = final_forward(sd, imgs1, imgs2, bmaps)
         loss_den = F.mse_loss(dc1, gt) + F.mse_loss(dc2, gt)

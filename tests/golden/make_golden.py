@@ -97,6 +97,13 @@ def gen_train(name, model_cls, kwargs, mode, B=2, H=64, W=64):
     with torch.no_grad():
         if mode in ("simple", "base"):
             out["out_d1"] = model(imgs1).numpy()
+        elif mode == "add":
+            d1, d2, loss_con = model.forward_train(imgs1, imgs2)
+            out["out_d1"], out["out_d2"] = d1.numpy(), d2.numpy()
+            out["out_loss_con"] = np.array([loss_con.item()])
+        elif mode == "cls":
+            d1, c1 = model(imgs1, bmaps)
+            out["out_d1"], out["out_c1"] = d1.numpy(), c1.numpy()
         else:
             dc1, dc2, c1, c2, c_err, loss_con, _ = model.forward_train(imgs1, imgs2, bmaps)
             out["out_dc1"] = dc1.numpy()
@@ -398,6 +405,16 @@ if __name__ == "__main__":
         gen_train("simple_base", "DGModel_base", {"den_dropout": 0.0}, "simple")
     if "final" in which:
         gen_train("final", "DGModel_final", {"den_dropout": 0.0, "cls_dropout": 0.0}, "final")
+    # DGTrainer modes of the ablation configs (configs/ablation/*: base/mem -> 'base',
+    # memadd -> 'add', cls/memcls -> 'cls'); every dropout off
+    for key, cls_name, kw, mode in [("base_base", "DGModel_base", {"den_dropout": 0.0}, "base"),
+                                    ("mem_base", "DGModel_mem", {"den_dropout": 0.0}, "base"),
+                                    ("memadd_add", "DGModel_memadd", {"den_dropout": 0.0}, "add"),
+                                    ("cls_cls", "DGModel_cls", {"den_dropout": 0.0, "cls_dropout": 0.0}, "cls"),
+                                    ("memcls_cls", "DGModel_memcls", {"den_dropout": 0.0, "cls_dropout": 0.0},
+                                     "cls")]:
+        if "modes" in which or key in which:
+            gen_train(key, cls_name, kw, mode)
     if "bl" in which:
         gen_bl()
     if "keys" in which:

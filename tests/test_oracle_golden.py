@@ -43,23 +43,38 @@ def test_dmap_oracle_bit_exact():
         assert np.array_equal(mine, g[f"{name}__dmap"]), name
 
 
-@pytest.mark.parametrize("name,mode", [("simple_base", "simple"), ("final", "final")])
-def test_train_step_oracle(name, mode):
+MODE_CASES = [("simple_base", "simple", "DGModel_base"), ("final", "final", "DGModel_final"),
+              ("base_base", "base", "DGModel_base"), ("mem_base", "base", "DGModel_mem"),
+              ("memadd_add", "add", "DGModel_memadd"), ("cls_cls", "cls", "DGModel_cls"),
+              ("memcls_cls", "cls", "DGModel_memcls")]
+
+
+def state_template(cls_name):
+    """The reference's state_dict key order and shapes (tests/golden/state_dict_keys.json)."""
+    import json
+    keys = json.load(open(os.path.join(GOLD, "state_dict_keys.json")))[cls_name]
+    return {k: (torch.zeros(s, dtype=torch.int64) if k.endswith("num_batches_tracked") else torch.zeros(s))
+            for k, s in keys}
+
+
+@pytest.mark.parametrize("name,mode,cls_name", MODE_CASES)
+def test_train_step_oracle(name, mode, cls_name):
     g = load(f"train_{name}.npz")
     B, H, W = (int(v) for v in g["shape"])
-    if mode == "simple":
-        from dgvcc_amd.models.models import DGModel_base as M
-        model = M(pretrained=False, den_dropout=0.0)
-    else:
-        from dgvcc_amd.models.models import DGModel_final as M
-        model = M(pretrained=False, den_dropout=0.0, cls_dropout=0.0)
-    sd0 = O.seeded_state_dict(model.state_dict())
+    sd0 = O.seeded_state_dict(state_template(cls_name))
     batch = O.synthetic_batch(B, H, W, seed=2112)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     loss, outs, grads, sd1 = O.train_step(sd0, batch, mode)
     assert abs(loss.item() - g["loss"][0]) <= 1e-5 * abs(g["loss"][0])
-    if mode == "simple":
+    if mode in ("simple", "base"):
         assert np.allclose(outs[0].numpy(), g["out_d1"], rtol=1e-5, atol=1e-6)
+    elif mode == "add":
+        assert np.allclose(outs[0].numpy(), g["out_d1"], rtol=1e-5, atol=1e-6)
+        assert np.allclose(outs[1].numpy(), g["out_d2"], rtol=1e-5, atol=1e-6)
+        assert abs(outs[2].item() - g["out_loss_con"][0]) <= 1e-5 * abs(g["out_loss_con"][0])
+    elif mode == "cls":
+        assert np.allclose(outs[0].numpy(), g["out_d1"], rtol=1e-5, atol=1e-6)
+        assert np.allclose(outs[2].numpy(), g["out_c1"], rtol=1e-5, atol=1e-6)
     else:
         assert np.allclose(outs[0].numpy(), g["out_dc1"], rtol=1e-5, atol=1e-5)
         assert np.allclose(outs[2].numpy(), g["out_c1"], rtol=1e-5, atol=1e-6)

@@ -151,25 +151,50 @@ def test_isw_covstat_and_train_fp32(dev):
 
 
 def test_isw_trainer_step(dev):
-    """DGTrainer mode 'isw' (dgtrainer.py:194-204): epoch > 5 adds 0.6 x the whitening loss."""
+    """DGTrainer mode 'isw' (dgtrainer.py:194-204) against the oracle: at epoch 0 the step's
+    loss is the counter's MSE alone, at epoch > 5 it adds 0.6 x the whitening loss
+    (apply_wtloss); the returned loss values match the float64 oracle on the same masks,
+    and the AdamW step leaves the torch-AdamW update of the oracle's gradients."""
     from dgvcc_amd.trainers.dgtrainer import DGTrainer
     model, sd0, batch = _setup("isw", dev)
-    img1, img2, _ = batch
+    img1, img2, (_, dmaps, _) = batch
     model.eval()
     with torch.no_grad():
         model([img1.to(dev), img2.to(dev)], cal_covstat=True)
-    with tempfile.TemporaryDirectory() as td:
-        cwd = os.getcwd()
-        os.chdir(td)
-        try:
-            tr = DGTrainer(2112, "t", dev, 1000, 10000, "isw")
-            opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
-            model.train()
-            l0 = tr.train_step(model, torch.nn.MSELoss(), opt, batch, 0)
-            l6 = tr.train_step(model, torch.nn.MSELoss(), opt, batch, 6)
-        finally:
-            os.chdir(cwd)
-    assert l0 > 0 and l6 > 0 and torch.isfinite(torch.tensor([l0, l6])).all()
+    model.set_mask_matrix()
+    masks = _masks_from_model(model)
+    out64, (l64, wt64), g64 = _oracle("isw", sd0, img1, dmaps, torch.float64, masks)
+    _, (l32, wt32), _ = _oracle("isw", sd0, img1, dmaps, torch.float32, masks)
+    tol_l = max(3 * abs(l32.item() - l64.item()), 1e-4 * l64.item())
+    tol_w = max(3 * abs(wt32.item() - wt64.item()), 1e-4 * wt64.item())
+    losses = {}
+    for epoch in (0, 6):
+        model.load_state_dict(sd0)
+        with tempfile.TemporaryDirectory() as td:
+            cwd = os.getcwd()
+            os.chdir(td)
+            try:
+                tr = DGTrainer(2112, "t", dev, 1000, 10000, "isw")
+                opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+                model.train()
+                losses[epoch] = tr.train_step(model, torch.nn.MSELoss(), opt, batch, epoch)
+            finally:
+                os.chdir(cwd)
+    assert abs(losses[0] - l64.item()) <= tol_l, (losses[0], l64.item())
+    assert abs(losses[6] - (l64.item() + 0.6 * wt64.item())) <= tol_l + 0.6 * tol_w, (losses[6], l64, wt64)
+    # the epoch-6 step's update: AdamW step 1 moves each live parameter by ~lr * sign(g)
+    # (|m/sqrt(v)| = 1 at step 1), so the post-step parameters pin the gradient signs
+    sd = model.state_dict()
+    n_ok = n_all = moved = 0
+    for k, g in g64.items():
+        if g.abs().max() == 0 or k not in sd:
+            continue
+        delta = (sd[k].double().cpu() - sd0[k].double() * (1 - 1e-4 * 1e-4))
+        big = g.abs() > 1e-2 * g.abs().max()  # fp32-noise-level gradients may flip sign
+        n_ok += int((torch.sign(delta[big]) == -torch.sign(g[big])).sum())
+        n_all += int(big.sum())
+        moved += 1
+    assert moved > 100 and n_ok >= 0.995 * n_all, (moved, n_ok, n_all)
 
 
 @pytest.mark.parametrize("kind", ["ibn", "sw", "isw"])
