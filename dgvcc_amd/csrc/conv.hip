@@ -1699,6 +1699,17 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
       (void*)(a.x + (long long)xlo * a.ldx * sizeof(T)), 0, x_bytes, 0x00020000);
 
   u4v ra[AR], rb[BR];
+  // (n, p, q) of each X row's output pixel, advanced by BKP per K-step: the per-step integer
+  // divisions (3 per row) had made non-MFMA VALU instructions 2x the MFMA count (PMC)
+  int cn[BR], cp[BR], cq[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int px = kbeg + (tid + NT * i) / CPRB;
+    cn[i] = px / PQ;
+    const int rem = px - cn[i] * PQ;
+    cp[i] = rem / a.Q;
+    cq[i] = rem - cp[i] * a.Q;
+  }
   auto gload = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
@@ -1714,12 +1725,16 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
       const int idx = tid + NT * i;
       const int row = idx / CPRB, ch = idx % CPRB;
       const int px = k0 + row;
-      const int rem = px % PQ;
-      const int h = (rem / a.Q) * a.stride + dh, ww = (rem % a.Q) * a.stride + dw;
+      const int h = cp[i] * a.stride + dh, ww = cq[i] * a.stride + dw;
       const bool ok = px < kend && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-      const long long pin = (long long)(px / PQ) * HW + (long long)h * a.W + ww - xlo;
+      const long long pin = (long long)cn[i] * HW + (long long)h * a.W + ww - xlo;
       const unsigned off = ok ? (unsigned)((pin * a.ldx + c0 + ch * EPC) * (long long)sizeof(T)) : 0xFFFFFFF0u;
       rb[i] = bload(xr, off);
+      cq[i] += BKP;  // next K-step's pixel
+      while (cq[i] >= a.Q) {
+        cq[i] -= a.Q;
+        if (++cp[i] == a.P) { cp[i] = 0; ++cn[i]; }
+      }
     }
   };
   auto swrite = [&](int buf) __attribute__((always_inline)) {
@@ -2328,9 +2343,21 @@ WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S, long long ldx
   const int bco = (Cout % 128 == 0) ? 128 : 64;
   const int bc = (C % 128 == 0) ? 128 : 64;
   const long long tiles = (long long)(Cout / bco) * (C / bc) * R * S;
-  long long splits = (1024 + tiles - 1) / tiles;
   const long long max_split = (M + BKP * 4 - 1) / (BKP * 4);  // >= 4 K-tiles per block
-  if (splits > max_split) splits = max_split;
+  // Whole rounds of resident blocks (conv_wgrad_kernel: 2 per CU, 256 CUs): the blocks of a
+  // split plan all run the same K length, so a grid of 2.04 rounds (the old "about 1024
+  // blocks" plan: 36 tiles x 29 splits = 1044 on 512 slots) costs 3 rounds: 62% MFMA-busy
+  // on the f32 layers.  Pick the fewest rounds whose last round is >= 96% full.
+  const long long slots = 512;
+  long long splits = 1;
+  double best_eff = -1.0;
+  for (int rounds = 1; rounds <= 32; ++rounds) {
+    long long sp = std::max(1ll, std::min(slots * rounds / tiles, max_split));
+    const long long blocks = tiles * sp;
+    const double eff = (double)blocks / (double)(slots * ((blocks + slots - 1) / slots));
+    if (eff > best_eff + 1e-9) { best_eff = eff; splits = sp; }
+    if (eff >= 0.96 || sp == max_split) break;
+  }
   if (splits < 1) splits = 1;
   long long pps = (M + splits - 1) / splits;
   pps = (pps + BKP - 1) / BKP * BKP;

@@ -8,7 +8,7 @@ from dgvcc_amd import kernels as K
 
 H, W, C, Cout, R, B = (int(v) for v in sys.argv[1:7])
 kinds = sys.argv[7] if len(sys.argv) > 7 else "fwd,wgrad"
-dt = torch.bfloat16
+dt = torch.float32 if os.environ.get("DGVCC_PROF_DT", "bf16") == "f32" else torch.bfloat16
 dev = "cuda"
 x = K.Act(torch.randn(B, H, W, C, device=dev).to(dt))
 gy = K.Act(torch.randn(B, H, W, Cout, device=dev).to(dt))
