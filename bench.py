@@ -50,6 +50,14 @@ CONFIG_FILES = {"final": "configs/sta_final.yml", "simple": "configs/stb_reg_bas
                 "base": "configs/ablation (mode base)"}
 
 
+def config_file(args):
+    if args.model == "DensityRegressorBase" and args.height >= 2048:
+        return "configs/qnrf_final.yml (dgnet, 2048-px crops)"
+    if args.model == "DensityRegressorBase":
+        return "configs/stb_reg_base.yml (dgnet)"
+    return CONFIG_FILES.get(args.mode, "")
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,6 +213,8 @@ FWD_KERNEL_NAMES = {
     "fp32": "conv_fwd_kernel<float> (implicit-GEMM conv on v_mfma_f32_16x16x4_f32: forward + dgrad launches)",
     "bf16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
             "(implicit-GEMM conv on v_mfma_f32_16x16x32_bf16: forward + dgrad launches)",
+    "fp16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
+            "(implicit-GEMM conv on v_mfma_f32_16x16x32_f16: forward + dgrad launches)",
 }
 
 
@@ -314,6 +324,34 @@ def roofline(args, precision, r):
             out["encoder_gemm_frac"] = round(r["enc_gemm_flops"] / (r["enc_gemm_ms"] * 1e-3) / 1e12 / peak, 4)
     if enc_tot is not None:
         out["encoder_tflop_per_step_algorithmic"] = round(enc_tot / 1e12, 4)
+    return out
+
+
+def dmap_roofline(args, dev, reps=20):
+    """The Gaussian density-map scatter (utils/dmap_gen.py:53-81) for one batch of the
+    workload's synthetic frames: algorithmic bytes 4*H*W (the map, written once) + 8*N (the
+    points) per frame over the launch time, HIP events on the launch stream."""
+    from dgvcc_amd.utils.dmap_gen import gaussian_filter_density_fixed_batch
+    B, H, W = args.batch, args.height, args.width
+    g = torch.Generator(device="cpu").manual_seed(1000)
+    n = torch.poisson(torch.full((B,), 500.0 * H * W / (H0 * W0)), generator=g).long().clamp_min(1)
+    pts = [(torch.rand(int(k), 2, generator=g) * torch.tensor([W, H], dtype=torch.float32)).to(dev) for k in n]
+    nbytes = 4.0 * B * H * W + 8.0 * int(n.sum())
+    out = {"bound": "hbm", "peak": 8000.0, "unit": "GB/s", "frames": B, "points": int(n.sum()),
+           "algorithmic_bytes_per_launch": nbytes}
+    for det in (True, False):
+        gaussian_filter_density_fixed_batch(pts, H, W, deterministic=det)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            gaussian_filter_density_fixed_batch(pts, H, W, deterministic=det)
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) * 1e3 / reps
+        key = "deterministic" if det else "atomic"
+        out[key] = {"us_per_launch": round(us, 2), "achieved": round(nbytes / (us * 1e-6) / 1e9, 1),
+                    "frac": round(nbytes / (us * 1e-6) / 1e9 / 8000.0, 4)}
+    out["kernel"] = "dmap_fixed_tiled_kernel (default, bit-identical to the reference) / dmap_fixed_kernel (atomics)"
     return out
 
 
@@ -448,7 +486,7 @@ def main():
     value = r["frames"] / r["elapsed"]
     workload = (f"{r['model']} {r['mode']}-mode DGTrainer.train_step (configs/baselines/sta_{args.trunk}.yml)"
                 if args.trunk else
-                f"{r['model']} {r['mode']}-mode DGTrainer.train_step ({CONFIG_FILES.get(args.mode, '')}: "
+                f"{r['model']} {r['mode']}-mode DGTrainer.train_step ({config_file(args)}: "
                 + ("two views, MSE x log_para 1000 + 10 BCE(class maps) + 10 JSD-MSE, AdamW"
                    if r["mode"] == "final" else "MSE x log_para 1000, AdamW") + ")")
     out = {
@@ -483,6 +521,8 @@ def main():
                             "last_loss": rb["last_loss"], "roofline": roofline(args, "bf16", rb)}
         if "params_in_sync" in rb:
             out["perf_bf16"]["params_in_sync"] = rb["params_in_sync"]
+    if rank == 0 and not args.trunk:
+        out["dmap"] = dmap_roofline(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.trunk:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:

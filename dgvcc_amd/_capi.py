@@ -20,7 +20,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(os.path.dirname(_PKG), "include", "dgvcc.h")
 LIB_PATH = os.path.join(_PKG, "lib", "libdgvcc_hip.so")
 
-DG_F32, DG_BF16 = 0, 1
+DG_F32, DG_BF16, DG_F16 = 0, 1, 2
 _ERRORS = {-1: "invalid argument", -2: "unsupported shape/dtype", -3: "HIP error"}
 
 
@@ -118,4 +118,6 @@ def dtype_code(dt: torch.dtype) -> int:
         return DG_F32
     if dt == torch.bfloat16:
         return DG_BF16
+    if dt == torch.float16:
+        return DG_F16
     raise DGError(f"unsupported dtype {dt}")

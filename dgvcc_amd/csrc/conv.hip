@@ -135,12 +135,12 @@ __device__ __forceinline__ void epi_stats(f4v (&acc)[TI][TJ], const bool (&valid
 // Epilogue BatchNorm-backward partial sums of the stored (bf16-rounded) gradient tile:
 // the separate pass over (g, z) of norm.hip's bn_bwd_partial, computed where g is
 // produced; z is read here at the tile's pixels (8-B loads), once.
-template <int TI, int TJ, int NPW, int BN>
+template <int TI, int TJ, int NPW, int BN, typename T = bf16>
 __device__ __forceinline__ void epi_bnbwd(f4v (&acc)[TI][TJ], const bool (&valid)[TJ], int pw, int cw, int wpx,
                                           char* lds, const FwdArgs& a, int px0, int co0, int tid, int fr, int fc) {
   float* sh = (float*)lds;  // [NPW][3][BN]
   lds_barrier();            // every wave is done reading the operand ring
-  const bf16* z = (const bf16*)a.bz;
+  const T* z = (const T*)a.bz;
 #pragma unroll
   for (int i = 0; i < TI; ++i) {
     const int cl = cw + 16 * i + 4 * fc;
@@ -204,8 +204,8 @@ __device__ __forceinline__ u4v bload(__amdgpu_buffer_rsrc_t r, unsigned off) {
 
 template <typename T>
 __device__ __forceinline__ void mfma_frag(f4v& acc, const u4v& a, const u4v& b) {
-  if constexpr (std::is_same<T, bf16>::value) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(s8v, a), __builtin_bit_cast(s8v, b), acc, 0, 0, 0);
+  if constexpr (Is16<T>::value) {
+    acc = mfma16x16x32<T>(__builtin_bit_cast(s8v, a), __builtin_bit_cast(s8v, b), acc);
   } else {
     // 4 consecutive k of one 16-byte fragment; A and B use the same k order.
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a[0]), __uint_as_float(b[0]), acc, 0, 0, 0);
@@ -547,9 +547,8 @@ constexpr int PSTAGES = 3;
 // EPI selects the epilogue at compile time (each variant's registers stay out of the
 // others'; runtime branches on all four spilled the 256-wide kernel): 0 = bias / accumulate /
 // statistics, 1 = split-K f32 partials, 2 = BN-backward partials (dgrad), 3 = eval BN+ReLU.
-template <int BN, int STG, int VAR = 0, int EPI = 0>
+template <int BN, int STG, int VAR = 0, int EPI = 0, typename T = bf16>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
-  using T = bf16;
   constexpr int BK = 64;                    // bf16 channels per K-step (128-B rows)
   constexpr int AI = BN / 64;               // A (weight) DMA instructions per wave per K-step
   constexpr int BI = PBM / 64;              // B (pixel) DMA instructions per wave per K-step
@@ -707,7 +706,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
       if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
     }
   }
   if constexpr (EPI == 0) {
@@ -715,7 +714,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
       epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / PBM) * 3 * a.Cout, a.Cout,
                                co0, tid, fr, fc);
   }
-  if constexpr (EPI == 2) epi_bnbwd<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, wpx, smem, a, px0, co0, tid, fr, fc);
+  if constexpr (EPI == 2) epi_bnbwd<TI, TJ, 4, BN, T>(acc, valid, wid & 3, wco, wpx, smem, a, px0, co0, tid, fr, fc);
 }
 
 // Persistent form of conv_fwd_pipe_kernel (VAR 2 schedule): one block per CU walks its
@@ -725,9 +724,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 // MFMAs and epilogue stores.  The epilogue-statistics scratch gets its own LDS so the
 // in-flight ring stages are never touched.  Requires KT > PF (K-steps per tile).
 constexpr int PERS_BIAS_MAX = 1024;  // Cout limit of the persistent forward (LDS bias)
-template <int BN, int STG, int EPI = 0>
+template <int BN, int STG, int EPI = 0, typename T = bf16>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
-  using T = bf16;
   constexpr int BK = 64;
   constexpr int AI = BN / 64;
   constexpr int BI = PBM / 64;
@@ -741,6 +739,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   // compiler drain vmcnt to 0, i.e. wait for the next tile's in-flight DMA steps and every
   // earlier store of the tile (vector-memory operations retire in issue order)
   float* bbuf = (float*)(epi_lds + EPI_B);
+  // eval BN (EPI 3, no statistics scratch needed): bias, scale and shift all staged in LDS
+  // (the statistics scratch + bias region, 3 x Cout floats) when they fit, else global loads
+  constexpr int E3_MAX = (EPI_B + PERS_BIAS_MAX * 4) / 12;
+  const bool e3_lds = EPI == 3 && a.Cout <= E3_MAX;
+  float* ebias = (float*)epi_lds;
+  float* escl = ebias + E3_MAX;
+  float* eshf = escl + E3_MAX;
 
   const int HW = a.H * a.W;
   const int M = a.N * HW;
@@ -805,8 +810,15 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
 
   int lin = blockIdx.x;
   if (lin >= ntile) return;
-  if (a.bias)
+  if (e3_lds) {
+    for (int c = tid; c < a.Cout; c += 512) {
+      ebias[c] = a.bias ? a.bias[c] : 0.f;
+      escl[c] = a.escale[c];
+      eshf[c] = a.eshift[c];
+    }
+  } else if (a.bias) {
     for (int c = tid; c < a.Cout; c += 512) bbuf[c] = a.bias[c];
+  }
   Ctx cur, nxt;
   setup(lin, cur);
   bool has_next = lin + G < ntile;
@@ -872,7 +884,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       for (int i = 0; i < TI; ++i) {
         const int co = cur.co0 + wco + 16 * i + 4 * fc;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (a.bias) {
+        if (e3_lds) {
+          const f4v b = *(const f4v*)(ebias + co);
+          v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+        } else if (a.bias) {
           const f4v b = *(const f4v*)(bbuf + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         }
@@ -881,10 +896,22 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
           ld4(yrow + co, o);
           v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
         }
-        if constexpr (EPI == 3) epi_affine(v, a, co);
+        if constexpr (EPI == 3) {
+          if (e3_lds) {  // same fmaf / ReLU as epi_affine on the same f32 value
+            const f4v sc = *(const f4v*)(escl + co), sf = *(const f4v*)(eshf + co);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float tt = fmaf(v[r], sc[r], sf[r]);
+              if (a.eact == 1) tt = tt > 0.f ? tt : 0.f;
+              v[r] = tt;
+            }
+          } else {
+            epi_affine(v, a, co);
+          }
+        }
         st4(yrow + co, v);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
       }
     }
     if (EPI == 0 && a.part)
@@ -961,7 +988,7 @@ __global__ __launch_bounds__(1024) void splitk_reduce_kernel(const float* __rest
     ++cnt;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      v[k][r] = std::is_same<T, bf16>::value ? bf2f(f2bf(o[r])) : o[r];  // the stored value
+      v[k][r] = Is16<T>::value ? round_to<T>(o[r]) : o[r];  // the stored value
       s[r] += v[k][r];
     }
   }
@@ -1097,10 +1124,9 @@ constexpr int T3_XROWS = 264;
 
 // Epilogue of the 3-tap kernels: bias / accumulate / eval-BN affine, bf16 store, and the
 // per-256-pixel BN statistics row of the stored values.
-template <int PADK, int TI, int TJ, int BN, int BM, typename Unpad>
+template <int PADK, int TI, int TJ, int BN, int BM, typename Unpad, typename T = bf16>
 __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs& a, int px0, int wpx, int fr, int fc,
                                               int wid, int tid, char* smem, Unpad unpad) {
-  using T = bf16;
   T* y = (T*)a.y;
   bool valid[TJ];
   // bias read once, ahead of the stores (see conv_fwd_pipe_kernel); on the padded index the
@@ -1131,7 +1157,7 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
       epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] = bf2f(f2bf(v[r]));  // the stored value, for the statistics
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
     }
   }
   if (a.part)
@@ -1144,9 +1170,8 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
 // a tile may span rows and images; each kernel row's X strip is contiguous in u and the taps'
 // +-1 shifts land on zero pad cells exactly where the convolution pads.  Outputs on pad cells
 // are computed and dropped ((H+2)(W+2)/HW more MFMA work: +1.3% at 320x320).
-template <int PADK = 0>
+template <int PADK = 0, typename T = bf16>
 __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
-  using T = bf16;
   constexpr int BN = 64, BM = 256;
   constexpr int A_BYTES = 3 * BN * 128, X_BYTES = T3_XROWS * 128;
   constexpr int A_INST = A_BYTES / 1024, X_INST = X_BYTES / 1024;   // 24 + 33
@@ -1237,7 +1262,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
     asm volatile("" ::: "memory");
   }
 
-  tap3_epilogue<PADK, TI, TJ, BN, BM>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
+  tap3_epilogue<PADK, TI, TJ, BN, BM, decltype(unpad), T>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
 }
 
 // Narrow-K 3-tap forward/dgrad (same tiles and outputs as conv_fwd_tap3_kernel): a K-step is
@@ -1250,7 +1275,7 @@ __global__ __launch_bounds__(256, 2) void conv_fwd_tap3_kernel(FwdArgs a) {
 constexpr int T3N_XROWS = 272;
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + ((chunk ^ (((row >> 2) & 1) << 1)) << 4); }
 
-template <int PADK = 0>
+template <int PADK = 0, typename T = bf16>
 __global__ __launch_bounds__(256, 5) void conv_fwd_tap3n_kernel(FwdArgs a) {
   constexpr int BN = 64, BM = 256, BKC = 32;
   constexpr int A_BYTES = 3 * BN * 64, X_BYTES = T3N_XROWS * 64;
@@ -1331,13 +1356,13 @@ __global__ __launch_bounds__(256, 5) void conv_fwd_tap3n_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) mfma_frag<bf16>(acc[i][j], af[i], bfr[j]);
+        for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
   }
-  tap3_epilogue<PADK, TI, TJ, BN, BM>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
+  tap3_epilogue<PADK, TI, TJ, BN, BM, decltype(unpad), T>(acc, a, px0, wpx, fr, fc, wid, tid, smem, unpad);
 }
 
 // Persistent 3-tap forward/dgrad for C = Cout = 64 on row-aligned tiles (the full-resolution
@@ -1348,15 +1373,14 @@ __global__ __launch_bounds__(256, 5) void conv_fwd_tap3n_kernel(FwdArgs a) {
 // through a two-slot ring that runs across tile boundaries: the next strip (possibly the next
 // tile's first) is in flight during the current step's MFMAs and the epilogue's stores.
 // One block of 8 waves per CU (2 per SIMD), wave tile 64 px x 32 co.  Per tile the K order
-// (dh, tap, k-half) and the statistics merge are those of conv_fwd_tap3_kernel<0>, so
+// (dh, tap, k-half) and the statistics merge are those of (conv_fwd_tap3_kernel<0, T>), so
 // outputs and BN partials are bit-identical to it.  (A four-slot ring of 32-channel
 // half-strips, three steps ahead, measured slower: 1.41 vs 1.35 ms on 16x768x1024: twice the
 // barriers per tile cost more than the deeper lookahead gained.)
 constexpr int T3P_FILT = 9 * 64 * 128;    // resident filters, 72 KB
 constexpr int T3P_XS = T3_XROWS * 128;    // one X strip, 33 KB
-template <int ROWS>
+template <int ROWS, typename T = bf16>
 __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
-  using T = bf16;
   constexpr int BN = 64, BM = 256, TI = 2, TJ = 4;
   constexpr int X_INST = T3P_XS / 1024;   // 33 DMA instructions per strip
   constexpr int EPI_B = 4 * 3 * BN * 4;   // epi_stats scratch [4][3][BN] f32
@@ -1515,7 +1539,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
         }
         st4(yrow + co, v);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[r][i][j][e] = bf2f(f2bf(v[e]));  // the stored value, for the statistics
+        for (int e = 0; e < 4; ++e) acc[r][i][j][e] = round_to<T>(v[e]);  // the stored value, for the statistics
       }
     }
     if (a.part)
@@ -1566,7 +1590,7 @@ static bool tap3_pad_ok(const FwdArgs& a) {
 template <typename T>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
-  if constexpr (std::is_same<T, bf16>::value) {
+  if constexpr (Is16<T>::value) {
     if (use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
         (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31)) {
       const int np = dg_cdiv(M, PBM);
@@ -1574,34 +1598,34 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
       const int epi = a.ksplit > 1 ? 1 : a.bpart ? 2 : a.escale ? 3 : 0;
 #define PIPE_LAUNCH(BN_, STG_, G_) \
       do { \
-        if (epi == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 1>), dim3(G_), dim3(512), 0, st, a); \
-        else if (epi == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 2>), dim3(G_), dim3(512), 0, st, a); \
-        else if (epi == 3) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 3>), dim3(G_), dim3(512), 0, st, a); \
-        else if (var == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 1>), dim3(G_), dim3(512), 0, st, a); \
-        else if (var == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2>), dim3(G_), dim3(512), 0, st, a); \
-        else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 0>), dim3(G_), dim3(512), 0, st, a); \
+        if (epi == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 1, T>), dim3(G_), dim3(512), 0, st, a); \
+        else if (epi == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 2, T>), dim3(G_), dim3(512), 0, st, a); \
+        else if (epi == 3) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 3, T>), dim3(G_), dim3(512), 0, st, a); \
+        else if (var == 1) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 1, 0, T>), dim3(G_), dim3(512), 0, st, a); \
+        else if (var == 2) hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 2, 0, T>), dim3(G_), dim3(512), 0, st, a); \
+        else hipLaunchKernelGGL((conv_fwd_pipe_kernel<BN_, STG_, 0, 0, T>), dim3(G_), dim3(512), 0, st, a); \
       } while (0)
       if (a.ksplit > 1) {  // BN and stage count as the unsplit choice below
         const unsigned g = (unsigned)(np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : 128)) * a.ksplit);
         if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, g);
         else PIPE_LAUNCH(128, 3, g);
         DG_CHECK_LAUNCH();
-        hipLaunchKernelGGL(splitk_reduce_kernel<bf16>, dim3((unsigned)dg_cdiv(M, 256), a.Cout / 64), dim3(1024), 0, st,
-                           (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (bf16*)a.y, a.ldy, a.accumulate,
+        hipLaunchKernelGGL(splitk_reduce_kernel<T>, dim3((unsigned)dg_cdiv(M, 256), a.Cout / 64), dim3(1024), 0, st,
+                           (const float*)a.kpart, a.ksplit, (int)M, a.Cout, a.bias, (T*)a.y, a.ldy, a.accumulate,
                            a.part, a.escale, a.eshift, a.eact);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
         if (a.C == 64 && !a.bpart && use_tap3p()) {
           const unsigned g = (unsigned)std::min<long long>(M / 256, persist_grid());
           if (a.H % 2 == 0 && tap3p_rows() == 2)
-            hipLaunchKernelGGL(conv_fwd_tap3p_kernel<2>, dim3((unsigned)std::min<long long>(M / 512, g)), dim3(512), 0, st, a);
+            hipLaunchKernelGGL((conv_fwd_tap3p_kernel<2, T>), dim3((unsigned)std::min<long long>(M / 512, g)), dim3(512), 0, st, a);
           else
-            hipLaunchKernelGGL(conv_fwd_tap3p_kernel<1>, dim3(g), dim3(512), 0, st, a);
-        } else if (tap3_bk(false) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(conv_fwd_tap3_kernel<0>, dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+            hipLaunchKernelGGL((conv_fwd_tap3p_kernel<1, T>), dim3(g), dim3(512), 0, st, a);
+        } else if (tap3_bk(false) == 32) hipLaunchKernelGGL((conv_fwd_tap3n_kernel<0, T>), dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_fwd_tap3_kernel<0, T>), dim3((unsigned)(M / 256)), dim3(256), 0, st, a);
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && !a.part && tap3_pad_ok(a)) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
-        if (tap3_bk(true) == 32) hipLaunchKernelGGL(conv_fwd_tap3n_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(conv_fwd_tap3_kernel<1>, dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
+        if (tap3_bk(true) == 32) hipLaunchKernelGGL((conv_fwd_tap3n_kernel<1, T>), dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_fwd_tap3_kernel<1, T>), dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
       } else if (use_persist() && !a.bpart && var == 2 && a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX &&
                  (long long)np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64))) >
                      2 * 256) {
@@ -1609,13 +1633,13 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         const long long tiles = (long long)np * (a.Cout / bn);
         const unsigned g = (unsigned)std::min<long long>(tiles, persist_grid());
         if (epi == 3) {
-          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3>), dim3(g), dim3(512), 0, st, a);
-          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3>), dim3(g), dim3(512), 0, st, a);
-          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3>), dim3(g), dim3(512), 0, st, a);
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3, T>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
         } else {
-          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2>), dim3(g), dim3(512), 0, st, a);
-          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3>), dim3(g), dim3(512), 0, st, a);
-          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3>), dim3(g), dim3(512), 0, st, a);
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
         }
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
@@ -1653,6 +1677,7 @@ struct WgArgs {
 
 template <typename T> struct WgCfg;
 template <> struct WgCfg<bf16> { static constexpr int BKP = 64, PAD = 32; };
+template <> struct WgCfg<f16> { static constexpr int BKP = 64, PAD = 32; };
 template <> struct WgCfg<float> { static constexpr int BKP = 32, PAD = 64; };
 
 template <typename T, int BCO, int BC>
@@ -1770,7 +1795,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
     if (kt + 1 < nkt) gload(kbeg + (kt + 1) * BKP);
     const char* As = smem + cur * TILE_BYTES;
     const char* Bs = As + BKP * ROWA;
-    if constexpr (std::is_same<T, bf16>::value) {
+    if constexpr (Is16<T>::value) {
       // ds_read_b64_tr_b16: lane 4q+p of each 16-lane group supplies row q,
       // columns 4p..4p+3; lane i receives column i of the 4 rows.  The logical
       // k = 8g + j maps to physical pixel row 4g + (j&3) + 16*(j>>2) for both
@@ -1799,7 +1824,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
         for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16x16x32<T>(af[i], bfv[j], acc[i][j]);
       }
     } else {
       const int fcol = lane & 15;
@@ -1873,7 +1898,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
 template <int CPR>
 __device__ __forceinline__ int wg_swz(int r) { return CPR >= 16 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }
 
-template <int BCO, int BC>
+template <int BCO, int BC, typename T = bf16>
 __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(WgArgs a) {
   constexpr int BKP = 64;
   constexpr int RA = BCO * 2, RB = BC * 2;                 // bytes per LDS row
@@ -2015,7 +2040,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_pipe_kernel(WgArgs a) {
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = mfma16x16x32<T>(af[i], bfv[j], acc[i][j]);
     }
   }
 #undef WG_ISSUE
@@ -2062,7 +2087,7 @@ constexpr int W9_XROWS = 72;
 // conv_fwd_pipe_kernel (A/B in one call: wgrad 881 -> 949 TF/s, 15.1 -> 14.0 ms per step).
 // Measured and dropped: setprio alone (no change), priority without the moved issue (-0.7%),
 // the issue split over two points of the substep loop (777 TF/s).
-template <int BCO, int WT = 0, int PADK = 0, int SCH = 0>
+template <int BCO, int WT = 0, int PADK = 0, int SCH = 0, typename T = bf16>
 __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int BKP = 64, BC = 64;
   constexpr int RA = BCO * 2, RX = BC * 2;                    // bytes per LDS row
@@ -2228,7 +2253,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
 #pragma unroll
             for (int j = 0; j < TJ; ++j)
               acc[dhi * 3 + sw][i][j] =
-                  __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[dhi * 3 + sw][i][j], 0, 0, 0);
+                  mfma16x16x32<T>(af[i], bfv[j], acc[dhi * 3 + sw][i][j]);
         }
       }
       if constexpr (SCH == 2) __builtin_amdgcn_s_setprio(0);
@@ -2334,9 +2359,9 @@ template <typename T>
 WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S, long long ldx = -1, long long lddy = -1,
                bool pad_ok = false) {  // H, W: output grid
   constexpr int BKP = WgCfg<T>::BKP;
-  if (std::is_same<T, bf16>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2))
+  if (Is16<T>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2))
     return wg9_plan((long long)N * H * W, C, Cout);
-  if (std::is_same<T, bf16>::value && pad_ok &&
+  if (Is16<T>::value && pad_ok &&
       wg9p_ok(N, H, W, C, Cout, R, S, (R - 1) / 2, ldx < 0 ? C : ldx, lddy < 0 ? Cout : lddy))
     return wg9_plan((long long)N * (H + 2) * (W + 2), C, Cout);
   const long long M = (long long)N * H * W;
@@ -2373,7 +2398,7 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   const dim3 grid(tiles * a.splits);
   bool done = false;
   int slab_splits = a.splits;
-  if constexpr (std::is_same<T, bf16>::value) {
+  if constexpr (Is16<T>::value) {
     const bool w9 = a.stride == 1 && !a.whole_x && wg9_ok(a.C, a.Cout, a.R, a.S, a.W, a.pad);
     const bool w9p = a.stride == 1 && !a.whole_x && !w9 && a.pad_ok &&
                      wg9p_ok(a.N, a.H, a.W, a.C, a.Cout, a.R, a.S, a.pad, a.ldx, a.lddy);
@@ -2384,34 +2409,34 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
       const bool kh2 = b9 == 64 && sch == 2 && wg9_khalf();
       if (kh2) slab_splits = 2 * a.splits;  // one slab split per k-half
       if (w9) {
-        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2>), g9, dim3(512), 0, st, a);
-        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1>), g9, dim3(512), 0, st, a);
-        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128>), g9, dim3(512), 0, st, a);
-        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 0, 2>), g9, dim3(512), 0, st, a);
-        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 2>), g9, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_wgrad9_kernel<64>), g9, dim3(512), 0, st, a);
+        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2, T>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 0, T>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 0, 0, T>), g9, dim3(512), 0, st, a);
+        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 0, 2, T>), g9, dim3(512), 0, st, a);
+        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 2, T>), g9, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 0, T>), g9, dim3(512), 0, st, a);
       } else {
-        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1, 2>), g9, dim3(512), 0, st, a);
-        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1>), g9, dim3(512), 0, st, a);
-        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 1>), g9, dim3(512), 0, st, a);
-        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 1, 2>), g9, dim3(512), 0, st, a);
-        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1, 2>), g9, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1>), g9, dim3(512), 0, st, a);
+        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1, 2, T>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1, 0, T>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 1, 0, T>), g9, dim3(512), 0, st, a);
+        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 1, 2, T>), g9, dim3(512), 0, st, a);
+        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1, 2, T>), g9, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 1, 0, T>), g9, dim3(512), 0, st, a);
       }
       done = true;
     } else if (use_wgrad_pipe()) {  // opt-in: measured slower than the register-staged kernel (round 1)
       const int RS = a.R * a.S;
       if (bco == 128 && a.C % 256 == 0) {
-        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 256>), dim3((a.Cout / 128) * (a.C / 256) * RS * a.splits),
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 256, T>), dim3((a.Cout / 128) * (a.C / 256) * RS * a.splits),
                            dim3(512), 0, st, a);
       } else if (bco == 128 && bc == 128) {
-        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 128, T>), grid, dim3(512), 0, st, a);
       } else if (bco == 128) {
-        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 64>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<128, 64, T>), grid, dim3(512), 0, st, a);
       } else if (bc == 128) {
-        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 128, T>), grid, dim3(512), 0, st, a);
       } else {
-        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 64>), grid, dim3(512), 0, st, a);
+        hipLaunchKernelGGL((conv_wgrad_pipe_kernel<64, 64, T>), grid, dim3(512), 0, st, a);
       }
       done = true;
     }
@@ -2572,15 +2597,15 @@ extern "C" int dg_conv_fwd(int dtype, const void* x, int64_t ldx, int N, int H, 
                            int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                            int accumulate, void* stream) {
   DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1);
   DG_SUPPORTED(Cout % 64 == 0);
-  DG_SUPPORTED(dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0));
+  DG_SUPPORTED(DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0));
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate};
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : dtype == DG_F16 ? launch_fwd<f16>(a, st) : launch_fwd<float>(a, st);
 }
 
 // Which forward kernel serves this shape (bf16): 1 = pipelined / fused 3-tap (epilogue
@@ -2598,7 +2623,7 @@ extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, i
                                  int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy, float* part,
                                  void* stream) {
   DG_REQUIRE(x && w && y && part && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
-  DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  DG_SUPPORTED(DG_IS16(dtype) && fwd_has_epi_stats(C, Cout, ldx, R, S));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
@@ -2608,13 +2633,13 @@ extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, i
     q.part = nullptr;
     if (Cout == 64 && R == 3 && S == 3 && pad == 1 && tap3_pad_ok(q)) return DG_ERR_UNSUPPORTED;
   }
-  return launch_fwd<bf16>(a, (hipStream_t)stream);
+  return dtype == DG_F16 ? launch_fwd<f16>(a, (hipStream_t)stream) : launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 
 extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
   const long long M = (long long)N * H * W;
-  if (dtype != DG_BF16 || !fwd_has_epi_stats(C, Cout, C, R, S)) return 0;
+  if (!DG_IS16(dtype) || !fwd_has_epi_stats(C, Cout, C, R, S)) return 0;
   const int ks = fwd_ksplit(M, Cout, C, R, S);
   return ks > 1 ? (int64_t)ks * M * Cout * 4 : 0;
 }
@@ -2625,21 +2650,21 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
                               int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                               int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream) {
   DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
-  DG_SUPPORTED(dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0));
+  DG_SUPPORTED(DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0));
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
-  if (part) DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  if (part) DG_SUPPORTED(DG_IS16(dtype) && fwd_has_epi_stats(C, Cout, ldx, R, S));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate, part};
   {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
      // runs dg_conv_fwd + the statistics pass instead
     FwdArgs q = a;
     q.part = nullptr;
-    if (part && dtype == DG_BF16 && Cout == 64 && R == 3 && S == 3 && pad == 1 && tap3_pad_ok(q))
+    if (part && DG_IS16(dtype) && Cout == 64 && R == 3 && S == 3 && pad == 1 && tap3_pad_ok(q))
       return DG_ERR_UNSUPPORTED;
   }
-  if (dtype == DG_BF16 && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
+  if (DG_IS16(dtype) && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
     const long long M = (long long)N * H * W;
     const int ks = fwd_ksplit(M, Cout, C, R, S);
     if (ks > 1 && ws_bytes >= (int64_t)ks * M * Cout * 4) {
@@ -2648,7 +2673,7 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
     }
   }
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : dtype == DG_F16 ? launch_fwd<f16>(a, st) : launch_fwd<float>(a, st);
 }
 
 // dgrad (or any bf16 pipelined forward) that also emits the BatchNorm-backward partial sums
@@ -2667,16 +2692,16 @@ extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N,
                                    int64_t ws_bytes, void* stream) {
   DG_REQUIRE(x && w && y && scale && shift && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0 &&
              (act == 0 || act == 1));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
-  DG_SUPPORTED(dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0));
+  DG_SUPPORTED(DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0));
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, 0};
   a.escale = scale;
   a.eshift = shift;
   a.eact = act;
-  if (dtype == DG_BF16 && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
+  if (DG_IS16(dtype) && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
     const long long M = (long long)N * H * W;
     const int ks = fwd_ksplit(M, Cout, C, R, S);
     if (ks > 1 && ws_bytes >= (int64_t)ks * M * Cout * 4) {
@@ -2685,7 +2710,7 @@ extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N,
     }
   }
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : launch_fwd<float>(a, st);
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : dtype == DG_F16 ? launch_fwd<f16>(a, st) : launch_fwd<float>(a, st);
 }
 
 extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
@@ -2694,7 +2719,7 @@ extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, i
                                  int act, const float* drop, int HW, float* bpart, void* stream) {
   DG_REQUIRE(x && w && y && z && bpart && scale && shift && mean && invstd && N > 0 && H > 0 && W > 0 && C > 0 &&
              Cout > 0 && R > 0 && S > 0 && (act == 0 || act == 1) && (!drop || HW > 0));
-  DG_SUPPORTED(dtype == DG_BF16 && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  DG_SUPPORTED(DG_IS16(dtype) && fwd_has_epi_stats(C, Cout, ldx, R, S));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 128 == 0);  // the pipe kernel's 128/256 tiles
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldy % 4 == 0 && ldz >= Cout && ldz % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
@@ -2706,7 +2731,7 @@ extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, i
   a.bsc = scale; a.bsf = shift; a.bmu = mean; a.bis = invstd; a.bdrop = drop;
   a.bact = act; a.bHW = drop ? HW : 1;
   a.bpart = bpart;
-  return launch_fwd<bf16>(a, (hipStream_t)stream);
+  return dtype == DG_F16 ? launch_fwd<f16>(a, (hipStream_t)stream) : launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 
 extern "C" int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream) {
@@ -2716,6 +2741,9 @@ extern "C" int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, 
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(flip_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)w, Cout, C, R,
                        S, (bf16*)wflip);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(flip_weight_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, st, (const f16*)w, Cout, C, R,
+                       S, (f16*)wflip);
   else if (dtype == DG_F32)
     hipLaunchKernelGGL(flip_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)w, Cout, C,
                        R, S, (float*)wflip);
@@ -2729,13 +2757,16 @@ extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int
                              int C, int R, int S, int pad, void* wflip, void* dx, int64_t lddx, int accumulate,
                              void* stream) {
   DG_REQUIRE(dy && w && wflip && dx);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(C % 64 == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)Cout * C * R * S;
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(flip_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)w, Cout, C, R,
                        S, (bf16*)wflip);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(flip_weight_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, st, (const f16*)w, Cout, C, R,
+                       S, (f16*)wflip);
   else
     hipLaunchKernelGGL(flip_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)w, Cout, C,
                        R, S, (float*)wflip);
@@ -2746,12 +2777,12 @@ extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int
 
 extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
-  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S, -1, -1, true)
+  WgPlan p = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S, -1, -1, true)
                               : wg_plan<float>(N, H, W, C, Cout, R, S);
   // the padded 9-tap plan may be refused at launch (pixel strides too large): cover the
   // fallback plan too
-  WgPlan q = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
-  const int kh = (dtype == DG_BF16 && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
+  WgPlan q = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
+  const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
   return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
 }
 
@@ -2759,22 +2790,22 @@ extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H
                              int64_t lddy, int Cout, int R, int S, int pad, float* dw, void* workspace,
                              int64_t ws_bytes, int accumulate, void* stream) {
   DG_REQUIRE(x && dy && dw && workspace);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1);
   DG_SUPPORTED(Cout % 64 == 0 && C % 64 == 0);
   DG_REQUIRE(ldx % 8 == 0 && lddy % 8 == 0 && ldx >= C && lddy >= Cout);
   const int64_t need = dg_conv_wgrad_workspace(dtype, N, H, W, C, Cout, R, S);
   DG_REQUIRE(ws_bytes >= need);
-  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, H, W, C, Cout, R, S, ldx, lddy, true)
+  WgPlan p = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S, ldx, lddy, true)
                               : wg_plan<float>(N, H, W, C, Cout, R, S);
-  const bool padk = dtype == DG_BF16 && !wg9_ok(C, Cout, R, S, W, pad) &&
+  const bool padk = DG_IS16(dtype) && !wg9_ok(C, Cout, R, S, W, pad) &&
                     wg9p_ok(N, H, W, C, Cout, R, S, pad, ldx, lddy);
   if (!padk) DG_SUPPORTED((long long)(p.pps + 2 * pad * (W + 1)) * std::max(ldx, lddy) * 4 < (1ll << 31));
   WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
            1, H, W, 0};
   a.pad_ok = 1;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
+  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
 }
 
 extern "C" int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R, int S, int Cpad, int row_len,
@@ -2785,6 +2816,9 @@ extern "C" int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R,
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(pack_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S, Cpad,
                        row_len, (bf16*)out);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(pack_weight_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S, Cpad,
+                       row_len, (f16*)out);
   else if (dtype == DG_F32)
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S, Cpad,
                        row_len, (float*)out);
@@ -2801,6 +2835,9 @@ extern "C" int dg_im2col3x3_c3(int dtype, const float* img, int N, int H, int W,
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(im2col_c3_kernel<bf16>, dim3(grid_for(M, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
                        (bf16*)out);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(im2col_c3_kernel<f16>, dim3(grid_for(M, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
+                       (f16*)out);
   else if (dtype == DG_F32)
     hipLaunchKernelGGL(im2col_c3_kernel<float>, dim3(grid_for(M, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
                        (float*)out);
@@ -2828,16 +2865,16 @@ extern "C" int dg_conv2d_fwd(int dtype, const void* x, int64_t ldx, int N, int H
                              int Cout, int R, int S, int stride, int pad, const float* bias, void* y, int64_t ldy,
                              int accumulate, void* stream) {
   DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0 && stride >= 1 && pad >= 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  DG_SUPPORTED(Cout % 64 == 0 && (dtype == DG_BF16 ? (C % 64 == 0) : (C % 32 == 0)));
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(Cout % 64 == 0 && (DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0)));
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
-  DG_SUPPORTED((((long long)N * H * W - 1) * ldx + C) * (dtype == DG_BF16 ? 2 : 4) < (1ll << 31));
+  DG_SUPPORTED((((long long)N * H * W - 1) * ldx + C) * (DG_IS16(dtype) ? 2 : 4) < (1ll << 31));
   const int P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
   DG_REQUIRE(P > 0 && Q > 0);
   GenArgs a{(const char*)x, ldx, N, H, W, C, P, Q, (const char*)w, Cout, R, S, stride, pad, 0, bias, (char*)y, ldy,
             accumulate};
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_gen<bf16>(a, st) : launch_gen<float>(a, st);
+  return dtype == DG_BF16 ? launch_gen<bf16>(a, st) : dtype == DG_F16 ? launch_gen<f16>(a, st) : launch_gen<float>(a, st);
 }
 
 extern "C" int dg_transpose_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wt, void* stream) {
@@ -2847,6 +2884,9 @@ extern "C" int dg_transpose_weight(int dtype, const void* w, int Cout, int C, in
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(transpose_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, (const bf16*)w, Cout, C,
                        R, S, (bf16*)wt);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(transpose_weight_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, st, (const f16*)w, Cout, C,
+                       R, S, (f16*)wt);
   else if (dtype == DG_F32)
     hipLaunchKernelGGL(transpose_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, (const float*)w, Cout,
                        C, R, S, (float*)wt);
@@ -2862,15 +2902,15 @@ extern "C" int dg_conv2d_dgrad(int dtype, const void* dy, int64_t lddy, int N, i
                                int C, int H, int W, int R, int S, int stride, int pad, void* dx, int64_t lddx,
                                int accumulate, void* stream) {
   DG_REQUIRE(dy && wt && dx && N > 0 && P > 0 && Q > 0 && H > 0 && W > 0 && stride >= 1 && pad >= 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  DG_SUPPORTED(C % 64 == 0 && (dtype == DG_BF16 ? (Cout % 64 == 0) : (Cout % 32 == 0)));
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(C % 64 == 0 && (DG_IS16(dtype) ? (Cout % 64 == 0) : (Cout % 32 == 0)));
   DG_REQUIRE(conv_out(H, R, stride, pad) == P && conv_out(W, S, stride, pad) == Q);
   DG_REQUIRE(lddy % 8 == 0 && lddx % 4 == 0);
-  DG_SUPPORTED((((long long)N * P * Q - 1) * lddy + Cout) * (dtype == DG_BF16 ? 2 : 4) < (1ll << 31));
+  DG_SUPPORTED((((long long)N * P * Q - 1) * lddy + Cout) * (DG_IS16(dtype) ? 2 : 4) < (1ll << 31));
   GenArgs a{(const char*)dy, lddy, N, P, Q, Cout, H, W, (const char*)wt, C, R, S, stride, pad, 1, nullptr, (char*)dx,
             lddx, accumulate};
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_gen<bf16>(a, st) : launch_gen<float>(a, st);
+  return dtype == DG_BF16 ? launch_gen<bf16>(a, st) : dtype == DG_F16 ? launch_gen<f16>(a, st) : launch_gen<float>(a, st);
 }
 
 extern "C" int64_t dg_conv2d_wgrad_workspace(int dtype, int N, int P, int Q, int C, int Cout, int R, int S) {
@@ -2881,20 +2921,20 @@ extern "C" int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int
                                int64_t lddy, int Cout, int R, int S, int stride, int pad, float* dw, void* workspace,
                                int64_t ws_bytes, int accumulate, void* stream) {
   DG_REQUIRE(x && dy && dw && workspace && stride >= 1 && pad >= 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(Cout % 64 == 0 && C % 64 == 0);
   DG_REQUIRE(ldx % 8 == 0 && lddy % 8 == 0 && ldx >= C && lddy >= Cout);
   const int P = conv_out(H, R, stride, pad), Q = conv_out(W, S, stride, pad);
   DG_REQUIRE(P > 0 && Q > 0);
   const int64_t need = dg_conv_wgrad_workspace(dtype, N, P, Q, C, Cout, R, S);
   DG_REQUIRE(ws_bytes >= need);
-  WgPlan p = dtype == DG_BF16 ? wg_plan<bf16>(N, P, Q, C, Cout, R, S) : wg_plan<float>(N, P, Q, C, Cout, R, S);
-  DG_SUPPORTED((((long long)N * H * W - 1) * ldx + C) * (dtype == DG_BF16 ? 2 : 4) < (1ll << 31));
+  WgPlan p = DG_IS16(dtype) ? wg_plan<bf16>(N, P, Q, C, Cout, R, S) : wg_plan<float>(N, P, Q, C, Cout, R, S);
+  DG_SUPPORTED((((long long)N * H * W - 1) * ldx + C) * (DG_IS16(dtype) ? 2 : 4) < (1ll << 31));
   DG_SUPPORTED((long long)p.pps * lddy * 4 < (1ll << 31));
   WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
            stride, P, Q, 1};
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
+  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
 }
 
 
@@ -2905,10 +2945,13 @@ extern "C" int dg_im2col_c3(int dtype, const float* img, int N, int H, int W, in
   DG_REQUIRE(P > 0 && Q > 0);
   DG_SUPPORTED(Kpad % 8 == 0 && (long long)N * P * Q < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  const long long total = (long long)N * P * Q * (Kpad / (dtype == DG_BF16 ? 8 : 4));
+  const long long total = (long long)N * P * Q * (Kpad / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(im2col_c3_ex_kernel<bf16>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
                        R, S, stride, pad, P, Q, Kpad, (bf16*)out);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(im2col_c3_ex_kernel<f16>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
+                       R, S, stride, pad, P, Q, Kpad, (f16*)out);
   else if (dtype == DG_F32)
     hipLaunchKernelGGL(im2col_c3_ex_kernel<float>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H,
                        W, R, S, stride, pad, P, Q, Kpad, (float*)out);

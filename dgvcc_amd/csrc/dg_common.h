@@ -9,6 +9,12 @@
 #include "../../include/dgvcc.h"
 
 typedef __bf16 bf16;
+typedef _Float16 f16;  // fp16 storage mode (configs/qnrf_final.yml): same 16-bit layouts as bf16
+typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+#define DG_IS16(dt) ((dt) == DG_BF16 || (dt) == DG_F16)
+template <typename T> struct Is16 { static constexpr bool value = false; };
+template <> struct Is16<bf16> { static constexpr bool value = true; };
+template <> struct Is16<f16> { static constexpr bool value = true; };
 typedef short s8v __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef float f4v __attribute__((ext_vector_type(4)));
@@ -37,9 +43,30 @@ __device__ __forceinline__ unsigned short f2bf(float x) { return __builtin_bit_c
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+__device__ __forceinline__ float to_f(f16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);
 template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> __device__ __forceinline__ f16 from_f<f16>(float x) { return (f16)x; }
+// x rounded to the storage type T and back (the value a later pass will read)
+template <typename T> __device__ __forceinline__ float round_to(float x) { return to_f(from_f<T>(x)); }
+__device__ __forceinline__ float h2f(unsigned short u) { return (float)__builtin_bit_cast(f16, u); }
+__device__ __forceinline__ unsigned short f2h(float x) { return __builtin_bit_cast(unsigned short, (f16)x); }
+// 16-bit payload <-> float for a storage type H (bf16 or f16)
+template <typename H> __device__ __forceinline__ float u16_to_f(unsigned short u) {
+  if constexpr (std::is_same<H, bf16>::value) return bf2f(u); else return h2f(u);
+}
+template <typename H> __device__ __forceinline__ unsigned short f_to_u16(float x) {
+  if constexpr (std::is_same<H, bf16>::value) return f2bf(x); else return f2h(x);
+}
+// v_mfma_f32_16x16x32_{bf16,f16}: the same operand/accumulator layouts (cdna_hip_programming.md §3)
+template <typename H> __device__ __forceinline__ f4v mfma16x16x32(const s8v& a, const s8v& b, const f4v& c) {
+  if constexpr (std::is_same<H, bf16>::value)
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, a), __builtin_bit_cast(h8v, b), c, 0, 0,
+                                                    0);
+}
 
 typedef unsigned u2v __attribute__((ext_vector_type(2)));
 
@@ -52,6 +79,17 @@ __device__ __forceinline__ void ld4(const bf16* p, float v[4]) {
   u2v t = *(const u2v*)p;
   v[0] = __uint_as_float(t[0] << 16); v[1] = __uint_as_float(t[0] & 0xffff0000u);
   v[2] = __uint_as_float(t[1] << 16); v[3] = __uint_as_float(t[1] & 0xffff0000u);
+}
+__device__ __forceinline__ void ld4(const f16* p, float v[4]) {
+  u2v t = *(const u2v*)p;
+  v[0] = h2f((unsigned short)(t[0] & 0xffffu)); v[1] = h2f((unsigned short)(t[0] >> 16));
+  v[2] = h2f((unsigned short)(t[1] & 0xffffu)); v[3] = h2f((unsigned short)(t[1] >> 16));
+}
+__device__ __forceinline__ unsigned pack_h2(float lo, float hi) {
+  return (unsigned)f2h(lo) | ((unsigned)f2h(hi) << 16);
+}
+__device__ __forceinline__ void st4(f16* p, const float v[4]) {
+  *(u2v*)p = u2v{pack_h2(v[0], v[1]), pack_h2(v[2], v[3])};
 }
 __device__ __forceinline__ void st4(float* p, const float v[4]) { *(f4v*)p = f4v{v[0], v[1], v[2], v[3]}; }
 __device__ __forceinline__ unsigned pack_bf2(float lo, float hi) {
@@ -68,6 +106,14 @@ __device__ __forceinline__ void ldv(const bf16* p, float v[8]) {
   u4v t = *(const u4v*)p;
 #pragma unroll
   for (int i = 0; i < 4; ++i) { v[2 * i] = __uint_as_float(t[i] << 16); v[2 * i + 1] = __uint_as_float(t[i] & 0xffff0000u); }
+}
+__device__ __forceinline__ void ldv(const f16* p, float v[8]) {
+  u4v t = *(const u4v*)p;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { v[2 * i] = h2f((unsigned short)(t[i] & 0xffffu)); v[2 * i + 1] = h2f((unsigned short)(t[i] >> 16)); }
+}
+__device__ __forceinline__ void stv(f16* p, const float v[8]) {
+  *(u4v*)p = u4v{pack_h2(v[0], v[1]), pack_h2(v[2], v[3]), pack_h2(v[4], v[5]), pack_h2(v[6], v[7])};
 }
 __device__ __forceinline__ void stv(float* p, const float v[4]) { st4(p, v); }
 __device__ __forceinline__ void stv(bf16* p, const float v[8]) {

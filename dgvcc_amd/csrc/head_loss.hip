@@ -341,6 +341,76 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
   }
 }
 
+// Deterministic variant (no atomics): one 256-thread block per 16x16 output tile of one image
+// walks that image's points in order and each thread sums its pixel's stamp values in that
+// order, the reference's `density += gaussian_filter(pt2d)` f32 accumulation (dmap_gen.py:
+// 72-79) exactly, so the map is bit-identical to the reference's and stable run to run.
+// Points are staged 256 at a time in LDS as (row, col) after int() truncation and numpy's
+// negative-index wrap; a point whose stamp misses the tile costs one uniform compare.
+constexpr int DMT = 16;
+__global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __restrict__ pts,
+                                                               const int64_t* __restrict__ offsets, int H, int W,
+                                                               float sigma, int radius, float* __restrict__ dmap) {
+  __shared__ float stamp[32 * 32];
+  __shared__ double wd[64];
+  __shared__ float wf[64];
+  __shared__ int prow[256], pcol[256];
+  const int K = 2 * radius + 1;
+  const int tid = threadIdx.x;
+  if (tid < K) {
+    double s = 0.0;
+    for (int i = -radius; i <= radius; ++i) s += exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+    const int i = tid - radius;
+    wd[tid] = exp(-0.5 / ((double)sigma * sigma) * (double)(i * i)) / s;
+    wf[tid] = (float)wd[tid];
+  }
+  __syncthreads();
+  for (int cell = tid; cell < K * K; cell += 256) {
+    const int di = cell / K, dj = cell - (cell / K) * K;
+    stamp[di * 32 + dj] = (float)((double)wf[di] * wd[dj]);  // scipy's two float32 passes
+  }
+  const int tiles_w = (W + DMT - 1) / DMT;
+  const int ty0 = (blockIdx.x / tiles_w) * DMT, tx0 = (blockIdx.x % tiles_w) * DMT;
+  const int n = blockIdx.y;
+  const int pr = ty0 + tid / DMT, pc = tx0 + tid % DMT;
+  const long long p0 = offsets[n], p1 = offsets[n + 1];
+  float acc = 0.f;
+  for (long long base = p0; base < p1; base += 256) {
+    __syncthreads();
+    const long long q = base + tid;
+    if (q < p1) {
+      int r = (int)pts[2 * q + 1], c = (int)pts[2 * q];
+      bool ok = r < H && c < W;
+      if (r < 0) r += H;
+      if (c < 0) c += W;
+      ok = ok && r >= 0 && c >= 0;
+      prow[tid] = ok ? r : -1000000;
+      pcol[tid] = ok ? c : -1000000;
+    }
+    __syncthreads();
+    const int cnt = (int)min(256ll, p1 - base);
+    for (int j = 0; j < cnt; ++j) {
+      const int r = prow[j], c = pcol[j];
+      if (r + radius < ty0 || r - radius >= ty0 + DMT || c + radius < tx0 || c - radius >= tx0 + DMT) continue;
+      const int di = pr - r + radius, dj = pc - c + radius;
+      if ((unsigned)di < (unsigned)K && (unsigned)dj < (unsigned)K) acc += stamp[di * 32 + dj];
+    }
+  }
+  if (pr < H && pc < W) dmap[((long long)n * H + pr) * W + pc] = acc;
+}
+
+// fp16 mode loss scaling: g *= inv_scale in place; any non-finite element sets *nonfinite = 1
+// (plain vector stores of the same value; the flag is zeroed by the caller)
+__global__ void grad_unscale_kernel(float* __restrict__ g, long long n, float inv_scale, int* __restrict__ nonfinite) {
+  bool bad = false;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = g[i];
+    bad |= !isfinite(v);
+    g[i] = v * inv_scale;
+  }
+  if (bad) nonfinite[0] = 1;
+}
+
 __global__ void tanh_fwd_kernel(const float* __restrict__ x, long long n, float* __restrict__ y) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
     y[i] = tanhf(x[i]);
@@ -374,8 +444,8 @@ extern "C" int dg_dmap_adaptive(const float* points, const int64_t* offsets, int
 extern "C" int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, const float* w, const float* bias,
                            int act, float* y, void* stream) {
   DG_REQUIRE(x && w && y && M > 0 && C > 0 && act >= 0 && act <= 2);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ldx % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const int tpp_need = C / V;
@@ -383,6 +453,8 @@ extern "C" int dg_head_fwd(int dtype, const void* x, int64_t ldx, int M, int C, 
 #define HF(T, TPP) hipLaunchKernelGGL((head_fwd_kernel<T, TPP>), dim3(grid), dim3(NT), 0, st, (const T*)x, ldx, M, C, w, bias, act, y)
   if (dtype == DG_BF16) {
     if (tpp_need >= 32) HF(bf16, 32); else if (tpp_need >= 16) HF(bf16, 16); else HF(bf16, 8);
+  } else if (dtype == DG_F16) {
+    if (tpp_need >= 32) HF(f16, 32); else if (tpp_need >= 16) HF(f16, 16); else HF(f16, 8);
   } else {
     if (tpp_need >= 32) HF(float, 32); else if (tpp_need >= 16) HF(float, 16); else HF(float, 8);
   }
@@ -400,8 +472,8 @@ extern "C" int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, 
                            const float* y, const float* gy, void* gx, int64_t ldgx, int accumulate_gx, float* gw,
                            float* gbias, void* workspace, void* stream) {
   DG_REQUIRE(x && w && y && gy && gw && workspace && M > 0 && C > 0 && act >= 0 && act <= 2);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && C / V <= NT && ldx % V == 0 && (!gx || ldgx % V == 0));
   hipStream_t st = (hipStream_t)stream;
   const int nblk = head_nblk(M), ppb = dg_cdiv(M, nblk);
@@ -409,6 +481,9 @@ extern "C" int dg_head_bwd(int dtype, const void* x, int64_t ldx, int M, int C, 
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(head_bwd_kernel<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)x, ldx, M, C, w, act, y, gy,
                        (bf16*)gx, ldgx, accumulate_gx, ppb, part);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(head_bwd_kernel<f16>, dim3(nblk), dim3(NT), 0, st, (const f16*)x, ldx, M, C, w, act, y, gy,
+                       (f16*)gx, ldgx, accumulate_gx, ppb, part);
   else
     hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(nblk), dim3(NT), 0, st, (const float*)x, ldx, M, C, w, act, y, gy,
                        (float*)gx, ldgx, accumulate_gx, ppb, part);
@@ -495,6 +570,27 @@ extern "C" int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx
   const int grid = (int)std::min<long long>(16384, (n + 255) / 256);
   hipLaunchKernelGGL(tanh_bwd_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, y, gy, (long long)n, gx,
                      accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W, float sigma,
+                                   int radius, float* dmap, void* stream) {
+  DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
+  DG_REQUIRE(points || true);
+  const dim3 grid((unsigned)(((H + DMT - 1) / DMT) * ((W + DMT - 1) / DMT)), (unsigned)N);
+  hipLaunchKernelGGL(dmap_fixed_tiled_kernel, grid, dim3(256), 0, (hipStream_t)stream, points, offsets, H, W, sigma,
+                     radius, dmap);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_grad_unscale(float* g, int64_t n, float inv_scale, int* nonfinite, void* stream) {
+  DG_REQUIRE(g && nonfinite && n > 0);
+  hipStream_t st = (hipStream_t)stream;
+  if (hipMemsetAsync(nonfinite, 0, sizeof(int), st) != hipSuccess) return DG_ERR_HIP;
+  const int grid = (int)std::min<long long>(8192, (n + 255) / 256);
+  hipLaunchKernelGGL(grad_unscale_kernel, dim3(grid), dim3(256), 0, st, g, (long long)n, inv_scale, nonfinite);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

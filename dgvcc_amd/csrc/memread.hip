@@ -472,7 +472,7 @@ extern "C" int64_t dg_instnorm_workspace(int N, int HW, int C) {
 extern "C" int dg_instnorm_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float eps, float* mean,
                                  float* invstd, void* workspace, void* stream) {
   DG_REQUIRE(x && mean && invstd && workspace && N > 0 && HW > 0 && C > 0);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && C / V <= NT && ldx % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const int nb = std::max(1, std::min(64, dg_cdiv(HW, 256)));
@@ -482,6 +482,12 @@ extern "C" int dg_instnorm_stats(int dtype, const void* x, int64_t ldx, int N, i
                        (float*)workspace);
     DG_CHECK_LAUNCH();
     hipLaunchKernelGGL(in_stats_finalize<bf16>, dim3(dg_cdiv(N * C, 256)), dim3(256), 0, st, (const bf16*)x, ldx, N,
+                       HW, C, nb, (const float*)workspace, eps, mean, invstd);
+  } else if (dtype == DG_F16) {
+    hipLaunchKernelGGL(in_stats_partial<f16>, dim3(nb, N), dim3(NT), 0, st, (const f16*)x, ldx, HW, C, ppb,
+                       (float*)workspace);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_stats_finalize<f16>, dim3(dg_cdiv(N * C, 256)), dim3(256), 0, st, (const f16*)x, ldx, N,
                        HW, C, nb, (const float*)workspace, eps, mean, invstd);
   } else {
     hipLaunchKernelGGL(in_stats_partial<float>, dim3(nb, N), dim3(NT), 0, st, (const float*)x, ldx, HW, C, ppb,
@@ -499,13 +505,17 @@ extern "C" int dg_emask_fwd(int dtype, const void* y1, const void* y2, int64_t l
                             const float* drop1, const float* drop2, void* m1, void* m2, unsigned char* mask,
                             void* stream) {
   DG_REQUIRE(y1 && y2 && mu1 && is1 && mu2 && is2 && m1 && m2 && mask && N > 0 && HW > 0 && C > 0);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ld % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * HW * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(emask_fwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)y1,
                        (const bf16*)y2, ld, N, HW, C, mu1, is1, mu2, is2, thr, drop1, drop2, (bf16*)m1, (bf16*)m2,
+                       mask);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(emask_fwd_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)y1,
+                       (const f16*)y2, ld, N, HW, C, mu1, is1, mu2, is2, thr, drop1, drop2, (f16*)m1, (f16*)m2,
                        mask);
   else
     hipLaunchKernelGGL(emask_fwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)y1,
@@ -519,13 +529,16 @@ extern "C" int dg_emask_bwd(int dtype, const void* gm1, const void* gm2, int N, 
                             const unsigned char* mask, const float* drop1, const float* drop2, void* gy1, void* gy2,
                             int64_t ldgy, void* stream) {
   DG_REQUIRE(gm1 && gm2 && mask && gy1 && gy2 && N > 0 && HW > 0 && C > 0);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ldgy % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * HW * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(emask_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)gm1,
                        (const bf16*)gm2, N, HW, C, mask, drop1, drop2, (bf16*)gy1, (bf16*)gy2, ldgy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(emask_bwd_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)gm1,
+                       (const f16*)gm2, N, HW, C, mask, drop1, drop2, (f16*)gy1, (f16*)gy2, ldgy);
   else
     hipLaunchKernelGGL(emask_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)gm1,
                        (const float*)gm2, N, HW, C, mask, drop1, drop2, (float*)gy1, (float*)gy2, ldgy);
@@ -549,6 +562,9 @@ extern "C" int dg_softmax_pair_fwd(int dtype, const void* L1, const void* L2, in
   if (dtype == DG_BF16)
     SOFTMAX_DISPATCH(softmax_pair_fwd, bf16, C, (const bf16*)L1, (const bf16*)L2, M, C, (bf16*)P1, (bf16*)P2,
                      (float*)workspace);
+  else if (dtype == DG_F16)
+    SOFTMAX_DISPATCH(softmax_pair_fwd, f16, C, (const f16*)L1, (const f16*)L2, M, C, (f16*)P1, (f16*)P2,
+                     (float*)workspace);
   else
     SOFTMAX_DISPATCH(softmax_pair_fwd, float, C, (const float*)L1, (const float*)L2, M, C, (float*)P1, (float*)P2,
                      (float*)workspace);
@@ -567,6 +583,9 @@ extern "C" int dg_softmax_pair_bwd(int dtype, const void* P1, const void* P2, co
   if (dtype == DG_BF16)
     SOFTMAX_DISPATCH(softmax_pair_bwd, bf16, C, (const bf16*)P1, (const bf16*)P2, (const bf16*)G1, (const bf16*)G2,
                      M, C, coef, (bf16*)GL1, (bf16*)GL2);
+  else if (dtype == DG_F16)
+    SOFTMAX_DISPATCH(softmax_pair_bwd, f16, C, (const f16*)P1, (const f16*)P2, (const f16*)G1, (const f16*)G2,
+                     M, C, coef, (f16*)GL1, (f16*)GL2);
   else
     SOFTMAX_DISPATCH(softmax_pair_bwd, float, C, (const float*)P1, (const float*)P2, (const float*)G1,
                      (const float*)G2, M, C, coef, (float*)GL1, (float*)GL2);
@@ -582,6 +601,9 @@ extern "C" int dg_softmax_jsd_fwd(int dtype, const void* L1, const void* L2, int
   const int grid = std::min(4096, dg_cdiv(M, 4));
   if (dtype == DG_BF16)
     SOFTMAX_DISPATCH(softmax_jsd_fwd, bf16, C, (const bf16*)L1, (const bf16*)L2, M, C, (bf16*)P1, (bf16*)P2,
+                     (float*)workspace);
+  else if (dtype == DG_F16)
+    SOFTMAX_DISPATCH(softmax_jsd_fwd, f16, C, (const f16*)L1, (const f16*)L2, M, C, (f16*)P1, (f16*)P2,
                      (float*)workspace);
   else
     SOFTMAX_DISPATCH(softmax_jsd_fwd, float, C, (const float*)L1, (const float*)L2, M, C, (float*)P1, (float*)P2,
@@ -601,6 +623,9 @@ extern "C" int dg_softmax_jsd_bwd(int dtype, const void* P1, const void* P2, con
   if (dtype == DG_BF16)
     SOFTMAX_DISPATCH(softmax_jsd_bwd, bf16, C, (const bf16*)P1, (const bf16*)P2, (const bf16*)G1, (const bf16*)G2,
                      M, C, coef, (bf16*)GL1, (bf16*)GL2);
+  else if (dtype == DG_F16)
+    SOFTMAX_DISPATCH(softmax_jsd_bwd, f16, C, (const f16*)P1, (const f16*)P2, (const f16*)G1, (const f16*)G2,
+                     M, C, coef, (f16*)GL1, (f16*)GL2);
   else
     SOFTMAX_DISPATCH(softmax_jsd_bwd, float, C, (const float*)P1, (const float*)P2, (const float*)G1,
                      (const float*)G2, M, C, coef, (float*)GL1, (float*)GL2);
@@ -617,14 +642,17 @@ extern "C" int dg_in_l1_fwd(int dtype, const void* y1, const void* y2, int64_t l
                             const float* mu1, const float* is1, const float* mu2, const float* is2, float* loss,
                             void* workspace, void* stream) {
   DG_REQUIRE(y1 && y2 && mu1 && is1 && mu2 && is2 && loss && workspace && N > 0 && HW > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ld % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * HW * (C / V);
   const int grid = ew_grid(total, 4096);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(in_l1_fwd_kernel<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)y1, (const bf16*)y2, ld, N,
+                       HW, C, mu1, is1, mu2, is2, (float*)workspace);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(in_l1_fwd_kernel<f16>, dim3(grid), dim3(NT), 0, st, (const f16*)y1, (const f16*)y2, ld, N,
                        HW, C, mu1, is1, mu2, is2, (float*)workspace);
   else
     hipLaunchKernelGGL(in_l1_fwd_kernel<float>, dim3(grid), dim3(NT), 0, st, (const float*)y1, (const float*)y2, ld,
@@ -639,14 +667,17 @@ extern "C" int dg_in_l1_bwd(int dtype, const void* y1, const void* y2, int64_t l
                             const float* mu1, const float* is1, const float* mu2, const float* is2, const float* coef,
                             void* g1, void* g2, void* stream) {
   DG_REQUIRE(y1 && y2 && mu1 && is1 && mu2 && is2 && coef && g1 && g2 && N > 0 && HW > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ld % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * HW * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(in_l1_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)y1,
                        (const bf16*)y2, ld, N, HW, C, mu1, is1, mu2, is2, coef, (bf16*)g1, (bf16*)g2);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(in_l1_bwd_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)y1,
+                       (const f16*)y2, ld, N, HW, C, mu1, is1, mu2, is2, coef, (f16*)g1, (f16*)g2);
   else
     hipLaunchKernelGGL(in_l1_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)y1,
                        (const float*)y2, ld, N, HW, C, mu1, is1, mu2, is2, coef, (float*)g1, (float*)g2);
@@ -660,6 +691,7 @@ extern "C" int dg_softmax_fwd(int dtype, const void* L, int M, int C, void* P, v
   hipStream_t st = (hipStream_t)stream;
   const int grid = std::min(4096, dg_cdiv(M, 4));
   if (dtype == DG_BF16) SOFTMAX_DISPATCH(softmax_fwd, bf16, C, (const bf16*)L, M, C, (bf16*)P);
+  else if (dtype == DG_F16) SOFTMAX_DISPATCH(softmax_fwd, f16, C, (const f16*)L, M, C, (f16*)P);
   else SOFTMAX_DISPATCH(softmax_fwd, float, C, (const float*)L, M, C, (float*)P);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -671,6 +703,7 @@ extern "C" int dg_softmax_bwd(int dtype, const void* P, const void* G, int M, in
   hipStream_t st = (hipStream_t)stream;
   const int grid = std::min(4096, dg_cdiv(M, 4));
   if (dtype == DG_BF16) SOFTMAX_DISPATCH(softmax_bwd, bf16, C, (const bf16*)P, (const bf16*)G, M, C, (bf16*)GL);
+  else if (dtype == DG_F16) SOFTMAX_DISPATCH(softmax_bwd, f16, C, (const f16*)P, (const f16*)G, M, C, (f16*)GL);
   else SOFTMAX_DISPATCH(softmax_bwd, float, C, (const float*)P, (const float*)G, M, C, (float*)GL);
   DG_CHECK_LAUNCH();
   return DG_OK;

@@ -577,8 +577,8 @@ extern "C" int64_t dg_bn_workspace(int M, int C) {
 
 // C/V must divide NT (power of two <= 256): every thread then owns one channel chunk.
 #define BN_SHAPE_OK(dtype, C, ld)                                                        \
-  ((C) % (dtype == DG_BF16 ? 8 : 4) == 0 && NT % ((C) / (dtype == DG_BF16 ? 8 : 4)) == 0 && \
-   (ld) % (dtype == DG_BF16 ? 8 : 4) == 0)
+  ((C) % (DG_IS16(dtype) ? 8 : 4) == 0 && NT % ((C) / (DG_IS16(dtype) ? 8 : 4)) == 0 && \
+   (ld) % (DG_IS16(dtype) ? 8 : 4) == 0)
 
 extern "C" int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C, const float* gamma,
                                const float* beta, float* running_mean, float* running_var, float momentum, float eps,
@@ -586,12 +586,13 @@ extern "C" int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int
                                void* stream) {
   DG_REQUIRE(z && save_mean && save_invstd && scale && shift && workspace && M > 0 && C > 0 && ldz >= C);
   DG_REQUIRE((running_mean == nullptr) == (running_var == nullptr));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? bn_fwd_impl<bf16>(z, ldz, M, C, gamma, beta, running_mean, running_var, momentum, eps,
                                               save_mean, save_invstd, scale, shift, workspace, st)
-                          : bn_fwd_impl<float>(z, ldz, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                          : dtype == DG_F16 ? bn_fwd_impl<f16>(z, ldz, M, C, gamma, beta, running_mean, running_var, momentum, eps,
+                                              save_mean, save_invstd, scale, shift, workspace, st) : bn_fwd_impl<float>(z, ldz, M, C, gamma, beta, running_mean, running_var, momentum, eps,
                                                save_mean, save_invstd, scale, shift, workspace, st);
 }
 
@@ -599,13 +600,16 @@ extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, 
                            int act, const float* drop, int HW, void* y, int64_t ldy, void* stream) {
   DG_REQUIRE(z && y && scale && shift && M > 0 && C > 0 && ldz >= C && ldy >= C && (act == 0 || act == 1));
   DG_REQUIRE(!drop || HW > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, ldy));
   hipStream_t st = (hipStream_t)stream;
-  const long long total = (long long)M * (C / (dtype == DG_BF16 ? 8 : 4));
+  const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
                        shift, act, drop, HW, (bf16*)y, ldy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_apply_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
+                       shift, act, drop, HW, (f16*)y, ldy);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
                        scale, shift, act, drop, HW, (float*)y, ldy);
@@ -620,13 +624,14 @@ extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, i
   DG_REQUIRE(g && z && dz && workspace && M > 0 && C > 0);
   DG_REQUIRE((save_mean && save_invstd && scale && shift) || (!save_mean && !save_invstd));
   DG_REQUIRE(!drop || HW > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16
              ? bn_bwd_impl<bf16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW, dz,
                                  lddz, dgamma, dbeta, dbias, workspace, st)
-             : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+             : dtype == DG_F16 ? bn_bwd_impl<f16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW, dz,
+                                 lddz, dgamma, dbeta, dbias, workspace, st) : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
                                   dz, lddz, dgamma, dbeta, dbias, workspace, st);
 }
 
@@ -639,7 +644,7 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
                                    float* dbias, float* coef, void* stream) {
   DG_REQUIRE(part && nblk > 0 && g && z && dz && coef && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
   DG_REQUIRE(!drop || HW > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, save_invstd,
@@ -649,6 +654,10 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL(bn_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
+  } else if (dtype == DG_F16) {
+    const long long total = (long long)M * (C / 8);
+    hipLaunchKernelGGL(bn_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz);
   } else {
     const long long total = (long long)M * (C / 4);
     hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
@@ -678,13 +687,14 @@ extern "C" int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void*
                               void* stream) {
   DG_REQUIRE(g && z && coef && workspace && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
   DG_REQUIRE(!drop || HW > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16
              ? bn_bwd_impl<bf16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
                                  nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef)
-             : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+             : dtype == DG_F16 ? bn_bwd_impl<f16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+                                 nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef) : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
                                   nullptr, 0, dgamma, dbeta, dbias, workspace, st, coef);
 }
 
@@ -693,15 +703,18 @@ extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, in
                                 int64_t ldy, void* yp, int64_t ldyp, void* stream) {
   DG_REQUIRE(z && yp && scale && shift && N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
   DG_REQUIRE(ldz >= C && ldyp >= C && (!y || ldy >= C));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldz) &&
                BN_SHAPE_OK(dtype, C, ldyp) && (!y || BN_SHAPE_OK(dtype, C, ldy)));
   hipStream_t st = (hipStream_t)stream;
   const long long Mp = (long long)N * (H / 2) * (W / 2);
-  const long long total = Mp * (C / (dtype == DG_BF16 ? 8 : 4));
+  const long long total = Mp * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_apply_pool_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, H, W,
                        Mp, C, scale, shift, act, drop, H * W, (bf16*)y, ldy, (bf16*)yp, ldyp);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_apply_pool_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, H, W,
+                       Mp, C, scale, shift, act, drop, H * W, (f16*)y, ldy, (f16*)yp, ldyp);
   else
     hipLaunchKernelGGL(bn_apply_pool_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, H,
                        W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp);
@@ -741,7 +754,7 @@ extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const voi
                               void* workspace, void* stream) {
   DG_REQUIRE(gp && z && dz && workspace && save_mean && save_invstd && scale && shift);
   DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldgp) &&
                BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz) && (!gd || BN_SHAPE_OK(dtype, C, ldgd)) &&
                C % POOL_V == 0 && NT % (C / POOL_V) == 0);
@@ -749,6 +762,7 @@ extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const voi
   return dtype == DG_BF16
              ? bn_pool_bwd_impl<bf16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
                                       shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st)
-             : bn_pool_bwd_impl<float>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
+             : dtype == DG_F16 ? bn_pool_bwd_impl<f16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
+                                      shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st) : bn_pool_bwd_impl<float>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
                                        shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st);
 }

@@ -630,14 +630,17 @@ int up_bwd(const void* gy, long long ldgy, const void* gy2, long long ldgy2, int
 extern "C" int dg_maxpool2_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, void* y,
                                int64_t ldy, void* stream) {
   DG_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && C % V == 0 && ldx % V == 0 && ldy % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * (H / 2) * (W / 2) * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(maxpool_fwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, H, W,
                        C, (bf16*)y, ldy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(maxpool_fwd_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)x, ldx, N, H, W,
+                       C, (f16*)y, ldy);
   else
     hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, H,
                        W, C, (float*)y, ldy);
@@ -648,14 +651,17 @@ extern "C" int dg_maxpool2_fwd(int dtype, const void* x, int64_t ldx, int N, int
 extern "C" int dg_maxpool2_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy, int N, int H,
                                int W, int C, void* gx, int64_t ldgx, int accumulate, void* stream) {
   DG_REQUIRE(x && gy && gx && N > 0 && H > 0 && W > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && C % V == 0 && ldx % V == 0 && ldgy % V == 0 && ldgx % V == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * (H / 2) * (W / 2) * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(maxpool_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx,
                        (const bf16*)gy, ldgy, N, H, W, C, (bf16*)gx, ldgx, accumulate);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(maxpool_bwd_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)x, ldx,
+                       (const f16*)gy, ldgy, N, H, W, C, (f16*)gx, ldgx, accumulate);
   else
     hipLaunchKernelGGL(maxpool_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx,
                        (const float*)gy, ldgy, N, H, W, C, (float*)gx, ldgx, accumulate);
@@ -666,28 +672,28 @@ extern "C" int dg_maxpool2_bwd(int dtype, const void* x, int64_t ldx, const void
 extern "C" int dg_upsample_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int scale, int mode,
                                void* y, int64_t ldy, void* stream) {
   DG_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0 && scale >= 1 && mode >= 0 && mode <= 2);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? up_fwd<bf16>(x, ldx, N, H, W, C, scale, mode, y, ldy, st)
-                          : up_fwd<float>(x, ldx, N, H, W, C, scale, mode, y, ldy, st);
+                          : dtype == DG_F16 ? up_fwd<f16>(x, ldx, N, H, W, C, scale, mode, y, ldy, st) : up_fwd<float>(x, ldx, N, H, W, C, scale, mode, y, ldy, st);
 }
 
 extern "C" int dg_upsample_bwd(int dtype, const void* gy, int64_t ldgy, const void* gy2, int64_t ldgy2, int N, int H,
                                int W, int C, int scale, int mode, void* gx, int64_t ldgx, int accumulate,
                                void* stream) {
   DG_REQUIRE(gy && gx && N > 0 && H > 0 && W > 0 && C > 0 && scale >= 1 && mode >= 0 && mode <= 2);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? up_bwd<bf16>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st)
-                          : up_bwd<float>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st);
+                          : dtype == DG_F16 ? up_bwd<f16>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st) : up_bwd<float>(gy, ldgy, gy2, ldgy2, N, H, W, C, scale, mode, gx, ldgx, accumulate, st);
 }
 
 
 extern "C" int dg_maxpool_fwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, int k, int stride,
                               int pad, void* y, int64_t ldy, void* stream) {
   DG_REQUIRE(x && y && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && stride > 0 && pad >= 0 && 2 * pad <= k);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ldx % V == 0 && ldy % V == 0);
   const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
   hipStream_t st = (hipStream_t)stream;
@@ -695,6 +701,9 @@ extern "C" int dg_maxpool_fwd(int dtype, const void* x, int64_t ldx, int N, int 
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(maxpool_gen_fwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, H, W, C, k,
                        stride, pad, P, Q, (bf16*)y, ldy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(maxpool_gen_fwd<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)x, ldx, N, H, W, C, k,
+                       stride, pad, P, Q, (f16*)y, ldy);
   else
     hipLaunchKernelGGL(maxpool_gen_fwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, H, W,
                        C, k, stride, pad, P, Q, (float*)y, ldy);
@@ -705,8 +714,8 @@ extern "C" int dg_maxpool_fwd(int dtype, const void* x, int64_t ldx, int N, int 
 extern "C" int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void* gy, int64_t ldgy, int N, int H, int W,
                               int C, int k, int stride, int pad, void* gx, int64_t ldgx, int accumulate, void* stream) {
   DG_REQUIRE(x && gy && gx && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && stride > 0 && pad >= 0 && 2 * pad <= k);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ldx % V == 0 && ldgy % V == 0 && ldgx % V == 0);
   const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
   hipStream_t st = (hipStream_t)stream;
@@ -714,6 +723,9 @@ extern "C" int dg_maxpool_bwd(int dtype, const void* x, int64_t ldx, const void*
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(maxpool_gen_bwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx,
                        (const bf16*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (bf16*)gx, ldgx, accumulate);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(maxpool_gen_bwd<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)x, ldx,
+                       (const f16*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (f16*)gx, ldgx, accumulate);
   else
     hipLaunchKernelGGL(maxpool_gen_bwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx,
                        (const float*)gy, ldgy, N, H, W, C, k, stride, pad, P, Q, (float*)gx, ldgx, accumulate);
@@ -725,8 +737,8 @@ extern "C" int dg_maxpool_fwd_idx(int dtype, const void* x, int64_t ldx, int N, 
                                   int pad, void* y, int64_t ldy, unsigned char* idx, void* stream) {
   DG_REQUIRE(x && y && idx && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && k <= 15 && stride > 0 && pad >= 0 &&
              2 * pad <= k);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ldx % V == 0 && ldy % V == 0 && (long long)N * H * W * (C / V) < (1LL << 30));
   const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
   hipStream_t st = (hipStream_t)stream;
@@ -734,6 +746,9 @@ extern "C" int dg_maxpool_fwd_idx(int dtype, const void* x, int64_t ldx, int N, 
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(maxpool_idx_fwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)x, ldx, N, H, W, C, k,
                        stride, pad, P, Q, (bf16*)y, ldy, idx);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(maxpool_idx_fwd<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)x, ldx, N, H, W, C, k,
+                       stride, pad, P, Q, (f16*)y, ldy, idx);
   else
     hipLaunchKernelGGL(maxpool_idx_fwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)x, ldx, N, H, W,
                        C, k, stride, pad, P, Q, (float*)y, ldy, idx);
@@ -746,8 +761,8 @@ extern "C" int dg_maxpool_bwd_idx(int dtype, const unsigned char* idx, const voi
                                   void* stream) {
   DG_REQUIRE(idx && gy && gx && N > 0 && H > 0 && W > 0 && C > 0 && k > 0 && k <= 15 && stride > 0 && pad >= 0 &&
              2 * pad <= k);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(C % V == 0 && ldgy % V == 0 && ldgx % V == 0 && (long long)N * H * W * (C / V) < (1LL << 30));
   const int P = (H + 2 * pad - k) / stride + 1, Q = (W + 2 * pad - k) / stride + 1;
   hipStream_t st = (hipStream_t)stream;
@@ -755,6 +770,9 @@ extern "C" int dg_maxpool_bwd_idx(int dtype, const unsigned char* idx, const voi
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(maxpool_idx_bwd<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, idx, (const bf16*)gy, ldgy, N, H,
                        W, C, k, stride, pad, P, Q, (bf16*)gx, ldgx, accumulate);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(maxpool_idx_bwd<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, idx, (const f16*)gy, ldgy, N, H,
+                       W, C, k, stride, pad, P, Q, (f16*)gx, ldgx, accumulate);
   else
     hipLaunchKernelGGL(maxpool_idx_bwd<float>, dim3(ew_grid(total)), dim3(NT), 0, st, idx, (const float*)gy, ldgy, N,
                        H, W, C, k, stride, pad, P, Q, (float*)gx, ldgx, accumulate);
@@ -771,8 +789,8 @@ extern "C" int dg_cat_combine(int dtype, const void* z1, int64_t ldz1, const voi
                               int64_t ldz3, int N, int H, int W, int C, const float* bias, void* z, int64_t ldz,
                               float* part, void* stream) {
   DG_REQUIRE(z1 && z2 && z3 && z && N > 0 && H > 0 && W > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(H % 4 == 0 && W % 4 == 0 && (long long)N * H * W < (1LL << 31) && C % V == 0 && 256 % (C / V) == 0 &&
                ldz1 % V == 0 && ldz2 % V == 0 &&
                ldz3 % V == 0 && ldz % V == 0);
@@ -784,6 +802,10 @@ extern "C" int dg_cat_combine(int dtype, const void* z1, int64_t ldz1, const voi
     hipLaunchKernelGGL(cat_combine_kernel<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)z1, (long long)ldz1,
                        (const bf16*)z2, (long long)ldz2, (const bf16*)z3, (long long)ldz3, H, W, M, C, ppb, bias,
                        (bf16*)z, (long long)ldz, part);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(cat_combine_kernel<f16>, dim3(nblk), dim3(NT), 0, st, (const f16*)z1, (long long)ldz1,
+                       (const f16*)z2, (long long)ldz2, (const f16*)z3, (long long)ldz3, H, W, M, C, ppb, bias,
+                       (f16*)z, (long long)ldz, part);
   else
     hipLaunchKernelGGL(cat_combine_kernel<float>, dim3(nblk), dim3(NT), 0, st, (const float*)z1, (long long)ldz1,
                        (const float*)z2, (long long)ldz2, (const float*)z3, (long long)ldz3, H, W, M, C, ppb, bias,

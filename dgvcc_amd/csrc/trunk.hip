@@ -243,20 +243,23 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
 
 }  // namespace
 
-#define VOK(dtype, C, ld) ((C) % ((dtype) == DG_BF16 ? 8 : 4) == 0 && (ld) % ((dtype) == DG_BF16 ? 8 : 4) == 0)
+#define VOK(dtype, C, ld) ((C) % (DG_IS16(dtype) ? 8 : 4) == 0 && (ld) % (DG_IS16(dtype) ? 8 : 4) == 0)
 
 extern "C" int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, int C, const float* scale1,
                                const float* shift1, const void* z2, int64_t ld2, const float* scale2,
                                const float* shift2, int act, void* y, int64_t ldy, void* stream) {
   DG_REQUIRE(z1 && z2 && y && scale1 && shift1 && M > 0 && C > 0 && (!scale2 || shift2));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(VOK(dtype, C, ld1) && VOK(dtype, C, ld2) && VOK(dtype, C, ldy) && NT % (C / V) == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)M * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_add_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z1, ld1, M, C, scale1,
                        shift1, (const bf16*)z2, ld2, scale2, shift2, act, (bf16*)y, ldy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_add_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)z1, ld1, M, C, scale1,
+                       shift1, (const f16*)z2, ld2, scale2, shift2, act, (f16*)y, ldy);
   else
     hipLaunchKernelGGL(bn_add_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z1, ld1, M, C,
                        scale1, shift1, (const float*)z2, ld2, scale2, shift2, act, (float*)y, ldy);
@@ -267,14 +270,17 @@ extern "C" int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, in
 extern "C" int dg_relu_bwd(int dtype, const void* g, int64_t ldg, const void* y, int64_t ldy, int M, int C, void* out,
                            int64_t ldo, void* stream) {
   DG_REQUIRE(g && y && out && M > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(VOK(dtype, C, ldg) && VOK(dtype, C, ldy) && VOK(dtype, C, ldo));
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)M * (C / V);
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(relu_bwd_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg,
                        (const bf16*)y, ldy, M, C, (bf16*)out, ldo);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(relu_bwd_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg,
+                       (const f16*)y, ldy, M, C, (f16*)out, ldo);
   else
     hipLaunchKernelGGL(relu_bwd_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)y, ldy, M, C, (float*)out, ldo);
@@ -286,8 +292,8 @@ extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, i
                                  const float* invstd, const float* gamma, const float* beta, int act, void* y,
                                  int64_t ldy, void* stream) {
   DG_REQUIRE(x && y && mean && invstd && N > 0 && HW > 0 && C > 0 && (!gamma || beta));
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   const long long total = (long long)N * HW * (C / V);
   DG_SUPPORTED(VOK(dtype, C, ldx) && VOK(dtype, C, ldy) && total < (1LL << 30));
   hipStream_t st = (hipStream_t)stream;
@@ -295,6 +301,9 @@ extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, i
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(in_apply_kernel<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (bf16*)y, ldy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(in_apply_kernel<f16>, dim3(grid), dim3(NT), 0, st, (const f16*)x, ldx, N, HW, C,
+                       mean, invstd, gamma, beta, act, (f16*)y, ldy);
   else
     hipLaunchKernelGGL(in_apply_kernel<float>, dim3(grid), dim3(NT), 0, st, (const float*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (float*)y, ldy);
@@ -314,8 +323,8 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
                                const float* mean, const float* invstd, const float* gamma, void* dx, int64_t lddx,
                                int accumulate, float* dgamma, float* dbeta, void* workspace, void* stream) {
   DG_REQUIRE(g && x && dx && mean && invstd && workspace && N > 0 && HW > 0 && C > 0);
-  DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);
-  const int V = dtype == DG_BF16 ? 8 : 4;
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  const int V = DG_IS16(dtype) ? 8 : 4;
   const long long total = (long long)N * HW * (C / V);
   DG_SUPPORTED(VOK(dtype, C, ldg) && VOK(dtype, C, ldx) && VOK(dtype, C, lddx) && C / V <= NT &&
                total < (1LL << 30));
@@ -333,6 +342,14 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
     DG_CHECK_LAUNCH();
     hipLaunchKernelGGL(in_bwd_apply<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x,
                        ldx, N, HW, C, mean, invstd, coef, (bf16*)dx, lddx, accumulate);
+  } else if (dtype == DG_F16) {
+    hipLaunchKernelGGL(in_bwd_partial<f16>, dim3(nb, N), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)x, ldx,
+                       HW, C, ppb, mean, invstd, part);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
+    DG_CHECK_LAUNCH();
+    hipLaunchKernelGGL(in_bwd_apply<f16>, dim3(grid), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)x,
+                       ldx, N, HW, C, mean, invstd, coef, (f16*)dx, lddx, accumulate);
   } else {
     hipLaunchKernelGGL(in_bwd_partial<float>, dim3(nb, N), dim3(NT), 0, st, (const float*)g, ldg, (const float*)x,
                        ldx, HW, C, ppb, mean, invstd, part);

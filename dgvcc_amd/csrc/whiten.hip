@@ -707,8 +707,8 @@ extern "C" int64_t dg_sw_workspace(int N, int HW, int C) {
 
 #define SW_CHECK_SHAPE(dtype, C, T_, ...)                                                           \
   do {                                                                                              \
-    DG_REQUIRE(dtype == DG_F32 || dtype == DG_BF16);                                                \
-    const int V_ = dtype == DG_BF16 ? 8 : 4;                                                        \
+    DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));                                                \
+    const int V_ = DG_IS16(dtype) ? 8 : 4;                                                        \
     DG_SUPPORTED(C % SWC == 0 && C <= 256 && (T_) <= SW_MAXT);                                      \
     for (int64_t ld_ : {__VA_ARGS__}) DG_SUPPORTED(ld_ % V_ == 0);                                  \
   } while (0)
@@ -730,6 +730,8 @@ extern "C" int dg_sw_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int
   if (rc) return rc;
   if (dtype == DG_BF16)
     SW_DISPATCH_G(sw_cov_partial, bf16, dim3(nb, N), dim3(256), 0, st, (const bf16*)x, ldx, HW, C, ppb, mu, part);
+  else if (dtype == DG_F16)
+    SW_DISPATCH_G(sw_cov_partial, f16, dim3(nb, N), dim3(256), 0, st, (const f16*)x, ldx, HW, C, ppb, mu, part);
   else
     SW_DISPATCH_G(sw_cov_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)x, ldx, HW, C, ppb, mu, part);
   DG_CHECK_LAUNCH();
@@ -761,6 +763,9 @@ extern "C" int dg_sw_fwd_finish(int dtype, const void* x, int64_t ldx, int N, in
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(sw_apply<bf16>, dim3(anb, N), dim3(256), lds, st, (const bf16*)x, ldx, HW, C, appb, aff, bias,
                        act, (bf16*)y, ldy);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(sw_apply<f16>, dim3(anb, N), dim3(256), lds, st, (const f16*)x, ldx, HW, C, appb, aff, bias,
+                       act, (f16*)y, ldy);
   else
     hipLaunchKernelGGL(sw_apply<float>, dim3(anb, N), dim3(256), lds, st, (const float*)x, ldx, HW, C, appb, aff,
                        bias, act, (float*)y, ldy);
@@ -800,6 +805,9 @@ extern "C" int dg_sw_bwd_stats(int dtype, const void* gy, int64_t ldg, const voi
   if (dtype == DG_BF16)
     SW_DISPATCH_G(sw_bwd_partial, bf16, dim3(nb, N), dim3(256), 0, st, (const bf16*)gy, ldg, (const bf16*)y, ldy,
                   (const bf16*)x, ldx, HW, C, ppb, act, mu, part);
+  else if (dtype == DG_F16)
+    SW_DISPATCH_G(sw_bwd_partial, f16, dim3(nb, N), dim3(256), 0, st, (const f16*)gy, ldg, (const f16*)y, ldy,
+                  (const f16*)x, ldx, HW, C, ppb, act, mu, part);
   else
     SW_DISPATCH_G(sw_bwd_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)gy, ldg, (const float*)y, ldy,
                   (const float*)x, ldx, HW, C, ppb, act, mu, part);
@@ -835,6 +843,9 @@ extern "C" int dg_sw_bwd_finish(int dtype, const void* gy, int64_t ldg, const vo
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(sw_bwd_apply<bf16>, dim3(anb, N), dim3(256), lds, st, (const bf16*)gy, ldg, (const bf16*)y, ldy,
                        (const bf16*)x, ldx, HW, C, appb, act, mu, coef, (bf16*)dx, lddx, accumulate);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(sw_bwd_apply<f16>, dim3(anb, N), dim3(256), lds, st, (const f16*)gy, ldg, (const f16*)y, ldy,
+                       (const f16*)x, ldx, HW, C, appb, act, mu, coef, (f16*)dx, lddx, accumulate);
   else
     hipLaunchKernelGGL(sw_bwd_apply<float>, dim3(anb, N), dim3(256), lds, st, (const float*)gy, ldg, (const float*)y,
                        ldy, (const float*)x, ldx, HW, C, appb, act, mu, coef, (float*)dx, lddx, accumulate);

@@ -12,7 +12,7 @@ import torch
 
 from ._capi import DGError, call, dtype_code, lib_call_status, ptr, query, stream
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 
 
 @dataclass
@@ -448,9 +448,12 @@ def adamw_step(p, g, m, v, lr, beta1, beta2, eps, wd, step):
 
 
 def dmap_fixed(points: torch.Tensor, offsets: torch.Tensor, N: int, H: int, W: int,
-               sigma: float = 4.0, radius: int = 7) -> torch.Tensor:
+               sigma: float = 4.0, radius: int = 7, deterministic: bool = True) -> torch.Tensor:
+    """deterministic: per-tile in-order sums (bit-identical to the reference); False: one
+    wave per point with f32 atomics (order-dependent in the last ulp)."""
     out = torch.empty((N, H, W), dtype=torch.float32, device=offsets.device)
-    call("dg_dmap_fixed", ptr(points) if points.numel() else None, ptr(offsets), N, H, W,
+    fn = "dg_dmap_fixed_tiled" if deterministic else "dg_dmap_fixed"
+    call(fn, ptr(points) if points.numel() else None, ptr(offsets), N, H, W,
          float(sigma), int(radius), ptr(out), stream())
     return out
 

@@ -4,8 +4,9 @@ Same class names, constructor signatures, sub-module names and therefore the
 same `state_dict` keys as the reference; the forward/backward math runs on
 the HIP kernel plans of `dgvcc_amd.engine` (NHWC activations, implicit-GEMM
 MFMA convolutions).  Precision: "fp32" (default; exact-f32 MFMA, parity with
-the reference CPU path) or "bf16" (bf16 storage/MFMA, f32 accumulation and
-statistics) — `model.set_precision(...)` or env DGVCC_PRECISION.
+the reference CPU path), "bf16" (bf16 storage/MFMA, f32 accumulation and
+statistics) or "fp16" (fp16 storage + f16 MFMA, f32 accumulation and statistics:
+configs/qnrf_final.yml) — `model.set_precision(...)` or env DGVCC_PRECISION.
 """
 from __future__ import annotations
 
@@ -18,7 +19,7 @@ import torch.nn as nn
 from .. import engine as E
 
 _VGG16_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512, "M"]
-_PRECISIONS = {"fp32": torch.float32, "bf16": torch.bfloat16}
+_PRECISIONS = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
 
 
 def vgg16_bn_features() -> nn.Sequential:

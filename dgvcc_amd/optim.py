@@ -26,6 +26,10 @@ class AdamW(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.allreduce = allreduce
+        # fp16 mode: the loss was multiplied by grad_scale before backward (LossScaler); the
+        # step unscales the flat gradient and skips the update when it holds inf/NaN
+        self.grad_scale = None
+        self.found_inf = False
         for group in self.param_groups:
             ps = group["params"]
             if any(p.dtype != torch.float32 or p.device != ps[0].device for p in ps):
@@ -113,6 +117,8 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         invalidate_frozen()  # the update below writes parameters behind torch's version counters
+        self.found_inf = False
+        staged = []
         for group in self.param_groups:
             if all(p.grad is None for p in group["params"]):
                 continue
@@ -121,6 +127,16 @@ class AdamW(torch.optim.Optimizer):
             g = group["_g"]
             if self.allreduce:
                 average_flat_(g)
+            if self.grad_scale is not None and self.grad_scale != 1.0:
+                flag = group.setdefault("_inf", torch.zeros(1, dtype=torch.int32, device=g.device))
+                call("dg_grad_unscale", ptr(g), g.numel(), 1.0 / float(self.grad_scale), ptr(flag), stream())
+                if int(flag.item()):  # one device->host flag per group (the trainer syncs per step anyway)
+                    self.found_inf = True
+            staged.append((group, runs))
+        if self.found_inf:  # GradScaler semantics: no update, no step count, for any group
+            return loss
+        for group, runs in staged:
+            g = group["_g"]
             b1, b2 = group["betas"]
             flat, m, v = group["_flat"], group["_m"], group["_v"]
             for a, b, step in self._step_runs(group, runs):
@@ -152,3 +168,26 @@ class AdamW(torch.optim.Optimizer):
 
     def zero_grad(self, set_to_none: bool = True):
         super().zero_grad(set_to_none=set_to_none)
+
+
+class LossScaler:
+    """Dynamic loss scaling for the fp16 mode (torch.cuda.amp.GradScaler's defaults: init
+    2^16, x2 after 2000 finite steps, x0.5 on an inf/NaN step).  Gradients of the density
+    losses are ~1e-7 per element at 2048x2048 (MSE over 3.4e7 pixels): below fp16's normal
+    range unless scaled."""
+
+    def __init__(self, init_scale=65536.0, growth_factor=2.0, backoff_factor=0.5, growth_interval=2000):
+        self.scale = float(init_scale)
+        self.growth_factor, self.backoff_factor = growth_factor, backoff_factor
+        self.growth_interval = growth_interval
+        self._good = 0
+
+    def update(self, found_inf: bool):
+        if found_inf:
+            self.scale *= self.backoff_factor
+            self._good = 0
+        else:
+            self._good += 1
+            if self._good >= self.growth_interval:
+                self.scale *= self.growth_factor
+                self._good = 0

@@ -148,9 +148,40 @@ class DGTrainer(Trainer):
                 loss_total = loss_total + 0.6 * losses[1]
         else:
             raise ValueError(f"Unknown mode: {self.mode}")
-        loss_total.backward()
-        optimizer.step()
+        scaler = self._scaler(model, optimizer)
+        if scaler is None:
+            loss_total.backward()
+            optimizer.step()
+        else:  # fp16 mode: scaled backward, unscaled (or skipped) update
+            (loss_total * scaler.scale).backward()
+            self._scaled_step(optimizer, scaler.scale)
+            scaler.update(getattr(optimizer, "found_inf", False))
         return loss_total.detach().item()
+
+    def _scaler(self, model, optimizer):
+        models = model if isinstance(model, (list, tuple)) else [model]
+        if not any(getattr(m, "precision", None) == "fp16" for m in models):
+            return None
+        if getattr(self, "loss_scaler", None) is None:
+            from ..optim import LossScaler
+            self.loss_scaler = LossScaler()
+        return self.loss_scaler
+
+    @staticmethod
+    def _scaled_step(optimizer, scale):
+        from ..optim import AdamW
+        if isinstance(optimizer, AdamW):
+            optimizer.grad_scale = scale
+            optimizer.step()
+            optimizer.grad_scale = None
+            return
+        grads = [p.grad for g in optimizer.param_groups for p in g["params"] if p.grad is not None]
+        inf = any(not torch.isfinite(gr).all() for gr in grads)
+        optimizer.found_inf = inf
+        if not inf:
+            for gr in grads:
+                gr.div_(scale)
+            optimizer.step()
 
     def _val_batch(self, batch):
         """DenClsDataset val/test samples collated with batch size 1 carry the uint8 image and

@@ -3,10 +3,14 @@ utils/dmap_gen.py.
 
 The reference adds one full-frame scipy.ndimage.gaussian_filter per point
 (O(N*H*W), ~15 ms/point at 768x1024, dmap_gen.py:72-79).  Here every point is a
-15x15 stamp scattered by one wave of a single HIP launch per batch of images
-(dg_dmap_fixed): O(N*225) work.  Values follow scipy's two-pass float32
-rounding; overlapping stamps are summed with fp32 atomics, so the result is
-order-independent to ~1 ulp of the sum (the reference sums in point order).
+15x15 stamp of scipy's two-pass float32 values, in one HIP launch per batch of images:
+
+* default (`deterministic=True`, dg_dmap_fixed_tiled): one block per 16x16 tile sums its
+  points' stamps in point order -- the reference's f32 accumulation order, so the map is
+  bit-identical to the reference and run to run (the reference runs under
+  torch.use_deterministic_algorithms, utils/misc.py:131);
+* `deterministic=False` (or DGVCC_DMAP_ATOMIC=1): one wave per point with f32 atomics
+  (dg_dmap_fixed), order-dependent in the last ulp of overlapping stamps.
 """
 from __future__ import annotations
 
@@ -27,8 +31,11 @@ def _device():
     return torch.device("cuda", torch.cuda.current_device())
 
 
+_ATOMIC = os.environ.get("DGVCC_DMAP_ATOMIC", "0") == "1"
+
+
 def gaussian_filter_density_fixed_batch(points_list, H: int, W: int, sigma: float = SIGMA_FIXED,
-                                        radius: int = RADIUS_FIXED) -> torch.Tensor:
+                                        radius: int = RADIUS_FIXED, deterministic: bool | None = None) -> torch.Tensor:
     """points_list: N tensors [n_i, 2] (x=col, y=row).  Returns [N, H, W] f32 on device."""
     dev = points_list[0].device if len(points_list) and points_list[0].is_cuda else _device()
     counts = [int(p.shape[0]) for p in points_list]
@@ -37,7 +44,8 @@ def gaussian_filter_density_fixed_batch(points_list, H: int, W: int, sigma: floa
         pts = torch.cat([p.to(dev, torch.float32).reshape(-1, 2) for p in points_list]).contiguous()
     else:
         pts = torch.empty((0, 2), dtype=torch.float32, device=dev)
-    return K.dmap_fixed(pts, offs, len(points_list), H, W, sigma, radius)
+    det = (not _ATOMIC) if deterministic is None else deterministic
+    return K.dmap_fixed(pts, offs, len(points_list), H, W, sigma, radius, deterministic=det)
 
 
 def gaussian_filter_density_batch(points_list, H: int, W: int) -> torch.Tensor:

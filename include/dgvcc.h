@@ -11,8 +11,9 @@
  *   - activations are NHWC with an explicit pixel stride `ld` (elements between
  *     consecutive pixels) so channel slices of concatenation buffers are
  *     addressed in place (replaces torch.cat, models/models.py:72,76,84);
- *   - dtype: DG_F32 (parity mode, exact-f32 MFMA) or DG_BF16 (perf mode, bf16
- *     storage + bf16 MFMA, f32 accumulation/statistics).
+ *   - dtype: DG_F32 (parity mode, exact-f32 MFMA), DG_BF16 (perf mode, bf16
+ *     storage + bf16 MFMA, f32 accumulation/statistics) or DG_F16 (fp16 storage +
+ *     f16 MFMA, f32 accumulation/statistics; configs/qnrf_final.yml's precision).
  *   - the library is stateless: no globals, safe to call from any thread.
  */
 #ifndef DGVCC_H
@@ -29,6 +30,7 @@ extern "C" {
 
 #define DG_F32 0
 #define DG_BF16 1
+#define DG_F16 2
 
 /* ---- library ----------------------------------------------------------- */
 int dg_version(void); /* returns DGVCC_ABI_VERSION */
@@ -472,6 +474,9 @@ int dg_bl_prob(const float* points, const int64_t* offsets, int64_t total_points
 int dg_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
                   float beta1, float beta2, float eps, float weight_decay, int step,
                   void* stream);
+/* fp16 mode dynamic loss scaling (torch.cuda.amp.GradScaler semantics): g *= inv_scale in
+ * place over the flat gradient; *nonfinite (device int) = 1 if any element was inf/NaN. */
+int dg_grad_unscale(float* g, int64_t n, float inv_scale, int* nonfinite, void* stream);
 /* Gather `count` tensors (ptrs[i], sizes[i]; device arrays) into a flat buffer. */
 int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
                    int64_t total, float* flat, void* stream);
@@ -482,6 +487,13 @@ int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
  * radius 7 (15x15 normalized separable Gaussian, constant-0 borders). */
 int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
                   float sigma, int radius, float* dmap, void* stream);
+
+/* Deterministic dg_dmap_fixed (no atomics): each 16x16 tile sums its points' stamp values
+ * in point order, the reference's f32 accumulation order: bit-identical to
+ * gaussian_filter_density_fixed and run to run.  dmap fully written (no memset needed);
+ * points may be NULL only when offsets[N] == 0. */
+int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W,
+                        float sigma, int radius, float* dmap, void* stream);
 
 /* gaussian_filter_density (utils/dmap_gen.py:14-51): per-point sigma from the
  * 3 nearest neighbours (0.1 * sum; 15 when <= 3 points), truncate 4.

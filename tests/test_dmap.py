@@ -27,11 +27,38 @@ def test_dmap_fixed_hip(dev, name):
     g = dict(np.load(os.path.join(GOLD, "dmap_fixed.npz")))
     H, W = (int(v) for v in g[name + "__shape"])
     ref = g[name + "__dmap"]
+    # default: the tile-reduce kernel sums in point order like the reference -> bit-identical
     mine = gaussian_filter_density_fixed(np.zeros((H, W)), g[name + "__points"])
+    assert np.array_equal(mine, ref), np.abs(mine - ref).max()
+    # the atomic scatter: order-independent sum vs the reference's point-order sum
+    from dgvcc_amd.utils.dmap_gen import gaussian_filter_density_fixed_batch
+    pts = torch.as_tensor(g[name + "__points"]).reshape(-1, 2).to(dev)
+    at = gaussian_filter_density_fixed_batch([pts], H, W, deterministic=False)[0].cpu().numpy()
     scale = max(np.abs(ref).max(), 1e-30)
-    # fp32 atomics: order-independent sum vs the reference's point-order sum
-    assert np.abs(mine - ref).max() <= 1e-6 * scale
-    assert abs(mine.sum(dtype=np.float64) - ref.sum(dtype=np.float64)) <= 1e-5 * max(1.0, abs(ref.sum()))
+    assert np.abs(at - ref).max() <= 1e-6 * scale
+    assert abs(at.sum(dtype=np.float64) - ref.sum(dtype=np.float64)) <= 1e-5 * max(1.0, abs(ref.sum()))
+
+
+@pytest.mark.gpu
+def test_dmap_fixed_tiled_dense_bit_exact_and_stable(dev):
+    """QNRF-like dense crowd (4000 points, clustered, many overlapping stamps, some outside
+    or on the border, negative coordinates): the deterministic kernel equals the oracle's
+    point-order f32 sum bit for bit, twice in a row, for a batch of ragged images."""
+    from dgvcc_amd.utils.dmap_gen import gaussian_filter_density_fixed_batch
+    rng = np.random.default_rng(5)
+    H, W = 200, 328
+    sets = []
+    for n in (4000, 0, 37):
+        c = rng.uniform([0, 0], [W, H], (max(n // 50, 1), 2))
+        p = c[rng.integers(0, len(c), n)] + rng.normal(0, 6, (n, 2))
+        p[: n // 40] = rng.uniform([-8, -8], [W + 2, H + 2], (n // 40, 2))
+        sets.append(p.astype(np.float32))
+    tp = [torch.from_numpy(p).to(dev) for p in sets]
+    a = gaussian_filter_density_fixed_batch(tp, H, W).cpu().numpy()
+    b = gaussian_filter_density_fixed_batch(tp, H, W).cpu().numpy()
+    assert np.array_equal(a, b)
+    for i, p in enumerate(sets):
+        assert np.array_equal(a[i], dmap_fixed(p, H, W)), i
 
 
 @pytest.mark.gpu

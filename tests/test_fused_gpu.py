@@ -104,7 +104,7 @@ def test_stem_fwd_bwd(dev, N, H, W):
     assert relerr(dw1, dw) < 1e-4
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("with_y,with_gd", [(False, False), (True, True)])
 @pytest.mark.parametrize("C,H,W", [(64, 8, 12), (256, 6, 4), (512, 4, 8)])
 def test_bn_relu_pool_fused(dev, dtype, with_y, with_gd, C, H, W):
@@ -119,9 +119,9 @@ def test_bn_relu_pool_fused(dev, dtype, with_y, with_gd, C, H, W):
     bet = torch.randn(C, generator=g) * 0.2
     gp = torch.randn(N, C, H // 2, W // 2, generator=g)
     gd = torch.randn(N, C, H, W, generator=g) if with_gd else None
-    if dtype == torch.bfloat16:
-        z, gp = z.bfloat16().float(), gp.bfloat16().float()
-        gd = gd.bfloat16().float() if gd is not None else None
+    if dtype != torch.float32:
+        z, gp = z.to(dtype).float(), gp.to(dtype).float()
+        gd = gd.to(dtype).float() if gd is not None else None
     zd = K.Act(to_nhwc(z).to(dev, dtype))
     stats = K.bn_fwd_train(zd, gam.to(dev), bet.to(dev), torch.zeros(C, device=dev),
                            torch.ones(C, device=dev), 0.1, 1e-5)
@@ -334,7 +334,7 @@ def test_dgrad_epilogue_bn_partials(dev, monkeypatch, N, H, W, C, Cin_next, act,
     assert (dz1.buf.float() - dz0.buf.float()).abs().max() <= 2 * dz0.buf.float().abs().max() * 2 ** -8
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("N,H,W,C,Cout,act", [(1, 24, 32, 256, 512, 1), (2, 16, 256, 64, 64, 1), (1, 32, 48, 128, 128, 0)])
 def test_conv_bn_eval_epilogue(dev, dtype, N, H, W, C, Cout, act):
     """dg_conv_fwd_bn_eval (eval BN + ReLU in the conv epilogue) against dg_conv_fwd +
@@ -395,11 +395,15 @@ def test_tap3_padded_index(dev, monkeypatch, N, H, W, C, acc):
 
 
 @pytest.mark.parametrize("N,H,W,C,Cout,stats", [(5, 128, 256, 64, 256, True), (3, 96, 320, 128, 128, True),
-                                                (5, 128, 256, 128, 256, False)])
+                                                (5, 128, 256, 128, 256, False), (2, 48, 64, 128, 1024, False),
+                                                (2, 48, 64, 128, 1024, "eval"), (3, 64, 64, 64, 256, "eval"),
+                                                (3, 64, 64, 128, 128, "eval")])
 def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
     """The persistent pipelined forward (tiles walked by one block per CU, DMA ring running
     across tile boundaries) against the one-tile-per-block kernel: bit-identical outputs and
-    statistics partials (same K order per tile)."""
+    statistics partials (same K order per tile); Cout = 1024 (two passes of the block's LDS
+    bias fill); the eval-BN epilogue (bias, scale, shift staged in LDS, or read from global
+    memory when 3 x Cout floats exceed the statistics scratch: the 1024-channel 128-wide case)."""
     K = _k()
     bf = torch.bfloat16
     g = torch.Generator().manual_seed(13)
@@ -412,7 +416,12 @@ def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
         monkeypatch.setenv("DGVCC_PERSIST", pers)
         K.call("dg_set_persist", int(pers))
         z = K.Act(K.nhwc(N, H, W, Cout, bf, dev))
-        if stats:
+        if stats == "eval":
+            st = torch.stack([torch.zeros(Cout), torch.ones(Cout), torch.rand(Cout, generator=g) + 0.5,
+                              torch.randn(Cout, generator=g) * 0.1]).to(dev) if pers == "0" else st
+            K.conv_fwd_bn_eval(K.Act(x), wp, Cout, 3, 1, z, b, st, 1)
+            outs.append((z.buf.clone(), None))
+        elif stats:
             res = K.conv_fwd_stats(K.Act(x), wp, Cout, 3, 1, z, bias=b)
             outs.append((z.buf.clone(), res[0].clone()))
         else:
@@ -421,7 +430,7 @@ def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
     K.call("dg_set_persist", -1)
     torch.cuda.synchronize()
     assert torch.equal(outs[0][0], outs[1][0])
-    if stats:
+    if stats is True:
         assert torch.equal(outs[0][1], outs[1][1])
 
 

@@ -30,6 +30,8 @@ def relerr(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
+DTYPES = [torch.float32, torch.bfloat16, torch.float16]
+
 CONV_CASES = [
     # N, H, W, C, Cout, R
     (2, 20, 24, 64, 128, 3),
@@ -44,7 +46,7 @@ CONV_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", CONV_CASES)
 def test_conv_fwd_dgrad_wgrad(dev, dtype, case):
     K = _k()
@@ -55,10 +57,10 @@ def test_conv_fwd_dgrad_wgrad(dev, dtype, case):
     w = torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5
     b = torch.randn(Cout, generator=g)
     gy = torch.randn(N, Cout, H, W, generator=g)
-    if dtype == torch.bfloat16:  # reference on the rounded operands
-        x = x.bfloat16().float()
-        w = w.bfloat16().float()
-        gy = gy.bfloat16().float()
+    if dtype != torch.float32:  # reference on the rounded operands
+        x = x.to(dtype).float()
+        w = w.to(dtype).float()
+        gy = gy.to(dtype).float()
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, b, padding=pad)
@@ -125,7 +127,7 @@ def test_first_layer_im2col(dev):
     assert relerr(dw, wr.grad) < 2e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("C,H,W", [(64, 12, 10), (256, 16, 16), (512, 8, 8), (1024, 6, 4), (128, 40, 33)])
 def test_bn_train_fwd_bwd(dev, dtype, act, C, H, W):
@@ -133,13 +135,13 @@ def test_bn_train_fwd_bwd(dev, dtype, act, C, H, W):
     N = 2
     g = torch.Generator().manual_seed(3)
     z = (torch.randn(N, C, H, W, generator=g) * 3 + 5)
-    if dtype == torch.bfloat16:
-        z = z.bfloat16().float()
+    if dtype != torch.float32:
+        z = z.to(dtype).float()
     gam = torch.rand(C, generator=g) + 0.5
     bet = torch.randn(C, generator=g)
     gy = torch.randn(N, C, H, W, generator=g)
-    if dtype == torch.bfloat16:
-        gy = gy.bfloat16().float()
+    if dtype != torch.float32:
+        gy = gy.to(dtype).float()
     bn = torch.nn.BatchNorm2d(C)
     bn.weight.data.copy_(gam)
     bn.bias.data.copy_(bet)
@@ -167,7 +169,7 @@ def test_bn_train_fwd_bwd(dev, dtype, act, C, H, W):
     assert relerr(dgam, bn.weight.grad) < 1e-4 and relerr(dbet, bn.bias.grad) < 1e-4
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", DTYPES)
 def test_maxpool(dev, dtype):
     K = _k()
     N, H, W, C = 2, 8, 12, 64
@@ -187,7 +189,7 @@ def test_maxpool(dev, dtype):
     assert torch.equal(to_nchw(gx.buf.float()).cpu(), xr.grad)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("scale,mode,C", [(2, 0, 64), (4, 0, 512), (4, 2, 1), (16, 1, 1), (4, 0, 1), (2, 1, 16)])
 def test_upsample(dev, dtype, scale, mode, C):
     K = _k()

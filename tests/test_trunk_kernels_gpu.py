@@ -29,7 +29,7 @@ CONV2D_CASES = [
 ]
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("case", CONV2D_CASES)
 def test_conv2d_general(dev, dtype, case):
     K = _k()
@@ -40,8 +40,8 @@ def test_conv2d_general(dev, dtype, case):
     b = torch.randn(Cout, generator=g)
     P, Q = K.conv_out(H, R, s, p), K.conv_out(W, R, s, p)
     gy = torch.randn(N, Cout, P, Q, generator=g)
-    if dtype == torch.bfloat16:
-        x, w, gy = x.bfloat16().float(), w.bfloat16().float(), gy.bfloat16().float()
+    if dtype != torch.float32:
+        x, w, gy = x.to(dtype).float(), w.to(dtype).float(), gy.to(dtype).float()
     xr = x.clone().requires_grad_(True)
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(xr, wr, b, stride=s, padding=p)
@@ -85,7 +85,7 @@ def test_conv2d_slices_accumulate(dev):
     assert relerr(out, exp) < 2e-5
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_stem_im2col_7x7(dev, dtype):
     """ResNet stem conv1 7x7/2 pad 3, Cin=3 -> 64 (resnet_ibn.py:158) as a 1x1 GEMM
     over im2col rows (K = 147 padded to 192)."""
@@ -96,8 +96,8 @@ def test_stem_im2col_7x7(dev, dtype):
     w = torch.randn(Cout, 3, R, R, generator=g) / 147 ** 0.5
     P, Q = K.conv_out(H, R, s, p), K.conv_out(W, R, s, p)
     gy = torch.randn(N, Cout, P, Q, generator=g)
-    if dtype == torch.bfloat16:
-        img, w, gy = img.bfloat16().float(), w.bfloat16().float(), gy.bfloat16().float()
+    if dtype != torch.float32:
+        img, w, gy = img.to(dtype).float(), w.to(dtype).float(), gy.to(dtype).float()
     wr = w.clone().requires_grad_(True)
     yr = F.conv2d(img, wr, stride=s, padding=p)
     yr.backward(gy)
@@ -117,7 +117,7 @@ def test_stem_im2col_7x7(dev, dtype):
     assert relerr(dw, wr.grad) < (2e-5 if dtype == torch.float32 else 2e-3)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(2, 64, 17, 15), (1, 128, 16, 16), (1, 64, 2, 3)])
 def test_maxpool_3x3_s2(dev, dtype, shape):
     """nn.MaxPool2d(3, 2, 1) with ties (first max wins, as ATen's CPU kernel)."""
@@ -128,8 +128,8 @@ def test_maxpool_3x3_s2(dev, dtype, shape):
     xr = x.clone().requires_grad_(True)
     yr = F.max_pool2d(xr, 3, 2, 1)
     gy = torch.randn(yr.shape, generator=g)
-    if dtype == torch.bfloat16:
-        gy = gy.bfloat16().float()
+    if dtype != torch.float32:
+        gy = gy.to(dtype).float()
     yr.backward(gy)
     P, Q = yr.shape[2:]
     xd = K.Act(to_nhwc(x).to(dev, dtype))
@@ -150,7 +150,7 @@ def test_maxpool_3x3_s2(dev, dtype, shape):
     assert torch.equal(y2.buf, y.buf) and torch.equal(gx2.buf, gx.buf)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("downsample", [False, True])
 def test_bn_add_relu_join(dev, dtype, downsample):
     K = _k()
@@ -160,8 +160,8 @@ def test_bn_add_relu_join(dev, dtype, downsample):
     z2 = torch.randn(N, H, W, C, generator=g)
     st1 = torch.randn(4, C, generator=g)
     st2 = torch.randn(4, C, generator=g)
-    if dtype == torch.bfloat16:
-        z1, z2 = z1.bfloat16().float(), z2.bfloat16().float()
+    if dtype != torch.float32:
+        z1, z2 = z1.to(dtype).float(), z2.to(dtype).float()
     short = z2 * st2[2] + st2[3] if downsample else z2
     ref = torch.relu(z1 * st1[2] + st1[3] + short)
     y = K.Act(K.nhwc(N, H, W, C, dtype, dev))
@@ -177,7 +177,7 @@ def test_bn_add_relu_join(dev, dtype, downsample):
     assert torch.equal(gout.buf.float().cpu(), gg.to(dtype).float() * mask)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("affine", [True, False])
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("shape", [(2, 64, 13, 11), (3, 128, 32, 20)])
@@ -190,8 +190,8 @@ def test_instance_norm(dev, dtype, affine, act, shape):
     gam = torch.randn(C, generator=g) if affine else None
     bet = torch.randn(C, generator=g) if affine else None
     gy = torch.randn(N, C, H, W, generator=g)
-    if dtype == torch.bfloat16:
-        x, gy = x.bfloat16().float(), gy.bfloat16().float()
+    if dtype != torch.float32:
+        x, gy = x.to(dtype).float(), gy.to(dtype).float()
     xr = x.clone().requires_grad_(True)
     gr = gam.clone().requires_grad_(True) if affine else None
     br = bet.clone().requires_grad_(True) if affine else None
@@ -228,7 +228,7 @@ def _sw_params(C, g):
                 running_cov=torch.eye(16).repeat(C // 16, 1, 1))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("shape", [(3, 64, 9, 7), (2, 256, 6, 5), (2, 32, 12, 10)])
 @pytest.mark.parametrize("act", [0, 1])
 def test_switch_whiten(dev, dtype, shape, act):
@@ -240,8 +240,8 @@ def test_switch_whiten(dev, dtype, shape, act):
     g = torch.Generator().manual_seed(7)
     x = torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3
     gy = torch.randn(N, C, H, W, generator=g)
-    if dtype == torch.bfloat16:
-        x, gy = x.bfloat16().float(), gy.bfloat16().float()
+    if dtype != torch.float32:
+        x, gy = x.to(dtype).float(), gy.to(dtype).float()
     p = _sw_params(C, g)
     sd = {k: v.double().clone().requires_grad_(k in ("sw_mean_weight", "sw_var_weight", "weight", "bias"))
           for k, v in p.items()}
@@ -271,7 +271,7 @@ def test_switch_whiten(dev, dtype, shape, act):
     assert relerr(pd["running_cov"], sd["running_cov"]) < (1e-4 if f32 else 1e-2)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("C", [64, 256])
 def test_iw_loss_and_grad(dev, dtype, C):
     """instance_whitening_loss (models/ISW/instance_whitening.py:19-39): per-instance
@@ -283,8 +283,8 @@ def test_iw_loss_and_grad(dev, dtype, C):
     g = torch.Generator().manual_seed(8)
     f = torch.randn(N, C, H, W, generator=g)
     f = f + 0.4 * f[:, :1]
-    if dtype == torch.bfloat16:
-        f = f.bfloat16().float()
+    if dtype != torch.float32:
+        f = f.to(dtype).float()
     var = TO.cov_variance(f.double())
     mask, ns = TO.sensitive_mask(var, 1)
     fr = f.double().requires_grad_(True)
@@ -299,16 +299,19 @@ def test_iw_loss_and_grad(dev, dtype, C):
     nsd = torch.tensor(ns, device=dev)
     K.iw_loss(fraw, H * W, mask.float().to(dev), nsd, 1.0 / 3.0, loss, accumulate=True, want_grad=False)
     gt = K.Act(K.nhwc(N, H, W, C, dtype, dev, zero=True))
-    hook = TR._iw_grad_hook(w, fraw, mask.float().to(dev), nsd, 1.0 / 3.0, torch.ones((), device=dev))
+    # fp16: the trainer's loss scale reaches this hook as its upstream coefficient (the unscaled
+    # gradient, ~1e-5 here, would sit in f16's subnormal range)
+    gscale = 1024.0 if dtype == torch.float16 else 1.0
+    hook = TR._iw_grad_hook(w, fraw, mask.float().to(dev), nsd, 1.0 / 3.0, torch.full((), gscale, device=dev))
     hook(gt)
     torch.cuda.synchronize()
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert relerr(vd, var) < (1e-4 if dtype == torch.float32 else 3e-2)
     assert abs(loss.item() - loss_ref.item()) <= tol * abs(loss_ref.item())
-    assert relerr(to_nchw(gt.buf.float()), fr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
+    assert relerr(to_nchw(gt.buf.float()) / gscale, fr.grad) < (1e-5 if dtype == torch.float32 else 1e-2)
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 def test_bias_relu_bwd_no_norm(dev, dtype):
     """dg_bn_bwd without normalisation (counter-head Conv+bias+ReLU): dz = g*(z>0),
     dbias = sum dz."""
@@ -317,8 +320,8 @@ def test_bias_relu_bwd_no_norm(dev, dtype):
     g = torch.Generator().manual_seed(9)
     z = torch.randn(N, H, W, C, generator=g)
     gy = torch.randn(N, H, W, C, generator=g)
-    if dtype == torch.bfloat16:
-        z, gy = z.bfloat16().float(), gy.bfloat16().float()
+    if dtype != torch.float32:
+        z, gy = z.to(dtype).float(), gy.to(dtype).float()
     dz = K.Act(K.nhwc(N, H, W, C, dtype, dev))
     db = torch.empty(C, device=dev)
     dbias = torch.empty(C, device=dev)
