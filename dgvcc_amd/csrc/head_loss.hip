@@ -341,20 +341,87 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
   }
 }
 
-// Deterministic variant (no atomics): one 256-thread block per 16x16 output tile of one image
-// walks that image's points in order and each thread sums its pixel's stamp values in that
-// order, the reference's `density += gaussian_filter(pt2d)` f32 accumulation (dmap_gen.py:
-// 72-79) exactly, so the map is bit-identical to the reference's and stable run to run.
-// Points are staged 256 at a time in LDS as (row, col) after int() truncation and numpy's
-// negative-index wrap; a point whose stamp misses the tile costs one uniform compare.
+// Deterministic variant (no atomics on the map): every output pixel sums its stamp values in
+// point order, the reference's `density += gaussian_filter(pt2d)` f32 accumulation
+// (dmap_gen.py:72-79) exactly, so the map is bit-identical to the reference's and stable run
+// to run.  The points are first binned by 16x16 output tile (count -> scan -> fill; a point
+// lands in the <= 4 tiles its 15x15 stamp touches), then one 256-thread block per tile sorts
+// its bin back into point order in LDS (rank sort: bins arrive in atomic order) and each
+// thread accumulates its pixel.  Work is O(points + pixels); a tile whose bin exceeds DM_CAP
+// (an extremely dense crowd) walks all of its image's points instead, same order, same sums.
 constexpr int DMT = 16;
+constexpr int DM_CAP = 1024;
+
+// int() truncation and numpy's negative-index wrap of gaussian_filter_density_fixed
+__device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long long q, int H, int W, int& r, int& c) {
+  r = (int)pts[2 * q + 1];
+  c = (int)pts[2 * q];
+  const bool in = r < H && c < W;
+  if (r < 0) r += H;
+  if (c < 0) c += W;
+  return in && r >= 0 && c >= 0;
+}
+
+// pass 0 (count) / 1 (fill): bin every point into the tiles its stamp touches
+template <int PASS>
+__global__ __launch_bounds__(256) void dmap_bin_kernel(const float* __restrict__ pts, const int64_t* __restrict__ offsets,
+                                                       int H, int W, int radius, int* __restrict__ cnt,
+                                                       int* __restrict__ list) {
+  const int n = blockIdx.y;
+  const int tiles_h = (H + DMT - 1) / DMT, tiles_w = (W + DMT - 1) / DMT;
+  const long long T = (long long)tiles_h * tiles_w;
+  const long long p0 = offsets[n], p1 = offsets[n + 1];
+  for (long long q = p0 + blockIdx.x * 256ll + threadIdx.x; q < p1; q += (long long)gridDim.x * 256) {
+    int r, c;
+    if (!dm_point(pts, q, H, W, r, c)) continue;
+    const int tr0 = max(0, r - radius) / DMT, tr1 = min(H - 1, r + radius) / DMT;
+    const int tc0 = max(0, c - radius) / DMT, tc1 = min(W - 1, c + radius) / DMT;
+    for (int tr = tr0; tr <= tr1; ++tr)
+      for (int tc = tc0; tc <= tc1; ++tc) {
+        int* slot = cnt + n * T + (long long)tr * tiles_w + tc;
+        if (PASS == 0) {
+          atomicAdd(slot, 1);
+        } else {
+          list[atomicAdd(slot, 1)] = (int)(q - p0);
+        }
+      }
+  }
+}
+
+// exclusive scan of the bin counts (one 1024-thread block): start[i], start[total] = sum;
+// cnt becomes the fill cursor (= start)
+__global__ __launch_bounds__(1024) void dmap_bin_scan(int* __restrict__ cnt, long long total, int* __restrict__ start) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const long long seg = (total + 1023) / 1024, a = t * seg, b = min(total, a + seg);
+  int s = 0;
+  for (long long i = a; i < b; ++i) s += cnt[i];
+  part[t] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int run = part[t] - s;
+  for (long long i = a; i < b; ++i) {
+    const int c = cnt[i];
+    start[i] = run;
+    cnt[i] = run;
+    run += c;
+  }
+  if (t == 1023) start[total] = part[1023];
+}
+
 __global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __restrict__ pts,
                                                                const int64_t* __restrict__ offsets, int H, int W,
-                                                               float sigma, int radius, float* __restrict__ dmap) {
+                                                               float sigma, int radius, const int* __restrict__ start,
+                                                               const int* __restrict__ list, float* __restrict__ dmap) {
   __shared__ float stamp[32 * 32];
   __shared__ double wd[64];
   __shared__ float wf[64];
-  __shared__ int prow[256], pcol[256];
+  __shared__ int sidx[DM_CAP], prow[DM_CAP], pcol[DM_CAP];
   const int K = 2 * radius + 1;
   const int tid = threadIdx.x;
   if (tid < K) {
@@ -370,30 +437,49 @@ __global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __re
     stamp[di * 32 + dj] = (float)((double)wf[di] * wd[dj]);  // scipy's two float32 passes
   }
   const int tiles_w = (W + DMT - 1) / DMT;
+  const long long T = (long long)((H + DMT - 1) / DMT) * tiles_w;
   const int ty0 = (blockIdx.x / tiles_w) * DMT, tx0 = (blockIdx.x % tiles_w) * DMT;
   const int n = blockIdx.y;
   const int pr = ty0 + tid / DMT, pc = tx0 + tid % DMT;
   const long long p0 = offsets[n], p1 = offsets[n + 1];
+  const long long b = n * T + blockIdx.x;
+  const int s0 = start ? start[b] : 0, m = start ? start[b + 1] - s0 : 0;
   float acc = 0.f;
-  for (long long base = p0; base < p1; base += 256) {
+  if (m <= DM_CAP) {
+    for (int e = tid; e < m; e += 256) sidx[e] = list[s0 + e];
     __syncthreads();
-    const long long q = base + tid;
-    if (q < p1) {
-      int r = (int)pts[2 * q + 1], c = (int)pts[2 * q];
-      bool ok = r < H && c < W;
-      if (r < 0) r += H;
-      if (c < 0) c += W;
-      ok = ok && r >= 0 && c >= 0;
-      prow[tid] = ok ? r : -1000000;
-      pcol[tid] = ok ? c : -1000000;
+    for (int e = tid; e < m; e += 256) {  // rank = position in point order (indices are unique)
+      const int v = sidx[e];
+      int rank = 0;
+      for (int j = 0; j < m; ++j) rank += sidx[j] < v;
+      int r, c;
+      dm_point(pts, p0 + v, H, W, r, c);
+      prow[rank] = r;
+      pcol[rank] = c;
     }
     __syncthreads();
-    const int cnt = (int)min(256ll, p1 - base);
-    for (int j = 0; j < cnt; ++j) {
-      const int r = prow[j], c = pcol[j];
-      if (r + radius < ty0 || r - radius >= ty0 + DMT || c + radius < tx0 || c - radius >= tx0 + DMT) continue;
-      const int di = pr - r + radius, dj = pc - c + radius;
+    for (int j = 0; j < m; ++j) {
+      const int di = pr - prow[j] + radius, dj = pc - pcol[j] + radius;
       if ((unsigned)di < (unsigned)K && (unsigned)dj < (unsigned)K) acc += stamp[di * 32 + dj];
+    }
+  } else {  // over-full bin: walk every point of the image in order, 256 at a time
+    for (long long base = p0; base < p1; base += 256) {
+      __syncthreads();
+      const long long q = base + tid;
+      if (q < p1) {
+        int r, c;
+        const bool ok = dm_point(pts, q, H, W, r, c);
+        prow[tid] = ok ? r : -1000000;
+        pcol[tid] = ok ? c : -1000000;
+      }
+      __syncthreads();
+      const int cnt = (int)min(256ll, p1 - base);
+      for (int j = 0; j < cnt; ++j) {
+        const int r = prow[j], c = pcol[j];
+        if (r + radius < ty0 || r - radius >= ty0 + DMT || c + radius < tx0 || c - radius >= tx0 + DMT) continue;
+        const int di = pr - r + radius, dj = pc - c + radius;
+        if ((unsigned)di < (unsigned)K && (unsigned)dj < (unsigned)K) acc += stamp[di * 32 + dj];
+      }
     }
   }
   if (pr < H && pc < W) dmap[((long long)n * H + pr) * W + pc] = acc;
@@ -574,13 +660,36 @@ extern "C" int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx
   return DG_OK;
 }
 
+static int64_t dmap_tiles(int H, int W) { return (int64_t)((H + DMT - 1) / DMT) * ((W + DMT - 1) / DMT); }
+
+extern "C" int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints) {
+  if (N <= 0 || H <= 0 || W <= 0 || radius < 0 || radius >= 32 || npoints < 0) return DG_ERR_INVALID;
+  const int64_t per_axis = (2 * radius) / DMT + 2;  // tiles one stamp can touch along an axis
+  const int64_t bins = (int64_t)N * dmap_tiles(H, W);
+  return (2 * (bins + 1) + per_axis * per_axis * npoints) * (int64_t)sizeof(int);
+}
+
 extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W, float sigma,
-                                   int radius, float* dmap, void* stream) {
-  DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
-  DG_REQUIRE(points || true);
-  const dim3 grid((unsigned)(((H + DMT - 1) / DMT) * ((W + DMT - 1) / DMT)), (unsigned)N);
-  hipLaunchKernelGGL(dmap_fixed_tiled_kernel, grid, dim3(256), 0, (hipStream_t)stream, points, offsets, H, W, sigma,
-                     radius, dmap);
+                                   int radius, int64_t npoints, void* workspace, float* dmap, void* stream) {
+  DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32 && npoints >= 0);
+  DG_REQUIRE(npoints == 0 || (points && workspace));
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t T = dmap_tiles(H, W), bins = (int64_t)N * T;
+  DG_REQUIRE(T < (1ll << 31) && bins < (1ll << 31));
+  int *cnt = nullptr, *start = nullptr, *list = nullptr;
+  if (npoints > 0) {
+    cnt = (int*)workspace;
+    start = cnt + bins + 1;
+    list = start + bins + 1;
+    if (hipMemsetAsync(cnt, 0, (size_t)bins * sizeof(int), st) != hipSuccess) return DG_ERR_HIP;
+    const dim3 bg((unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (npoints / N + 255) / 256)), (unsigned)N);
+    hipLaunchKernelGGL((dmap_bin_kernel<0>), bg, dim3(256), 0, st, points, offsets, H, W, radius, cnt, list);
+    hipLaunchKernelGGL(dmap_bin_scan, dim3(1), dim3(1024), 0, st, cnt, (long long)bins, start);
+    hipLaunchKernelGGL((dmap_bin_kernel<1>), bg, dim3(256), 0, st, points, offsets, H, W, radius, cnt, list);
+  }
+  const dim3 grid((unsigned)T, (unsigned)N);
+  hipLaunchKernelGGL(dmap_fixed_tiled_kernel, grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius,
+                     (const int*)start, (const int*)list, dmap);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -103,34 +103,64 @@ constexpr int SWC = 16;  // channels per whitening group (sw_cfg num_pergroup)
 constexpr int SW_MAXT = 8;
 
 // Per-(n, block) partial 16x16 covariance of every group, centred on the
-// instance mean: part[n][blk][g][16*16].  A wave owns groups w, w+4, ...; one
-// f32 MFMA 16x16x4 consumes 4 pixels x 16 channels with a == b (lane l holds
-// xc[p + l/16][g*16 + l%16]), so D = sum_p xc xc^T.
+// instance mean: part[n][blk][g][16*16].  The block stages PT pixels x C channels in LDS
+// as centred f32 (16-B vector loads of whole pixel rows: coalesced), then a wave owns groups
+// w, w+4, ...; one f32 MFMA 16x16x4 consumes 4 pixels x 16 channels with a == b (lane l reads
+// xc[p + l/16][g*16 + l%16]), so D = sum_p xc xc^T.  Rows are padded by 16 floats so the
+// four pixel rows of one MFMA operand fall in distinct LDS banks.
+__host__ __device__ inline int sw_pt(int C) { return C <= 128 ? 32 : 16; }
+
+template <typename T>
+__device__ __forceinline__ void sw_stage(const T* __restrict__ src, long long ld, int pb, int p1, int C, int PT,
+                                         const float* __restrict__ sub, float* __restrict__ dst, int RS) {
+  constexpr int V = 16 / (int)sizeof(T);
+  const int cpr = C / V;
+  for (int e = threadIdx.x; e < PT * cpr; e += 256) {
+    const int r = e / cpr, cc = (e - r * cpr) * V;
+    const int p = pb + r;
+    float v[V];
+    if (p < p1) {
+      ldv(src + (long long)p * ld + cc, v);
+      if (sub) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] -= sub[cc + k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) v[k] = 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < V; k += 4) *(f4v*)(dst + r * RS + cc + k) = f4v{v[k], v[k + 1], v[k + 2], v[k + 3]};
+  }
+}
+
 template <typename T, int MAXG>
 __global__ __launch_bounds__(256) void sw_cov_partial(const T* __restrict__ x, long long ldx, int HW, int C, int ppb,
                                                       const float* __restrict__ mu, float* __restrict__ part) {
-  const int n = blockIdx.y, nb = gridDim.x, G = C / SWC;
+  extern __shared__ float sm[];  // Xs[PT][C + 16] | mu[C]
+  const int n = blockIdx.y, nb = gridDim.x, G = C / SWC, RS = C + 16, PT = sw_pt(C);
+  float* Xs = sm;
+  float* ms = sm + PT * RS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kq = lane >> 4, ch = lane & 15;
+  for (int e = threadIdx.x; e < C; e += 256) ms[e] = mu[(long long)n * C + e];
   f4v acc[MAXG];
-  float m[MAXG];
 #pragma unroll
-  for (int q = 0; q < MAXG; ++q) {
-    acc[q] = f4v{0.f, 0.f, 0.f, 0.f};
-    const int g = wave + 4 * q;
-    m[q] = g < G ? mu[(long long)n * C + g * SWC + ch] : 0.f;
-  }
+  for (int q = 0; q < MAXG; ++q) acc[q] = f4v{0.f, 0.f, 0.f, 0.f};
   const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
   const T* xn = x + (long long)n * HW * ldx;
-  for (int p = p0; p < p1; p += 4) {
-    const int pp = p + kq;
-    const bool ok = pp < p1;
+  for (int pb = p0; pb < p1; pb += PT) {
+    __syncthreads();
+    sw_stage(xn, ldx, pb, p1, C, PT, ms, Xs, RS);
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < MAXG; ++q) {
       const int g = wave + 4 * q;
       if (g < G) {
-        const float v = ok ? to_f(xn[(long long)pp * ldx + g * SWC + ch]) - m[q] : 0.f;
-        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, acc[q], 0, 0, 0);
+        for (int k = 0; k < PT; k += 4) {
+          const float v = Xs[(k + kq) * RS + g * SWC + ch];
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(v, v, acc[q], 0, 0, 0);
+        }
       }
     }
   }
@@ -222,18 +252,25 @@ __device__ float sw_newton(SwLds& L, float* Ps, int T, int t) {
 // these [G][272] doubles over ranks between sw_inst_stats and sw_finalize.
 constexpr int SW_MOM = 272;
 
-// One block per group: instance covariances (partials / HW) and the batch moments.
+// One block per (group, instance): the instance covariance (partials / HW).
 __global__ __launch_bounds__(256) void sw_inst_stats(const float* __restrict__ part, int N, int nb, int HW, int C,
-                                                     float* __restrict__ save, double* __restrict__ moments) {
+                                                     float* __restrict__ save) {
+  const int g = blockIdx.x, n = blockIdx.y, G = C / SWC, t = threadIdx.x;
+  float* cov_in = save + (long long)N * C;
+  double s = 0.0;
+  for (int k = 0; k < nb; ++k) s += part[(((long long)n * nb + k) * G + g) * 256 + t];
+  cov_in[((long long)n * G + g) * 256 + t] = (float)(s / HW);
+}
+
+// One block per group: the batch moments over this rank's instances, in instance order.
+__global__ __launch_bounds__(256) void sw_moments(int N, int C, const float* __restrict__ save,
+                                                  double* __restrict__ moments) {
   const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
   const float* mu_in = save;
-  float* cov_in = save + (long long)N * C;
+  const float* cov_in = save + (long long)N * C;
   double s2 = 0.0, s1 = 0.0;
   for (int n = 0; n < N; ++n) {
-    double s = 0.0;
-    for (int k = 0; k < nb; ++k) s += part[(((long long)n * nb + k) * G + g) * 256 + t];
-    const float ci = (float)(s / HW);
-    cov_in[((long long)n * G + g) * 256 + t] = ci;
+    const float ci = cov_in[((long long)n * G + g) * 256 + t];
     const double mi = mu_in[(long long)n * C + g * 16 + i], mj = mu_in[(long long)n * C + g * 16 + j];
     s2 += (double)ci + mi * mj;
     if (t < 16) s1 += mu_in[(long long)n * C + g * 16 + t];
@@ -242,16 +279,18 @@ __global__ __launch_bounds__(256) void sw_inst_stats(const float* __restrict__ p
   if (t < 16) moments[(long long)g * SW_MOM + t] = s1;
 }
 
-// One block per group: batch mean/cov from the (possibly all-reduced) moments over
-// `count` instances (or the running statistics in eval), running-stat update, and
-// for every local instance the Newton-Schulz whitening matrix folded with the affine.
+// One block per (group, instance): batch mean/cov from the (possibly all-reduced) moments
+// over `count` instances (or the running statistics in eval; recomputed per block, the
+// instance-0 block writes them and updates the running statistics), then this instance's
+// Newton-Schulz whitening matrix folded with the affine.
 __global__ __launch_bounds__(256) void sw_finalize(const double* __restrict__ moments, double count, int N, int C,
                                                    int T, float eps, float momentum, const float* mean_w,
                                                    const float* var_w, const float* gamma, const float* beta,
                                                    float* running_mean, float* running_cov, int training,
                                                    float* __restrict__ save) {
   __shared__ SwLds L;
-  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  const int g = blockIdx.x, n = blockIdx.y, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  const bool lead = n == 0;
   float* mu_in = save;
   float* cov_in = mu_in + (long long)N * C;
   float* mu_bn = cov_in + (long long)N * G * 256;
@@ -261,49 +300,50 @@ __global__ __launch_bounds__(256) void sw_finalize(const double* __restrict__ mo
   __shared__ double mbd[16];
   if (t < 16) mbd[t] = moments[(long long)g * SW_MOM + t] / count;
   __syncthreads();
-  float mb, cbn;
+  float cbn;
   if (training) {
     cbn = (float)(moments[(long long)g * SW_MOM + 16 + t] / count - mbd[i] * mbd[j]);
     if (t < 16) {
-      mb = (float)mbd[t];
-      mu_bn[g * 16 + t] = mb;
+      const float mb = (float)mbd[t];
       L.vec[0][t] = mb;
-      float* rm = running_mean + g * 16 + t;
-      *rm = *rm * momentum + (1.f - momentum) * mb;
+      if (lead) {
+        mu_bn[g * 16 + t] = mb;
+        float* rm = running_mean + g * 16 + t;
+        *rm = *rm * momentum + (1.f - momentum) * mb;
+      }
     }
-    cov_bn[g * 256 + t] = cbn;
-    float* rc = running_cov + g * 256 + t;
-    *rc = *rc * momentum + (1.f - momentum) * cbn;
+    if (lead) {
+      cov_bn[g * 256 + t] = cbn;
+      float* rc = running_cov + g * 256 + t;
+      *rc = *rc * momentum + (1.f - momentum) * cbn;
+    }
   } else {
     if (t < 16) {
-      mb = running_mean[g * 16 + t];
-      mu_bn[g * 16 + t] = mb;
+      const float mb = running_mean[g * 16 + t];
       L.vec[0][t] = mb;
+      if (lead) mu_bn[g * 16 + t] = mb;
     }
     cbn = running_cov[g * 256 + t];
-    cov_bn[g * 256 + t] = cbn;
+    if (lead) cov_bn[g * 256 + t] = cbn;
   }
   __syncthreads();
   float a0, a1, b0, b1;
   softmax2(mean_w, a0, a1);
   softmax2(var_w, b0, b1);
-  for (int n = 0; n < N; ++n) {
-    const float ci = cov_in[((long long)n * G + g) * 256 + t];
-    L.S[t] = b0 * cbn + b1 * ci + (i == j ? eps : 0.f);
-    if (t < 16) L.vec[1][t] = a0 * L.vec[0][t] + a1 * mu_in[(long long)n * C + g * 16 + t];  // mixed mean
-    __syncthreads();
-    const float r = sw_newton(L, nullptr, T, t);
-    const float w = L.P[t] * sqrtf(r);
-    const float gi = gamma ? gamma[g * 16 + i] : 1.f;
-    L.X[t] = gi * w;
-    __syncthreads();
-    aff[((long long)n * G + g) * 256 + t] = L.X[t];
-    if (t < 16) {
-      float sacc = 0.f;
-      for (int k = 0; k < 16; ++k) sacc = fmaf(L.X[t * 16 + k], L.vec[1][k], sacc);
-      bias[(long long)n * C + g * 16 + t] = (beta ? beta[g * 16 + t] : 0.f) - sacc;
-    }
-    __syncthreads();
+  const float ci = cov_in[((long long)n * G + g) * 256 + t];
+  L.S[t] = b0 * cbn + b1 * ci + (i == j ? eps : 0.f);
+  if (t < 16) L.vec[1][t] = a0 * L.vec[0][t] + a1 * mu_in[(long long)n * C + g * 16 + t];  // mixed mean
+  __syncthreads();
+  const float r = sw_newton(L, nullptr, T, t);
+  const float w = L.P[t] * sqrtf(r);
+  const float gi = gamma ? gamma[g * 16 + i] : 1.f;
+  L.X[t] = gi * w;
+  __syncthreads();
+  aff[((long long)n * G + g) * 256 + t] = L.X[t];
+  if (t < 16) {
+    float sacc = 0.f;
+    for (int k = 0; k < 16; ++k) sacc = fmaf(L.X[t * 16 + k], L.vec[1][k], sacc);
+    bias[(long long)n * C + g * 16 + t] = (beta ? beta[g * 16 + t] : 0.f) - sacc;
   }
 }
 
@@ -341,43 +381,66 @@ __global__ __launch_bounds__(256) void sw_apply(const T* __restrict__ x, long lo
 
 // ---------------------------------------------------------------- SW bwd --
 // Per-(n, block) partials: GXc[g] = sum_p ge_p (x_p - mu_n)^T (MFMA, a = ge, b = xc)
-// and sgy[g] = sum_p ge_p, where ge = gy * (y > 0) when act == 1.
+// and sgy[g] = sum_p ge_p, where ge = gy * (y > 0) when act == 1.  ge and xc are staged
+// PT pixels at a time in LDS as f32 (coalesced 16-B loads), as in sw_cov_partial.
 // part layout: [n][blk][g][256 + 16]
 template <typename T, int MAXG>
 __global__ __launch_bounds__(256) void sw_bwd_partial(const T* __restrict__ gy, long long ldg, const T* __restrict__ y,
                                                       long long ldy, const T* __restrict__ x, long long ldx, int HW,
                                                       int C, int ppb, int act, const float* __restrict__ mu,
                                                       float* __restrict__ part) {
-  const int n = blockIdx.y, nb = gridDim.x, G = C / SWC;
+  extern __shared__ float sm[];  // Gs[PT][C + 16] | Xs[PT][C + 16] | mu[C]
+  const int n = blockIdx.y, nb = gridDim.x, G = C / SWC, RS = C + 16, PT = sw_pt(C);
+  float* Gs = sm;
+  float* Xs = sm + PT * RS;
+  float* ms = Xs + PT * RS;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kq = lane >> 4, ch = lane & 15;
+  for (int e = threadIdx.x; e < C; e += 256) ms[e] = mu[(long long)n * C + e];
   f4v acc[MAXG];
-  float m[MAXG], sg[MAXG];
+  float sg[MAXG];
 #pragma unroll
   for (int q = 0; q < MAXG; ++q) {
     acc[q] = f4v{0.f, 0.f, 0.f, 0.f};
     sg[q] = 0.f;
-    const int g = wave + 4 * q;
-    m[q] = g < G ? mu[(long long)n * C + g * SWC + ch] : 0.f;
   }
   const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
   const long long base = (long long)n * HW;
-  for (int p = p0; p < p1; p += 4) {
-    const int pp = p + kq;
-    const bool ok = pp < p1;
+  constexpr int V = 16 / (int)sizeof(T);
+  const int cpr = C / V;
+  for (int pb = p0; pb < p1; pb += PT) {
+    __syncthreads();
+    sw_stage(x + base * ldx, ldx, pb, p1, C, PT, ms, Xs, RS);
+    for (int e = threadIdx.x; e < PT * cpr; e += 256) {
+      const int r = e / cpr, cc = (e - r * cpr) * V;
+      const long long p = pb + r;
+      float v[V];
+      if (p < p1) {
+        ldv(gy + (base + p) * ldg + cc, v);
+        if (act == 1) {
+          float yv[V];
+          ldv(y + (base + p) * ldy + cc, yv);
+#pragma unroll
+          for (int k = 0; k < V; ++k) v[k] = yv[k] > 0.f ? v[k] : 0.f;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < V; ++k) v[k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < V; k += 4) *(f4v*)(Gs + r * RS + cc + k) = f4v{v[k], v[k + 1], v[k + 2], v[k + 3]};
+    }
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < MAXG; ++q) {
       const int g = wave + 4 * q;
       if (g < G) {
-        const int c = g * SWC + ch;
-        float ge = 0.f, xc = 0.f;
-        if (ok) {
-          ge = to_f(gy[(base + pp) * ldg + c]);
-          if (act == 1 && !(to_f(y[(base + pp) * ldy + c]) > 0.f)) ge = 0.f;
-          xc = to_f(x[(base + pp) * ldx + c]) - m[q];
+        for (int k = 0; k < PT; k += 4) {
+          const int o = (k + kq) * RS + g * SWC + ch;
+          const float ge = Gs[o];
+          sg[q] += ge;
+          acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ge, Xs[o], acc[q], 0, 0, 0);
         }
-        sg[q] += ge;
-        acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(ge, xc, acc[q], 0, 0, 0);
       }
     }
   }
@@ -396,19 +459,21 @@ __global__ __launch_bounds__(256) void sw_bwd_partial(const T* __restrict__ gy, 
   }
 }
 
-// One block per group: exact adjoint of sw_finalize for every instance (phase A).
+// One block per (group, instance): exact adjoint of sw_finalize for that instance (phase A).
 // coef layout: [n][g][ K(256) | L(256) | c(16) ]  so that
 //   dx_p = K ge_p + L (x_p - mu_n) + c.
-// wpart[g][4] = (da0, da1, db0, db1) partial over n; dgamma/dbeta written.
+// The cross-instance sums leave as per-(n, g) rows of npart [n][g][SW_NP]:
+//   dcov_bn(256) | dmu_bn(16) | dgamma(16) | dbeta(16) | da0-da1 db0-db1
+// and sw_bwd_reduce adds them in instance order.
+constexpr int SW_NP = 320;
 __global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ part, int N, int nb, int HW, int C, int T,
                                                     float eps, const float* mean_w, const float* var_w,
                                                     const float* gamma, const float* __restrict__ save,
-                                                    float* __restrict__ coef, float* __restrict__ wpart,
-                                                    double* __restrict__ bmoments, float* dgamma, float* dbeta) {
+                                                    float* __restrict__ coef, float* __restrict__ npart) {
   __shared__ SwLds L;
   __shared__ float Ps[(SW_MAXT + 1) * 256];
   __shared__ float mv[4][16];  // mu_bn, mixed mean, mu_n, sgy
-  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
+  const int g = blockIdx.x, n = blockIdx.y, G = C / SWC, t = threadIdx.x, i = t >> 4, j = t & 15;
   const float* mu_in = save;
   const float* cov_in = mu_in + (long long)N * C;
   const float* mu_bn = cov_in + (long long)N * G * 256;
@@ -419,108 +484,125 @@ __global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ pa
   const float cbn = cov_bn[g * 256 + t];
   const float gam_i = gamma ? gamma[g * 16 + i] : 1.f;
   const float gam_j = gamma ? gamma[g * 16 + j] : 1.f;
-  if (t < 16) mv[0][t] = mu_bn[g * 16 + t];
-  float dcov_bn = 0.f, dmu_bn = 0.f, dgam = 0.f, dbet = 0.f;
-  float da0 = 0.f, da1 = 0.f, db0 = 0.f, db1 = 0.f;
-  for (int n = 0; n < N; ++n) {
-    const float ci = cov_in[((long long)n * G + g) * 256 + t];
-    // reduce partials of this (n, g)
-    float gx = 0.f, sg = 0.f;
-    for (int k = 0; k < nb; ++k) {
-      const float* o = part + (((long long)n * nb + k) * G + g) * 272;
-      gx += o[t];
-      if (t < 16) sg += o[256 + t];
-    }
-    if (t < 16) {
-      mv[2][t] = mu_in[(long long)n * C + g * 16 + t];
-      mv[1][t] = a0 * mv[0][t] + a1 * mv[2][t];
-      mv[3][t] = sg;
-    }
-    L.S[t] = b0 * cbn + b1 * ci + (i == j ? eps : 0.f);
-    __syncthreads();
-    const float r = sw_newton(L, Ps, T, t);
-    const float sr = sqrtf(r);
-    const float PT = L.P[t];
-    const float W = PT * sr;
-    // H = GXc - sgy (m - mu_n)^T ; dW = diag(gamma) H
-    const float H = gx - mv[3][i] * (mv[1][j] - mv[2][j]);
-    const float dW = gam_i * H;
-    // dgamma_i += sum_j W_ij H_ij ; dbeta_i += sgy_i
-    float wh = W * H;
+  const float ci = cov_in[((long long)n * G + g) * 256 + t];
+  // reduce partials of this (n, g)
+  float gx = 0.f, sg = 0.f;
+  for (int k = 0; k < nb; ++k) {
+    const float* o = part + (((long long)n * nb + k) * G + g) * 272;
+    gx += o[t];
+    if (t < 16) sg += o[256 + t];
+  }
+  if (t < 16) {
+    mv[0][t] = mu_bn[g * 16 + t];
+    mv[2][t] = mu_in[(long long)n * C + g * 16 + t];
+    mv[1][t] = a0 * mv[0][t] + a1 * mv[2][t];
+    mv[3][t] = sg;
+  }
+  L.S[t] = b0 * cbn + b1 * ci + (i == j ? eps : 0.f);
+  __syncthreads();
+  const float r = sw_newton(L, Ps, T, t);
+  const float sr = sqrtf(r);
+  const float PT = L.P[t];
+  const float W = PT * sr;
+  // H = GXc - sgy (m - mu_n)^T ; dW = diag(gamma) H
+  const float H = gx - mv[3][i] * (mv[1][j] - mv[2][j]);
+  const float dW = gam_i * H;
+  // dgamma_i = sum_j W_ij H_ij ; dbeta_i = sgy_i
+  float wh = W * H;
 #pragma unroll
-    for (int o = 8; o > 0; o >>= 1) wh += __shfl_xor(wh, o, 16);
-    if (j == 0) { dgam += wh; dbet += mv[3][i]; }
-    // K = W^T diag(gamma): K_ij = W_ji gamma_j  (store W into X for the transpose)
-    L.X[t] = W;
-    __syncthreads();
-    float* cf = coef + ((long long)n * G + g) * 528;
-    cf[t] = L.X[j * 16 + i] * gam_j;
-    // dm_t = -sum_k W_kt gamma_k sgy_k  (t < 16)
-    float dm = 0.f;
-    if (t < 16) {
-      for (int k = 0; k < 16; ++k) dm -= L.X[k * 16 + t] * (gamma ? gamma[g * 16 + k] : 1.f) * mv[3][k];
-    }
-    // Newton adjoint: G = dP_T
-    L.G[t] = dW * sr;
-    const float dr_w = block_sum256(dW * PT, L.red) * 0.5f / sr;
-    float dA = 0.f;
-    __syncthreads();
-    for (int k = T - 1; k >= 0; --k) {
-      const float* P = Ps + k * 256;
-      L.P2[t] = mm16<false, false>(P, P, i, j);           // P^2
-      L.X[t] = mm16<false, false>(P, L.A, i, j);          // P A
-      __syncthreads();
-      L.P3[t] = mm16<false, false>(L.P2, P, i, j);        // P^3
-      L.Y[t] = mm16<false, false>(L.P2, L.A, i, j);       // P^2 A
-      __syncthreads();
-      dA -= 0.5f * mm16<true, false>(L.P3, L.G, i, j);    // (P^3)^T G
-      const float t1 = mm16<false, true>(L.G, L.Y, i, j);  // G (P^2 A)^T
-      const float u = mm16<false, true>(L.G, L.X, i, j);   // G (P A)^T
-      const float v = mm16<false, true>(L.G, L.A, i, j);   // G A^T
-      __syncthreads();
-      L.Y[t] = u;
-      L.X[t] = v;
-      __syncthreads();
-      const float t2 = mm16<true, false>(P, L.Y, i, j);      // P^T G (P A)^T
-      const float t3 = mm16<true, false>(L.P2, L.X, i, j);   // (P^2)^T G A^T
-      const float gn = 1.5f * L.G[t] - 0.5f * (t1 + t2 + t3);
-      __syncthreads();
-      L.G[t] = gn;
-      __syncthreads();
-    }
-    // A = S r ; r = 1/tr(S)
-    const float dr = dr_w + block_sum256(dA * L.S[t], L.red);
-    const float dS = r * dA + (i == j ? -r * r * dr : 0.f);
-    db0 += block_sum256(dS * cbn, L.red);
-    db1 += block_sum256(dS * ci, L.red);
-    dcov_bn += b0 * dS;
-    // D_n = b1 (dS + dS^T) / HW  (stored in the L slot; E added below)
-    L.X[t] = dS;
-    __syncthreads();
-    cf[256 + t] = b1 * (dS + L.X[j * 16 + i]) / (float)HW;
-    if (t < 16) {
-      da0 += dm * mv[0][t];
-      da1 += dm * mv[2][t];
-      dmu_bn += a0 * dm;
-      cf[512 + t] = a1 * dm / (float)HW;  // dmu_n / HW (completed below)
-    }
-    __syncthreads();
-  }
-  // the batch-statistics adjoints leave through bmoments (all-reduced over ranks by
-  // SyncSwitchWhiten); sw_bwd_coef completes the per-instance coefficients.
-  bmoments[(long long)g * SW_MOM + 16 + t] = dcov_bn;
-  if (t < 16) bmoments[(long long)g * SW_MOM + t] = dmu_bn;
+  for (int o = 8; o > 0; o >>= 1) wh += __shfl_xor(wh, o, 16);
+  float* np = npart + ((long long)n * G + g) * SW_NP;
   if (j == 0) {
-    if (dgamma) dgamma[g * 16 + i] = dgam;
-    if (dbeta) dbeta[g * 16 + i] = dbet;
+    np[272 + i] = wh;
+    np[288 + i] = mv[3][i];
   }
-  const float s0 = block_sum256(t < 16 ? da0 : 0.f, L.red);
-  const float s1 = block_sum256(t < 16 ? da1 : 0.f, L.red);
+  // K = W^T diag(gamma): K_ij = W_ji gamma_j  (store W into X for the transpose)
+  L.X[t] = W;
+  __syncthreads();
+  float* cf = coef + ((long long)n * G + g) * 528;
+  cf[t] = L.X[j * 16 + i] * gam_j;
+  // dm_t = -sum_k W_kt gamma_k sgy_k  (t < 16)
+  float dm = 0.f;
+  if (t < 16) {
+    for (int k = 0; k < 16; ++k) dm -= L.X[k * 16 + t] * (gamma ? gamma[g * 16 + k] : 1.f) * mv[3][k];
+  }
+  // Newton adjoint: G = dP_T
+  L.G[t] = dW * sr;
+  const float dr_w = block_sum256(dW * PT, L.red) * 0.5f / sr;
+  float dA = 0.f;
+  __syncthreads();
+  for (int k = T - 1; k >= 0; --k) {
+    const float* P = Ps + k * 256;
+    L.P2[t] = mm16<false, false>(P, P, i, j);           // P^2
+    L.X[t] = mm16<false, false>(P, L.A, i, j);          // P A
+    __syncthreads();
+    L.P3[t] = mm16<false, false>(L.P2, P, i, j);        // P^3
+    L.Y[t] = mm16<false, false>(L.P2, L.A, i, j);       // P^2 A
+    __syncthreads();
+    dA -= 0.5f * mm16<true, false>(L.P3, L.G, i, j);    // (P^3)^T G
+    const float t1 = mm16<false, true>(L.G, L.Y, i, j);  // G (P^2 A)^T
+    const float u = mm16<false, true>(L.G, L.X, i, j);   // G (P A)^T
+    const float v = mm16<false, true>(L.G, L.A, i, j);   // G A^T
+    __syncthreads();
+    L.Y[t] = u;
+    L.X[t] = v;
+    __syncthreads();
+    const float t2 = mm16<true, false>(P, L.Y, i, j);      // P^T G (P A)^T
+    const float t3 = mm16<true, false>(L.P2, L.X, i, j);   // (P^2)^T G A^T
+    const float gn = 1.5f * L.G[t] - 0.5f * (t1 + t2 + t3);
+    __syncthreads();
+    L.G[t] = gn;
+    __syncthreads();
+  }
+  // A = S r ; r = 1/tr(S)
+  const float dr = dr_w + block_sum256(dA * L.S[t], L.red);
+  const float dS = r * dA + (i == j ? -r * r * dr : 0.f);
+  // mixing-weight adjoints in difference form: softmax2's backward only needs da0 - da1
+  // (dtheta = a0 a1 (da0 - da1) (1, -1)), and summing dm (mu_bn - mu_n), dS (C_bn - C_n)
+  // directly avoids the cancellation of two large sums
+  const float ddb = block_sum256(dS * (cbn - ci), L.red);
+  np[t] = b0 * dS;  // this instance's dcov_bn
+  // D_n = b1 (dS + dS^T) / HW  (stored in the L slot; E added by sw_bwd_coef)
+  L.X[t] = dS;
+  __syncthreads();
+  cf[256 + t] = b1 * (dS + L.X[j * 16 + i]) / (float)HW;
+  if (t < 16) {
+    np[256 + t] = a0 * dm;               // dmu_bn
+    cf[512 + t] = a1 * dm / (float)HW;  // dmu_n / HW (completed by sw_bwd_coef)
+  }
+  const float dda = block_sum256(t < 16 ? dm * (mv[0][t] - mv[2][t]) : 0.f, L.red);
   if (t == 0) {
-    wpart[g * 4 + 0] = s0;
-    wpart[g * 4 + 1] = s1;
-    wpart[g * 4 + 2] = db0;
-    wpart[g * 4 + 3] = db1;
+    np[304] = dda;
+    np[305] = ddb;
+  }
+}
+
+// One block per group: the batch-statistics adjoints (bmoments, all-reduced over ranks by
+// SyncSwitchWhiten), dgamma/dbeta and the mixing-weight partials, summed over this rank's
+// instances in order.
+__global__ __launch_bounds__(256) void sw_bwd_reduce(const float* __restrict__ npart, int N, int C,
+                                                     double* __restrict__ bmoments, float* dgamma, float* dbeta,
+                                                     float* __restrict__ wpart) {
+  const int g = blockIdx.x, G = C / SWC, t = threadIdx.x;
+  double dc = 0.0, dmu = 0.0, dga = 0.0, dbe = 0.0, w4 = 0.0;
+  for (int n = 0; n < N; ++n) {
+    const float* np = npart + ((long long)n * G + g) * SW_NP;
+    dc += np[t];
+    if (t < 16) {
+      dmu += np[256 + t];
+      dga += np[272 + t];
+      dbe += np[288 + t];
+    } else if (t < 18) {
+      w4 += np[304 + t - 16];
+    }
+  }
+  bmoments[(long long)g * SW_MOM + 16 + t] = dc;
+  if (t < 16) {
+    bmoments[(long long)g * SW_MOM + t] = dmu;
+    if (dgamma) dgamma[g * 16 + t] = (float)dga;
+    if (dbeta) dbeta[g * 16 + t] = (float)dbe;
+  } else if (t < 18) {
+    wpart[g * 4 + t - 16] = (float)w4;
   }
 }
 
@@ -552,19 +634,22 @@ __global__ __launch_bounds__(256) void sw_bwd_coef(const double* __restrict__ bm
   }
 }
 
-// softmax backward of the two mixing weights: dtheta = a (da - <a, da>)
+// softmax backward of the two mixing weights: dtheta = a (da - <a, da>) = a0 a1 (da0 - da1) (1, -1)
+// from the per-group differences wpart[g] = (da0 - da1, db0 - db1)
 __global__ void sw_bwd_weights(const float* __restrict__ wpart, int G, const float* mean_w, const float* var_w,
                                float* dmean_w, float* dvar_w) {
   if (threadIdx.x != 0) return;
-  double s[4] = {0, 0, 0, 0};
-  for (int g = 0; g < G; ++g)
-    for (int k = 0; k < 4; ++k) s[k] += wpart[g * 4 + k];
+  double da = 0.0, db = 0.0;
+  for (int g = 0; g < G; ++g) {
+    da += wpart[g * 4 + 0];
+    db += wpart[g * 4 + 1];
+  }
   float a0, a1, b0, b1;
   softmax2(mean_w, a0, a1);
   softmax2(var_w, b0, b1);
-  const double ma = a0 * s[0] + a1 * s[1], mb = b0 * s[2] + b1 * s[3];
-  if (dmean_w) { dmean_w[0] = (float)(a0 * (s[0] - ma)); dmean_w[1] = (float)(a1 * (s[1] - ma)); }
-  if (dvar_w) { dvar_w[0] = (float)(b0 * (s[2] - mb)); dvar_w[1] = (float)(b1 * (s[3] - mb)); }
+  const double ca = (double)a0 * a1 * da, cb = (double)b0 * b1 * db;
+  if (dmean_w) { dmean_w[0] = (float)ca; dmean_w[1] = (float)-ca; }
+  if (dvar_w) { dvar_w[0] = (float)cb; dvar_w[1] = (float)-cb; }
 }
 
 // dx_p = K ge_p + L (x_p - mu_n) + c ; thread = (pixel, group)
@@ -685,7 +770,8 @@ static int64_t sw_ws_core(int N, int HW, int C) {  // partials + coefficients, 8
   const int64_t G = C / SWC, nb = sw_nb(HW);
   const int64_t fwd = std::max<int64_t>(dg_instnorm_workspace(N, HW, C), 0) + (int64_t)N * C * 4 +
                       (int64_t)N * nb * G * 256 * 4;
-  const int64_t bwd = (int64_t)N * nb * G * 272 * 4 + (int64_t)N * G * 528 * 4 + G * 4 * 4;
+  const int64_t bwd = (int64_t)N * nb * G * 272 * 4 + (int64_t)N * G * 528 * 4 + G * 4 * 4 +
+                      (int64_t)N * G * SW_NP * 4;
   return (std::max(fwd, bwd) + 7) / 8 * 8;
 }
 
@@ -728,14 +814,16 @@ extern "C" int dg_sw_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int
   float* part = invstd_scratch + (int64_t)N * C;
   int rc = dg_instnorm_stats(dtype, x, ldx, N, HW, C, 1e-5f, mu, invstd_scratch, w, stream);
   if (rc) return rc;
+  const size_t lds = (size_t)(sw_pt(C) * (C + 16) + C) * 4;
   if (dtype == DG_BF16)
-    SW_DISPATCH_G(sw_cov_partial, bf16, dim3(nb, N), dim3(256), 0, st, (const bf16*)x, ldx, HW, C, ppb, mu, part);
+    SW_DISPATCH_G(sw_cov_partial, bf16, dim3(nb, N), dim3(256), lds, st, (const bf16*)x, ldx, HW, C, ppb, mu, part);
   else if (dtype == DG_F16)
-    SW_DISPATCH_G(sw_cov_partial, f16, dim3(nb, N), dim3(256), 0, st, (const f16*)x, ldx, HW, C, ppb, mu, part);
+    SW_DISPATCH_G(sw_cov_partial, f16, dim3(nb, N), dim3(256), lds, st, (const f16*)x, ldx, HW, C, ppb, mu, part);
   else
-    SW_DISPATCH_G(sw_cov_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)x, ldx, HW, C, ppb, mu, part);
+    SW_DISPATCH_G(sw_cov_partial, float, dim3(nb, N), dim3(256), lds, st, (const float*)x, ldx, HW, C, ppb, mu, part);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sw_inst_stats, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, save, moments);
+  hipLaunchKernelGGL(sw_inst_stats, dim3(G, N), dim3(256), 0, st, part, N, nb, HW, C, save);
+  hipLaunchKernelGGL(sw_moments, dim3(G), dim3(256), 0, st, N, C, (const float*)save, moments);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -752,7 +840,7 @@ extern "C" int dg_sw_fwd_finish(int dtype, const void* x, int64_t ldx, int N, in
   SW_CHECK_SHAPE(dtype, C, T, ldx, ldy);
   hipStream_t st = (hipStream_t)stream;
   const int G = C / SWC;
-  hipLaunchKernelGGL(sw_finalize, dim3(G), dim3(256), 0, st, moments, (double)count, N, C, T, eps, momentum, mean_w,
+  hipLaunchKernelGGL(sw_finalize, dim3(G, N), dim3(256), 0, st, moments, (double)count, N, C, T, eps, momentum, mean_w,
                      var_w, gamma, beta, running_mean, running_cov, training, save);
   DG_CHECK_LAUNCH();
   const float* aff = save + (int64_t)N * C + (int64_t)N * G * 256 + C + (int64_t)G * 256;
@@ -802,18 +890,22 @@ extern "C" int dg_sw_bwd_stats(int dtype, const void* gy, int64_t ldg, const voi
   float* part = (float*)workspace;
   float* coef = part + (int64_t)N * nb * G * 272;
   float* wpart = coef + (int64_t)N * G * 528;
+  float* npart = wpart + (int64_t)G * 4;
+  const size_t lds = (size_t)(2 * sw_pt(C) * (C + 16) + C) * 4;
   if (dtype == DG_BF16)
-    SW_DISPATCH_G(sw_bwd_partial, bf16, dim3(nb, N), dim3(256), 0, st, (const bf16*)gy, ldg, (const bf16*)y, ldy,
+    SW_DISPATCH_G(sw_bwd_partial, bf16, dim3(nb, N), dim3(256), lds, st, (const bf16*)gy, ldg, (const bf16*)y, ldy,
                   (const bf16*)x, ldx, HW, C, ppb, act, mu, part);
   else if (dtype == DG_F16)
-    SW_DISPATCH_G(sw_bwd_partial, f16, dim3(nb, N), dim3(256), 0, st, (const f16*)gy, ldg, (const f16*)y, ldy,
+    SW_DISPATCH_G(sw_bwd_partial, f16, dim3(nb, N), dim3(256), lds, st, (const f16*)gy, ldg, (const f16*)y, ldy,
                   (const f16*)x, ldx, HW, C, ppb, act, mu, part);
   else
-    SW_DISPATCH_G(sw_bwd_partial, float, dim3(nb, N), dim3(256), 0, st, (const float*)gy, ldg, (const float*)y, ldy,
+    SW_DISPATCH_G(sw_bwd_partial, float, dim3(nb, N), dim3(256), lds, st, (const float*)gy, ldg, (const float*)y, ldy,
                   (const float*)x, ldx, HW, C, ppb, act, mu, part);
   DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(sw_bwd_small, dim3(G), dim3(256), 0, st, part, N, nb, HW, C, T, eps, mean_w, var_w, gamma, save,
-                     coef, wpart, bmoments, dgamma, dbeta);
+  hipLaunchKernelGGL(sw_bwd_small, dim3(G, N), dim3(256), 0, st, part, N, nb, HW, C, T, eps, mean_w, var_w, gamma,
+                     save, coef, npart);
+  hipLaunchKernelGGL(sw_bwd_reduce, dim3(G), dim3(256), 0, st, (const float*)npart, N, C, bmoments, dgamma, dbeta,
+                     wpart);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

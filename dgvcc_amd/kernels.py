@@ -452,9 +452,15 @@ def dmap_fixed(points: torch.Tensor, offsets: torch.Tensor, N: int, H: int, W: i
     """deterministic: per-tile in-order sums (bit-identical to the reference); False: one
     wave per point with f32 atomics (order-dependent in the last ulp)."""
     out = torch.empty((N, H, W), dtype=torch.float32, device=offsets.device)
-    fn = "dg_dmap_fixed_tiled" if deterministic else "dg_dmap_fixed"
-    call(fn, ptr(points) if points.numel() else None, ptr(offsets), N, H, W,
-         float(sigma), int(radius), ptr(out), stream())
+    pp = ptr(points) if points.numel() else None
+    if not deterministic:
+        call("dg_dmap_fixed", pp, ptr(offsets), N, H, W, float(sigma), int(radius), ptr(out), stream())
+        return out
+    npts = points.numel() // 2
+    ws = query("dg_dmap_fixed_tiled_workspace", N, H, W, int(radius), npts)
+    work = torch.empty(ws // 4 + 1, dtype=torch.int32, device=offsets.device) if npts else None
+    call("dg_dmap_fixed_tiled", pp, ptr(offsets), N, H, W, float(sigma), int(radius), npts,
+         ptr(work) if work is not None else None, ptr(out), stream())
     return out
 
 

@@ -488,12 +488,15 @@ int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
 int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
                   float sigma, int radius, float* dmap, void* stream);
 
-/* Deterministic dg_dmap_fixed (no atomics): each 16x16 tile sums its points' stamp values
- * in point order, the reference's f32 accumulation order: bit-identical to
- * gaussian_filter_density_fixed and run to run.  dmap fully written (no memset needed);
- * points may be NULL only when offsets[N] == 0. */
+/* Deterministic dg_dmap_fixed (no atomics on the map): the points are binned by 16x16 tile,
+ * each tile's bin is sorted back into point order and every pixel sums its stamp values in
+ * that order, the reference's f32 accumulation order: bit-identical to
+ * gaussian_filter_density_fixed and run to run.  dmap fully written (no memset needed).
+ * npoints = offsets[N] (host value); workspace: dg_dmap_fixed_tiled_workspace bytes (points
+ * and workspace may be NULL when npoints == 0). */
+int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints);
 int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W,
-                        float sigma, int radius, float* dmap, void* stream);
+                        float sigma, int radius, int64_t npoints, void* workspace, float* dmap, void* stream);
 
 /* gaussian_filter_density (utils/dmap_gen.py:14-51): per-point sigma from the
  * 3 nearest neighbours (0.1 * sum; 15 when <= 3 points), truncate 4.

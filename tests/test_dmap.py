@@ -62,6 +62,23 @@ def test_dmap_fixed_tiled_dense_bit_exact_and_stable(dev):
 
 
 @pytest.mark.gpu
+def test_dmap_fixed_tiled_overfull_bin(dev):
+    """A bin above the in-LDS sort capacity (1500 points inside one 16x16 tile, plus a
+    sparse background): that tile walks the image's points in order instead; still
+    bit-identical to the oracle and run to run."""
+    from dgvcc_amd.utils.dmap_gen import gaussian_filter_density_fixed_batch
+    rng = np.random.default_rng(9)
+    H, W = 96, 128
+    p = np.concatenate([rng.uniform([40, 40], [56, 56], (1500, 2)), rng.uniform([0, 0], [W, H], (300, 2))])
+    p = p[rng.permutation(len(p))].astype(np.float32)
+    tp = [torch.from_numpy(p).to(dev)]
+    a = gaussian_filter_density_fixed_batch(tp, H, W).cpu().numpy()
+    b = gaussian_filter_density_fixed_batch(tp, H, W).cpu().numpy()
+    assert np.array_equal(a, b)
+    assert np.array_equal(a[0], dmap_fixed(p, H, W))
+
+
+@pytest.mark.gpu
 def test_dmap_fixed_batch_full_size_mass(dev):
     """768x1024 property: interior points integrate to 1 (the normalized stamp)."""
     from dgvcc_amd.utils.dmap_gen import gaussian_filter_density_fixed_batch
