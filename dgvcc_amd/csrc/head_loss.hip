@@ -344,12 +344,13 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
 // Deterministic variant (no atomics on the map): every output pixel sums its stamp values in
 // point order, the reference's `density += gaussian_filter(pt2d)` f32 accumulation
 // (dmap_gen.py:72-79) exactly, so the map is bit-identical to the reference's and stable run
-// to run.  The points are first binned by 16x16 output tile (count -> scan -> fill; a point
+// to run.  The points are first binned by 16x64 output tile (count -> scan -> fill; a point
 // lands in the <= 4 tiles its 15x15 stamp touches), then one 256-thread block per tile sorts
 // its bin back into point order in LDS (rank sort: bins arrive in atomic order) and each
 // thread accumulates its pixel.  Work is O(points + pixels); a tile whose bin exceeds DM_CAP
 // (an extremely dense crowd) walks all of its image's points instead, same order, same sums.
-constexpr int DMT = 16;
+constexpr int DMT = 16;   // tile rows
+constexpr int DMTW = 64;  // tile columns: 4 consecutive pixels per thread (one 16-B store)
 constexpr int DM_CAP = 1024;
 
 // int() truncation and numpy's negative-index wrap of gaussian_filter_density_fixed
@@ -368,14 +369,14 @@ __global__ __launch_bounds__(256) void dmap_bin_kernel(const float* __restrict__
                                                        int H, int W, int radius, int* __restrict__ cnt,
                                                        int* __restrict__ list) {
   const int n = blockIdx.y;
-  const int tiles_h = (H + DMT - 1) / DMT, tiles_w = (W + DMT - 1) / DMT;
+  const int tiles_h = (H + DMT - 1) / DMT, tiles_w = (W + DMTW - 1) / DMTW;
   const long long T = (long long)tiles_h * tiles_w;
   const long long p0 = offsets[n], p1 = offsets[n + 1];
   for (long long q = p0 + blockIdx.x * 256ll + threadIdx.x; q < p1; q += (long long)gridDim.x * 256) {
     int r, c;
     if (!dm_point(pts, q, H, W, r, c)) continue;
     const int tr0 = max(0, r - radius) / DMT, tr1 = min(H - 1, r + radius) / DMT;
-    const int tc0 = max(0, c - radius) / DMT, tc1 = min(W - 1, c + radius) / DMT;
+    const int tc0 = max(0, c - radius) / DMTW, tc1 = min(W - 1, c + radius) / DMTW;
     for (int tr = tr0; tr <= tr1; ++tr)
       for (int tc = tc0; tc <= tc1; ++tc) {
         int* slot = cnt + n * T + (long long)tr * tiles_w + tc;
@@ -388,42 +389,65 @@ __global__ __launch_bounds__(256) void dmap_bin_kernel(const float* __restrict__
   }
 }
 
-// exclusive scan of the bin counts (one 1024-thread block): start[i], start[total] = sum;
-// cnt becomes the fill cursor (= start)
-__global__ __launch_bounds__(1024) void dmap_bin_scan(int* __restrict__ cnt, long long total, int* __restrict__ start) {
-  __shared__ int part[1024];
+// exclusive scan of the bin counts in three parallel passes: per-1024-bin block scans
+// (start = local prefix, bsum = block total), one block scanning the block totals, then
+// start += block offset (the fill cursor cnt := start, start[total] = sum)
+constexpr int DM_SB = 1024;
+__global__ __launch_bounds__(DM_SB) void dmap_scan_blocks(const int* __restrict__ cnt, long long total,
+                                                          int* __restrict__ start, int* __restrict__ bsum) {
+  __shared__ int sh[DM_SB];
   const int t = threadIdx.x;
-  const long long seg = (total + 1023) / 1024, a = t * seg, b = min(total, a + seg);
-  int s = 0;
-  for (long long i = a; i < b; ++i) s += cnt[i];
-  part[t] = s;
+  const long long i = (long long)blockIdx.x * DM_SB + t;
+  const int v = i < total ? cnt[i] : 0;
+  sh[t] = v;
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = t >= o ? part[t - o] : 0;
+  for (int o = 1; o < DM_SB; o <<= 1) {
+    const int u = t >= o ? sh[t - o] : 0;
     __syncthreads();
-    part[t] += v;
+    sh[t] += u;
     __syncthreads();
   }
-  int run = part[t] - s;
-  for (long long i = a; i < b; ++i) {
-    const int c = cnt[i];
-    start[i] = run;
-    cnt[i] = run;
-    run += c;
-  }
-  if (t == 1023) start[total] = part[1023];
+  if (i < total) start[i] = sh[t] - v;
+  if (t == DM_SB - 1) bsum[blockIdx.x] = sh[t];
 }
 
-__global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __restrict__ pts,
-                                                               const int64_t* __restrict__ offsets, int H, int W,
-                                                               float sigma, int radius, const int* __restrict__ start,
-                                                               const int* __restrict__ list, float* __restrict__ dmap) {
-  __shared__ float stamp[32 * 32];
+__global__ __launch_bounds__(DM_SB) void dmap_scan_sums(int* __restrict__ bsum, int nb, int* __restrict__ total_out) {
+  __shared__ int sh[DM_SB];
+  const int t = threadIdx.x;
+  const int seg = (nb + DM_SB - 1) / DM_SB, a = t * seg, b = min(nb, a + seg);
+  int s = 0;
+  for (int i = a; i < b; ++i) s += bsum[i];
+  sh[t] = s;
+  __syncthreads();
+  for (int o = 1; o < DM_SB; o <<= 1) {
+    const int u = t >= o ? sh[t - o] : 0;
+    __syncthreads();
+    sh[t] += u;
+    __syncthreads();
+  }
+  int run = sh[t] - s;
+  for (int i = a; i < b; ++i) {
+    const int c = bsum[i];
+    bsum[i] = run;
+    run += c;
+  }
+  if (t == DM_SB - 1) *total_out = sh[t];
+}
+
+__global__ __launch_bounds__(256) void dmap_scan_add(int* __restrict__ start, int* __restrict__ cursor, long long total,
+                                                     const int* __restrict__ boff) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int v = start[i] + boff[i / DM_SB];
+  start[i] = v;
+  cursor[i] = v;
+}
+
+// the normalized 15x15 stamp, once per launch: scipy's two float32 passes of the f64 weights
+__global__ void dmap_stamp_kernel(float sigma, int radius, float* __restrict__ stamp) {
   __shared__ double wd[64];
   __shared__ float wf[64];
-  __shared__ int sidx[DM_CAP], prow[DM_CAP], pcol[DM_CAP];
-  const int K = 2 * radius + 1;
-  const int tid = threadIdx.x;
+  const int K = 2 * radius + 1, tid = threadIdx.x;
   if (tid < K) {
     double s = 0.0;
     for (int i = -radius; i <= radius; ++i) s += exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
@@ -432,19 +456,40 @@ __global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __re
     wf[tid] = (float)wd[tid];
   }
   __syncthreads();
-  for (int cell = tid; cell < K * K; cell += 256) {
+  for (int cell = tid; cell < K * K; cell += blockDim.x) {
     const int di = cell / K, dj = cell - (cell / K) * K;
-    stamp[di * 32 + dj] = (float)((double)wf[di] * wd[dj]);  // scipy's two float32 passes
+    stamp[di * 32 + dj] = (float)((double)wf[di] * wd[dj]);
   }
-  const int tiles_w = (W + DMT - 1) / DMT;
+}
+
+__global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __restrict__ pts,
+                                                               const int64_t* __restrict__ offsets, int H, int W,
+                                                               int radius, const float* __restrict__ gstamp,
+                                                               const int* __restrict__ start,
+                                                               const int* __restrict__ list, float* __restrict__ dmap) {
+  __shared__ float stamp[32 * 32];
+  __shared__ int sidx[DM_CAP], prow[DM_CAP], pcol[DM_CAP];
+  const int K = 2 * radius + 1;
+  const int tid = threadIdx.x;
+  for (int cell = tid; cell < K * 32; cell += 256) stamp[cell] = gstamp[cell];
+  const int tiles_w = (W + DMTW - 1) / DMTW;
   const long long T = (long long)((H + DMT - 1) / DMT) * tiles_w;
-  const int ty0 = (blockIdx.x / tiles_w) * DMT, tx0 = (blockIdx.x % tiles_w) * DMT;
+  const int ty0 = (blockIdx.x / tiles_w) * DMT, tx0 = (blockIdx.x % tiles_w) * DMTW;
   const int n = blockIdx.y;
-  const int pr = ty0 + tid / DMT, pc = tx0 + tid % DMT;
+  const int pr = ty0 + tid / 16, pc = tx0 + (tid % 16) * 4;  // pixels (pr, pc .. pc+3)
   const long long p0 = offsets[n], p1 = offsets[n + 1];
   const long long b = n * T + blockIdx.x;
   const int s0 = start ? start[b] : 0, m = start ? start[b + 1] - s0 : 0;
-  float acc = 0.f;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto add = [&](int r, int c) {
+    const int di = pr - r + radius;
+    if ((unsigned)di >= (unsigned)K) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int dj = pc + k - c + radius;
+      if ((unsigned)dj < (unsigned)K) acc[k] += stamp[di * 32 + dj];
+    }
+  };
   if (m <= DM_CAP) {
     for (int e = tid; e < m; e += 256) sidx[e] = list[s0 + e];
     __syncthreads();
@@ -458,10 +503,7 @@ __global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __re
       pcol[rank] = c;
     }
     __syncthreads();
-    for (int j = 0; j < m; ++j) {
-      const int di = pr - prow[j] + radius, dj = pc - pcol[j] + radius;
-      if ((unsigned)di < (unsigned)K && (unsigned)dj < (unsigned)K) acc += stamp[di * 32 + dj];
-    }
+    for (int j = 0; j < m; ++j) add(prow[j], pcol[j]);
   } else {  // over-full bin: walk every point of the image in order, 256 at a time
     for (long long base = p0; base < p1; base += 256) {
       __syncthreads();
@@ -476,13 +518,21 @@ __global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __re
       const int cnt = (int)min(256ll, p1 - base);
       for (int j = 0; j < cnt; ++j) {
         const int r = prow[j], c = pcol[j];
-        if (r + radius < ty0 || r - radius >= ty0 + DMT || c + radius < tx0 || c - radius >= tx0 + DMT) continue;
-        const int di = pr - r + radius, dj = pc - c + radius;
-        if ((unsigned)di < (unsigned)K && (unsigned)dj < (unsigned)K) acc += stamp[di * 32 + dj];
+        if (r + radius < ty0 || r - radius >= ty0 + DMT || c + radius < tx0 || c - radius >= tx0 + DMTW) continue;
+        add(r, c);
       }
     }
   }
-  if (pr < H && pc < W) dmap[((long long)n * H + pr) * W + pc] = acc;
+  if (pr < H) {
+    float* o = dmap + ((long long)n * H + pr) * W + pc;
+    if (pc + 3 < W && (W & 3) == 0) {
+      *(f4v*)o = f4v{acc[0], acc[1], acc[2], acc[3]};
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (pc + k < W) o[k] = acc[k];
+    }
+  }
 }
 
 // fp16 mode loss scaling: g *= inv_scale in place; any non-finite element sets *nonfinite = 1
@@ -660,36 +710,43 @@ extern "C" int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx
   return DG_OK;
 }
 
-static int64_t dmap_tiles(int H, int W) { return (int64_t)((H + DMT - 1) / DMT) * ((W + DMT - 1) / DMT); }
+static int64_t dmap_tiles(int H, int W) { return (int64_t)((H + DMT - 1) / DMT) * ((W + DMTW - 1) / DMTW); }
 
+// workspace (ints): stamp [32*32 floats] | cnt/cursor [bins] | start [bins+1] | bsum [nb+1] | list
 extern "C" int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints) {
   if (N <= 0 || H <= 0 || W <= 0 || radius < 0 || radius >= 32 || npoints < 0) return DG_ERR_INVALID;
-  const int64_t per_axis = (2 * radius) / DMT + 2;  // tiles one stamp can touch along an axis
-  const int64_t bins = (int64_t)N * dmap_tiles(H, W);
-  return (2 * (bins + 1) + per_axis * per_axis * npoints) * (int64_t)sizeof(int);
+  const int64_t per_axis = (2 * radius) / DMT + 2;  // tiles one stamp can touch along an axis (rows bound cols)
+  const int64_t bins = (int64_t)N * dmap_tiles(H, W), nb = (bins + DM_SB - 1) / DM_SB;
+  return (1024 + 2 * bins + 1 + nb + 1 + per_axis * per_axis * npoints) * (int64_t)sizeof(int);
 }
 
 extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W, float sigma,
                                    int radius, int64_t npoints, void* workspace, float* dmap, void* stream) {
-  DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32 && npoints >= 0);
-  DG_REQUIRE(npoints == 0 || (points && workspace));
+  DG_REQUIRE(offsets && dmap && workspace && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
+  DG_REQUIRE(npoints >= 0 && (npoints == 0 || points));
   hipStream_t st = (hipStream_t)stream;
-  const int64_t T = dmap_tiles(H, W), bins = (int64_t)N * T;
+  const int64_t T = dmap_tiles(H, W), bins = (int64_t)N * T, nb = (bins + DM_SB - 1) / DM_SB;
   DG_REQUIRE(T < (1ll << 31) && bins < (1ll << 31));
-  int *cnt = nullptr, *start = nullptr, *list = nullptr;
+  float* stamp = (float*)workspace;
+  int* cnt = (int*)workspace + 1024;
+  int* start = cnt + bins;
+  int* bsum = start + bins + 1;
+  int* list = bsum + nb + 1;
+  hipLaunchKernelGGL(dmap_stamp_kernel, dim3(1), dim3(256), 0, st, sigma, radius, stamp);
   if (npoints > 0) {
-    cnt = (int*)workspace;
-    start = cnt + bins + 1;
-    list = start + bins + 1;
     if (hipMemsetAsync(cnt, 0, (size_t)bins * sizeof(int), st) != hipSuccess) return DG_ERR_HIP;
     const dim3 bg((unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (npoints / N + 255) / 256)), (unsigned)N);
     hipLaunchKernelGGL((dmap_bin_kernel<0>), bg, dim3(256), 0, st, points, offsets, H, W, radius, cnt, list);
-    hipLaunchKernelGGL(dmap_bin_scan, dim3(1), dim3(1024), 0, st, cnt, (long long)bins, start);
+    hipLaunchKernelGGL(dmap_scan_blocks, dim3((unsigned)nb), dim3(DM_SB), 0, st, (const int*)cnt, (long long)bins,
+                       start, bsum);
+    hipLaunchKernelGGL(dmap_scan_sums, dim3(1), dim3(DM_SB), 0, st, bsum, (int)nb, start + bins);
+    hipLaunchKernelGGL(dmap_scan_add, dim3((unsigned)((bins + 255) / 256)), dim3(256), 0, st, start, cnt,
+                       (long long)bins, (const int*)bsum);
     hipLaunchKernelGGL((dmap_bin_kernel<1>), bg, dim3(256), 0, st, points, offsets, H, W, radius, cnt, list);
   }
   const dim3 grid((unsigned)T, (unsigned)N);
-  hipLaunchKernelGGL(dmap_fixed_tiled_kernel, grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius,
-                     (const int*)start, (const int*)list, dmap);
+  hipLaunchKernelGGL(dmap_fixed_tiled_kernel, grid, dim3(256), 0, st, points, offsets, H, W, radius,
+                     (const float*)stamp, npoints > 0 ? (const int*)start : nullptr, (const int*)list, dmap);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

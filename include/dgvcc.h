@@ -488,12 +488,12 @@ int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
 int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
                   float sigma, int radius, float* dmap, void* stream);
 
-/* Deterministic dg_dmap_fixed (no atomics on the map): the points are binned by 16x16 tile,
+/* Deterministic dg_dmap_fixed (no atomics on the map): the points are binned by 16x64 tile,
  * each tile's bin is sorted back into point order and every pixel sums its stamp values in
  * that order, the reference's f32 accumulation order: bit-identical to
  * gaussian_filter_density_fixed and run to run.  dmap fully written (no memset needed).
  * npoints = offsets[N] (host value); workspace: dg_dmap_fixed_tiled_workspace bytes (points
- * and workspace may be NULL when npoints == 0). */
+ * may be NULL when npoints == 0). */
 int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints);
 int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W,
                         float sigma, int radius, int64_t npoints, void* workspace, float* dmap, void* stream);

@@ -1,0 +1,16 @@
+"""Time the density-map scatter (deterministic binned vs atomic) at the bench shapes:
+768x1024 x16 frames (Poisson(500) points) and 2048x2048 x8 (qnrf scale).  usage:
+python tools/bench_dmap.py"""
+import os
+import sys
+from types import SimpleNamespace
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+
+dev = torch.device("cuda", 0)
+for B, H, W in ((16, 768, 1024), (8, 2048, 2048)):
+    r = bench.dmap_roofline(SimpleNamespace(batch=B, height=H, width=W), dev)
+    print(B, H, W, r["points"], "det", r["deterministic"], "atomic", r["atomic"], flush=True)
