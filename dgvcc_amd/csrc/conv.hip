@@ -726,7 +726,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 constexpr int PERS_BIAS_MAX = 1024;  // Cout limit of the persistent forward (LDS bias)
 template <int BN, int STG, int EPI = 0, typename T = bf16>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
-  constexpr int BK = 64;
+  constexpr int ES = (int)sizeof(T);  // element bytes: a K-step row is 128 B (64 x 16-bit or 32 x f32)
+  constexpr int BK = 128 / ES;
   constexpr int AI = BN / 64;
   constexpr int BI = PBM / 64;
   constexpr int TI = BN / 32, TJ = 4;
@@ -762,7 +763,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   const unsigned cbytes = (unsigned)(gchunk * 16);
   unsigned aoff[AI];
 #pragma unroll
-  for (int i = 0; i < AI; ++i) aoff[i] = (unsigned)((((wid * AI + i) * 8 + lrow) * ldw + gchunk * 8) * 2);
+  for (int i = 0; i < AI; ++i) aoff[i] = (unsigned)(((wid * AI + i) * 8 + lrow) * ldw * ES + gchunk * 16);
 
   struct Ctx {
     int px0, co0;
@@ -776,9 +777,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
     const int halo = a.pad * (a.W + 1);
     const int plo = max(0, c.px0 - halo);
     const int phi = min(M, c.px0 + PBM + halo);
-    const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 2);
-    c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 2), 0, win_bytes, 0x00020000);
-    c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.w + (long long)c.co0 * ldw * 2), 0, (unsigned)(BN * ldw * 2),
+    const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * ES);
+    c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * ES), 0, win_bytes, 0x00020000);
+    c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.w + (long long)c.co0 * ldw * ES), 0, (unsigned)(BN * ldw * ES),
                                              0x00020000);
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -794,7 +795,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
     const int r = rs / a.S, s2 = rs - r * a.S;
     char* As = smem + stage * STAGE;
     char* Bs = As + BN * 128;
-    const unsigned kofs = (unsigned)((rs * a.C + cb * BK) * 2);
+    const unsigned kofs = (unsigned)((rs * a.C + cb * BK) * ES);
 #pragma unroll
     for (int i = 0; i < AI; ++i) lds_dma16(c.wr, As + (wid * AI + i) * 1024, aoff[i] + kofs);
     const int dh = r - a.pad, dw = s2 - a.pad;
@@ -803,7 +804,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       const int hh = c.pp[i] + dh, ww = c.pq[i] + dw;
       const bool ok = (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
       const unsigned off =
-          ok ? (unsigned)(((long long)(c.prow[i] + dh * a.W + dw) * a.ldx + cb * BK) * 2) + cbytes : 0xFFFFFFF0u;
+          ok ? (unsigned)(((long long)(c.prow[i] + dh * a.W + dw) * a.ldx + cb * BK) * ES) + cbytes : 0xFFFFFFF0u;
       lds_dma16(c.xr, Bs + (wid * BI + i) * 1024, off);
     }
   };
@@ -1065,6 +1066,14 @@ static bool use_persist() {
   }
   return v == 1;
 }
+
+// DGVCC_F32_PERSIST=0: f32 forwards on the register-staged conv_fwd_kernel (A/B switch)
+static bool use_f32_persist() {
+  const char* e = getenv("DGVCC_F32_PERSIST");
+  return !(e && e[0] == '0');
+}
+static int f32_pers_bn(int Cout);
+static bool f32_pers_ok(const FwdArgs& a);
 
 static int persist_grid() {  // one block per CU (the ring takes most of the LDS)
   static int g = -1;
@@ -1587,6 +1596,19 @@ static bool tap3_pad_ok(const FwdArgs& a) {
   return M * a.ldx * 2 < (1ll << 31) && (long long)a.N * (a.H + 2) * (a.W + 2) < (1ll << 30);
 }
 
+static int f32_pers_bn(int Cout) { return Cout % 256 == 0 && pipe_wide() ? 256 : (Cout % 128 == 0 ? 128 : 64); }
+
+// the shapes the f32 persistent forward serves (and so the f32 shapes with epilogue statistics):
+// more tiles than CUs, > PF K-steps per tile, no split-K / BN-backward epilogue
+static bool f32_pers_ok(const FwdArgs& a) {
+  if (!(use_f32_persist() && use_persist() && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 && a.ldx % 4 == 0 &&
+        a.Cout % 64 == 0 && a.Cout <= PERS_BIAS_MAX && a.R * a.S * (a.C / 32) > 2 &&
+        (long long)a.Cout * a.R * a.S * a.C * 4 < (1ll << 31)))
+    return false;
+  const long long M = (long long)a.N * a.H * a.W;
+  return (long long)dg_cdiv(M, PBM) * (a.Cout / f32_pers_bn(a.Cout)) > 256;
+}
+
 template <typename T>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
@@ -1647,6 +1669,30 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 #undef PIPE_LAUNCH
       DG_CHECK_LAUNCH();
       return DG_OK;
+    }
+  }
+  if constexpr (!Is16<T>::value) {
+    // f32: the persistent LDS-DMA pipeline with 128-B (32-channel) K-steps; each K-step is 4x
+    // the MFMA work of a 16-bit one (v_mfma_f32_16x16x4_f32), so the 2-stage 256-wide ring
+    // hides the DMA latency comfortably.  Epilogue BN statistics (a.part) as in 16-bit.
+    if (f32_pers_ok(a)) {
+      const int np = dg_cdiv(M, PBM);
+      const int bn = f32_pers_bn(a.Cout);
+      const long long tiles = (long long)np * (a.Cout / bn);
+      {
+        const unsigned g = (unsigned)std::min<long long>(tiles, persist_grid());
+        if (a.escale) {
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3, T>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
+        } else {
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
+        }
+        DG_CHECK_LAUNCH();
+        return DG_OK;
+      }
     }
   }
   const int npx = dg_cdiv(M, 128);
@@ -2655,8 +2701,8 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   DG_SUPPORTED(DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0));
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
-  if (part) DG_SUPPORTED(DG_IS16(dtype) && fwd_has_epi_stats(C, Cout, ldx, R, S));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate, part};
+  if (part) DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S) : f32_pers_ok(a));
   {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
      // runs dg_conv_fwd + the statistics pass instead
     FwdArgs q = a;

@@ -127,6 +127,28 @@ def test_first_layer_im2col(dev):
     assert relerr(dw, wr.grad) < 2e-5
 
 
+@pytest.mark.parametrize("case", [(1, 256, 288, 64, 256, 3), (1, 256, 288, 128, 128, 3), (1, 256, 288, 64, 64, 3),
+                                  (1, 256, 288, 256, 512, 1)])
+def test_conv_f32_persistent(dev, monkeypatch, case):
+    """f32 forward/dgrad on the persistent LDS-DMA kernel (> 256 tiles of 256 pixels, 32-channel
+    K-steps; BN = 256 / 128 / 64 and a 1x1) against torch fp32, and against the register-staged
+    conv_fwd_kernel (DGVCC_F32_PERSIST=0, read per launch) within f32 summation-order noise."""
+    test_conv_fwd_dgrad_wgrad(dev, torch.float32, case)
+    K = _k()
+    N, H, W, C, Cout, R = case
+    g = torch.Generator().manual_seed(1)
+    x = K.Act(torch.randn(N, H, W, C, generator=g).to(dev))
+    wp = K.pack_weight((torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5).to(dev), torch.float32)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("DGVCC_F32_PERSIST", flag)
+        y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+        K.conv_fwd(x, wp, Cout, R, R // 2, y)
+        outs.append(y.buf.clone())
+    torch.cuda.synchronize()
+    assert relerr(outs[0], outs[1]) < 2e-6
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("act", [0, 1])
 @pytest.mark.parametrize("C,H,W", [(64, 12, 10), (256, 16, 16), (512, 8, 8), (1024, 6, 4), (128, 40, 33)])
