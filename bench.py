@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 F32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector peak
+HBM_PEAK_GBPS = 8000.0
 PEAKS = {"fp32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_DENSE_PEAK_TFLOPS, "fp16": BF16_DENSE_PEAK_TFLOPS}
 H0, W0 = 768, 1024
 METRIC = "train-step frames/sec at 768×1024, ShanghaiTech-A; MAE vs reference"
@@ -174,6 +175,26 @@ class ConvTimer:
                 n += 1
         return ms, fl, n, nb
 
+    def attainable(self, kinds, peak_tflops, peak_gbps=HBM_PEAK_GBPS):
+        """Per-launch roofline: each launch's lower bound max(FLOP / MFMA peak, algorithmic bytes /
+        HBM peak), summed over the launches, divided by their measured time.  For families that
+        mix MFMA-bound and HBM-bound shapes (the ResNet trunks' 1x1 convs with K = 64..256 are
+        at 25-60 FLOP/B, i.e. HBM-bound) this is the fraction of the attainable rate; the
+        FLOP-only `frac` understates them.  Also the share of launches (by time) that are
+        MFMA-bound."""
+        torch.cuda.synchronize()
+        tmin = tact = tmf = 0.0
+        for k, _sc, s, e, f, b in self.ev:
+            if k not in kinds:
+                continue
+            t = s.elapsed_time(e) * 1e-3
+            tf, tb = f / (peak_tflops * 1e12), b / (peak_gbps * 1e9)
+            tmin += max(tf, tb)
+            tact += t
+            if tf >= tb:
+                tmf += t
+        return (tmin / tact if tact else None), (tmf / tact if tact else None)
+
 
 def build_model(args, precision, dev):
     from dgvcc_amd.models import models as MM
@@ -271,6 +292,9 @@ def run_leg(args, precision, dev, world, rank):
     enc_kinds = ("fwd", "dgrad", "wgrad", "stem", "stem_wgrad")
     enc_ms, enc_flops, _, _ = timer.summary(enc_kinds, scopes=("enc",))
     enc_gemm_ms, enc_gemm_flops, _, _ = timer.summary(("fwd", "dgrad", "wgrad"), scopes=("enc",))
+    att, att_mf = timer.attainable(("fwd", "dgrad"), PEAKS[precision])
+    watt, _ = timer.attainable(("wgrad",), PEAKS[precision])
+    res.update(attainable_frac=att, mfma_bound_share=att_mf, wgrad_attainable_frac=watt)
     res.update(conv_ms=conv_ms, conv_flops=conv_flops, conv_n=conv_n, conv_bytes=conv_bytes,
                wg_ms=wg_ms, wg_flops=wg_flops, enc_ms=enc_ms, enc_flops=enc_flops,
                enc_gemm_ms=enc_gemm_ms, enc_gemm_flops=enc_gemm_flops)
@@ -312,6 +336,9 @@ def roofline(args, precision, r):
            "wgrad_achieved": round(r["wg_flops"] / (r["wg_ms"] * 1e-3) / 1e12, 2) if r["wg_ms"] > 0 else None,
            "wgrad_frac": round(r["wg_flops"] / (r["wg_ms"] * 1e-3) / 1e12 / peak, 4) if r["wg_ms"] > 0 else None,
            "wgrad_ms_per_step": round(r["wg_ms"] / steps, 3),
+           "attainable_frac": round(r["attainable_frac"], 4) if r.get("attainable_frac") else None,
+           "mfma_bound_time_share": round(r["mfma_bound_share"], 4) if r.get("mfma_bound_share") else None,
+           "wgrad_attainable_frac": round(r["wgrad_attainable_frac"], 4) if r.get("wgrad_attainable_frac") else None,
            "step_gemm_tflop_algorithmic": round(tot / 1e12, 4),
            "whole_step_mfma_frac": round(tot / step_s / 1e12 / peak, 4)}
     if r["enc_ms"] > 0:
