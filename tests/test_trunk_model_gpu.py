@@ -44,7 +44,9 @@ def _setup(kind, dev, B=2, H=64, W=64, precision="fp32"):
 
 
 def _oracle(kind, sd0, img, dmaps, dtype, masks=None):
-    sd = {k: (v.to(dtype) if v.is_floating_point() else v.clone()) for k, v in sd0.items()}
+    # detached copies: requires_grad_ below must never reach the caller's sd0 (a later call's
+    # .to() would then return non-leaf tensors whose .grad stays None)
+    sd = {k: (v.detach().to(dtype).clone() if v.is_floating_point() else v.clone()) for k, v in sd0.items()}
     sd = {k: v.requires_grad_(v.is_floating_point() and "running" not in k) for k, v in sd.items()}
     if kind == "isw":
         l1, wt, out = TO.isw_train_forward(img.to(dtype), dmaps.to(dtype), sd,
@@ -82,9 +84,6 @@ def _check_grads(model, g64, g32, tol=GRAD_TOL, sens=None):
             continue
         if mine > max(2 * ref, tol, 3 * (sens or {}).get(k, 0.0)):
             bad[k] = (mine, ref, (sens or {}).get(k))
-    if sens:
-        worst = sorted(((v, k) for k, v in sens.items() if "sw_mean_weight" in k or "sw_var_weight" in k), reverse=True)[:3]
-        print("sensitivity (largest, mixing weights):", worst)
     assert not bad, bad
 
 
