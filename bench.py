@@ -292,6 +292,11 @@ def run_leg(args, precision, dev, world, rank):
     enc_kinds = ("fwd", "dgrad", "wgrad", "stem", "stem_wgrad")
     enc_ms, enc_flops, _, _ = timer.summary(enc_kinds, scopes=("enc",))
     enc_gemm_ms, enc_gemm_flops, _, _ = timer.summary(("fwd", "dgrad", "wgrad"), scopes=("enc",))
+    dump = os.environ.get("DGVCC_BENCH_LAUNCHES")
+    if dump and rank == 0:  # per-launch (kind, scope, ms, GFLOP, MB) of the timed steps, for analysis
+        torch.cuda.synchronize()
+        with open(f"{dump}_{precision}.json", "w") as f:
+            json.dump([(k, sc, s.elapsed_time(e), fl / 1e9, nb / 1e6) for k, sc, s, e, fl, nb in timer.ev], f)
     att, att_mf = timer.attainable(("fwd", "dgrad"), PEAKS[precision])
     watt, _ = timer.attainable(("wgrad",), PEAKS[precision])
     res.update(attainable_frac=att, mfma_bound_share=att_mf, wgrad_attainable_frac=watt)

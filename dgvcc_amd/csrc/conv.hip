@@ -365,6 +365,11 @@ struct GenArgs {
   const float* bias;
   char* y; long long ldy;
   int accumulate;
+  // mode 1 with stride > 1: one launch per output parity class (pa, pb): rows are the dX pixels
+  // with p % stride == pa, q % stride == pb, and the K loop runs over just the taps that reach
+  // them ((p + pad - r) divisible by the stride) -- 1/stride^2 of the taps on average, where the
+  // plain transposed gather multiplies zeros for the rest
+  int pa = -1, pb = -1;
 };
 
 __device__ __forceinline__ bool gen_src(const GenArgs& a, int n, int p, int q, int r, int s, long long& src) {
@@ -392,8 +397,14 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
   constexpr int TILE_BYTES = (BCO + BPX) * 128;
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
 
-  const int PQ = a.P * a.Q;
+  const bool par = a.pa >= 0;  // parity class launch (mode 1, stride > 1)
+  const int Pc = par ? (a.P - a.pa + a.stride - 1) / a.stride : a.P;
+  const int Qc = par ? (a.Q - a.pb + a.stride - 1) / a.stride : a.Q;
+  const int PQ = Pc * Qc;
   const int M = a.N * PQ;
+  const int r0 = par ? (a.pa + a.pad) % a.stride : 0, s0 = par ? (a.pb + a.pad) % a.stride : 0;
+  const int rst = par ? a.stride : 1;
+  const int nr = par ? (a.R - r0 + rst - 1) / rst : a.R, ns = par ? (a.S - s0 + rst - 1) / rst : a.S;
   const int nco = a.Cout / BCO;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int co0 = (bid % nco) * BCO;
@@ -410,19 +421,25 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
     const int m = px0 + rbase + 32 * i;
     const int rem = m % PQ;
     rn[i] = (m < M) ? m / PQ : -1;
-    rp[i] = rem / a.Q;
-    rq[i] = rem % a.Q;
+    rp[i] = rem / Qc;
+    rq[i] = rem % Qc;
+    if (par) {
+      rp[i] = rp[i] * a.stride + a.pa;
+      rq[i] = rq[i] * a.stride + a.pb;
+    }
   }
   const int CB = a.C / BK;
-  const int KT = a.R * a.S * CB;
+  const int KT = nr * ns * CB;
   const long long ldw = (long long)a.R * a.S * a.C;
   const T* wp = (const T*)a.w + (long long)(co0 + rbase) * ldw + chunk * EPC;
 
   u4v ra[AR], rb[BR];
 #define GEN_GLOAD(t_) \
   do { \
-    const int rs = (t_) / CB, cb = (t_) - rs * CB; \
-    const int r = rs / a.S, s = rs - r * a.S; \
+    const int ti = (t_) / CB, cb = (t_) - ti * CB; \
+    const int tr = ti / ns; \
+    const int r = r0 + rst * tr, s = s0 + rst * (ti - tr * ns); \
+    const int rs = r * a.S + s; \
     const int coff = cb * BK + chunk * EPC; \
     _Pragma("unroll") for (int i = 0; i < AR; ++i) ra[i] = *(const u4v*)(wp + (long long)(32 * i) * ldw + rs * a.C + cb * BK); \
     _Pragma("unroll") for (int i = 0; i < BR; ++i) { \
@@ -448,8 +465,10 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
   const int wco = (wid >> 1) * (BCO / 2), wpx = (wid & 1) * (BPX / 2);
   const int fr = lane & 15, fc = lane >> 4;
 
-  GEN_GLOAD(0);
-  GEN_SWRITE(0);
+  if (KT > 0) {  // (a parity class no tap reaches, e.g. the odd rows of a 1x1/2 dgrad: zeros)
+    GEN_GLOAD(0);
+    GEN_SWRITE(0);
+  }
   __syncthreads();
   for (int t = 0; t < KT; ++t) {
     const int cur = t & 1;
@@ -479,7 +498,12 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
     if (px >= M) continue;
-    T* yrow = y + (long long)px * a.ldy;
+    long long orow = px;
+    if (par) {  // class pixel -> dX pixel (n, stride*i + pa, stride*j + pb)
+      const int n = px / PQ, rem = px - n * PQ, i = rem / Qc, jj = rem - i * Qc;
+      orow = ((long long)n * a.P + i * a.stride + a.pa) * a.Q + jj * a.stride + a.pb;
+    }
+    T* yrow = y + orow * a.ldy;
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
@@ -498,15 +522,31 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
   }
 }
 
+static bool gen_parity() {  // DGVCC_GEN_PARITY=0: strided dgrad as one transposed gather (A/B switch)
+  const char* e = getenv("DGVCC_GEN_PARITY");
+  return !(e && e[0] == '0');
+}
+
 template <typename T>
-int launch_gen(const GenArgs& a, hipStream_t st) {
-  const long long M = (long long)a.N * a.P * a.Q;
-  const int npx = dg_cdiv(M, 128);
-  if (a.Cout % 128 == 0)
-    hipLaunchKernelGGL((conv_gen_kernel<T, 128, 128>), dim3(npx * (a.Cout / 128)), dim3(NT), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_gen_kernel<T, 64, 128>), dim3(npx * (a.Cout / 64)), dim3(NT), 0, st, a);
-  DG_CHECK_LAUNCH();
+int launch_gen(const GenArgs& a0, hipStream_t st) {
+  const int ncls = (a0.mode == 1 && a0.stride > 1 && gen_parity()) ? a0.stride * a0.stride : 1;
+  for (int c = 0; c < ncls; ++c) {
+    GenArgs a = a0;
+    long long M = (long long)a.N * a.P * a.Q;
+    if (ncls > 1) {
+      a.pa = c / a.stride;
+      a.pb = c % a.stride;
+      const long long Pc = (a.P - a.pa + a.stride - 1) / a.stride, Qc = (a.Q - a.pb + a.stride - 1) / a.stride;
+      M = (long long)a.N * Pc * Qc;
+      if (M == 0) continue;
+    }
+    const int npx = dg_cdiv(M, 128);
+    if (a.Cout % 128 == 0)
+      hipLaunchKernelGGL((conv_gen_kernel<T, 128, 128>), dim3(npx * (a.Cout / 128)), dim3(NT), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_gen_kernel<T, 64, 128>), dim3(npx * (a.Cout / 64)), dim3(NT), 0, st, a);
+    DG_CHECK_LAUNCH();
+  }
   return DG_OK;
 }
 
@@ -1067,6 +1107,13 @@ static bool use_persist() {
   return v == 1;
 }
 
+// DGVCC_SHORTK_REG=1: 16-bit forwards with <= 2 K-steps (the ResNet trunks' 1x1 convs from 64
+// or 128 channels, HBM-bound) on the register-staged two-blocks-per-CU kernel (A/B switch)
+static bool short_k_reg() {
+  const char* e = getenv("DGVCC_SHORTK_REG");
+  return e && e[0] == '1';
+}
+
 // DGVCC_F32_PERSIST=0: f32 forwards on the register-staged conv_fwd_kernel (A/B switch)
 static bool use_f32_persist() {
   const char* e = getenv("DGVCC_F32_PERSIST");
@@ -1613,7 +1660,7 @@ template <typename T>
 int launch_fwd(const FwdArgs& a, hipStream_t st) {
   const long long M = (long long)a.N * a.H * a.W;
   if constexpr (Is16<T>::value) {
-    if (use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
+    if (use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 && !(short_k_reg() && a.R * a.S * (a.C / 64) <= 2) &&
         (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31)) {
       const int np = dg_cdiv(M, PBM);
       const int var = pipe_var();
