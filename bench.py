@@ -7,7 +7,10 @@ Default workload = the config BASELINE.json's metric is quoted on, configs/sta_f
 (ShanghaiTech-A "final"): DGModel_final, DGTrainer 'final' mode (two photometric views,
 MSE count loss x log_para 1000 + 10 BCE class-map loss + 10 JSD-MSE consistency loss,
 fused AdamW), batch 16 per GPU of synthetic 3x768x1024 frames resident in HBM (no dataset
-offline), computed in fp32 like the reference (exact-f32 MFMA).  A step is
+offline), computed in fp32 like the reference: f32 storage, statistics and accumulation, the conv
+GEMMs on the bf16 matrix cores through an exact 3-way split of each f32 operand (six bf16
+products per f32 product, dropped terms < 2^-24 relative: f32-grade; `--f32-math exact`
+runs them on v_mfma_f32_16x16x4_f32 instead, reported beside it as `f32_exact`).  A step is
 DGTrainer.train_step: forward + loss + backward + optimizer step + the reference's per-step
 `.item()`; a frame is one 3x768x1024 view through forward and backward (final mode counts
 both views).  The same step in bf16 (bf16 storage/MFMA, f32 accumulation and
@@ -44,7 +47,11 @@ sys.path.insert(0, ROOT)
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 F32_MFMA_PEAK_TFLOPS = 157.3      # MI355X_MICROARCH.md: f32-input MFMA = the f32 vector peak
 HBM_PEAK_GBPS = 8000.0
-PEAKS = {"fp32": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_DENSE_PEAK_TFLOPS, "fp16": BF16_DENSE_PEAK_TFLOPS}
+# f32 GEMMs through the 3-way bf16 split issue six bf16 MFMA products per f32 product: their
+# f32-equivalent ceiling is the dense bf16 peak / 6
+F32_SPLIT_PEAK_TFLOPS = BF16_DENSE_PEAK_TFLOPS / 6.0
+PEAKS = {"fp32": F32_SPLIT_PEAK_TFLOPS, "fp32_exact": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_DENSE_PEAK_TFLOPS,
+         "fp16": BF16_DENSE_PEAK_TFLOPS}
 H0, W0 = 768, 1024
 METRIC = "train-step frames/sec at 768×1024, ShanghaiTech-A; MAE vs reference"
 CONFIG_FILES = {"final": "configs/sta_final.yml", "simple": "configs/stb_reg_base.yml",
@@ -73,6 +80,9 @@ def parse():
                     help="secondary workload: ResNet-50 DG counter (IBN-b / SW / ISW) train step")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
     ap.add_argument("--no-bf16", action="store_true", help="skip the perf_bf16 leg")
+    ap.add_argument("--f32-math", default="split", choices=["split", "exact"],
+                    help="f32 conv GEMM arithmetic: exact 3-way bf16 split (default) or v_mfma_f32_16x16x4_f32")
+    ap.add_argument("--no-f32-exact", action="store_true", help="skip the f32_exact leg")
     ap.add_argument("--height", type=int, default=H0)
     ap.add_argument("--width", type=int, default=W0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -231,7 +241,11 @@ def measured_traffic(args, precision):
 
 
 FWD_KERNEL_NAMES = {
-    "fp32": "conv_fwd_kernel<float> (implicit-GEMM conv on v_mfma_f32_16x16x4_f32: forward + dgrad launches)",
+    "fp32": "conv_fwd_pers_kernel<float, split> (implicit-GEMM conv, f32 operands split exactly into 3 bf16 parts, "
+            "6 x v_mfma_f32_16x16x32_bf16 per 32-deep block, f32 accumulation: forward + dgrad launches; peak = "
+            "dense bf16 / 6)",
+    "fp32_exact": "conv_fwd_pers_kernel<float> (implicit-GEMM conv on v_mfma_f32_16x16x4_f32: forward + dgrad "
+                  "launches)",
     "bf16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
             "(implicit-GEMM conv on v_mfma_f32_16x16x32_bf16: forward + dgrad launches)",
     "fp16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
@@ -240,8 +254,11 @@ FWD_KERNEL_NAMES = {
 
 
 def run_leg(args, precision, dev, world, rank):
-    """Build, warm up and time one precision of the workload; returns the measurements."""
+    """Build, warm up and time one precision of the workload; returns the measurements.
+    precision "fp32_exact" = fp32 with the conv GEMMs on v_mfma_f32_16x16x4_f32."""
     from dgvcc_amd import kernels as K
+    K.call("dg_set_f32_math", 0 if precision == "fp32_exact" else 1)
+    precision = "fp32" if precision == "fp32_exact" else precision
     from dgvcc_amd.losses import MSELoss
     from dgvcc_amd.optim import AdamW
     from dgvcc_amd.trainers.dgtrainer import DGTrainer
@@ -324,13 +341,15 @@ def run_leg(args, precision, dev, world, rank):
 
 def roofline(args, precision, r):
     peak = PEAKS[precision]
+    kname = FWD_KERNEL_NAMES.get(precision, "implicit-GEMM conv forward + dgrad")
+    precision = "fp32" if precision == "fp32_exact" else precision
     achieved = r["conv_flops"] / (r["conv_ms"] * 1e-3) / 1e12 if r["conv_ms"] > 0 else 0.0
     traffic, tsrc = measured_traffic(args, precision)
     steps = args.steps
     tot, enc_tot = step_flops(args.batch, args.height, args.width, r["mode"]) if not args.trunk else \
         ((r["conv_flops"] + r["wg_flops"]) / steps, None)
     step_s = r["elapsed"] / steps
-    out = {"bound": "mfma", "kernel": FWD_KERNEL_NAMES.get(precision, "implicit-GEMM conv forward + dgrad"),
+    out = {"bound": "mfma", "kernel": kname,
            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
            "traffic": traffic, "traffic_source": tsrc,
            "algorithmic_bytes_per_launch": round(r["conv_bytes"] / max(r["conv_n"], 1)),
@@ -522,7 +541,8 @@ def main():
     torch.cuda.set_device(dev)
 
     prec = args.precision
-    r = run_leg(args, prec, dev, world, rank)
+    leg = "fp32_exact" if prec == "fp32" and args.f32_math == "exact" else prec
+    r = run_leg(args, leg, dev, world, rank)
     value = r["frames"] / r["elapsed"]
     workload = (f"{r['model']} {r['mode']}-mode DGTrainer.train_step (configs/baselines/sta_{args.trunk}.yml)"
                 if args.trunk else
@@ -548,10 +568,21 @@ def main():
                    "resolution": f"{args.height}x{args.width}", "parallelism": f"dp{world}",
                    "rccl_world_size": dist_world, "backend": backend if world > 1 else None,
                    "last_loss": r["last_loss"]},
-        "roofline": roofline(args, prec, r),
+        "roofline": roofline(args, leg, r),
     }
+    if prec == "fp32":
+        out["f32_math"] = ("exact 3-way bf16 split of both f32 operands, 6 bf16 MFMA products per f32 product, "
+                           "f32 accumulation" if leg == "fp32" else "v_mfma_f32_16x16x4_f32")
     if "params_in_sync" in r:
         out["params_in_sync"] = r["params_in_sync"]
+    if leg == "fp32" and not args.no_f32_exact:
+        re_ = run_leg(args, "fp32_exact", dev, world, rank)
+        out["f32_exact"] = {"value": round(re_["frames"] / re_["elapsed"], 3), "unit": "frames/s", "dtype": "fp32",
+                            "ms_per_step": round(re_["elapsed"] / args.steps * 1e3, 3),
+                            "note": "same fp32 workload with the conv GEMMs on v_mfma_f32_16x16x4_f32",
+                            "last_loss": re_["last_loss"], "roofline": roofline(args, "fp32_exact", re_)}
+        K_ = __import__("dgvcc_amd.kernels", fromlist=["call"])
+        K_.call("dg_set_f32_math", 1)
     if prec == "fp32" and not args.no_bf16:
         rb = run_leg(args, "bf16", dev, world, rank)
         out["perf_bf16"] = {"value": round(rb["frames"] / rb["elapsed"], 3), "unit": "frames/s", "dtype": "bf16",

@@ -764,7 +764,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 // MFMAs and epilogue stores.  The epilogue-statistics scratch gets its own LDS so the
 // in-flight ring stages are never touched.  Requires KT > PF (K-steps per tile).
 constexpr int PERS_BIAS_MAX = 1024;  // Cout limit of the persistent forward (LDS bias)
-template <int BN, int STG, int EPI = 0, typename T = bf16>
+// SPL = 1 (T = float only): the f32 GEMM on the bf16 matrix cores through the exact 3-way
+// split (dg_common.h split3_8): one 32-channel K-step is one 16x16x32 block, the lane's 8
+// k values being its chunks fc and 4 + fc of the 128-B row for both operands.
+template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   constexpr int ES = (int)sizeof(T);  // element bytes: a K-step row is 128 B (64 x 16-bit or 32 x f32)
   constexpr int BK = 128 / ES;
@@ -890,6 +893,43 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       asm volatile("" ::: "memory");
       const char* As = smem + (gs % STG) * STAGE;
       const char* Bs = As + BN * 128;
+      if constexpr (SPL) {
+        static_assert(!Is16<T>::value, "split path is for f32 operands");
+        u4v b0[TJ], b1[TJ];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          b0[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, fc));
+          b1[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, 4 + fc));
+        }
+        // A fragments one row block ahead of their MFMAs (all TI at once spill at BN = 256)
+        u4v a0 = *(const u4v*)(As + swz(wco + fr, fc)), a1 = *(const u4v*)(As + swz(wco + fr, 4 + fc));
+        {  // the step PF ahead (its stage was last read before this step's barrier)
+          const int u = t + PF;
+          if (u < KT) issue(cur, u, (gs + PF) % STG);
+          else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+        }
+        s8v bh[TJ][3];
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) split3_8(b0[j], b1[j], bh[j][0], bh[j][1], bh[j][2]);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          s8v ah[3];
+          split3_8(a0, a1, ah[0], ah[1], ah[2]);
+          if (i + 1 < TI) {
+            a0 = *(const u4v*)(As + swz(wco + 16 * (i + 1) + fr, fc));
+            a1 = *(const u4v*)(As + swz(wco + 16 * (i + 1) + fr, 4 + fc));
+          }
+          __builtin_amdgcn_s_setprio(1);
+          constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+        continue;
+      }
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int ch = 4 * ks + fc;
@@ -1121,6 +1161,18 @@ static bool use_f32_persist() {
 }
 static int f32_pers_bn(int Cout);
 static bool f32_pers_ok(const FwdArgs& a);
+
+// f32 GEMM arithmetic: 0 = v_mfma_f32_16x16x4_f32, 1 = the exact 3-way bf16 split on
+// v_mfma_f32_16x16x32_bf16 (dg_common.h split3_8; f32-grade).
+// Default: DGVCC_F32_MATH (exact | split), else split; dg_set_f32_math overrides.
+static int g_f32_math = -1;
+static bool f32_split() {
+  if (g_f32_math < 0) {
+    const char* e = getenv("DGVCC_F32_MATH");
+    g_f32_math = (e && e[0] == 'e') ? 0 : 1;
+  }
+  return g_f32_math == 1;
+}
 
 static int persist_grid() {  // one block per CU (the ring takes most of the LDS)
   static int g = -1;
@@ -1726,20 +1778,24 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
       const int np = dg_cdiv(M, PBM);
       const int bn = f32_pers_bn(a.Cout);
       const long long tiles = (long long)np * (a.Cout / bn);
-      {
-        const unsigned g = (unsigned)std::min<long long>(tiles, persist_grid());
-        if (a.escale) {
-          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3, T>), dim3(g), dim3(512), 0, st, a);
-          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
-          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
-        } else {
-          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
-          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
-          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
-        }
-        DG_CHECK_LAUNCH();
-        return DG_OK;
-      }
+      const unsigned g = (unsigned)std::min<long long>(tiles, persist_grid());
+#define F32_PERS(SPL_) \
+      do { \
+        if (a.escale) { \
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
+        } else { \
+          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
+          else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
+        } \
+      } while (0)
+      if (f32_split()) F32_PERS(1);
+      else F32_PERS(0);
+#undef F32_PERS
+      DG_CHECK_LAUNCH();
+      return DG_OK;
     }
   }
   const int npx = dg_cdiv(M, 128);
@@ -1773,7 +1829,10 @@ template <> struct WgCfg<bf16> { static constexpr int BKP = 64, PAD = 32; };
 template <> struct WgCfg<f16> { static constexpr int BKP = 64, PAD = 32; };
 template <> struct WgCfg<float> { static constexpr int BKP = 32, PAD = 64; };
 
-template <typename T, int BCO, int BC>
+// SPL = 1 (T = float only): the exact 3-way bf16 split (dg_common.h split3_8); one
+// 32-pixel K-step is one 16x16x32 block, lane group g taking pixel rows 4m + g (m < 8),
+// conflict-free as the f32 reads below.
+template <typename T, int BCO, int BC, int SPL = 0>
 __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
   constexpr int BKP = WgCfg<T>::BKP;
   constexpr int EPC = 16 / (int)sizeof(T);
@@ -1918,6 +1977,32 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
             acc[i][j] = mfma16x16x32<T>(af[i], bfv[j], acc[i][j]);
+      }
+    } else if constexpr (SPL) {
+      static_assert(BKP == 32, "one 16x16x32 block per K-step");
+      const int fcol = lane & 15;
+      auto frag = [&](const char* base, int rowb, int col, s8v& h0, s8v& h1, s8v& h2) __attribute__((always_inline)) {
+        u4v x0, x1;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          x0[m] = *(const unsigned*)(base + (4 * m + g) * rowb + col * 4);
+          x1[m] = *(const unsigned*)(base + (4 * m + 16 + g) * rowb + col * 4);
+        }
+        split3_8(x0, x1, h0, h1, h2);
+      };
+      s8v bh[TJ][3];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) frag(Bs, ROWB, wc + 16 * j + fcol, bh[j][0], bh[j][1], bh[j][2]);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        s8v ah[3];
+        frag(As, ROWA, wco + 16 * i + fcol, ah[0], ah[1], ah[2]);
+        constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
       }
     } else {
       const int fcol = lane & 15;
@@ -2535,6 +2620,16 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
     }
   }
   if (done) {
+  } else if constexpr (!Is16<T>::value) {
+    if (f32_split()) {
+      if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128, 1>), grid, dim3(NT), 0, st, a);
+      else if (bco == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, 1>), grid, dim3(NT), 0, st, a);
+      else if (bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128, 1>), grid, dim3(NT), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 64, 1>), grid, dim3(NT), 0, st, a);
+      done = true;
+    }
+  }
+  if (done) {
   } else if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128>), grid, dim3(NT), 0, st, a);
   else if (bco == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64>), grid, dim3(NT), 0, st, a);
   else if (bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128>), grid, dim3(NT), 0, st, a);
@@ -2680,6 +2775,14 @@ extern "C" int dg_version(void) { return DGVCC_ABI_VERSION; }
 
 // Test hook: force the persistent pipelined forward on (1) / off (0), or back to the
 // DGVCC_PERSIST environment default (-1).
+extern "C" int dg_set_f32_math(int mode) {
+  DG_REQUIRE(mode == 0 || mode == 1);
+  g_f32_math = mode;
+  return DG_OK;
+}
+
+extern "C" int dg_get_f32_math(void) { return f32_split() ? 1 : 0; }
+
 extern "C" int dg_set_persist(int mode) {
   DG_REQUIRE(mode >= -1 && mode <= 1);
   g_persist_override = mode;

@@ -140,3 +140,48 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 static inline int dg_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+// ---------------------------------------------------------------------------
+// f32 arithmetic on the bf16 matrix cores ("3-way split", DG_F32 with
+// dg_set_f32_math(1)).  Each f32 x is cut EXACTLY into three bf16 parts by truncation,
+//   x = h0 + h1 + h2,  h0 = top 8 significant bits of x, h1 = top 8 of x - h0, h2 = the rest
+// (x - h0 has <= 16 significant bits and its remainder <= 8, so h2 is exact in bf16);
+// a product x*y is then sum_{i+j<=2} xi*yj, six v_mfma_f32_16x16x32_bf16 per 16x16x32
+// block with f32 accumulation: products of bf16 are exact in f32 and the dropped terms
+// (i+j >= 3) are below 2^-24 of |x*y|, i.e. f32-grade.  Six bf16 MFMAs (16 cycles each)
+// replace eight v_mfma_f32_16x16x4_f32 (32 cycles each) per 32-deep K block.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned hi16x2(unsigned lo, unsigned hi) {
+  return __builtin_amdgcn_perm(hi, lo, 0x07060302u);  // (lo >> 16) | (hi & 0xffff0000)
+}
+// 8 f32 (x0[0..3], x1[0..3]) -> bf16 parts h0/h1/h2, element k of each part = float k
+__device__ __forceinline__ void split3_8(const u4v& x0, const u4v& x1, s8v& h0, s8v& h1, s8v& h2) {
+  u4v p0, p1, p2;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const unsigned a = k < 2 ? x0[2 * k] : x1[2 * k - 4];
+    const unsigned b = k < 2 ? x0[2 * k + 1] : x1[2 * k - 3];
+    p0[k] = hi16x2(a, b);
+    const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
+    const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
+    const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
+    p1[k] = hi16x2(ua, ub);
+    const float sa = ra - __uint_as_float(ua & 0xffff0000u);
+    const float sb = rb - __uint_as_float(ub & 0xffff0000u);
+    p2[k] = hi16x2(__float_as_uint(sa), __float_as_uint(sb));
+  }
+  h0 = __builtin_bit_cast(s8v, p0);
+  h1 = __builtin_bit_cast(s8v, p1);
+  h2 = __builtin_bit_cast(s8v, p2);
+}
+// the six products of one block, smallest first (all into the same f32 accumulator)
+__device__ __forceinline__ f4v mfma_x6(const s8v& a0, const s8v& a1, const s8v& a2, const s8v& b0, const s8v& b1,
+                                       const s8v& b2, f4v c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, b0, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b2, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, c, 0, 0, 0);
+  return c;
+}

@@ -36,6 +36,12 @@ extern "C" {
 int dg_version(void); /* returns DGVCC_ABI_VERSION */
 /* test hook: 1/0 force the persistent pipelined conv forward on/off, -1 = DGVCC_PERSIST default */
 int dg_set_persist(int mode);
+/* f32 GEMM arithmetic of the DG_F32 convolutions: 0 = v_mfma_f32_16x16x4_f32;
+ * 1 = exact 3-way bf16 split of both operands (x = h0 + h1 + h2), six
+ * v_mfma_f32_16x16x32_bf16 products per block, f32 accumulation (f32-grade: dropped
+ * terms < 2^-24 relative).  Default from DGVCC_F32_MATH (exact | split), else 1. */
+int dg_set_f32_math(int mode);
+int dg_get_f32_math(void);
 #define DGVCC_ABI_VERSION 1
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------

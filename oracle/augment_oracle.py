@@ -1,6 +1,6 @@
 """TEST INFRASTRUCTURE ONLY (the product never imports this): CPU restatement of the
 reference's DenClsDataset pixel pipeline (datasets/den_cls_dataset.py:29-35, 77-158) for
-one parameter record of dgvcc_amd/datasets/augment.py.
+one parameter record of the product's datasets/augment.py.
 
 Pinning: the PIL steps call PIL itself (installed here, the library the reference runs):
 convert('L'), ImageEnhance.Brightness/Contrast/Color/Sharpness, convert('HSV').  The

@@ -1,6 +1,6 @@
 """TEST INFRASTRUCTURE ONLY — CPU fp32 restatement of the reference's training
 hot path, used by tests/, `__graft_entry__.smoke()` and bench.py's cpu_baseline
-leg as the checker.  Never imported by the product package (dgvcc_amd).
+leg as the checker.  Never imported by the product package.
 
 Functional torch-CPU code over a state_dict (same keys as the reference):
   base_forward      models/models.py:64-96  (DGModel_base.forward_fe/forward)

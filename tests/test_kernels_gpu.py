@@ -140,12 +140,16 @@ def test_conv_f32_persistent(dev, monkeypatch, case):
     x = K.Act(torch.randn(N, H, W, C, generator=g).to(dev))
     wp = K.pack_weight((torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5).to(dev), torch.float32)
     outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DGVCC_F32_PERSIST", flag)
-        y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
-        K.conv_fwd(x, wp, Cout, R, R // 2, y)
-        outs.append(y.buf.clone())
-    torch.cuda.synchronize()
+    K.call("dg_set_f32_math", 0)  # both on v_mfma_f32_16x16x4_f32 (the split math: test_conv_f32_split_math)
+    try:
+        for flag in ("1", "0"):
+            monkeypatch.setenv("DGVCC_F32_PERSIST", flag)
+            y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+            K.conv_fwd(x, wp, Cout, R, R // 2, y)
+            outs.append(y.buf.clone())
+        torch.cuda.synchronize()
+    finally:
+        K.call("dg_set_f32_math", 1)
     assert relerr(outs[0], outs[1]) < 2e-6
 
 
@@ -317,3 +321,41 @@ def test_fused_adamw_matches_torch_with_missing_grads(dev):
             continue  # live for fewer steps: torch keeps a per-param step count, ours per group
         assert torch.allclose(a.detach(), b.detach(), rtol=1e-5, atol=1e-6), i
     assert torch.equal(ours[2].detach().cpu(), base[2]) and torch.equal(ours[3].detach().cpu(), base[3])
+
+
+@pytest.mark.parametrize("case", [(1, 256, 288, 64, 256, 3), (1, 256, 288, 128, 128, 3), (1, 256, 288, 64, 64, 3),
+                                  (1, 256, 288, 256, 512, 1), (2, 20, 24, 64, 128, 3), (1, 64, 64, 512, 512, 3)])
+def test_conv_f32_split_math(dev, case):
+    """DG_F32 on the bf16 matrix cores (dg_set_f32_math(1): exact 3-way bf16 split, six products)
+    against float64 torch: forward, dgrad and wgrad within 5e-6 relative and no worse than 2x the
+    v_mfma_f32_16x16x4_f32 path's own error on the same launch (f32-grade)."""
+    K = _k()
+    N, H, W, C, Cout, R = case
+    pad = R // 2
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    xr = x.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    yr = F.conv2d(xr, wr, padding=pad)
+    yr.backward(gy.double())
+    xd = K.Act(to_nhwc(x).to(dev))
+    gyd = K.Act(to_nhwc(gy).to(dev))
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    errs = {}
+    try:
+        for mode in (0, 1):
+            K.call("dg_set_f32_math", mode)
+            y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+            K.conv_fwd(xd, wp, Cout, R, pad, y)
+            dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+            K.conv_dgrad(gyd, wp, C, R, pad, dx)
+            dw = torch.empty(Cout, C, R, R, device=dev)
+            K.conv_wgrad(xd, gyd, R, pad, dw)
+            torch.cuda.synchronize()
+            errs[mode] = (relerr(to_nchw(y.buf), yr.detach()), relerr(to_nchw(dx.buf), xr.grad), relerr(dw, wr.grad))
+    finally:
+        K.call("dg_set_f32_math", 1)
+    for e0, e1 in zip(errs[0], errs[1]):
+        assert e1 < 5e-6 and e1 < 2 * e0 + 2e-7, errs
