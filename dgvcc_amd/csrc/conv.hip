@@ -1006,6 +1006,249 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   }
 }
 
+// f32 forward/dgrad on the bf16 matrix cores with the filter panel PRE-SPLIT (dg_common.h
+// split3_8 applied once per launch by split_weight_kernel, not per wave per K-step): the A
+// operand arrives by LDS-DMA as three bf16 planes [part][BN rows][32 channels] (64-B rows,
+// 16-B chunk c of row r stored at c ^ ((r >> 2) & 3): conflict-free fragment reads), the
+// f32 pixel rows as in conv_fwd_pers_kernel; only the B (pixel) fragments are split in
+// registers.  192-pixel tiles (8 waves = 4 pixel x 2 channel, 48 x BN/2 each): the planes
+// make a K-step's A tile 1.5x the f32 bytes, and 2 x (48 + 24) KB + epilogue scratch fill
+// the 160-KB LDS exactly at BN = 256.  k order within a 32-channel block: lane group fc
+// holds channels 8fc..8fc+7 for both operands.
+constexpr int PSB = 192;  // pixels per tile of the pre-split kernel
+template <int BN, int STG, int EPI = 0>
+__global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int AROWB = 64;                        // bytes per A plane row (32 bf16)
+  constexpr int A_BYTES = 3 * BN * AROWB;
+  constexpr int AI = A_BYTES / 1024 / 8;           // A DMA instructions per wave per K-step
+  constexpr int BI = PSB / 64;                     // B DMA instructions per wave per K-step
+  constexpr int TI = BN / 32, TJ = PSB / 64;       // wave tile: BN/2 channels x 48 pixels
+  constexpr int STAGE = A_BYTES + PSB * 128;
+  constexpr int PF = STG - 1;
+  constexpr int EPI_B = 4 * 3 * BN * 4;
+  static_assert(AI * 8 * 1024 == A_BYTES, "A tile must split evenly over the 8 waves");
+  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B + PERS_BIAS_MAX * 4];
+  char* epi_lds = smem + STG * STAGE;
+  float* bbuf = (float*)(epi_lds + EPI_B);
+  constexpr int E3_MAX = (EPI_B + PERS_BIAS_MAX * 4) / 12;
+  const bool e3_lds = EPI == 3 && a.Cout <= E3_MAX;
+  float* ebias = (float*)epi_lds;
+  float* escl = ebias + E3_MAX;
+  float* eshf = escl + E3_MAX;
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BN;
+  const int ntile = (M + PSB - 1) / PSB * nco;
+  const int G = gridDim.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lrow = lane >> 3;
+  const int gchunk = (lane & 7) ^ lrow;
+  const int CB = a.C / 32;
+  const int KT = a.R * a.S * CB;
+  const unsigned cbytes = (unsigned)(gchunk * 16);
+  // A source offsets (bytes, K-step 0) of this wave's AI DMA pieces: piece q = plane p, rows rb*16..+15
+  unsigned aoff[AI];
+#pragma unroll
+  for (int q = 0; q < AI; ++q) {
+    const int gq = wid * AI + q;
+    const int pl = gq / (BN / 16), rb = gq % (BN / 16);
+    const int row = rb * 16 + (lane >> 2);
+    const int lch = (lane & 3) ^ ((row >> 2) & 3);
+    aoff[q] = (unsigned)(row * KT * 192 + pl * 64 + lch * 16);
+  }
+
+  struct Ctx {
+    int px0, co0;
+    __amdgpu_buffer_rsrc_t xr, wr;
+    int pp[BI], pq[BI], prow[BI];
+  };
+  auto setup = [&](int lin, Ctx& c) {
+    const int t = xcd_remap(lin, ntile);
+    c.co0 = (t % nco) * BN;
+    c.px0 = (t / nco) * PSB;
+    const int halo = a.pad * (a.W + 1);
+    const int plo = max(0, c.px0 - halo);
+    const int phi = min(M, c.px0 + PSB + halo);
+    const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 4);
+    c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 4), 0, win_bytes, 0x00020000);
+    c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(wsp + (long long)c.co0 * KT * 192), 0, (unsigned)(BN * KT * 192),
+                                             0x00020000);
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int m = c.px0 + (wid * BI + i) * 8 + lrow;
+      const int rem = m % HW;
+      c.prow[i] = m - plo;
+      c.pp[i] = (m < M) ? rem / a.W : -100000;
+      c.pq[i] = rem % a.W;
+    }
+  };
+  auto issue = [&](const Ctx& c, int kt, int stage) {
+    const int rs = kt / CB, cb = kt - rs * CB;
+    const int r = rs / a.S, s2 = rs - r * a.S;
+    char* As = smem + stage * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int q = 0; q < AI; ++q) lds_dma16(c.wr, As + (wid * AI + q) * 1024, aoff[q] + (unsigned)(kt * 192));
+    const int dh = r - a.pad, dw = s2 - a.pad;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int hh = c.pp[i] + dh, ww = c.pq[i] + dw;
+      const bool ok = (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const unsigned off =
+          ok ? (unsigned)(((long long)(c.prow[i] + dh * a.W + dw) * a.ldx + cb * 32) * 4) + cbytes : 0xFFFFFFF0u;
+      lds_dma16(c.xr, Bs + (wid * BI + i) * 1024, off);
+    }
+  };
+
+  int lin = blockIdx.x;
+  if (lin >= ntile) return;
+  if (e3_lds) {
+    for (int c = tid; c < a.Cout; c += 512) {
+      ebias[c] = a.bias ? a.bias[c] : 0.f;
+      escl[c] = a.escale[c];
+      eshf[c] = a.eshift[c];
+    }
+  } else if (a.bias) {
+    for (int c = tid; c < a.Cout; c += 512) bbuf[c] = a.bias[c];
+  }
+  Ctx cur, nxt;
+  setup(lin, cur);
+  bool has_next = lin + G < ntile;
+  if (has_next) setup(lin + G, nxt);
+  const int wpx = (wid & 3) * (PSB / 4), wco = (wid >> 2) * (BN / 2);
+  const int fr = lane & 15, fc = lane >> 4;
+  int gs = 0;
+  issue(cur, 0, 0);
+  if (PF > 1) issue(cur, 1, 1);
+  bool first_tile = true;
+  while (true) {
+    f4v acc[TI][TJ];
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < KT; ++t, ++gs) {
+      const bool more = t + 1 < KT || has_next;
+      if (PF > 1 && more && (t > 0 || first_tile)) {
+        if constexpr (AI + BI == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+        else if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      const char* As = smem + (gs % STG) * STAGE;
+      const char* Bs = As + A_BYTES;
+      u4v b0[TJ], b1[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        b0[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, 2 * fc));
+        b1[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, 2 * fc + 1));
+      }
+      auto aread = [&](int i, s8v (&ah)[3]) __attribute__((always_inline)) {
+        const int row = wco + 16 * i + fr;
+        const int off = row * AROWB + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) ah[pl] = *(const s8v*)(As + pl * BN * AROWB + off);
+      };
+      s8v ah[3];
+      aread(0, ah);
+      {
+        const int u = t + PF;
+        if (u < KT) issue(cur, u, (gs + PF) % STG);
+        else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+      }
+      s8v bh[TJ][3];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) split3_8(b0[j], b1[j], bh[j][0], bh[j][1], bh[j][2]);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        s8v an[3];
+        if (i + 1 < TI) aread(i + 1, an);
+        __builtin_amdgcn_s_setprio(1);
+        constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (i + 1 < TI) { ah[0] = an[0]; ah[1] = an[1]; ah[2] = an[2]; }
+      }
+    }
+    first_tile = false;
+    float* y = (float*)a.y;
+    bool valid[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = cur.px0 + wpx + 16 * j + fr;
+      valid[j] = px < M;
+      if (px >= M) continue;
+      float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = cur.co0 + wco + 16 * i + 4 * fc;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (e3_lds) {
+          const f4v b = *(const f4v*)(ebias + co);
+          v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+        } else if (a.bias) {
+          const f4v b = *(const f4v*)(bbuf + co);
+          v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+        }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
+          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+        }
+        if constexpr (EPI == 3) {
+          if (e3_lds) {
+            const f4v sc = *(const f4v*)(escl + co), sf = *(const f4v*)(eshf + co);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              float tt = fmaf(v[r], sc[r], sf[r]);
+              if (a.eact == 1) tt = tt > 0.f ? tt : 0.f;
+              v[r] = tt;
+            }
+          } else {
+            epi_affine(v, a, co);
+          }
+        }
+        st4(yrow + co, v);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+      }
+    }
+    if (EPI == 0 && a.part)
+      epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, epi_lds, a.part + (long long)(cur.px0 / PSB) * 3 * a.Cout,
+                               a.Cout, cur.co0, tid, fr, fc);
+    if (!has_next) break;
+    cur = nxt;
+    lin += G;
+    has_next = lin + G < ntile;
+    if (has_next) setup(lin + G, nxt);
+  }
+}
+
+// wsp[co][kb][part][32] (bf16) = the exact 3-way split of the packed f32 filter w[co][kb*32 + j]
+__global__ void split_weight_kernel(const float* __restrict__ w, long long n, unsigned short* __restrict__ wsp) {
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n; o += (long long)gridDim.x * blockDim.x) {
+    const unsigned u = __float_as_uint(w[o]);
+    const float r = __uint_as_float(u) - __uint_as_float(u & 0xffff0000u);
+    const unsigned ur = __float_as_uint(r);
+    const float q = r - __uint_as_float(ur & 0xffff0000u);
+    const long long blk = o >> 5, j = o & 31;
+    unsigned short* d = wsp + blk * 96 + j;
+    d[0] = (unsigned short)(u >> 16);
+    d[32] = (unsigned short)(ur >> 16);
+    d[64] = (unsigned short)(__float_as_uint(q) >> 16);
+  }
+}
+
 // Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored
 // as T, and — when part != NULL — the BN statistics partials of the stored values in the
 // epilogue's format (one (n, mean, M2) row per 256-pixel block, two passes over registers).
@@ -1697,6 +1940,41 @@ static bool tap3_pad_ok(const FwdArgs& a) {
 
 static int f32_pers_bn(int Cout) { return Cout % 256 == 0 && pipe_wide() ? 256 : (Cout % 128 == 0 ? 128 : 64); }
 
+// DGVCC_PSPLIT=0: split-math f32 forwards split the filter per wave (conv_fwd_pers_kernel SPL=1)
+static bool use_psplit() {
+  const char* e = getenv("DGVCC_PSPLIT");
+  return !(e && e[0] == '0');
+}
+
+// f32 split-math shapes served by conv_fwd_psplit_kernel (filter panel pre-split per launch)
+static bool psplit_ok(const FwdArgs& a) {
+  return use_psplit() && f32_split() && f32_pers_ok(a) && f32_pers_bn(a.Cout) >= 128 &&
+         (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
+}
+
+// Per-stream device scratch for the pre-split filter panels (grown on demand; a launch on
+// a stream only ever overlaps its own stream's earlier work, which hipFree waits for).
+static void* split_scratch(hipStream_t st, size_t bytes) {
+  struct Ent { hipStream_t st; void* p; size_t cap; };
+  static Ent ents[8];
+  static int n = 0;
+  int k = 0;
+  while (k < n && ents[k].st != st) ++k;
+  if (k == n) {
+    if (n == 8) return nullptr;
+    ents[n++] = Ent{st, nullptr, 0};
+  }
+  if (ents[k].cap < bytes) {
+    if (ents[k].p && hipFree(ents[k].p) != hipSuccess) return nullptr;
+    ents[k].p = nullptr;
+    ents[k].cap = 0;
+    const size_t cap = std::max(bytes, (size_t)16 << 20);
+    if (hipMalloc(&ents[k].p, cap) != hipSuccess) return nullptr;
+    ents[k].cap = cap;
+  }
+  return ents[k].p;
+}
+
 // the shapes the f32 persistent forward serves (and so the f32 shapes with epilogue statistics):
 // more tiles than CUs, > PF K-steps per tile, no split-K / BN-backward epilogue
 static bool f32_pers_ok(const FwdArgs& a) {
@@ -1791,7 +2069,23 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
         } \
       } while (0)
-      if (f32_split()) F32_PERS(1);
+      if (f32_split() && psplit_ok(a)) {
+        const long long nw = (long long)a.Cout * a.R * a.S * a.C;
+        unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
+        if (!wsp) return DG_ERR_HIP;
+        hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
+                           0, st, (const float*)a.w, nw, wsp);
+        const int bn2 = f32_pers_bn(a.Cout);
+        const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, PSB) * (a.Cout / bn2), persist_grid());
+        const char* wspc = (const char*)wsp;
+        if (a.escale) {
+          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 3>), dim3(g2), dim3(512), 0, st, a, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 3>), dim3(g2), dim3(512), 0, st, a, wspc);
+        } else {
+          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0>), dim3(g2), dim3(512), 0, st, a, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 0>), dim3(g2), dim3(512), 0, st, a, wspc);
+        }
+      } else if (f32_split()) F32_PERS(1);
       else F32_PERS(0);
 #undef F32_PERS
       DG_CHECK_LAUNCH();
@@ -2815,6 +3109,15 @@ extern "C" int64_t dg_conv_stats_rows(int N, int H, int W) {
   return dg_cdiv((long long)N * H * W, 256);
 }
 
+// rows of BN statistics partials a dg_conv_fwd_ex launch of this shape writes (one per tile
+// of 256 pixels, 192 on the pre-split f32 kernel)
+extern "C" int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, int64_t ldx, int Cout, int R, int S) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
+  const long long M = (long long)N * H * W;
+  FwdArgs a{nullptr, ldx, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0};
+  if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, PSB);
+  return dg_cdiv(M, 256);
+}
 extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                                  int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy, float* part,
                                  void* stream) {

@@ -243,7 +243,7 @@ def conv_fwd_stats(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act
     """conv_fwd with the BN statistics partials of y from the conv epilogue; returns
     (part, rows), or None (nothing launched) when the shape is served by a kernel without
     epilogue statistics."""
-    rows = query("dg_conv_stats_rows", x.N, x.H, x.W)
+    rows = query("dg_conv_stats_rows_ex", x.dt, x.N, x.H, x.W, x.C, x.ld, Cout, R, R)
     part = torch.empty((rows, 3, Cout), dtype=torch.float32, device=x.buf.device)
     flops = 2.0 * x.M * x.C * R * R * Cout
     es = x.buf.element_size()

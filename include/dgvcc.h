@@ -67,6 +67,9 @@ int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, 
  * Returns DG_ERR_UNSUPPORTED (nothing launched) where only the register-staged kernel
  * serves the shape; the caller then runs dg_conv_fwd + dg_bn_fwd_train. */
 int64_t dg_conv_stats_rows(int N, int H, int W);
+/* rows of (n, mean, M2) BN partials a dg_conv_fwd_ex launch of this shape writes: one per
+ * tile of 256 output pixels, or of 192 on the pre-split f32 kernel (DG_F32, split math) */
+int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, int64_t ldx, int Cout, int R, int S);
 int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                       const void* w, int Cout, int R, int S, int pad, const float* bias,
                       void* y, int64_t ldy, float* part, void* stream);

@@ -359,3 +359,44 @@ def test_conv_f32_split_math(dev, case):
         K.call("dg_set_f32_math", 1)
     for e0, e1 in zip(errs[0], errs[1]):
         assert e1 < 5e-6 and e1 < 2 * e0 + 2e-7, errs
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,epi", [(5, 128, 256, 64, 256, "stats"), (3, 96, 320, 128, 128, "stats"),
+                                              (3, 128, 256, 256, 512, "eval"), (8, 100, 130, 128, 256, "bias")])
+def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
+    """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128) with
+    bias + epilogue BN statistics (rows per 192-pixel tile: dg_conv_stats_rows_ex), the eval-BN
+    epilogue and a ragged last tile, against float64: y within 5e-6, the merged (n, mean, M2)
+    rows equal to the statistics of the stored y."""
+    K = _k()
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(N, H, W, C, generator=g)
+    w = torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    z = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double(), padding=1).permute(0, 2, 3, 1)
+    if epi == "eval":
+        st = torch.stack([torch.zeros(Cout), torch.ones(Cout), torch.rand(Cout, generator=g) + 0.5,
+                          torch.randn(Cout, generator=g) * 0.1])
+        K.conv_fwd_bn_eval(K.Act(x.to(dev)), wp, Cout, 3, 1, z, b.to(dev), st.to(dev), 1)
+        ref = (ref * st[2].double() + st[3].double()).clamp_min(0)
+    elif epi == "stats":
+        rows = K.query("dg_conv_stats_rows_ex", 0, N, H, W, C, C, Cout, 3, 3)
+        assert rows == -(-(N * H * W) // 192)
+        part, r2 = K.conv_fwd_stats(K.Act(x.to(dev)), wp, Cout, 3, 1, z, bias=b.to(dev))
+        assert r2 == rows
+    else:
+        K.conv_fwd(K.Act(x.to(dev)), wp, Cout, 3, 1, z, bias=b.to(dev))
+    torch.cuda.synchronize()
+    y = z.buf.cpu()
+    assert relerr(y, ref) < 5e-6
+    if epi == "stats":
+        p = part.double().cpu()
+        n, mean, m2 = p[:, 0], p[:, 1], p[:, 2]
+        tot = n.sum(0)
+        gm = (n * mean).sum(0) / tot
+        var = (m2 + n * (mean - gm) ** 2).sum(0) / tot
+        yd = y.double().reshape(-1, Cout)
+        assert torch.equal(tot, torch.full_like(tot, N * H * W))
+        assert relerr(gm, yd.mean(0)) < 1e-5 and relerr(var, yd.var(0, unbiased=False)) < 1e-5

@@ -9,8 +9,8 @@ timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py tests/test_model
 rc=$?
 tail -15 $OUT/tests.log
 [ $rc -eq 0 ] || exit $rc
-B="--steps 3 --warmup 1 --no-cpu-baseline --no-bf16"
+B="--steps 3 --warmup 1 --no-cpu-baseline --no-bf16 --no-f32-exact"
 timeout -k 10 300 python3 bench.py $B > $OUT/bench_split.json 2> $OUT/bench_split.err || { tail -20 $OUT/bench_split.err; exit 1; }
 cat $OUT/bench_split.json
-DGVCC_F32_MATH=exact timeout -k 10 300 python3 bench.py $B > $OUT/bench_exact.json 2> $OUT/bench_exact.err || { tail -20 $OUT/bench_exact.err; exit 1; }
+DGVCC_PSPLIT=0 timeout -k 10 300 python3 bench.py $B > $OUT/bench_exact.json 2> $OUT/bench_exact.err || { tail -20 $OUT/bench_exact.err; exit 1; }
 cat $OUT/bench_exact.json
