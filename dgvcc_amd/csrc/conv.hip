@@ -2108,6 +2108,8 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
 // weight gradient: split-K over pixels into f32 slabs, then a deterministic
 // reduce that also transposes to torch's [Cout][C][R][S] layout.
 // ---------------------------------------------------------------------------
+struct WgPlan { int splits, pps; };
+
 struct WgArgs {
   const char* x; long long ldx; int N, H, W, C;
   const char* dy; long long lddy; int Cout, R, S, pad;
@@ -2334,6 +2336,226 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
       }
     }
 }
+
+// f32 weight gradient on the bf16 matrix cores (split math), one block per CU: 8 waves
+// (WCO x 8/WCO over the BCO x BC tile of one (r,s) tap), K = 32 pixels per step.  The f32
+// pixel rows of dY and X are loaded to registers (one step ahead), split ONCE per block
+// (dg_common.h: x = h0 + h1 + h2 exactly) and stored as three bf16 planes [pixel][channel];
+// fragments are read transposed with ds_read_b64_tr_b16 as in the bf16 kernel (logical
+// k = 8g + j -> pixel row 4g + (j & 3) + 16 (j >> 2), both operands), six MFMA products
+// per 16x16x32 block.  The per-wave fragment split (conv_wgrad_kernel SPL = 1) did 4x the
+// split work of this per-block one.
+__device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const unsigned a = x[2 * k], b = x[2 * k + 1];
+    h0[k] = hi16x2(a, b);
+    const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
+    const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
+    const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
+    h1[k] = hi16x2(ua, ub);
+    const float sa = ra - __uint_as_float(ua & 0xffff0000u);
+    const float sb = rb - __uint_as_float(ub & 0xffff0000u);
+    h2[k] = hi16x2(__float_as_uint(sa), __float_as_uint(sb));
+  }
+}
+
+template <int BCO, int BC, int WCO>
+__global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
+  constexpr int BKP = 32;
+  constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
+  constexpr int PA = BKP * ROWA, PB = BKP * ROWB;          // bytes per plane
+  constexpr int TILE = 3 * (PA + PB);
+  constexpr int CPRA = BCO / 4, CPRB = BC / 4;             // 16-B f32 chunks per pixel row
+  constexpr int AR = BKP * CPRA / 512, BR = BKP * CPRB / 512;
+  constexpr int WC = 8 / WCO;
+  constexpr int TI = BCO / WCO / 16, TJ = BC / WC / 16;
+  static_assert(AR >= 1 && BR >= 1 && TI >= 1 && TJ >= 1, "tile too small for 512 threads");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
+
+  const int HW = a.H * a.W;
+  const int PQ = a.P * a.Q;
+  const int M = a.N * PQ;
+  const int RS = a.R * a.S;
+  const int nco = a.Cout / BCO, ncb = a.C / BC;
+  const int tiles = nco * ncb * RS;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  int t = bid - split * tiles;
+  const int cot = t % nco; t /= nco;
+  const int cbt = t % ncb;
+  const int rs = t / ncb;
+  const int co0 = cot * BCO, c0 = cbt * BC;
+  const int r = rs / a.S, s = rs - r * a.S;
+  const int dh = r - a.pad, dw = s - a.pad;
+  const int kbeg = split * a.pps;
+  const int kend = min(M, kbeg + a.pps);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 4);
+  __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.dy + (long long)kbeg * a.lddy * 4), 0, dy_bytes, 0x00020000);
+  const int halo = a.pad * (a.W + 1);
+  const int xlo = a.whole_x ? 0 : max(0, kbeg - halo);
+  const int xhi = a.whole_x ? a.N * HW : min(M, kend + halo);
+  const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 4);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * 4), 0, x_bytes, 0x00020000);
+
+  u4v ra[AR], rb[BR];
+  int cn[BR], cp[BR], cq[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int px = kbeg + (tid + 512 * i) / CPRB;
+    cn[i] = px / PQ;
+    const int rem = px - cn[i] * PQ;
+    cp[i] = rem / a.Q;
+    cq[i] = rem - cp[i] * a.Q;
+  }
+  auto gload = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx / CPRA, ch = idx % CPRA;
+      const int px = k0 + row;
+      const unsigned off = (px < kend) ? (unsigned)(((long long)(px - kbeg) * a.lddy + co0 + ch * 4) * 4) : 0xFFFFFFF0u;
+      ra[i] = bload(dyr, off);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx / CPRB, ch = idx % CPRB;
+      const int px = k0 + row;
+      const int h = cp[i] * a.stride + dh, ww = cq[i] * a.stride + dw;
+      const bool ok = px < kend && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pin = (long long)cn[i] * HW + (long long)h * a.W + ww - xlo;
+      const unsigned off = ok ? (unsigned)((pin * a.ldx + c0 + ch * 4) * 4) : 0xFFFFFFF0u;
+      rb[i] = bload(xr, off);
+      cq[i] += BKP;
+      while (cq[i] >= a.Q) {
+        cq[i] -= a.Q;
+        if (++cp[i] == a.P) { cp[i] = 0; ++cn[i]; }
+      }
+    }
+  };
+  auto swrite = [&](int buf) __attribute__((always_inline)) {
+    char* As = smem + buf * TILE;
+    char* Bs = As + 3 * PA;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int idx = tid + 512 * i;
+      const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
+      u2v h0, h1, h2;
+      split3_4(ra[i], h0, h1, h2);
+      *(u2v*)(As + o) = h0;
+      *(u2v*)(As + PA + o) = h1;
+      *(u2v*)(As + 2 * PA + o) = h2;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int idx = tid + 512 * i;
+      const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
+      u2v h0, h1, h2;
+      split3_4(rb[i], h0, h1, h2);
+      *(u2v*)(Bs + o) = h0;
+      *(u2v*)(Bs + PB + o) = h1;
+      *(u2v*)(Bs + 2 * PB + o) = h2;
+    }
+  };
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int wco = (wid / WC) * (BCO / WCO), wc = (wid % WC) * (BC / WC);
+  const int g = lane >> 4;
+  const int q = (lane & 15) >> 2, p4 = lane & 3;
+  const int r1 = 4 * g + q, r2 = r1 + 16;
+
+  const int nkt = (kend - kbeg + BKP - 1) / BKP;
+  gload(kbeg);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kbeg + (kt + 1) * BKP);
+    const char* As = smem + cur * TILE;
+    const char* Bs = As + 3 * PA;
+    s8v bh[TJ][3];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int col = (wc + 16 * j + 4 * p4) * 2;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const char* b = Bs + pl * PB;
+        s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r1 * ROWB + col));
+        s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r2 * ROWB + col));
+        bh[j][pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int col = (wco + 16 * i + 4 * p4) * 2;
+      s8v ah[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const char* b = As + pl * PA;
+        s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r1 * ROWA + col));
+        s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r2 * ROWA + col));
+        ah[pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  const long long ldk = (long long)RS * a.C;
+  float* out = a.slab + (long long)split * a.Cout * ldk;
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int c = c0 + wc + 16 * j + (lane & 15);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int co = co0 + wco + 16 * i + 4 * g + rr;
+        out[co * ldk + rs * a.C + c] = acc[i][j][rr];
+      }
+    }
+}
+
+// Split plan of conv_wgrad_split_kernel: one block per CU (256 slots), 32-pixel K-steps.
+static WgPlan wgs_plan(long long M, long long tiles) {
+  const long long slots = 256;
+  const long long max_split = (M + 32 * 4 - 1) / (32 * 4);
+  long long splits = 1;
+  double best_eff = -1.0;
+  for (int rounds = 1; rounds <= 32; ++rounds) {
+    long long sp = std::max(1ll, std::min(slots * rounds / tiles, max_split));
+    const long long blocks = tiles * sp;
+    const double eff = (double)blocks / (double)(slots * ((blocks + slots - 1) / slots));
+    if (eff > best_eff + 1e-9) { best_eff = eff; splits = sp; }
+    if (eff >= 0.96 || sp == max_split) break;
+  }
+  long long pps = (M + splits - 1) / splits;
+  pps = (pps + 31) / 32 * 32;
+  splits = (M + pps - 1) / pps;
+  return WgPlan{(int)splits, (int)pps};
+}
+static bool use_wgrad_split() {  // DGVCC_WGRAD_SPLIT=0: f32 split-math wgrad on conv_wgrad_kernel SPL = 1
+  const char* e = getenv("DGVCC_WGRAD_SPLIT");
+  return !(e && e[0] == '0');
+}
+static bool wgs_ok(int C, int Cout) { return use_wgrad_split() && Cout % 128 == 0 && C % 128 == 0; }
+static long long wgs_tiles(int C, int Cout, int RS) { return (long long)(Cout / 128) * (C / (C % 256 == 0 ? 256 : 128)) * RS; }
 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int C, int RS,
                                     float* __restrict__ dw, int accumulate) {
@@ -2795,7 +3017,6 @@ static bool wg9p_ok(int N, int H, int W, int C, int Cout, int R, int S, int pad,
          M * std::max(ldx, lddy) * 2 < (1ll << 31) && (long long)N * (H + 2) * (W + 2) < (1ll << 30);
 }
 
-struct WgPlan { int splits, pps; };
 
 // splits for the fused-tap kernel: >= 8 K-steps per block, block count chosen for
 // whole rounds of one block per CU (tail efficiency >= 90% where possible), starting from
@@ -2915,7 +3136,19 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   }
   if (done) {
   } else if constexpr (!Is16<T>::value) {
-    if (f32_split()) {
+    const bool wgs = f32_split() && wgs_ok(a.C, a.Cout);
+    const WgPlan pw = wgs ? wgs_plan((long long)a.N * a.P * a.Q, wgs_tiles(a.C, a.Cout, a.R * a.S)) : WgPlan{1, 0};
+    if (wgs &&
+        (long long)(pw.pps + 2 * a.pad * (a.W + 1)) * std::max(a.ldx, a.lddy) * 4 < (1ll << 31)) {
+      const WgPlan p = pw;
+      a.splits = p.splits;
+      a.pps = p.pps;
+      slab_splits = p.splits;
+      const dim3 gs((unsigned)(wgs_tiles(a.C, a.Cout, a.R * a.S) * p.splits));
+      if (a.C % 256 == 0) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2>), gs, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 128, 2>), gs, dim3(512), 0, st, a);
+      done = true;
+    } else if (f32_split()) {
       if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128, 1>), grid, dim3(NT), 0, st, a);
       else if (bco == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 64, 1>), grid, dim3(NT), 0, st, a);
       else if (bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 64, 128, 1>), grid, dim3(NT), 0, st, a);
@@ -3281,6 +3514,7 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
   // the padded 9-tap plan may be refused at launch (pixel strides too large): cover the
   // fallback plan too
   WgPlan q = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
+  if (!DG_IS16(dtype) && wgs_ok(C, Cout)) q = wgs_plan((long long)N * H * W, wgs_tiles(C, Cout, R * S));
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
   return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
 }
