@@ -2360,17 +2360,17 @@ __device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2
   }
 }
 
-template <int BCO, int BC, int WCO>
-__global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
+template <int BCO, int BC, int WCO, int NTH = 512>
+__global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs a) {
   constexpr int BKP = 32;
   constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
   constexpr int PA = BKP * ROWA, PB = BKP * ROWB;          // bytes per plane
   constexpr int TILE = 3 * (PA + PB);
   constexpr int CPRA = BCO / 4, CPRB = BC / 4;             // 16-B f32 chunks per pixel row
-  constexpr int AR = BKP * CPRA / 512, BR = BKP * CPRB / 512;
-  constexpr int WC = 8 / WCO;
+  constexpr int AR = BKP * CPRA / NTH, BR = BKP * CPRB / NTH;
+  constexpr int WC = NTH / 64 / WCO;
   constexpr int TI = BCO / WCO / 16, TJ = BC / WC / 16;
-  static_assert(AR >= 1 && BR >= 1 && TI >= 1 && TJ >= 1, "tile too small for 512 threads");
+  static_assert(AR >= 1 && BR >= 1 && TI >= 1 && TJ >= 1, "tile too small for the block");
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
 
   const int HW = a.H * a.W;
@@ -2406,7 +2406,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
   int cn[BR], cp[BR], cq[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
-    const int px = kbeg + (tid + 512 * i) / CPRB;
+    const int px = kbeg + (tid + NTH * i) / CPRB;
     cn[i] = px / PQ;
     const int rem = px - cn[i] * PQ;
     cp[i] = rem / a.Q;
@@ -2415,7 +2415,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
   auto gload = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const int idx = tid + 512 * i;
+      const int idx = tid + NTH * i;
       const int row = idx / CPRA, ch = idx % CPRA;
       const int px = k0 + row;
       const unsigned off = (px < kend) ? (unsigned)(((long long)(px - kbeg) * a.lddy + co0 + ch * 4) * 4) : 0xFFFFFFF0u;
@@ -2423,7 +2423,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int idx = tid + 512 * i;
+      const int idx = tid + NTH * i;
       const int row = idx / CPRB, ch = idx % CPRB;
       const int px = k0 + row;
       const int h = cp[i] * a.stride + dh, ww = cq[i] * a.stride + dw;
@@ -2443,7 +2443,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
     char* Bs = As + 3 * PA;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
-      const int idx = tid + 512 * i;
+      const int idx = tid + NTH * i;
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       u2v h0, h1, h2;
       split3_4(ra[i], h0, h1, h2);
@@ -2453,7 +2453,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int idx = tid + 512 * i;
+      const int idx = tid + NTH * i;
       const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
       u2v h0, h1, h2;
       split3_4(rb[i], h0, h1, h2);
@@ -2533,8 +2533,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad_split_kernel(WgArgs a) {
 }
 
 // Split plan of conv_wgrad_split_kernel: one block per CU (256 slots), 32-pixel K-steps.
-static WgPlan wgs_plan(long long M, long long tiles) {
-  const long long slots = 256;
+static WgPlan wgs_plan(long long M, long long tiles, long long slots = 256) {
   const long long max_split = (M + 32 * 4 - 1) / (32 * 4);
   long long splits = 1;
   double best_eff = -1.0;
@@ -2554,8 +2553,17 @@ static bool use_wgrad_split() {  // DGVCC_WGRAD_SPLIT=0: f32 split-math wgrad on
   const char* e = getenv("DGVCC_WGRAD_SPLIT");
   return !(e && e[0] == '0');
 }
-static bool wgs_ok(int C, int Cout) { return use_wgrad_split() && Cout % 128 == 0 && C % 128 == 0; }
-static long long wgs_tiles(int C, int Cout, int RS) { return (long long)(Cout / 128) * (C / (C % 256 == 0 ? 256 : 128)) * RS; }
+// tile (BCO x BC) and resident blocks per CU of conv_wgrad_split_kernel for a shape: 128 x 256 /
+// 128 x 128 / 128 x 64 (512 threads, one block per CU), 64 x 64 (256 threads, two per CU)
+static bool wgs_ok(int C, int Cout) { return use_wgrad_split() && Cout % 64 == 0 && C % 64 == 0; }
+static int wgs_bco(int C, int Cout) { return Cout % 128 == 0 ? 128 : 64; }
+static int wgs_bc(int C, int Cout) {
+  return wgs_bco(C, Cout) == 64 ? 64 : (C % 256 == 0 ? 256 : (C % 128 == 0 ? 128 : 64));
+}
+static long long wgs_tiles(int C, int Cout, int RS) {
+  return (long long)(Cout / wgs_bco(C, Cout)) * (C / wgs_bc(C, Cout)) * RS;
+}
+static long long wgs_slots(int C, int Cout) { return wgs_bco(C, Cout) == 64 ? 512 : 256; }
 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int C, int RS,
                                     float* __restrict__ dw, int accumulate) {
@@ -3137,7 +3145,8 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   if (done) {
   } else if constexpr (!Is16<T>::value) {
     const bool wgs = f32_split() && wgs_ok(a.C, a.Cout);
-    const WgPlan pw = wgs ? wgs_plan((long long)a.N * a.P * a.Q, wgs_tiles(a.C, a.Cout, a.R * a.S)) : WgPlan{1, 0};
+    const WgPlan pw = wgs ? wgs_plan((long long)a.N * a.P * a.Q, wgs_tiles(a.C, a.Cout, a.R * a.S), wgs_slots(a.C, a.Cout))
+                          : WgPlan{1, 0};
     if (wgs &&
         (long long)(pw.pps + 2 * a.pad * (a.W + 1)) * std::max(a.ldx, a.lddy) * 4 < (1ll << 31)) {
       const WgPlan p = pw;
@@ -3145,8 +3154,11 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
       a.pps = p.pps;
       slab_splits = p.splits;
       const dim3 gs((unsigned)(wgs_tiles(a.C, a.Cout, a.R * a.S) * p.splits));
-      if (a.C % 256 == 0) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2>), gs, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 128, 2>), gs, dim3(512), 0, st, a);
+      const int bco = wgs_bco(a.C, a.Cout), bcw = wgs_bc(a.C, a.Cout);
+      if (bco == 64) hipLaunchKernelGGL((conv_wgrad_split_kernel<64, 64, 2, 256>), gs, dim3(256), 0, st, a);
+      else if (bcw == 256) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2>), gs, dim3(512), 0, st, a);
+      else if (bcw == 128) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 128, 2>), gs, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 64, 4>), gs, dim3(512), 0, st, a);
       done = true;
     } else if (f32_split()) {
       if (bco == 128 && bc == 128) hipLaunchKernelGGL((conv_wgrad_kernel<T, 128, 128, 1>), grid, dim3(NT), 0, st, a);
@@ -3514,7 +3526,8 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
   // the padded 9-tap plan may be refused at launch (pixel strides too large): cover the
   // fallback plan too
   WgPlan q = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
-  if (!DG_IS16(dtype) && wgs_ok(C, Cout)) q = wgs_plan((long long)N * H * W, wgs_tiles(C, Cout, R * S));
+  if (!DG_IS16(dtype) && wgs_ok(C, Cout))
+    q = wgs_plan((long long)N * H * W, wgs_tiles(C, Cout, R * S), wgs_slots(C, Cout));
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
   return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
 }
