@@ -1234,6 +1234,166 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   }
 }
 
+// f32 forward/dgrad for Cout = 64 layers on the split math, both operands split ONCE per
+// block: the pre-split filter planes (split_weight_kernel) and the f32 pixel rows are loaded
+// to registers one K-step ahead; the pixel rows are split while being stored to LDS as three
+// bf16 planes (64-B rows, chunk c of row r at c ^ ((r >> 2) & 3), as the filter planes).
+// Tile 64 channels x 256 pixels, 8 waves of 64 pixels x 32 channels, 32-channel K-steps,
+// double-buffered LDS (2 x 60 KB).  With only two channel fragments per wave, the per-wave
+// pixel split of conv_fwd_pers_kernel<64, .., SPL = 1> cost more VALU than its MFMAs.
+template <int EPI = 0>
+__global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int BN = 64, BPX = 256;
+  constexpr int A_PL = BN * 64, B_PL = BPX * 64;  // plane bytes
+  constexpr int BUF = 3 * (A_PL + B_PL);
+  constexpr int TI = 2, TJ = 4;
+  constexpr int BR = BPX * 8 / 512;               // 16-B f32 chunks of the pixel tile per thread
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (bid % nco) * BN;
+  const int px0 = (bid / nco) * BPX;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = tid & 7, rbase = tid >> 3;
+  const int CB = a.C / 32;
+  const int KT = a.R * a.S * CB;
+
+  const int halo = a.pad * (a.W + 1);
+  const int plo = max(0, px0 - halo);
+  const int phi = min(M, px0 + BPX + halo);
+  const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 4);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 4), 0,
+                                                                win_bytes, 0x00020000);
+  int pp[BR], pq[BR], prow[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int m = px0 + rbase + 64 * i;
+    const int rem = m % HW;
+    prow[i] = m;
+    pp[i] = (m < M) ? rem / a.W : -100000;
+    pq[i] = rem % a.W;
+  }
+  // filter-plane chunks: q = tid (all threads) and q = tid + 512 (tid < 256); q -> (plane, row, chunk)
+  const char* wbase = wsp + (long long)co0 * KT * 192;
+  auto wq_off = [&](int q) { return (long long)((q & 255) >> 2) * KT * 192 + (q >> 8) * 64 + (q & 3) * 16; };
+  auto wq_lds = [&](int q) {
+    const int row = (q & 255) >> 2;
+    return (q >> 8) * A_PL + row * 64 + (((q & 3) ^ ((row >> 2) & 3)) << 4);
+  };
+  const long long wo0 = wq_off(tid), wo1 = wq_off(tid + 512);
+  const int wl0 = wq_lds(tid), wl1 = wq_lds(tid + 512);
+
+  u4v ra0, ra1, rb[BR];
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    const int rs = t / CB, cb = t - rs * CB;
+    const int r = rs / a.S, s2 = rs - r * a.S;
+    ra0 = *(const u4v*)(wbase + wo0 + (long long)t * 192);
+    if (tid < 256) ra1 = *(const u4v*)(wbase + wo1 + (long long)t * 192);
+    const int dh = r - a.pad, dw = s2 - a.pad;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int h = pp[i] + dh, ww = pq[i] + dw;
+      const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pin = (long long)(prow[i] + dh * a.W + dw - plo);
+      const unsigned off = ok ? (unsigned)((pin * a.ldx + cb * 32 + chunk * 4) * 4) : 0xFFFFFFF0u;
+      rb[i] = bload(xr, off);
+    }
+  };
+  auto swrite = [&](int buf) __attribute__((always_inline)) {
+    char* As = smem + buf * BUF;
+    char* Bs = As + 3 * A_PL;
+    *(u4v*)(As + wl0) = ra0;
+    if (tid < 256) *(u4v*)(As + wl1) = ra1;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = rbase + 64 * i;
+      const int o = row * 64 + ((((chunk >> 1) ^ ((row >> 2) & 3))) << 4) + (chunk & 1) * 8;
+      u2v h0, h1, h2;
+      split3_4(rb[i], h0, h1, h2);
+      *(u2v*)(Bs + o) = h0;
+      *(u2v*)(Bs + B_PL + o) = h1;
+      *(u2v*)(Bs + 2 * B_PL + o) = h2;
+    }
+  };
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int wpx = (wid & 3) * 64, wco = (wid >> 2) * 32;
+  const int fr = lane & 15, fc = lane >> 4;
+
+  gload(0);
+  swrite(0);
+  __syncthreads();
+  for (int t = 0; t < KT; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < KT) gload(t + 1);
+    const char* As = smem + cur * BUF;
+    const char* Bs = As + 3 * A_PL;
+    s8v bh[TJ][3], ah[TI][3];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int row = wpx + 16 * j + fr;
+      const int o = row * 64 + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
+    }
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int row = wco + 16 * i + fr;
+      const int o = row * 64 + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) ah[i][pl] = *(const s8v*)(As + pl * A_PL + o);
+    }
+    constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int i = 0; i < TI; ++i)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+    if (t + 1 < KT) swrite(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* y = (float*)a.y;
+  bool valid[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    valid[j] = px < M;
+    if (px >= M) continue;
+    float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco + 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      if constexpr (EPI == 3) epi_affine(v, a, co);
+      st4(yrow + co, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+    }
+  }
+  if (EPI == 0 && a.part)  // smem reuse: every wave is past the K loop's last barrier
+    epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / BPX) * 3 * a.Cout, a.Cout,
+                             co0, tid, fr, fc);
+}
+
 // wsp[co][kb][part][32] (bf16) = the exact 3-way split of the packed f32 filter w[co][kb*32 + j]
 __global__ void split_weight_kernel(const float* __restrict__ w, long long n, unsigned short* __restrict__ wsp) {
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n; o += (long long)gridDim.x * blockDim.x) {
@@ -1952,6 +2112,12 @@ static bool psplit_ok(const FwdArgs& a) {
          (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
 }
 
+// f32 split-math shapes served by conv_fwd_rsplit_kernel (64-wide channel tiles)
+static bool rsplit_ok(const FwdArgs& a) {
+  return use_psplit() && f32_split() && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 && a.ldx % 4 == 0 &&
+         a.Cout % 64 == 0 && f32_pers_bn(a.Cout) == 64 && (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
+}
+
 // Per-stream device scratch for the pre-split filter panels (grown on demand; a launch on
 // a stream only ever overlaps its own stream's earlier work, which hipFree waits for).
 static void* split_scratch(hipStream_t st, size_t bytes) {
@@ -2049,6 +2215,18 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
     }
   }
   if constexpr (!Is16<T>::value) {
+    if (rsplit_ok(a)) {  // split math, Cout = 64: both operands split once per block
+      const long long nw = (long long)a.Cout * a.R * a.S * a.C;
+      unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
+      if (!wsp) return DG_ERR_HIP;
+      hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
+                         0, st, (const float*)a.w, nw, wsp);
+      const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));
+      if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
+      else hipLaunchKernelGGL((conv_fwd_rsplit_kernel<0>), g, dim3(512), 0, st, a, (const char*)wsp);
+      DG_CHECK_LAUNCH();
+      return DG_OK;
+    }
     // f32: the persistent LDS-DMA pipeline with 128-B (32-channel) K-steps; each K-step is 4x
     // the MFMA work of a 16-bit one (v_mfma_f32_16x16x4_f32), so the 2-stage 256-wide ring
     // hides the DMA latency comfortably.  Epilogue BN statistics (a.part) as in 16-bit.
@@ -2345,21 +2523,6 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
 // k = 8g + j -> pixel row 4g + (j & 3) + 16 (j >> 2), both operands), six MFMA products
 // per 16x16x32 block.  The per-wave fragment split (conv_wgrad_kernel SPL = 1) did 4x the
 // split work of this per-block one.
-__device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2) {
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const unsigned a = x[2 * k], b = x[2 * k + 1];
-    h0[k] = hi16x2(a, b);
-    const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
-    const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
-    const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
-    h1[k] = hi16x2(ua, ub);
-    const float sa = ra - __uint_as_float(ua & 0xffff0000u);
-    const float sb = rb - __uint_as_float(ub & 0xffff0000u);
-    h2[k] = hi16x2(__float_as_uint(sa), __float_as_uint(sb));
-  }
-}
-
 template <int BCO, int BC, int WCO, int NTH = 512>
 __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs a) {
   constexpr int BKP = 32;
@@ -3400,7 +3563,7 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate, part};
-  if (part) DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S) : f32_pers_ok(a));
+  if (part) DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S) : (f32_pers_ok(a) || rsplit_ok(a)));
   {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
      // runs dg_conv_fwd + the statistics pass instead
     FwdArgs q = a;

@@ -185,3 +185,19 @@ __device__ __forceinline__ f4v mfma_x6(const s8v& a0, const s8v& a1, const s8v& 
   c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, c, 0, 0, 0);
   return c;
 }
+
+// 4 f32 -> the bf16 parts of each (element k of part p = part p of x[k])
+__device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const unsigned a = x[2 * k], b = x[2 * k + 1];
+    h0[k] = hi16x2(a, b);
+    const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
+    const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
+    const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
+    h1[k] = hi16x2(ua, ub);
+    const float sa = ra - __uint_as_float(ua & 0xffff0000u);
+    const float sb = rb - __uint_as_float(ub & 0xffff0000u);
+    h2[k] = hi16x2(__float_as_uint(sa), __float_as_uint(sb));
+  }
+}

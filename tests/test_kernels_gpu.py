@@ -362,9 +362,12 @@ def test_conv_f32_split_math(dev, case):
 
 
 @pytest.mark.parametrize("N,H,W,C,Cout,epi", [(5, 128, 256, 64, 256, "stats"), (3, 96, 320, 128, 128, "stats"),
-                                              (3, 128, 256, 256, 512, "eval"), (8, 100, 130, 128, 256, "bias")])
+                                              (3, 128, 256, 256, 512, "eval"), (8, 100, 130, 128, 256, "bias"),
+                                              (3, 70, 90, 64, 64, "stats"), (2, 64, 256, 128, 64, "eval"),
+                                              (2, 33, 40, 64, 64, "bias")])
 def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
-    """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128) with
+    """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128; Cout = 64 on
+    conv_fwd_rsplit_kernel, 256-pixel tiles) with
     bias + epilogue BN statistics (rows per 192-pixel tile: dg_conv_stats_rows_ex), the eval-BN
     epilogue and a ragged last tile, against float64: y within 5e-6, the merged (n, mean, M2)
     rows equal to the statistics of the stored y."""
@@ -383,7 +386,7 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
         ref = (ref * st[2].double() + st[3].double()).clamp_min(0)
     elif epi == "stats":
         rows = K.query("dg_conv_stats_rows_ex", 0, N, H, W, C, C, Cout, 3, 3)
-        assert rows == -(-(N * H * W) // 192)
+        assert rows == -(-(N * H * W) // (192 if Cout % 128 == 0 else 256))  # 64-wide tiles: conv_fwd_rsplit_kernel
         part, r2 = K.conv_fwd_stats(K.Act(x.to(dev)), wp, Cout, 3, 1, z, bias=b.to(dev))
         assert r2 == rows
     else:
