@@ -1352,13 +1352,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
     }
     constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-    for (int u = 0; u < 6; ++u)
+    for (int u = 0; u < 6; ++u) {
 #pragma unroll
       for (int i = 0; i < TI; ++i)
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
-    if (t + 1 < KT) swrite(cur ^ 1);
+      if (u == 2 && t + 1 < KT) swrite(cur ^ 1);  // overlapped with the remaining products
+    }
     __syncthreads();
   }
 
@@ -2675,8 +2676,11 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 #pragma unroll
         for (int j = 0; j < TJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+      // the next step's split + LDS stores between the MFMA blocks (the other buffer was last
+      // read before the previous barrier), so its VALU/LDS work overlaps this step's MFMAs
+      if (NTH == 512 && i == (TI - 1) / 2 && kt + 1 < nkt) swrite(cur ^ 1);
     }
-    if (kt + 1 < nkt) swrite(cur ^ 1);
+    if (NTH != 512 && kt + 1 < nkt) swrite(cur ^ 1);  // two blocks per CU overlap each other instead
     __syncthreads();
   }
 
