@@ -342,6 +342,9 @@ def run_leg(args, precision, dev, world, rank):
 def roofline(args, precision, r):
     peak = PEAKS[precision]
     kname = FWD_KERNEL_NAMES.get(precision, "implicit-GEMM conv forward + dgrad")
+    if args.trunk:  # ResNet-50 trunk: strided/non-"same" convs on conv_gen_kernel, 3x3/1x1 stride 1 as above
+        kname = ("conv_gen_kernel (strided / 7x7 stem im2col / parity-class dgrad) + " + kname.split(" (")[0] +
+                 " (ResNet-50 trunk convs: forward + dgrad launches)")
     precision = "fp32" if precision == "fp32_exact" else precision
     achieved = r["conv_flops"] / (r["conv_ms"] * 1e-3) / 1e12 if r["conv_ms"] > 0 else 0.0
     traffic, tsrc = measured_traffic(args, precision)
