@@ -454,6 +454,240 @@ __global__ void mul_kernel(const float* __restrict__ a, const float* __restrict_
     out[i] = a[i] * b[i];
 }
 
+// ------------------------------------------------------- memory read + head --
+// y_new = mem P (models/models.py:120-121) is consumed only by den_head, a 1x1 conv k -> 1 with
+// bias and ReLU (models/models.py:112-114, 130-131, 328-329; models2.py DensityRegressorM), so
+//   d = act(w . (mem P) + b) = act(v . P + b),   v = mem^T w   (one 1024-vector per step):
+// the readout GEMM (2 k S FLOP per pixel) becomes a 1024-long dot fused into the softmax pass.
+// Backward: g_ynew = gpre w^T is rank 1, hence
+//   gP = gpre v (formed in registers, never stored),  dmem_readout = w u^T,  dw = mem u,  db = sum gpre,
+//   u = sum_px gpre P  (per-block partial rows, reduced in a fixed order).
+// NV = views per launch (1 or 2); LOSS: 0 none, 1 JSD-MSE mean((P1-P2)^2) (models.py:286-296),
+// 2 KL-JSD of DensityRegressorM (models2.py:339-346).
+__device__ __forceinline__ float mh_act(float s, int act) {
+  if (act == 1) return s > 0.f ? s : 0.f;
+  if (act == 2) return 1.f / (1.f + expf(-s));
+  return s;
+}
+__device__ __forceinline__ float mh_gpre(float gy, float y, int act) {
+  if (act == 1) return y > 0.f ? gy : 0.f;
+  if (act == 2) return gy * y * (1.f - y);
+  return gy;
+}
+// v at this lane's slots, in load_row's element order
+template <typename T>
+__device__ __forceinline__ void load_vec_as_row(const float* v, int lane, float* o, int EPL) {
+  constexpr int V = 16 / (int)sizeof(T);
+  for (int j = 0; j < EPL; ++j) o[j] = v[(j / V) * 64 * V + lane * V + (j % V)];
+}
+
+template <typename T, int EPL, int NV, int LOSS>
+__global__ __launch_bounds__(NT) void softmax_head_fwd(const T* __restrict__ L1, const T* __restrict__ L2, int M,
+                                                       int C, const float* __restrict__ v, const float* bias, int act,
+                                                       T* __restrict__ P1, T* __restrict__ P2, float* __restrict__ yh1,
+                                                       float* __restrict__ yh2, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float vv[EPL];
+  load_vec_as_row<T>(v, lane, vv, EPL);
+  const float hb = bias ? bias[0] : 0.f;
+  float acc = 0.f;
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    float a[EPL], b[EPL], la[EPL], lb[EPL];
+    load_row(L1 + r * C, lane, C, a, EPL);
+    if (NV == 2) load_row(L2 + r * C, lane, C, b, EPL);
+    float ma = -INFINITY, mb = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      ma = fmaxf(ma, a[j]);
+      if (NV == 2) mb = fmaxf(mb, b[j]);
+    }
+    ma = wave_max(ma);
+    if (NV == 2) mb = wave_max(mb);
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      la[j] = a[j] - ma;
+      a[j] = expf(la[j]);
+      sa += a[j];
+      if (NV == 2) { lb[j] = b[j] - mb; b[j] = expf(lb[j]); sb += b[j]; }
+    }
+    sa = wave_sum(sa);
+    if (NV == 2) sb = wave_sum(sb);
+    const float ra = 1.f / sa, rb = NV == 2 ? 1.f / sb : 0.f;
+    const float dls = LOSS == 2 ? logf(sa) - logf(sb) : 0.f;
+    float z1 = 0.f, z2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      a[j] *= ra;
+      if (NV == 2) b[j] *= rb;
+      if (LOSS == 2) {  // cancellation-free 2 log pm - log p1 - log p2 (as softmax_jsd_fwd)
+        const float pm = 0.5f * (a[j] + b[j]);
+        const float e = expm1f((la[j] - lb[j]) - dls);
+        if (pm > 0.f) acc += pm * log1pf(e * e / (4.f * (1.f + e)));
+      }
+      a[j] = to_f(from_f<T>(a[j]));  // the loss and the head see the stored probabilities
+      if (NV == 2) b[j] = to_f(from_f<T>(b[j]));
+      if (LOSS == 1) { const float d = a[j] - b[j]; acc = fmaf(d, d, acc); }
+      z1 = fmaf(vv[j], a[j], z1);
+      if (NV == 2) z2 = fmaf(vv[j], b[j], z2);
+    }
+    if (P1) store_row(P1 + r * C, lane, a, EPL);
+    if (NV == 2 && P2) store_row(P2 + r * C, lane, b, EPL);
+    z1 = wave_sum(z1);
+    if (NV == 2) z2 = wave_sum(z2);
+    if (lane == 0) {
+      yh1[r] = mh_act(z1 + hb, act);
+      if (NV == 2) yh2[r] = mh_act(z2 + hb, act);
+    }
+  }
+  if (LOSS) {
+    acc = wave_sum(acc);
+    __shared__ float sh[4];
+    if (lane == 0) sh[w] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+  }
+}
+
+// gL_v = P_v (gP_v - <P_v, gP_v>) with gP_v = gpre_v v + (loss term); u/db partials per block:
+// part[blk][0:C] = sum_px sum_v gpre_v P_v, part[blk][C] = sum_px sum_v gpre_v.
+template <typename T, int EPL, int NV, int LOSS>
+__global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1, const T* __restrict__ P2, int M,
+                                                       int C, const float* __restrict__ v, int act,
+                                                       const float* __restrict__ yh1, const float* __restrict__ yh2,
+                                                       const float* __restrict__ gyh1, const float* __restrict__ gyh2,
+                                                       const float* __restrict__ coef, T* __restrict__ GL1,
+                                                       T* __restrict__ GL2, float* __restrict__ part) {
+  constexpr int V = 16 / (int)sizeof(T);
+  __shared__ float sh[4 * EPL * 64 + 4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float vv[EPL], u[EPL];
+  load_vec_as_row<T>(v, lane, vv, EPL);
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) u[j] = 0.f;
+  float sgb = 0.f;
+  const float k = !coef ? 0.f : (LOSS == 1 ? 2.f * coef[0] / ((float)M * (float)C) : coef[0] / (2.f * (float)M));
+  for (long long r = (long long)blockIdx.x * 4 + w; r < M; r += (long long)gridDim.x * 4) {
+    const float q1 = gyh1 ? mh_gpre(gyh1[r], yh1[r], act) : 0.f;
+    const float q2 = (NV == 2 && gyh2) ? mh_gpre(gyh2[r], yh2[r], act) : 0.f;
+    sgb += q1 + q2;
+    float p1[EPL], p2[EPL], g1[EPL], g2[EPL], A[EPL];
+    load_row(P1 + r * C, lane, C, p1, EPL);
+    if (NV == 2) load_row(P2 + r * C, lane, C, p2, EPL);
+    float s1 = 0.f, s2 = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      u[j] = fmaf(q1, p1[j], u[j]);
+      g1[j] = q1 * vv[j];
+      if (NV == 2) {
+        u[j] = fmaf(q2, p2[j], u[j]);
+        g2[j] = q2 * vv[j];
+      }
+      if (LOSS == 1) {
+        const float d = k * (p1[j] - p2[j]);
+        g1[j] += d;
+        g2[j] -= d;
+      }
+      if (LOSS == 2) {  // as softmax_jsd_bwd
+        const float pm = 0.5f * (p1[j] + p2[j]);
+        const float d = p1[j] - p2[j];
+        A[j] = (p1[j] > 0.f && p2[j] > 0.f) ? 0.5f * log1pf(d * d / (4.f * p1[j] * p2[j]))
+                                            : (pm > 0.f ? logf(pm) - 0.5f * (logf(p1[j]) + logf(p2[j])) : 0.f);
+        t1 += p1[j] > 0.f ? p1[j] * A[j] : 0.f;
+        t2 += p2[j] > 0.f ? p2[j] * A[j] : 0.f;
+      }
+      s1 = fmaf(p1[j], g1[j], s1);
+      if (NV == 2) s2 = fmaf(p2[j], g2[j], s2);
+    }
+    s1 = wave_sum(s1);
+    if (NV == 2) s2 = wave_sum(s2);
+    if (LOSS == 2) { t1 = wave_sum(t1); t2 = wave_sum(t2); }
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      g1[j] = p1[j] * (g1[j] - s1);
+      if (NV == 2) g2[j] = p2[j] * (g2[j] - s2);
+      if (LOSS == 2) {
+        const float pm = 0.5f * (p1[j] + p2[j]);
+        const float a1 = p1[j] > 0.f ? p1[j] * (A[j] - t1 + 1.f) : 0.f;
+        const float a2 = p2[j] > 0.f ? p2[j] * (A[j] - t2 + 1.f) : 0.f;
+        g1[j] += k * (a1 - pm);
+        g2[j] += k * (a2 - pm);
+      }
+    }
+    if (GL1) store_row(GL1 + r * C, lane, g1, EPL);  // NULL: head gradients only (u, db)
+    if (NV == 2 && GL2) store_row(GL2 + r * C, lane, g2, EPL);
+  }
+  // waves' u rows -> LDS at slot order, fixed-order sum over the 4 waves
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) sh[w * EPL * 64 + (j / V) * 64 * V + lane * V + (j % V)] = u[j];
+  if (lane == 0) sh[4 * EPL * 64 + w] = sgb;
+  __syncthreads();
+  float* o = part + (long long)blockIdx.x * (C + 1);
+  for (int c = threadIdx.x; c < C; c += NT) o[c] = ((sh[c] + sh[C + c]) + sh[2 * C + c]) + sh[3 * C + c];
+  if (threadIdx.x == 0) {
+    const float* q = sh + 4 * EPL * 64;
+    o[C] = ((q[0] + q[1]) + q[2]) + q[3];
+  }
+}
+
+// v[s] = sum_k w[k] mem[k][s]
+__global__ void mem_head_vec_kernel(const float* __restrict__ mem, const float* __restrict__ w, int k, int S,
+                                    float* __restrict__ v) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= S) return;
+  float a = 0.f;
+  for (int i = 0; i < k; ++i) a = fmaf(w[i], mem[(long long)i * S + s], a);
+  v[s] = a;
+}
+
+// column sums of part[nblk][ncol] in double: grid (cdiv(ncol, 64), MH_CHUNKS); 4 row lanes per column
+constexpr int MH_CHUNKS = 16;
+__global__ __launch_bounds__(256) void mem_head_colsum(const float* __restrict__ part, int nblk, int ncol,
+                                                       double* __restrict__ part2) {
+  __shared__ double sh[4][64];
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  const int per = (nblk + MH_CHUNKS - 1) / MH_CHUNKS;
+  const int r0 = blockIdx.y * per, r1 = min(nblk, r0 + per);
+  double a = 0.0;
+  if (c < ncol)
+    for (int r = r0 + rl; r < r1; r += 4) a += part[(long long)r * ncol + c];
+  sh[rl][cl] = a;
+  __syncthreads();
+  if (rl == 0 && c < ncol) part2[(long long)blockIdx.y * ncol + c] = ((sh[0][cl] + sh[1][cl]) + sh[2][cl]) + sh[3][cl];
+}
+
+__global__ void mem_head_u(const double* __restrict__ part2, int ncol, float* __restrict__ u, float* gb) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  double a = 0.0;
+  for (int i = 0; i < MH_CHUNKS; ++i) a += part2[(long long)i * ncol + c];
+  u[c] = (float)a;
+  if (c == ncol - 1 && gb) gb[0] = (float)a;
+}
+
+// block kk: dw[kk] = sum_s mem[kk][s] u[s] (fixed-order tree), dmem[kk][s] = w[kk] u[s]
+__global__ __launch_bounds__(256) void mem_head_grads(const float* __restrict__ mem, const float* __restrict__ w,
+                                                      const float* __restrict__ u, int S, float* __restrict__ dmem,
+                                                      float* __restrict__ gw) {
+  __shared__ float sh[256];
+  const int kk = blockIdx.x;
+  const float wk = w[kk];
+  float a = 0.f;
+  for (int s = threadIdx.x; s < S; s += 256) {
+    const float us = u[s];
+    a = fmaf(mem[(long long)kk * S + s], us, a);
+    if (dmem) dmem[(long long)kk * S + s] = wk * us;
+  }
+  sh[threadIdx.x] = a;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) gw[kk] = sh[0];
+}
+
 #define SOFTMAX_DISPATCH(KERNEL, T, C, ...)                                                           \
   do {                                                                                                 \
     if ((C) == 1024) hipLaunchKernelGGL((KERNEL<T, 16>), dim3(grid), dim3(NT), 0, st, __VA_ARGS__);   \
@@ -722,6 +956,146 @@ extern "C" int dg_cls_combine(const float* c1, const float* c2, const float* cgt
 extern "C" int dg_mul_f32(const float* a, const float* b, int64_t n, float* out, void* stream) {
   DG_REQUIRE(a && b && out && n > 0);
   hipLaunchKernelGGL(mul_kernel, dim3(ew_grid(n)), dim3(NT), 0, (hipStream_t)stream, a, b, (long long)n, out);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// ------------------------------------------------------- memory read + head --
+namespace {
+
+inline int mh_grid(int M) { return std::min(4096, dg_cdiv(M, 4)); }
+
+struct MhLayout {  // workspace: part f32 [grid][C+1] | part2 f64 [MH_CHUNKS][C+1] | u f32 [C+1]
+  int grid;
+  size_t part, part2, u, total;
+  MhLayout(int M, int C) {
+    grid = mh_grid(M);
+    part = 0;
+    part2 = ((size_t)grid * (C + 1) * 4 + 255) / 256 * 256;
+    u = part2 + ((size_t)MH_CHUNKS * (C + 1) * 8 + 255) / 256 * 256;
+    total = u + (size_t)(C + 1) * 4;
+  }
+};
+
+template <typename T, int NV, int LOSS>
+void mh_fwd_c(int C, int grid, hipStream_t st, const void* L1, const void* L2, int M, const float* v,
+              const float* bias, int act, void* P1, void* P2, float* yh1, float* yh2, float* part) {
+#define MHF(E) hipLaunchKernelGGL((softmax_head_fwd<T, E, NV, LOSS>), dim3(grid), dim3(NT), 0, st, (const T*)L1, \
+                                  (const T*)L2, M, C, v, bias, act, (T*)P1, (T*)P2, yh1, yh2, part)
+  if (C == 1024) MHF(16);
+  else if (C == 512) MHF(8);
+  else MHF(32);
+#undef MHF
+}
+
+template <typename T, int NV, int LOSS>
+void mh_bwd_c(int C, int grid, hipStream_t st, const void* P1, const void* P2, int M, const float* v, int act,
+              const float* yh1, const float* yh2, const float* g1, const float* g2, const float* coef, void* GL1,
+              void* GL2, float* part) {
+#define MHB(E)                                                                                                  \
+  hipLaunchKernelGGL((softmax_head_bwd<T, E, NV, LOSS>), dim3(grid), dim3(NT), 0, st, (const T*)P1, (const T*)P2, \
+                     M, C, v, act, yh1, yh2, g1, g2, coef, (T*)GL1, (T*)GL2, part)
+  if (C == 1024) MHB(16);
+  else if (C == 512) MHB(8);
+  else MHB(32);
+#undef MHB
+}
+
+template <typename T>
+void mh_fwd_t(int nv, int loss, int C, int grid, hipStream_t st, const void* L1, const void* L2, int M,
+              const float* v, const float* bias, int act, void* P1, void* P2, float* yh1, float* yh2, float* part) {
+  if (nv == 1) mh_fwd_c<T, 1, 0>(C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+  else if (loss == 0) mh_fwd_c<T, 2, 0>(C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+  else if (loss == 1) mh_fwd_c<T, 2, 1>(C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+  else mh_fwd_c<T, 2, 2>(C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+}
+
+template <typename T>
+void mh_bwd_t(int nv, int loss, int C, int grid, hipStream_t st, const void* P1, const void* P2, int M,
+              const float* v, int act, const float* yh1, const float* yh2, const float* g1, const float* g2,
+              const float* coef, void* GL1, void* GL2, float* part) {
+  if (nv == 1) mh_bwd_c<T, 1, 0>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
+  else if (loss == 0) mh_bwd_c<T, 2, 0>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
+  else if (loss == 1) mh_bwd_c<T, 2, 1>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
+  else mh_bwd_c<T, 2, 2>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
+}
+
+}  // namespace
+
+extern "C" int64_t dg_mem_head_workspace(int M, int C) {
+  if (M <= 0 || !SOFTMAX_C_OK(C)) return DG_ERR_INVALID;
+  return (int64_t)MhLayout(M, C).total;
+}
+
+extern "C" int dg_mem_head_vec(const float* mem, const float* w, int k, int S, float* v, void* stream) {
+  DG_REQUIRE(mem && w && v && k > 0 && S > 0);
+  hipLaunchKernelGGL(mem_head_vec_kernel, dim3(dg_cdiv(S, 256)), dim3(256), 0, (hipStream_t)stream, mem, w, k, S, v);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_head_fwd(int dtype, int nviews, int loss, const void* L1, const void* L2, int M, int C,
+                                   const float* v, const float* bias, int act, void* P1, void* P2, float* yh1,
+                                   float* yh2, float* loss_out, void* workspace, void* stream) {
+  DG_REQUIRE(L1 && v && yh1 && M > 0 && (nviews == 1 || nviews == 2) && loss >= 0 && loss <= 2 && act >= 0 &&
+             act <= 2);
+  DG_REQUIRE(nviews == 1 ? loss == 0 : (L2 && yh2));
+  DG_REQUIRE(!loss || (loss_out && workspace));
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = mh_grid(M);
+  float* part = (float*)workspace;
+  if (dtype == DG_BF16) mh_fwd_t<bf16>(nviews, loss, C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+  else if (dtype == DG_F16) mh_fwd_t<f16>(nviews, loss, C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+  else if (dtype == DG_F32) mh_fwd_t<float>(nviews, loss, C, grid, st, L1, L2, M, v, bias, act, P1, P2, yh1, yh2, part);
+  else return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  if (loss) {
+    const double denom = loss == 1 ? (double)M * C : 2.0 * (double)M;
+    hipLaunchKernelGGL(sum_final, dim3(1), dim3(64), 0, st, (const float*)workspace, grid, denom, loss_out);
+    DG_CHECK_LAUNCH();
+  }
+  return DG_OK;
+}
+
+extern "C" int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* P1, const void* P2, int M, int C,
+                                   const float* v, int act, const float* yh1, const float* yh2, const float* gyh1,
+                                   const float* gyh2, const float* coef, void* GL1, void* GL2, void* workspace,
+                                   void* stream) {
+  DG_REQUIRE(P1 && v && yh1 && workspace && M > 0 && (nviews == 1 || nviews == 2) && loss >= 0 && loss <= 2);
+  DG_REQUIRE(nviews == 1 ? loss == 0 : (P2 && yh2));
+  DG_REQUIRE(nviews == 1 || !GL1 == !GL2);  // logit gradients for every view or none
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const int grid = mh_grid(M);
+  float* part = (float*)workspace;
+  if (dtype == DG_BF16)
+    mh_bwd_t<bf16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part);
+  else if (dtype == DG_F16)
+    mh_bwd_t<f16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part);
+  else if (dtype == DG_F32)
+    mh_bwd_t<float>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part);
+  else return DG_ERR_INVALID;
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_mem_head_grads(void* workspace, int M, int C, const float* mem, const float* w, int k,
+                                 float* dmem, float* gw, float* gb, void* stream) {
+  DG_REQUIRE(workspace && mem && w && gw && M > 0 && k > 0);
+  DG_SUPPORTED(SOFTMAX_C_OK(C));
+  hipStream_t st = (hipStream_t)stream;
+  const MhLayout lay(M, C);
+  char* base = (char*)workspace;
+  const int ncol = C + 1;
+  hipLaunchKernelGGL(mem_head_colsum, dim3(dg_cdiv(ncol, 64), MH_CHUNKS), dim3(256), 0, st,
+                     (const float*)(base + lay.part), lay.grid, ncol, (double*)(base + lay.part2));
+  DG_CHECK_LAUNCH();
+  float* u = (float*)(base + lay.u);
+  hipLaunchKernelGGL(mem_head_u, dim3(dg_cdiv(ncol, 256)), dim3(256), 0, st, (const double*)(base + lay.part2), ncol,
+                     u, gb);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mem_head_grads, dim3(k), dim3(256), 0, st, mem, w, (const float*)u, C, dmem, gw);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -16,11 +16,18 @@ to the reference's.  Each plan is wrapped in one torch.autograd.Function.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
 from . import kernels as K
 from .kernels import Act
+
+# The memory readout y_new = mem P feeds only the 1x1 density head, so the head folds through it:
+# d = act((mem^T w) . P + b), fused into the slot-softmax pass (dg_softmax_head_*; memread.hip).
+# DGVCC_MEM_HEAD=0 restores the materialised readout GEMMs (A/B and cross-check).
+MEM_HEAD_FUSED = os.environ.get("DGVCC_MEM_HEAD", "1") != "0"
 
 ACT_NONE, ACT_RELU = 0, 1
 
@@ -714,6 +721,26 @@ class MemRead:
         K.conv_wgrad(P, g_yn, 1, 0, dmem)
         return gP, dmem.view(k, S)
 
+    # --- readout folded into the density head (MEM_HEAD_FUSED) -----------------
+    def head_vec(self, head_w) -> torch.Tensor:
+        """v = mem^T w [S] f32: den_head's weights pulled through the readout."""
+        m = self.mem.detach()[0]
+        k, S = m.shape
+        v = torch.empty(S, dtype=torch.float32, device=m.device)
+        K.call("dg_mem_head_vec", K.ptr(m), K.ptr(head_w.detach().reshape(-1)), k, S, K.ptr(v), K.stream())
+        return v
+
+    def head_grads(self, work, M: int, head_w, want_dmem: bool = True):
+        """After dg_softmax_head_bwd: (dmem_readout [k][S] or None, gw [k], gb [1])."""
+        m = self.mem.detach()[0]
+        k, S = m.shape
+        dmem = torch.empty((k, S), dtype=torch.float32, device=m.device) if want_dmem else None
+        gw = torch.empty(k, dtype=torch.float32, device=m.device)
+        gb = torch.empty(1, dtype=torch.float32, device=m.device)
+        K.call("dg_mem_head_grads", K.ptr(work), M, S, K.ptr(m), K.ptr(head_w.detach().reshape(-1)), k,
+               K.ptr(dmem), K.ptr(gw), K.ptr(gb), K.stream())
+        return dmem, gw, gb
+
     def bwd_logits(self, gL: Act, y: Act, mem_p, scale, dt):
         """g_y = gL . mem^T * scale ; dmem_b[k][slot] = scale * sum_px y[px][k] gL[px][slot]."""
         k, S = self.mem.shape[1], self.mem.shape[2]
@@ -770,6 +797,48 @@ class _Heads:
         if gb is not None:
             _acc(grads, self.head_b, gb)
         return g_y
+
+    def head_acc(self, grads, gw, gb):
+        _acc(grads, self.head_w, gw.view_as(self.head_w))
+        if self.head_b is not None:
+            _acc(grads, self.head_b, gb)
+
+    def mem_head_fwd(self, Ls, dt, loss: int, keep_p: bool):
+        """Slot softmax of 1 or 2 views' logits + the density head through the readout (+ loss):
+        returns (Ps or None, yhs, v, loss tensor or None)."""
+        L1 = Ls[0]
+        N, h, w = L1.N, L1.H, L1.W
+        dev = L1.buf.device
+        v = self.memr.head_vec(self.head_w)
+        Ps = [Act(torch.empty_like(L.buf)) for L in Ls] if keep_p else None
+        yhs = [torch.empty((N, h, w), dtype=torch.float32, device=dev) for _ in Ls]
+        loss_t = torch.empty((), dtype=torch.float32, device=dev) if loss else None
+        work = torch.empty(K.query("dg_mem_head_workspace", L1.M, L1.C) // 4 + 1, dtype=torch.float32, device=dev)
+        hb = self.head_b.detach() if self.head_b is not None else None
+        two = len(Ls) == 2
+        K.call("dg_softmax_head_fwd", L1.dt, len(Ls), loss, L1.ptr, Ls[1].ptr if two else None, L1.M, L1.C,
+               K.ptr(v), K.ptr(hb), self.head_act, Ps[0].ptr if Ps else None,
+               Ps[1].ptr if (Ps and two) else None, K.ptr(yhs[0]), K.ptr(yhs[1]) if two else None,
+               K.ptr(loss_t), K.ptr(work), K.stream())
+        return Ps, yhs, v, loss_t
+
+    def mem_head_bwd(self, Ps, yhs, v, g_hs, loss: int, coef, grads, want_gl: bool = True):
+        """Backward of mem_head_fwd: logit gradients (or None) and the head / readout-mem grads."""
+        P1 = Ps[0]
+        M, S = P1.M, P1.C
+        dev = P1.buf.device
+        two = len(Ps) == 2
+        work = torch.empty(K.query("dg_mem_head_workspace", M, S) // 4 + 1, dtype=torch.float32, device=dev)
+        gLs = [Act(torch.empty_like(P.buf)) for P in Ps] if want_gl else None
+        K.call("dg_softmax_head_bwd", P1.dt, len(Ps), loss, P1.ptr, Ps[1].ptr if two else None, M, S, K.ptr(v),
+               self.head_act, K.ptr(yhs[0]), K.ptr(yhs[1]) if two else None, K.ptr(g_hs[0]),
+               K.ptr(g_hs[1]) if two else None, K.ptr(coef), gLs[0].ptr if gLs else None,
+               gLs[1].ptr if (gLs and two) else None, K.ptr(work), K.stream())
+        dmem = None
+        if any(g is not None for g in g_hs):
+            dmem, gw, gb = self.memr.head_grads(work, M, self.head_w, want_dmem=want_gl)
+            self.head_acc(grads, gw, gb)
+        return gLs, dmem
 
     def cls_fwd(self, x3: torch.Tensor, training, tape, key):
         N, h, w, _ = x3.shape
@@ -835,14 +904,23 @@ class SinglePlan(_Heads):
         self.den.forward(cat, yden, training, sub, drop=drop)
         st = {"sub": sub, "yden": yden, "cat": cat, "raw": self.raw}
         y = yden
-        if self.memr is not None:
+        if self.memr is not None and MEM_HEAD_FUSED:
+            memT_s, _, scale = self.memr.packs(dt, training)
+            L = self.memr.logits(yden, memT_s, dt)
+            Ps, yhs, v, _ = self.mem_head_fwd([L], dt, 0, keep_p=tape is not None)
+            del L
+            yh = yhs[0]
+            st.update(P=Ps[0] if Ps else None, v=v, scale=scale)
+        elif self.memr is not None:
             memT_s, mem_p, scale = self.memr.packs(dt, training)
             L = self.memr.logits(yden, memT_s, dt)
             P = Act(torch.empty_like(L.buf))
             K.call("dg_softmax_fwd", L.dt, L.ptr, L.M, L.C, P.ptr, K.stream())
             y = self.memr.readout(P, mem_p, dt)
             st.update(P=P, ynew=y, mem_p=mem_p, scale=scale)
-        yh = self.head(y)
+            yh = self.head(y)
+        else:
+            yh = self.head(y)
         st["yh"] = yh
         if self.cls is None:
             out = _up4(yh, N, h, w)
@@ -873,9 +951,13 @@ class SinglePlan(_Heads):
             g_h = _up4_bwd(g_d, N, h, w)
             if self.cls is not None:
                 K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
-            y = st.get("ynew", st["yden"])
-            g_y = self.head_bwd(y, st["yh"], g_h, grads)
-            if self.memr is not None:
+            if st.get("v") is not None:  # fused memory head
+                (gL,), dmem_a = self.mem_head_bwd([st["P"]], [st["yh"]], st["v"], [g_h], 0, None, grads)
+                g_y, dmem_b = self.memr.bwd_logits(gL, st["yden"], None, st["scale"], gL.buf.dtype)
+                _acc(grads, self.memr.mem, (dmem_a + dmem_b).view_as(self.memr.mem))
+            else:
+                g_y = self.head_bwd(st.get("ynew", st["yden"]), st["yh"], g_h, grads)
+            if self.memr is not None and st.get("v") is None:
                 dt = y.buf.dtype
                 gP, dmem_a = self.memr.bwd_readout(g_y, st["P"], dt)
                 gL = Act(torch.empty_like(gP.buf))
@@ -892,7 +974,10 @@ class SinglePlan(_Heads):
                 g_h = _up4_bwd(g_d, N, h, w)
                 if self.cls is not None:
                     K.call("dg_mul_f32", K.ptr(g_h), K.ptr(st["cres"]), g_h.numel(), K.ptr(g_h), K.stream())
-                self.head_bwd(st["ynew"], st["yh"], g_h, grads)
+                if st.get("v") is not None:
+                    self.mem_head_bwd([st["P"]], [st["yh"]], st["v"], [g_h], 0, None, grads, want_gl=False)
+                else:
+                    self.head_bwd(st["ynew"], st["yh"], g_h, grads)
         if self.cls is not None and len(gouts) > 1 and gouts[1] is not None:
             g_x3 = self.cls_bwd(sub, "cls", gouts[1], grads)
         return (*g_cat, g_x3), grads
@@ -951,17 +1036,24 @@ class PairPlan(_Heads):
         memT_s, mem_p, scale = self.memr.packs(dt)
         L1 = self.memr.logits(m1, memT_s, dt)
         L2 = self.memr.logits(m2, memT_s, dt)
-        P1, P2 = Act(torch.empty_like(L1.buf)), Act(torch.empty_like(L2.buf))
-        loss_con = torch.empty((), dtype=torch.float32, device=dev)
-        ws = K.query("dg_softmax_workspace", L1.M)
-        work2 = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
-        fn = "dg_softmax_jsd_fwd" if self.variant == "M" else "dg_softmax_pair_fwd"
-        K.call(fn, L1.dt, L1.ptr, L2.ptr, L1.M, L1.C, P1.ptr, P2.ptr, K.ptr(loss_con), K.ptr(work2), K.stream())
-        yn1 = self.memr.readout(P1, mem_p, dt)
-        yn2 = self.memr.readout(P2, mem_p, dt)
-        yh1, yh2 = self.head(yn1), self.head(yn2)
+        v = None
+        if MEM_HEAD_FUSED:
+            (P1, P2), (yh1, yh2), v, loss_con = self.mem_head_fwd([L1, L2], dt, 2 if self.variant == "M" else 1,
+                                                                  keep_p=True)
+            yn1 = yn2 = None
+        else:
+            P1, P2 = Act(torch.empty_like(L1.buf)), Act(torch.empty_like(L2.buf))
+            loss_con = torch.empty((), dtype=torch.float32, device=dev)
+            ws = K.query("dg_softmax_workspace", L1.M)
+            work2 = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
+            fn = "dg_softmax_jsd_fwd" if self.variant == "M" else "dg_softmax_pair_fwd"
+            K.call(fn, L1.dt, L1.ptr, L2.ptr, L1.M, L1.C, P1.ptr, P2.ptr, K.ptr(loss_con), K.ptr(work2), K.stream())
+            yn1 = self.memr.readout(P1, mem_p, dt)
+            yn2 = self.memr.readout(P2, mem_p, dt)
+            yh1, yh2 = self.head(yn1), self.head(yn2)
+        del L1, L2
         st = dict(s1=s1, s2=s2, cat1=cat1, cat2=cat2, mask=mask, d1=d1, d2=d2, m1=m1, m2=m2, P1=P1,
-                  P2=P2, yn1=yn1, yn2=yn2, yh1=yh1, yh2=yh2, mem_p=mem_p, scale=scale)
+                  P2=P2, yn1=yn1, yn2=yn2, yh1=yh1, yh2=yh2, mem_p=mem_p, scale=scale, v=v)
         if self.cls is None:
             outs = (_up4(yh1, N, h, w), _up4(yh2, N, h, w), loss_con)
         elif self.variant == "M":
@@ -1035,22 +1127,37 @@ class PairPlan(_Heads):
                 K.call("dg_mul_f32", K.ptr(g_h), K.ptr(cres), g_h.numel(), K.ptr(g_h), K.stream())
             return self.head_bwd(yn, yh, g_h, grads)
 
-        g_yn1 = head_path(g_d1, st["yh1"], st["yn1"], st.get("cres1", st.get("cres")))
-        g_yn2 = head_path(g_d2, st["yh2"], st["yn2"], st.get("cres2", st.get("cres")))
-        gP1 = gP2 = None
-        dmem = torch.zeros((C, self.memr.mem.shape[2]), dtype=torch.float32, device=dev)
-        if g_yn1 is not None:
-            gP1, da = self.memr.bwd_readout(g_yn1, st["P1"], dt)
-            dmem += da
-        if g_yn2 is not None:
-            gP2, da = self.memr.bwd_readout(g_yn2, st["P2"], dt)
-            dmem += da
         P1, P2 = st["P1"], st["P2"]
-        gL1, gL2 = Act(torch.empty_like(P1.buf)), Act(torch.empty_like(P2.buf))
         coef = g_con.float().reshape(1).contiguous() if g_con is not None else None
-        fn = "dg_softmax_jsd_bwd" if self.variant == "M" else "dg_softmax_pair_bwd"
-        K.call(fn, P1.dt, P1.ptr, P2.ptr, gP1.ptr if gP1 is not None else None,
-               gP2.ptr if gP2 is not None else None, P1.M, P1.C, K.ptr(coef), gL1.ptr, gL2.ptr, K.stream())
+        dmem = torch.zeros((C, self.memr.mem.shape[2]), dtype=torch.float32, device=dev)
+        if st["v"] is not None:  # fused memory head: gP = gpre v formed in registers
+            def g_head(g_d, cres):
+                if g_d is None:
+                    return None
+                g_h = _up4_bwd(g_d, N, h, w)
+                if cres is not None:
+                    K.call("dg_mul_f32", K.ptr(g_h), K.ptr(cres), g_h.numel(), K.ptr(g_h), K.stream())
+                return g_h
+
+            g_hs = [g_head(g_d1, st.get("cres1", st.get("cres"))), g_head(g_d2, st.get("cres2", st.get("cres")))]
+            (gL1, gL2), da = self.mem_head_bwd([P1, P2], [st["yh1"], st["yh2"]], st["v"], g_hs,
+                                               2 if self.variant == "M" else 1, coef, grads)
+            if da is not None:
+                dmem += da
+        else:
+            g_yn1 = head_path(g_d1, st["yh1"], st["yn1"], st.get("cres1", st.get("cres")))
+            g_yn2 = head_path(g_d2, st["yh2"], st["yn2"], st.get("cres2", st.get("cres")))
+            gP1 = gP2 = None
+            if g_yn1 is not None:
+                gP1, da = self.memr.bwd_readout(g_yn1, P1, dt)
+                dmem += da
+            if g_yn2 is not None:
+                gP2, da = self.memr.bwd_readout(g_yn2, P2, dt)
+                dmem += da
+            gL1, gL2 = Act(torch.empty_like(P1.buf)), Act(torch.empty_like(P2.buf))
+            fn = "dg_softmax_jsd_bwd" if self.variant == "M" else "dg_softmax_pair_bwd"
+            K.call(fn, P1.dt, P1.ptr, P2.ptr, gP1.ptr if gP1 is not None else None,
+                   gP2.ptr if gP2 is not None else None, P1.M, P1.C, K.ptr(coef), gL1.ptr, gL2.ptr, K.stream())
         g_m1, db1 = self.memr.bwd_logits(gL1, st["m1"], st["mem_p"], st["scale"], dt)
         g_m2, db2 = self.memr.bwd_logits(gL2, st["m2"], st["mem_p"], st["scale"], dt)
         dmem += db1 + db2

@@ -437,6 +437,28 @@ int dg_softmax_jsd_fwd(int dtype, const void* L1, const void* L2, int M, int C, 
                        float* loss_kl, void* workspace, void* stream);
 int dg_softmax_jsd_bwd(int dtype, const void* P1, const void* P2, const void* G1, const void* G2,
                        int M, int C, const float* coef, void* GL1, void* GL2, void* stream);
+/* Memory read + density head fused (models/models.py:116-125 forward_mem feeding den_head
+ * :112-114; models2.py DensityRegressorM): y_new = mem P only feeds the 1x1 k->1 head, so
+ * d = act(v . P + b) with v = mem^T w (dg_mem_head_vec, [S] f32 from the f32 master mem [k][S]).
+ * dg_softmax_head_fwd: slot softmax of nviews (1|2) logit rows + head output yh_v [M] f32 +
+ *   loss (0 none, 1 mean((P1-P2)^2) as dg_softmax_pair_fwd, 2 KL-JSD as dg_softmax_jsd_fwd; nviews 2).
+ *   P_v may be NULL (no backward: eval).  workspace: dg_mem_head_workspace(M, C) bytes.
+ * dg_softmax_head_bwd: gL_v = P_v (gP_v - <P_v, gP_v>), gP_v = gpre_v v + loss term, gpre_v =
+ *   act'(yh_v) gyh_v (gyh_v NULL = 0); GL NULL = head gradients only.  Leaves per-block
+ *   partials of u = sum_px gpre P and sum gpre in the workspace for
+ * dg_mem_head_grads: dmem[k][S] = w u^T (the readout's mem gradient; NULL = skip), gw[k] = mem u,
+ *   gb = sum gpre (NULL = skip); fixed-order (deterministic) reductions. */
+int64_t dg_mem_head_workspace(int M, int C);
+int dg_mem_head_vec(const float* mem, const float* w, int k, int S, float* v, void* stream);
+int dg_softmax_head_fwd(int dtype, int nviews, int loss, const void* L1, const void* L2, int M, int C,
+                        const float* v, const float* bias, int act, void* P1, void* P2, float* yh1,
+                        float* yh2, float* loss_out, void* workspace, void* stream);
+int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* P1, const void* P2, int M, int C,
+                        const float* v, int act, const float* yh1, const float* yh2, const float* gyh1,
+                        const float* gyh2, const float* coef, void* GL1, void* GL2, void* workspace,
+                        void* stream);
+int dg_mem_head_grads(void* workspace, int M, int C, const float* mem, const float* w, int k,
+                      float* dmem, float* gw, float* gb, void* stream);
 /* loss_err = F.l1_loss(IN(y1), IN(y2)) (models/models2.py:334) from the instance-norm
  * statistics; backward writes g_IN1 = coef[0] sgn(IN1 - IN2)/(N HW C) and g_IN2 = -g_IN1
  * (dense [N*HW][C]) for dg_instnorm_bwd. */
