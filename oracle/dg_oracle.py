@@ -204,9 +204,11 @@ def trainable_keys(sd):
                                  or k.endswith("num_batches_tracked"))]
 
 
-def train_step(sd, batch, mode="simple", log_para=1000.0, lr=1e-4, weight_decay=1e-4):
+def train_step(sd, batch, mode="simple", log_para=1000.0, lr=1e-4, weight_decay=1e-4, e_mask_in=None,
+               c_pred_in=None):
     """One DGTrainer.train_step (trainers/dgtrainer.py:143-192, MSE loss, AdamW step 1).
-    Returns (loss, outputs, grads, new_sd)."""
+    Returns (loss, outputs, grads, new_sd).  Final mode takes final_forward's threshold
+    injection (e_mask_in, c_pred_in) so a checked path is compared on its own decisions."""
     sd = {k: v.clone() for k, v in sd.items()}
     keys = trainable_keys(sd)
     for k in keys:
@@ -233,7 +235,8 @@ def train_step(sd, batch, mode="simple", log_para=1000.0, lr=1e-4, weight_decay=
                 + 10 * (F.binary_cross_entropy(c1, bmaps) + F.binary_cross_entropy(c2, bmaps)))
         outs = (d1, d2, c1, c2)
     elif mode == "final":
-        dc1, dc2, c1, c2, c_err, loss_con, _ = final_forward(sd, imgs1, imgs2, bmaps)
+        dc1, dc2, c1, c2, c_err, loss_con, _ = final_forward(sd, imgs1, imgs2, bmaps, e_mask_in=e_mask_in,
+                                                             c_pred_in=c_pred_in)
         loss_den = F.mse_loss(dc1, gt) + F.mse_loss(dc2, gt)
         loss_cls = F.binary_cross_entropy(c1, bmaps) + F.binary_cross_entropy(c2, bmaps)
         loss = loss_den + 10 * loss_cls + 10 * loss_con
