@@ -1395,6 +1395,169 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
                              co0, tid, fr, fc);
 }
 
+// conv_fwd_rsplit_kernel with the three taps of a kernel row sharing one staged pixel strip
+// (3x3 / pad 1, W % 256 == 0, so a 256-pixel tile is one image-row segment): a K-step is
+// (kernel row r, 32-channel block); the strip X[258 px][32 c] of image row p + r - 1 (columns
+// q0 - 1 .. q0 + 256) is loaded, split ONCE into three bf16 planes and read by the taps
+// s = 0, 1, 2 at row offsets s, so the split and LDS-store work per MFMA is 1/3 of the per-tap
+// kernel's.  The three taps' pre-split filter planes (36 KB) are staged through registers into a
+// single LDS buffer (two barriers per K-step: the strip takes the double buffer); reading them
+// per wave straight from L2 measured no faster than the per-tap kernel (8 waves x 18 KB per
+// K-step per CU of L2 traffic).  Same tile (256 px x 64 co, 8 waves of 64 px x 32 co) and
+// epilogues as conv_fwd_rsplit_kernel; K order (r, c-block, s) instead of (r, s, c-block).
+template <int EPI = 0>
+__global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int BN = 64, BPX = 256, SR = 264;        // strip rows (258 used)
+  constexpr int B_PL = SR * 64, BUF = 3 * B_PL;      // strip plane / buffer bytes
+  constexpr int A_PL = BN * 64, A_TAP = 3 * A_PL;    // filter plane / tap bytes
+  constexpr int TI = 2, TJ = 4;
+  constexpr int NCH = (BPX + 2) * 8, BR = (NCH + 511) / 512;  // 16-B f32 chunks of the strip
+  constexpr int NA = 3 * 3 * BN * 4, AR = (NA + 511) / 512;  // 16-B chunks of the 3 taps' planes
+  __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 3 * A_TAP];
+  char* Asm = smem + 2 * BUF;
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (bid % nco) * BN;
+  const int px0 = (bid / nco) * BPX;
+  const int tn = px0 / HW, tp = (px0 - tn * HW) / a.W, tq = px0 - tn * HW - tp * a.W;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = tid & 7, rbase = tid >> 3;
+  const int CB = a.C / 32;
+  const int KT3 = 3 * CB;
+
+  const int plo = max(0, px0 - (a.W + 1));
+  const int phi = min(M, px0 + BPX + a.W + 1);
+  const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 4);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 4), 0,
+                                                                win_bytes, 0x00020000);
+  const int wpx = (wid & 3) * 64, wco = (wid >> 2) * 32;
+  const int fr = lane & 15, fc = lane >> 4;
+  // filter chunk q of a K-step: (tap s, plane, row co, 16-B chunk) = (q / 768, (q / 256) % 3, (q & 255) >> 2, q & 3)
+  const char* wbase = wsp + (long long)co0 * (9 * CB) * 192;
+  int a_src[AR], a_dst[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int q = tid + 512 * i;
+    const int ts = q / 768, pl = (q / 256) % 3, row = (q & 255) >> 2, ch = q & 3;
+    a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * 192 + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*192
+    a_dst[i] = ts * A_TAP + pl * A_PL + row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
+  }
+
+  u4v rb[BR], ra[AR];
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    const int r = t / CB, cb = t - r * CB;
+    const int h = tp + r - 1;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = rbase + 64 * i;
+      const int ww = tq - 1 + row;
+      const bool ok = row < BPX + 2 && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pin = (long long)tn * HW + (long long)h * a.W + ww - plo;
+      rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + cb * 32 + chunk * 4) * 4) : 0xFFFFFFF0u);
+    }
+    const long long koff = (long long)(r * 3 * CB + cb) * 192;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      if (a_src[i] >= 0) ra[i] = *(const u4v*)(wbase + a_src[i] + koff);
+  };
+  auto swrite = [&](int buf) __attribute__((always_inline)) {
+    char* Bs = smem + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = rbase + 64 * i;
+      if (row < BPX + 2) {
+        const int o = row * 64 + ((((chunk >> 1) ^ ((row >> 2) & 3))) << 4) + (chunk & 1) * 8;
+        u2v h0, h1, h2;
+        split3_4(rb[i], h0, h1, h2);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + B_PL + o) = h1;
+        *(u2v*)(Bs + 2 * B_PL + o) = h2;
+      }
+    }
+  };
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  swrite(0);
+  for (int t = 0; t < KT3; ++t) {
+    const int cur = t & 1;
+    __syncthreads();  // every wave is done with the previous K-step's filter planes
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      if (a_src[i] >= 0) *(u4v*)(Asm + a_dst[i]) = ra[i];
+    __syncthreads();  // filter planes of this K-step (and its strip, stored during the last one) visible
+    if (t + 1 < KT3) gload(t + 1);
+    const char* Bs = smem + cur * BUF;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      s8v ah[TI][3], bh[TJ][3];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int row = wco + 16 * i + fr;
+        const int o = s * A_TAP + row * 64 + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) ah[i][pl] = *(const s8v*)(Asm + pl * A_PL + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int row = wpx + 16 * j + fr + s;
+        const int o = row * 64 + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
+      }
+      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+      if (s == 1 && t + 1 < KT3) swrite(cur ^ 1);  // the other buffer was last read before this step's barriers
+    }
+  }
+  __syncthreads();  // smem reuse by the statistics epilogue
+
+  float* y = (float*)a.y;
+  bool valid[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    valid[j] = px < M;
+    if (px >= M) continue;
+    float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco + 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      if constexpr (EPI == 3) epi_affine(v, a, co);
+      st4(yrow + co, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+    }
+  }
+  if (EPI == 0 && a.part)
+    epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, smem, a.part + (long long)(px0 / BPX) * 3 * a.Cout, a.Cout,
+                             co0, tid, fr, fc);
+}
+
 // wsp[co][kb][part][32] (bf16) = the exact 3-way split of the packed f32 filter w[co][kb*32 + j]
 __global__ void split_weight_kernel(const float* __restrict__ w, long long n, unsigned short* __restrict__ wsp) {
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n; o += (long long)gridDim.x * blockDim.x) {
@@ -2119,6 +2282,12 @@ static bool rsplit_ok(const FwdArgs& a) {
          a.Cout % 64 == 0 && f32_pers_bn(a.Cout) == 64 && (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
 }
 
+// rows of W % 256 == 0 of a 3x3 / pad-1 Cout = 64 conv: the 3-tap strip kernel (DGVCC_RSPLIT3=0 off)
+static bool rsplit3_ok(const FwdArgs& a) {
+  const char* e = getenv("DGVCC_RSPLIT3");
+  return !(e && e[0] == '0') && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0;
+}
+
 // Per-stream device scratch for the pre-split filter panels (grown on demand; a launch on
 // a stream only ever overlaps its own stream's earlier work, which hipFree waits for).
 static void* split_scratch(hipStream_t st, size_t bytes) {
@@ -2223,7 +2392,10 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
       hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
                          0, st, (const float*)a.w, nw, wsp);
       const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));
-      if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
+      if (rsplit3_ok(a)) {
+        if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
+        else hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<0>), g, dim3(512), 0, st, a, (const char*)wsp);
+      } else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
       else hipLaunchKernelGGL((conv_fwd_rsplit_kernel<0>), g, dim3(512), 0, st, a, (const char*)wsp);
       DG_CHECK_LAUNCH();
       return DG_OK;
@@ -2699,6 +2871,183 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
     }
 }
 
+// f32 weight gradient of a 3x3 / stride-1 / pad-1 conv on the split math with the three taps of
+// one kernel row sharing their operands (the bf16 conv_wgrad9_kernel's idea on
+// conv_wgrad_split_kernel's split-once-per-block staging): a K-step is 32 consecutive pixels of
+// one image row (W % 32 == 0); dY[32 px][64 co] and the input strip X[34 px][64 c] of image row
+// p + r - 1 (columns q0 - 1 .. q0 + 32) are split once into bf16 planes, and the taps s = 0, 1, 2
+// read the strip at row offsets s.  Per staged value 3x the MFMA work of the per-tap kernel, whose
+// 64-channel tiles were bound by the split and LDS-store work (~30% MFMA-busy).  256 threads = 4
+// waves (2 co x 2 c of 32 x 32, all 3 taps), two blocks per CU.
+template <int NTH = 256>
+__global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
+  constexpr int BCO = 64, BC = 64, BKP = 32, XR = BKP + 2;
+  constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
+  constexpr int PA = BKP * ROWA, PB = XR * ROWB;           // bytes per plane
+  constexpr int TILE = 3 * (PA + PB);
+  constexpr int CPR = 16;                                  // 16-B f32 chunks per 64-channel row
+  constexpr int AR = BKP * CPR / NTH, BR = (XR * CPR + NTH - 1) / NTH;
+  constexpr int TI = 2, TJ = 2;                            // wave tile 32 co x 32 c
+  static_assert(NTH == 256 && AR * NTH == BKP * CPR, "4 waves");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BCO, ncb = a.C / BC;
+  const int tiles = nco * ncb * 3;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles;
+  int t = bid - split * tiles;
+  const int cot = t % nco; t /= nco;
+  const int cbt = t % ncb;
+  const int r = t / ncb;
+  const int co0 = cot * BCO, c0 = cbt * BC;
+  const int dh = r - 1;
+  const int kbeg = split * a.pps;
+  const int kend = min(M, kbeg + a.pps);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+
+  const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 4);
+  __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.dy + (long long)kbeg * a.lddy * 4), 0, dy_bytes, 0x00020000);
+  const int halo = a.W + 1;
+  const int xlo = max(0, kbeg - halo);
+  const int xhi = min(M, kend + halo);
+  const unsigned x_bytes = (unsigned)(((long long)(xhi - xlo - 1) * a.ldx + a.C) * 4);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.x + (long long)xlo * a.ldx * 4), 0, x_bytes, 0x00020000);
+
+  // pixel coordinates of the current K-step's first pixel (uniform over the block)
+  int sn = kbeg / HW, sp = (kbeg - sn * HW) / a.W, sq = kbeg - sn * HW - sp * a.W;
+  u4v ra[AR], rb[BR];
+  auto gload = [&](int k0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int idx = tid + NTH * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      ra[i] = bload(dyr, (unsigned)(((long long)(k0 + row - kbeg) * a.lddy + co0 + ch * 4) * 4));
+    }
+    const int h = sp + dh;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int idx = tid + NTH * i;
+      const int row = idx / CPR, ch = idx % CPR;
+      const int ww = sq - 1 + row;
+      const bool ok = idx < XR * CPR && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pin = (long long)sn * HW + (long long)h * a.W + ww - xlo;
+      rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + c0 + ch * 4) * 4) : 0xFFFFFFF0u);
+    }
+    sq += BKP;
+    if (sq >= a.W) {
+      sq = 0;
+      if (++sp == a.H) { sp = 0; ++sn; }
+    }
+  };
+  auto swrite = [&](int buf) __attribute__((always_inline)) {
+    char* As = smem + buf * TILE;
+    char* Bs = As + 3 * PA;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int idx = tid + NTH * i;
+      const int o = (idx / CPR) * ROWA + (idx % CPR) * 8;
+      u2v h0, h1, h2;
+      split3_4(ra[i], h0, h1, h2);
+      *(u2v*)(As + o) = h0;
+      *(u2v*)(As + PA + o) = h1;
+      *(u2v*)(As + 2 * PA + o) = h2;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int idx = tid + NTH * i;
+      if (idx < XR * CPR) {
+        const int o = (idx / CPR) * ROWB + (idx % CPR) * 8;
+        u2v h0, h1, h2;
+        split3_4(rb[i], h0, h1, h2);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + PB + o) = h1;
+        *(u2v*)(Bs + 2 * PB + o) = h2;
+      }
+    }
+  };
+
+  f4v acc[3][TI][TJ];
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) acc[s][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  const int wco = (wid >> 1) * 32, wc = (wid & 1) * 32;
+  const int g = lane >> 4;
+  const int q = (lane & 15) >> 2, p4 = lane & 3;
+  const int r1 = 4 * g + q, r2 = r1 + 16;
+
+  const int nkt = (kend - kbeg) / BKP;
+  gload(kbeg);
+  swrite(0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nkt) gload(kbeg + (kt + 1) * BKP);
+    const char* As = smem + cur * TILE;
+    const char* Bs = As + 3 * PA;
+    s8v ah[TI][3];
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int col = (wco + 16 * i + 4 * p4) * 2;
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        const char* b = As + pl * PA;
+        s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r1 * ROWA + col));
+        s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r2 * ROWA + col));
+        ah[i][pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      s8v bh[TJ][3];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int col = (wc + 16 * j + 4 * p4) * 2;
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          const char* b = Bs + pl * PB;
+          s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + (r1 + s) * ROWB + col));
+          s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + (r2 + s) * ROWB + col));
+          bh[j][pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+      }
+      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[s][i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nkt) swrite(cur ^ 1);  // two blocks per CU overlap each other's split with MFMAs
+    __syncthreads();
+  }
+
+  const long long ldk = 9ll * a.C;
+  float* out = a.slab + (long long)split * a.Cout * ldk;
+#pragma unroll
+  for (int s = 0; s < 3; ++s)
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int c = c0 + wc + 16 * j + (lane & 15);
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) {
+          const int co = co0 + wco + 16 * i + 4 * g + rr;
+          out[co * ldk + (r * 3 + s) * a.C + c] = acc[s][i][j][rr];
+        }
+      }
+}
+
 // Split plan of conv_wgrad_split_kernel: one block per CU (256 slots), 32-pixel K-steps.
 static WgPlan wgs_plan(long long M, long long tiles, long long slots = 256) {
   const long long max_split = (M + 32 * 4 - 1) / (32 * 4);
@@ -2731,6 +3080,20 @@ static long long wgs_tiles(int C, int Cout, int RS) {
   return (long long)(Cout / wgs_bco(C, Cout)) * (C / wgs_bc(C, Cout)) * RS;
 }
 static long long wgs_slots(int C, int Cout) { return wgs_bco(C, Cout) == 64 ? 512 : 256; }
+
+// conv_wgrad_split3_kernel (three taps of a kernel row share their operands) for 3x3 / pad 1 /
+// stride 1 rows of W % 32 == 0 with a 64-channel side (the per-tap kernel's 64-wide tiles);
+// DGVCC_WGRAD_SPLIT3=0 off, =2 every C % 64 == 0 shape
+static int wgrad_split3_mode() {
+  const char* e = getenv("DGVCC_WGRAD_SPLIT3");
+  return e ? (e[0] - '0') : 1;
+}
+static bool wgs3_shape_ok(int C, int Cout, int R, int S, int W) {
+  const int m = wgrad_split3_mode();
+  return use_wgrad_split() && m != 0 && R == 3 && S == 3 && W % 32 == 0 && C % 64 == 0 && Cout % 64 == 0 &&
+         (m == 2 || C == 64 || Cout == 64);
+}
+static long long wgs3_tiles(int C, int Cout) { return (long long)(Cout / 64) * (C / 64) * 3; }
 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int C, int RS,
                                     float* __restrict__ dw, int accumulate) {
@@ -3311,6 +3674,21 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   }
   if (done) {
   } else if constexpr (!Is16<T>::value) {
+    const long long M3 = (long long)a.N * a.P * a.Q;
+    if (f32_split() && a.stride == 1 && !a.whole_x && a.pad == 1 && wgs3_shape_ok(a.C, a.Cout, a.R, a.S, a.W)) {
+      const WgPlan p = wgs_plan(M3, wgs3_tiles(a.C, a.Cout), 512);
+      if ((long long)(p.pps + 2 * (a.W + 1)) * std::max(a.ldx, a.lddy) * 4 < (1ll << 31)) {
+        a.splits = p.splits;
+        a.pps = p.pps;
+        slab_splits = p.splits;
+        hipLaunchKernelGGL((conv_wgrad_split3_kernel<256>), dim3((unsigned)(wgs3_tiles(a.C, a.Cout) * p.splits)),
+                           dim3(256), 0, st, a);
+        done = true;
+      }
+    }
+  }
+  if (done) {
+  } else if constexpr (!Is16<T>::value) {
     const bool wgs = f32_split() && wgs_ok(a.C, a.Cout);
     const WgPlan pw = wgs ? wgs_plan((long long)a.N * a.P * a.Q, wgs_tiles(a.C, a.Cout, a.R * a.S), wgs_slots(a.C, a.Cout))
                           : WgPlan{1, 0};
@@ -3695,6 +4073,10 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
   WgPlan q = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S) : p;
   if (!DG_IS16(dtype) && wgs_ok(C, Cout))
     q = wgs_plan((long long)N * H * W, wgs_tiles(C, Cout, R * S), wgs_slots(C, Cout));
+  if (!DG_IS16(dtype) && wgs3_shape_ok(C, Cout, R, S, W)) {  // the 3-tap plan (launch may refuse it)
+    const WgPlan q3 = wgs_plan((long long)N * H * W, wgs3_tiles(C, Cout), 512);
+    if (q3.splits > q.splits) q = q3;
+  }
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
   return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
 }

@@ -364,7 +364,8 @@ def test_conv_f32_split_math(dev, case):
 @pytest.mark.parametrize("N,H,W,C,Cout,epi", [(5, 128, 256, 64, 256, "stats"), (3, 96, 320, 128, 128, "stats"),
                                               (3, 128, 256, 256, 512, "eval"), (8, 100, 130, 128, 256, "bias"),
                                               (3, 70, 90, 64, 64, "stats"), (2, 64, 256, 128, 64, "eval"),
-                                              (2, 33, 40, 64, 64, "bias")])
+                                              (2, 33, 40, 64, 64, "bias"), (2, 8, 256, 64, 64, "stats"),
+                                              (1, 6, 512, 128, 64, "bias"), (2, 5, 256, 64, 64, "eval")])
 def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
     """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128; Cout = 64 on
     conv_fwd_rsplit_kernel, 256-pixel tiles) with
@@ -403,3 +404,81 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
         yd = y.double().reshape(-1, Cout)
         assert torch.equal(tot, torch.full_like(tot, N * H * W))
         assert relerr(gm, yd.mean(0)) < 1e-5 and relerr(var, yd.var(0, unbiased=False)) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,mode", [(2, 9, 64, 64, 64, "1"), (3, 17, 96, 64, 128, "1"),
+                                               (2, 40, 32, 128, 64, "1"), (1, 48, 160, 256, 128, "2"),
+                                               (4, 5, 128, 64, 64, "1")])
+def test_conv_f32_wgrad_split3(dev, N, H, W, C, Cout, mode):
+    """3-tap shared f32 split-math wgrad (conv_wgrad_split3_kernel: a kernel row's three taps on one
+    staged dY tile and X strip, K-steps of 32 pixels of one image row) against float64 torch and
+    against the per-tap split kernel (DGVCC_WGRAD_SPLIT3=0) on the same launch shapes: image and
+    split boundaries inside the K range (small H, several images), both 64-channel sides."""
+    import os
+    K = _k()
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, C, H, W, generator=g)
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    xr = x.double()
+    wr = torch.zeros(Cout, C, 3, 3, dtype=torch.float64, requires_grad=True)
+    F.conv2d(xr, wr, padding=1).backward(gy.double())
+    xd = K.Act(to_nhwc(x).to(dev))
+    gyd = K.Act(to_nhwc(gy).to(dev))
+    out = {}
+    old = os.environ.get("DGVCC_WGRAD_SPLIT3")
+    try:
+        for m in (mode, "0"):
+            os.environ["DGVCC_WGRAD_SPLIT3"] = m
+            dw = torch.empty(Cout, C, 3, 3, device=dev)
+            K.conv_wgrad(xd, gyd, 3, 1, dw)
+            torch.cuda.synchronize()
+            out[m] = dw.cpu()
+    finally:
+        if old is None:
+            os.environ.pop("DGVCC_WGRAD_SPLIT3", None)
+        else:
+            os.environ["DGVCC_WGRAD_SPLIT3"] = old
+    e3, e1 = relerr(out[mode], wr.grad), relerr(out["0"], wr.grad)
+    assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, (e3, e1)
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout", [(2, 7, 256, 64, 64), (1, 5, 512, 64, 128), (1, 4, 256, 256, 64)])
+def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
+    """Cout = 64 split-math forward with the 3 taps of a kernel row on one staged strip
+    (conv_fwd_rsplit3_kernel, W % 256 == 0) and the dgrad that lands on it (64-channel dx): against
+    float64 torch and against the per-tap kernel (DGVCC_RSPLIT3=0), within the f32-grade bound."""
+    import os
+    K = _k()
+    g = torch.Generator().manual_seed(31)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    xr = x.double().requires_grad_(True)
+    yr = F.conv2d(xr, w.double(), padding=1)
+    yr.backward(gy.double())
+    xd, gyd = K.Act(to_nhwc(x).to(dev)), K.Act(to_nhwc(gy).to(dev))
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    errs = {}
+    old = os.environ.get("DGVCC_RSPLIT3")
+    try:
+        for m in ("1", "0"):
+            os.environ["DGVCC_RSPLIT3"] = m
+            e = []
+            if Cout == 64:
+                y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+                K.conv_fwd(xd, wp, Cout, 3, 1, y)
+                torch.cuda.synchronize()
+                e.append(relerr(to_nchw(y.buf), yr.detach()))
+            if C == 64:
+                dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+                K.conv_dgrad(gyd, wp, C, 3, 1, dx)
+                torch.cuda.synchronize()
+                e.append(relerr(to_nchw(dx.buf), xr.grad))
+            errs[m] = e
+    finally:
+        if old is None:
+            os.environ.pop("DGVCC_RSPLIT3", None)
+        else:
+            os.environ["DGVCC_RSPLIT3"] = old
+    for e3, e1 in zip(errs["1"], errs["0"]):
+        assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
