@@ -2874,21 +2874,23 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 // f32 weight gradient of a 3x3 / stride-1 / pad-1 conv on the split math with the three taps of
 // one kernel row sharing their operands (the bf16 conv_wgrad9_kernel's idea on
 // conv_wgrad_split_kernel's split-once-per-block staging): a K-step is 32 consecutive pixels of
-// one image row (W % 32 == 0); dY[32 px][64 co] and the input strip X[34 px][64 c] of image row
+// one image row (W % 32 == 0); dY[32 px][BCO] and the input strip X[34 px][BC] of image row
 // p + r - 1 (columns q0 - 1 .. q0 + 32) are split once into bf16 planes, and the taps s = 0, 1, 2
-// read the strip at row offsets s.  Per staged value 3x the MFMA work of the per-tap kernel, whose
-// 64-channel tiles were bound by the split and LDS-store work (~30% MFMA-busy).  256 threads = 4
-// waves (2 co x 2 c of 32 x 32, all 3 taps), two blocks per CU.
-template <int NTH = 256>
-__global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
-  constexpr int BCO = 64, BC = 64, BKP = 32, XR = BKP + 2;
+// read the strip at row offsets s.  Per staged value 3x the MFMA work of the per-tap kernel.
+// 64 x 64 (x 3 taps): 4 waves of 32 x 32, two blocks per CU (the per-tap kernel's 64-wide tiles
+// were bound by the split and LDS-store work, ~30% MFMA-busy); 128 x 128: 8 waves of 64 x 32,
+// one block per CU.
+template <int BCO, int BC, int WCO, int NTH>
+__global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArgs a) {
+  constexpr int BKP = 32, XR = BKP + 2;
   constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
   constexpr int PA = BKP * ROWA, PB = XR * ROWB;           // bytes per plane
   constexpr int TILE = 3 * (PA + PB);
-  constexpr int CPR = 16;                                  // 16-B f32 chunks per 64-channel row
-  constexpr int AR = BKP * CPR / NTH, BR = (XR * CPR + NTH - 1) / NTH;
-  constexpr int TI = 2, TJ = 2;                            // wave tile 32 co x 32 c
-  static_assert(NTH == 256 && AR * NTH == BKP * CPR, "4 waves");
+  constexpr int CPRA = BCO / 4, CPRB = BC / 4;             // 16-B f32 chunks per pixel row
+  constexpr int AR = BKP * CPRA / NTH, BR = (XR * CPRB + NTH - 1) / NTH;
+  constexpr int WC = NTH / 64 / WCO;
+  constexpr int TI = BCO / WCO / 16, TJ = BC / WC / 16;
+  static_assert(AR * NTH == BKP * CPRA && TI >= 1 && TJ >= 1, "tile / block mismatch");
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
 
   const int HW = a.H * a.W;
@@ -2924,16 +2926,16 @@ __global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int idx = tid + NTH * i;
-      const int row = idx / CPR, ch = idx % CPR;
+      const int row = idx / CPRA, ch = idx % CPRA;
       ra[i] = bload(dyr, (unsigned)(((long long)(k0 + row - kbeg) * a.lddy + co0 + ch * 4) * 4));
     }
     const int h = sp + dh;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int idx = tid + NTH * i;
-      const int row = idx / CPR, ch = idx % CPR;
+      const int row = idx / CPRB, ch = idx % CPRB;
       const int ww = sq - 1 + row;
-      const bool ok = idx < XR * CPR && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const bool ok = idx < XR * CPRB && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
       const long long pin = (long long)sn * HW + (long long)h * a.W + ww - xlo;
       rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + c0 + ch * 4) * 4) : 0xFFFFFFF0u);
     }
@@ -2949,7 +2951,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int idx = tid + NTH * i;
-      const int o = (idx / CPR) * ROWA + (idx % CPR) * 8;
+      const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       u2v h0, h1, h2;
       split3_4(ra[i], h0, h1, h2);
       *(u2v*)(As + o) = h0;
@@ -2959,8 +2961,8 @@ __global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int idx = tid + NTH * i;
-      if (idx < XR * CPR) {
-        const int o = (idx / CPR) * ROWB + (idx % CPR) * 8;
+      if (idx < XR * CPRB) {
+        const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
         u2v h0, h1, h2;
         split3_4(rb[i], h0, h1, h2);
         *(u2v*)(Bs + o) = h0;
@@ -2978,7 +2980,7 @@ __global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[s][i][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  const int wco = (wid >> 1) * 32, wc = (wid & 1) * 32;
+  const int wco = (wid / WC) * (BCO / WCO), wc = (wid % WC) * (BC / WC);
   const int g = lane >> 4;
   const int q = (lane & 15) >> 2, p4 = lane & 3;
   const int r1 = 4 * g + q, r2 = r1 + 16;
@@ -3026,8 +3028,10 @@ __global__ __launch_bounds__(NTH, 2) void conv_wgrad_split3_kernel(WgArgs a) {
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
             acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[s][i][j], 0, 0, 0);
+      // one block per CU: the next step's split + LDS stores between the taps' MFMA blocks
+      if (NTH == 512 && s == 1 && kt + 1 < nkt) swrite(cur ^ 1);
     }
-    if (kt + 1 < nkt) swrite(cur ^ 1);  // two blocks per CU overlap each other's split with MFMAs
+    if (NTH != 512 && kt + 1 < nkt) swrite(cur ^ 1);  // two blocks per CU overlap each other instead
     __syncthreads();
   }
 
@@ -3082,18 +3086,25 @@ static long long wgs_tiles(int C, int Cout, int RS) {
 static long long wgs_slots(int C, int Cout) { return wgs_bco(C, Cout) == 64 ? 512 : 256; }
 
 // conv_wgrad_split3_kernel (three taps of a kernel row share their operands) for 3x3 / pad 1 /
-// stride 1 rows of W % 32 == 0 with a 64-channel side (the per-tap kernel's 64-wide tiles);
-// DGVCC_WGRAD_SPLIT3=0 off, =2 every C % 64 == 0 shape
+// stride 1 rows of W % 32 == 0; DGVCC_WGRAD_SPLIT3 = 0 off, 1 / 2 / 3 below
 static int wgrad_split3_mode() {
   const char* e = getenv("DGVCC_WGRAD_SPLIT3");
-  return e ? (e[0] - '0') : 1;
+  return e ? (e[0] - '0') : 3;
 }
-static bool wgs3_shape_ok(int C, int Cout, int R, int S, int W) {
+// tile side of the 3-tap kernel for a shape: 64 (64 x 64, two blocks per CU), 128 (128 x 128, one
+// block per CU), 0 = not served.  Mode 1: 64-channel shapes; 2: 64-tiles for every C % 64 == 0
+// shape; 3 (default): mode 1 + 128-tiles for C, Cout % 128 == 0 (fp32 final step 454 -> 427 ms
+// against mode 1, same box, profiles/round2f/wgrad3_ab.txt)
+static int wgs3_tile(int C, int Cout, int R, int S, int W) {
   const int m = wgrad_split3_mode();
-  return use_wgrad_split() && m != 0 && R == 3 && S == 3 && W % 32 == 0 && C % 64 == 0 && Cout % 64 == 0 &&
-         (m == 2 || C == 64 || Cout == 64);
+  if (!use_wgrad_split() || m == 0 || R != 3 || S != 3 || W % 32 != 0 || C % 64 != 0 || Cout % 64 != 0) return 0;
+  if (C == 64 || Cout == 64 || m == 2) return 64;
+  if (m == 3 && C % 128 == 0 && Cout % 128 == 0) return 128;
+  return 0;
 }
-static long long wgs3_tiles(int C, int Cout) { return (long long)(Cout / 64) * (C / 64) * 3; }
+static bool wgs3_shape_ok(int C, int Cout, int R, int S, int W) { return wgs3_tile(C, Cout, R, S, W) != 0; }
+static long long wgs3_tiles(int C, int Cout, int b) { return (long long)(Cout / b) * (C / b) * 3; }
+static long long wgs3_slots(int b) { return b == 64 ? 512 : 256; }
 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int C, int RS,
                                     float* __restrict__ dw, int accumulate) {
@@ -3675,14 +3686,16 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   if (done) {
   } else if constexpr (!Is16<T>::value) {
     const long long M3 = (long long)a.N * a.P * a.Q;
-    if (f32_split() && a.stride == 1 && !a.whole_x && a.pad == 1 && wgs3_shape_ok(a.C, a.Cout, a.R, a.S, a.W)) {
-      const WgPlan p = wgs_plan(M3, wgs3_tiles(a.C, a.Cout), 512);
+    const int b3 = wgs3_tile(a.C, a.Cout, a.R, a.S, a.W);
+    if (f32_split() && a.stride == 1 && !a.whole_x && a.pad == 1 && b3) {
+      const WgPlan p = wgs_plan(M3, wgs3_tiles(a.C, a.Cout, b3), wgs3_slots(b3));
       if ((long long)(p.pps + 2 * (a.W + 1)) * std::max(a.ldx, a.lddy) * 4 < (1ll << 31)) {
         a.splits = p.splits;
         a.pps = p.pps;
         slab_splits = p.splits;
-        hipLaunchKernelGGL((conv_wgrad_split3_kernel<256>), dim3((unsigned)(wgs3_tiles(a.C, a.Cout) * p.splits)),
-                           dim3(256), 0, st, a);
+        const dim3 g3((unsigned)(wgs3_tiles(a.C, a.Cout, b3) * p.splits));
+        if (b3 == 64) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 256>), g3, dim3(256), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad_split3_kernel<128, 128, 2, 512>), g3, dim3(512), 0, st, a);
         done = true;
       }
     }
@@ -4074,7 +4087,8 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
   if (!DG_IS16(dtype) && wgs_ok(C, Cout))
     q = wgs_plan((long long)N * H * W, wgs_tiles(C, Cout, R * S), wgs_slots(C, Cout));
   if (!DG_IS16(dtype) && wgs3_shape_ok(C, Cout, R, S, W)) {  // the 3-tap plan (launch may refuse it)
-    const WgPlan q3 = wgs_plan((long long)N * H * W, wgs3_tiles(C, Cout), 512);
+    const int b3 = wgs3_tile(C, Cout, R, S, W);
+    const WgPlan q3 = wgs_plan((long long)N * H * W, wgs3_tiles(C, Cout, b3), wgs3_slots(b3));
     if (q3.splits > q.splits) q = q3;
   }
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half

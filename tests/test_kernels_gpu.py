@@ -408,7 +408,8 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
 
 @pytest.mark.parametrize("N,H,W,C,Cout,mode", [(2, 9, 64, 64, 64, "1"), (3, 17, 96, 64, 128, "1"),
                                                (2, 40, 32, 128, 64, "1"), (1, 48, 160, 256, 128, "2"),
-                                               (4, 5, 128, 64, 64, "1")])
+                                               (4, 5, 128, 64, 64, "1"), (2, 11, 96, 128, 256, "3"),
+                                               (1, 24, 64, 256, 128, "3")])
 def test_conv_f32_wgrad_split3(dev, N, H, W, C, Cout, mode):
     """3-tap shared f32 split-math wgrad (conv_wgrad_split3_kernel: a kernel row's three taps on one
     staged dY tile and X strip, K-steps of 32 pixels of one image row) against float64 torch and
