@@ -241,9 +241,9 @@ def measured_traffic(args, precision):
 
 
 FWD_KERNEL_NAMES = {
-    "fp32": "conv_fwd_pers_kernel<float, split> (implicit-GEMM conv, f32 operands split exactly into 3 bf16 parts, "
-            "6 x v_mfma_f32_16x16x32_bf16 per 32-deep block, f32 accumulation: forward + dgrad launches; peak = "
-            "dense bf16 / 6)",
+    "fp32": "conv_fwd_psplit_kernel<256|128> + conv_fwd_rsplit3_kernel + conv_fwd_rsplit_kernel (implicit-GEMM "
+            "conv, f32 operands split exactly into 3 bf16 parts, 6 x v_mfma_f32_16x16x32_bf16 per 32-deep block, "
+            "f32 accumulation: forward + dgrad launches; peak = dense bf16 / 6)",
     "fp32_exact": "conv_fwd_pers_kernel<float> (implicit-GEMM conv on v_mfma_f32_16x16x4_f32: forward + dgrad "
                   "launches)",
     "bf16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
