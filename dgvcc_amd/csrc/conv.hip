@@ -42,6 +42,7 @@ struct FwdArgs {
   const float* escale = nullptr;
   const float* eshift = nullptr;
   int eact = 0;
+  int tile_order = 0;  // f32 pre-split kernel: 1 = channel-tile-major tile walk (DGVCC_PSPLIT_ORDER)
 };
 
 __device__ __forceinline__ void epi_affine(float v[4], const FwdArgs& a, int co) {
@@ -1066,8 +1067,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   };
   auto setup = [&](int lin, Ctx& c) {
     const int t = xcd_remap(lin, ntile);
-    c.co0 = (t % nco) * BN;
-    c.px0 = (t / nco) * PSB;
+    if (a.tile_order) {  // channel-tile-major: an XCD's concurrent tiles share one filter panel
+      const int npx = ntile / nco;
+      c.co0 = (t / npx) * BN;
+      c.px0 = (t - (t / npx) * npx) * PSB;
+    } else {
+      c.co0 = (t % nco) * BN;
+      c.px0 = (t / nco) * PSB;
+    }
     const int halo = a.pad * (a.W + 1);
     const int plo = max(0, c.px0 - halo);
     const int phi = min(M, c.px0 + PSB + halo);
@@ -2429,12 +2436,17 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         const int bn2 = f32_pers_bn(a.Cout);
         const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, PSB) * (a.Cout / bn2), persist_grid());
         const char* wspc = (const char*)wsp;
+        FwdArgs ap = a;
+        {
+          const char* e = getenv("DGVCC_PSPLIT_ORDER");
+          ap.tile_order = (e && e[0] == '1') ? 1 : 0;
+        }
         if (a.escale) {
-          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 3>), dim3(g2), dim3(512), 0, st, a, wspc);
-          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 3>), dim3(g2), dim3(512), 0, st, a, wspc);
+          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
         } else {
-          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0>), dim3(g2), dim3(512), 0, st, a, wspc);
-          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 0>), dim3(g2), dim3(512), 0, st, a, wspc);
+          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
         }
       } else if (f32_split()) F32_PERS(1);
       else F32_PERS(0);

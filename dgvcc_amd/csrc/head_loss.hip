@@ -151,12 +151,14 @@ __global__ __launch_bounds__(NT) void mse_partial(const float* __restrict__ pred
   }
 }
 
+// launched as one block of >= 64 threads; wave 0 reduces: lane-strided double sums + fixed xor tree
 __global__ void mse_final(const float* __restrict__ part, int nblk, long long n, float* loss) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    double a = 0.0;
-    for (int i = 0; i < nblk; ++i) a += part[i];
-    loss[0] = (float)(a / (double)n);
-  }
+  if (threadIdx.x >= 64) return;
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += 64) a += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (threadIdx.x == 0) loss[0] = (float)(a / (double)n);
 }
 
 // ---------------------------------------------------------------- BCE ------

@@ -184,12 +184,13 @@ __global__ __launch_bounds__(NT) void softmax_pair_fwd(const T* __restrict__ L1,
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
 }
 
+// one 64-thread block: lane-strided double sums, then a fixed xor tree (deterministic)
 __global__ void sum_final(const float* __restrict__ part, int nblk, double denom, float* out) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    double a = 0.0;
-    for (int i = 0; i < nblk; ++i) a += part[i];
-    out[0] = (float)(a / denom);
-  }
+  double a = 0.0;
+  for (int i = threadIdx.x; i < nblk; i += 64) a += part[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o, 64);
+  if (threadIdx.x == 0) out[0] = (float)(a / denom);
 }
 
 // gL_v = P_v * (gP_v' - sum(P_v * gP_v')),  gP1' = gP1 + k (P1 - P2), gP2' = gP2 - k (P1 - P2),
