@@ -1016,17 +1016,28 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
 // make a K-step's A tile 1.5x the f32 bytes, and 2 x (48 + 24) KB + epilogue scratch fill
 // the 160-KB LDS exactly at BN = 256.  k order within a 32-channel block: lane group fc
 // holds channels 8fc..8fc+7 for both operands.
-constexpr int PSB = 192;  // pixels per tile of the pre-split kernel
-template <int BN, int STG, int EPI = 0>
+constexpr int PSB = 192;  // pixels per tile of the pre-split kernel at BN = 256
+// BN = 128: 384-pixel tiles with the 8 waves all on pixels (each 128 channels x 48 pixels, the
+// BN = 256 kernel's wave tile), two stages of (24 + 48) KB: the filter fragments are reused by 8
+// waves instead of 4 (the 192-pixel 2 x 4 layout ran 52% MFMA-busy against 65% at BN = 256)
+__host__ __device__ constexpr int psplit_psb(int BN, int wide = 1) { return BN == 128 && wide ? 384 : PSB; }
+static bool psplit_wide() {  // DGVCC_PSPLIT_WIDE=0: BN = 128 on 192-pixel tiles of 2 x 4 waves
+  const char* e = getenv("DGVCC_PSPLIT_WIDE");
+  return !(e && e[0] == '0');
+}
+template <int BN, int STG, int EPI = 0, int WIDE = 1>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int PSB = psplit_psb(BN, WIDE);
+  constexpr int NCOG = (BN == 128 && WIDE) ? 1 : 2;  // channel groups of waves
+  constexpr int NPXG = 8 / NCOG;                   // pixel groups of waves
   constexpr int AROWB = 64;                        // bytes per A plane row (32 bf16)
   constexpr int A_BYTES = 3 * BN * AROWB;
   constexpr int AI = A_BYTES / 1024 / 8;           // A DMA instructions per wave per K-step
   constexpr int BI = PSB / 64;                     // B DMA instructions per wave per K-step
-  constexpr int TI = BN / 32, TJ = PSB / 64;       // wave tile: BN/2 channels x 48 pixels
+  constexpr int TI = BN / NCOG / 16, TJ = PSB / NPXG / 16;  // wave tile: 128 channels x 48 pixels
   constexpr int STAGE = A_BYTES + PSB * 128;
   constexpr int PF = STG - 1;
-  constexpr int EPI_B = 4 * 3 * BN * 4;
+  constexpr int EPI_B = NPXG * 3 * BN * 4;
   static_assert(AI * 8 * 1024 == A_BYTES, "A tile must split evenly over the 8 waves");
   __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B + PERS_BIAS_MAX * 4];
   char* epi_lds = smem + STG * STAGE;
@@ -1124,7 +1135,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   setup(lin, cur);
   bool has_next = lin + G < ntile;
   if (has_next) setup(lin + G, nxt);
-  const int wpx = (wid & 3) * (PSB / 4), wco = (wid >> 2) * (BN / 2);
+  const int wpx = (wid % NPXG) * (PSB / NPXG), wco = (wid / NPXG) * (BN / NCOG);
   const int fr = lane & 15, fc = lane >> 4;
   int gs = 0;
   issue(cur, 0, 0);
@@ -1231,7 +1242,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       }
     }
     if (EPI == 0 && a.part)
-      epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, epi_lds, a.part + (long long)(cur.px0 / PSB) * 3 * a.Cout,
+      epi_stats<TI, TJ, NPXG, BN>(acc, valid, wid % NPXG, wco, epi_lds, a.part + (long long)(cur.px0 / PSB) * 3 * a.Cout,
                                a.Cout, cur.co0, tid, fr, fc);
     if (!has_next) break;
     cur = nxt;
@@ -2434,7 +2445,9 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
                            0, st, (const float*)a.w, nw, wsp);
         const int bn2 = f32_pers_bn(a.Cout);
-        const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, PSB) * (a.Cout / bn2), persist_grid());
+        const bool wide = psplit_wide();
+        const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_psb(bn2, wide)) * (a.Cout / bn2),
+                                                          persist_grid());
         const char* wspc = (const char*)wsp;
         FwdArgs ap = a;
         {
@@ -2443,10 +2456,12 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
         }
         if (a.escale) {
           if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
-          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (wide) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 3, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
         } else {
           if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
-          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (wide) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 0, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
         }
       } else if (f32_split()) F32_PERS(1);
       else F32_PERS(0);
@@ -3930,7 +3945,7 @@ extern "C" int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, 
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
   const long long M = (long long)N * H * W;
   FwdArgs a{nullptr, ldx, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0};
-  if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, PSB);
+  if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, psplit_psb(f32_pers_bn(Cout), psplit_wide()));
   return dg_cdiv(M, 256);
 }
 extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,

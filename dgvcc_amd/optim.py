@@ -103,9 +103,12 @@ class AdamW(torch.optim.Optimizer):
         _, runs, dev_offs = cache
         tables = []
         for (i0, i1), o in zip(runs, dev_offs):
-            table = torch.tensor([ps[i].grad.data_ptr() for i in range(i0, i1)], dtype=torch.int64).to(g.device)
+            # pinned host table, copied on the stream without a host stall (kept alive with the launch)
+            host = torch.tensor([ps[i].grad.data_ptr() for i in range(i0, i1)], dtype=torch.int64,
+                                pin_memory=g.is_cuda)
+            table = host.to(g.device, non_blocking=True)
             call("dg_gather_flat", ptr(table), ptr(o), i1 - i0, g.numel(), ptr(g), stream())
-            tables.append(table)
+            tables.append((host, table))
         group["_table"] = tables  # keep alive until the launches retire
         offs = group["_offs"]
         return [(offs[i0], offs[i1 - 1] + ps[i1 - 1].numel()) for i0, i1 in runs]

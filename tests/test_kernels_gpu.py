@@ -387,7 +387,9 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
         ref = (ref * st[2].double() + st[3].double()).clamp_min(0)
     elif epi == "stats":
         rows = K.query("dg_conv_stats_rows_ex", 0, N, H, W, C, C, Cout, 3, 3)
-        assert rows == -(-(N * H * W) // (192 if Cout % 128 == 0 else 256))  # 64-wide tiles: conv_fwd_rsplit_kernel
+        # tiles: 192 px at 256 channels, 384 px at 128 (conv_fwd_psplit_kernel), 256 px at 64 (rsplit)
+        tile = 192 if Cout % 256 == 0 else (384 if Cout % 128 == 0 else 256)
+        assert rows == -(-(N * H * W) // tile)
         part, r2 = K.conv_fwd_stats(K.Act(x.to(dev)), wp, Cout, 3, 1, z, bias=b.to(dev))
         assert r2 == rows
     else:
