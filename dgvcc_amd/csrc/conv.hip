@@ -1576,6 +1576,161 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
                              co0, tid, fr, fc);
 }
 
+// conv_fwd_rsplit3_kernel on 512-pixel tiles (W % 512 == 0) with all 8 waves on pixels, each
+// 64 channels x 64 pixels (twice the per-wave fragment reuse of the 2 x 4 layout): the 514-pixel
+// strip (99 KB of planes) and the three taps' filter planes (36 KB) are single-buffered, both
+// stored between the K-step's two barriers from registers loaded during the previous K-step.
+template <int EPI = 0>
+__global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int BN = 64, BPX = 512, SR = 520;        // strip rows (514 used)
+  constexpr int B_PL = SR * 64, BUF = 3 * B_PL;      // strip plane / buffer bytes
+  constexpr int A_PL = BN * 64, A_TAP = 3 * A_PL;    // filter plane / tap bytes
+  constexpr int TI = 4, TJ = 4;
+  constexpr int NCH = (BPX + 2) * 8, BR = (NCH + 511) / 512;  // 16-B f32 chunks of the strip
+  constexpr int NA = 3 * 3 * BN * 4, AR = (NA + 511) / 512;  // 16-B chunks of the 3 taps' planes
+  __shared__ __attribute__((aligned(16))) char smem[BUF + 3 * A_TAP];
+  char* Asm = smem + BUF;
+
+  const int HW = a.H * a.W;
+  const int M = a.N * HW;
+  const int nco = a.Cout / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int co0 = (bid % nco) * BN;
+  const int px0 = (bid / nco) * BPX;
+  const int tn = px0 / HW, tp = (px0 - tn * HW) / a.W, tq = px0 - tn * HW - tp * a.W;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int chunk = tid & 7, rbase = tid >> 3;
+  const int CB = a.C / 32;
+  const int KT3 = 3 * CB;
+
+  const int plo = max(0, px0 - (a.W + 1));
+  const int phi = min(M, px0 + BPX + a.W + 1);
+  const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 4);
+  __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 4), 0,
+                                                                win_bytes, 0x00020000);
+  const int wpx = wid * 64, wco = 0;
+  const int fr = lane & 15, fc = lane >> 4;
+  // filter chunk q of a K-step: (tap s, plane, row co, 16-B chunk) = (q / 768, (q / 256) % 3, (q & 255) >> 2, q & 3)
+  const char* wbase = wsp + (long long)co0 * (9 * CB) * 192;
+  int a_src[AR], a_dst[AR];
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int q = tid + 512 * i;
+    const int ts = q / 768, pl = (q / 256) % 3, row = (q & 255) >> 2, ch = q & 3;
+    a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * 192 + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*192
+    a_dst[i] = ts * A_TAP + pl * A_PL + row * 64 + ((ch ^ ((row >> 2) & 3)) << 4);
+  }
+
+  u4v rb[BR], ra[AR];
+  auto gload = [&](int t) __attribute__((always_inline)) {
+    const int r = t / CB, cb = t - r * CB;
+    const int h = tp + r - 1;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = rbase + 64 * i;
+      const int ww = tq - 1 + row;
+      const bool ok = row < BPX + 2 && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const long long pin = (long long)tn * HW + (long long)h * a.W + ww - plo;
+      rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + cb * 32 + chunk * 4) * 4) : 0xFFFFFFF0u);
+    }
+    const long long koff = (long long)(r * 3 * CB + cb) * 192;
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      if (a_src[i] >= 0) ra[i] = *(const u4v*)(wbase + a_src[i] + koff);
+  };
+  auto swrite = [&](int buf) __attribute__((always_inline)) {
+    char* Bs = smem + buf * 0;
+#pragma unroll
+    for (int i = 0; i < BR; ++i) {
+      const int row = rbase + 64 * i;
+      if (row < BPX + 2) {
+        const int o = row * 64 + ((((chunk >> 1) ^ ((row >> 2) & 3))) << 4) + (chunk & 1) * 8;
+        u2v h0, h1, h2;
+        split3_4(rb[i], h0, h1, h2);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + B_PL + o) = h1;
+        *(u2v*)(Bs + 2 * B_PL + o) = h2;
+      }
+    }
+  };
+
+  f4v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  for (int t = 0; t < KT3; ++t) {
+    __syncthreads();  // every wave is done with the previous K-step's strip and filter planes
+    swrite(0);
+#pragma unroll
+    for (int i = 0; i < AR; ++i)
+      if (a_src[i] >= 0) *(u4v*)(Asm + a_dst[i]) = ra[i];
+    __syncthreads();
+    if (t + 1 < KT3) gload(t + 1);
+    const char* Bs = smem;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      s8v ah[TI][3], bh[TJ][3];
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int row = wco + 16 * i + fr;
+        const int o = s * A_TAP + row * 64 + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) ah[i][pl] = *(const s8v*)(Asm + pl * A_PL + o);
+      }
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int row = wpx + 16 * j + fr + s;
+        const int o = row * 64 + ((fc ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
+      }
+      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int u = 0; u < 6; ++u)
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();  // smem reuse by the statistics epilogue
+
+  float* y = (float*)a.y;
+  bool valid[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    valid[j] = px < M;
+    if (px >= M) continue;
+    float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const int co = co0 + wco + 16 * i + 4 * fc;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (a.bias) {
+        const f4v b = *(const f4v*)(a.bias + co);
+        v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+      }
+      if (a.accumulate) {
+        float o[4];
+        ld4(yrow + co, o);
+        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+      }
+      if constexpr (EPI == 3) epi_affine(v, a, co);
+      st4(yrow + co, v);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+    }
+  }
+  if (EPI == 0 && a.part)
+    epi_stats<TI, TJ, 8, BN>(acc, valid, wid, wco, smem, a.part + (long long)(px0 / BPX) * 3 * a.Cout, a.Cout,
+                             co0, tid, fr, fc);
+}
+
 // wsp[co][kb][part][32] (bf16) = the exact 3-way split of the packed f32 filter w[co][kb*32 + j]
 __global__ void split_weight_kernel(const float* __restrict__ w, long long n, unsigned short* __restrict__ wsp) {
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n; o += (long long)gridDim.x * blockDim.x) {
@@ -2300,11 +2455,16 @@ static bool rsplit_ok(const FwdArgs& a) {
          a.Cout % 64 == 0 && f32_pers_bn(a.Cout) == 64 && (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
 }
 
-// rows of W % 256 == 0 of a 3x3 / pad-1 Cout = 64 conv: the 3-tap strip kernel (DGVCC_RSPLIT3=0 off)
-static bool rsplit3_ok(const FwdArgs& a) {
+// rows of W % 256 == 0 of a 3x3 / pad-1 Cout = 64 conv: the 3-tap strip kernel (DGVCC_RSPLIT3=0 off;
+// =1 only the 256-pixel 2 x 4-wave form; default 2: the 512-pixel all-pixel-wave form where W % 512 == 0)
+static int rsplit3_mode() {
   const char* e = getenv("DGVCC_RSPLIT3");
-  return !(e && e[0] == '0') && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0;
+  return e ? e[0] - '0' : 2;
 }
+static bool rsplit3_ok(const FwdArgs& a) {
+  return rsplit3_mode() != 0 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0;
+}
+static bool rsplit3w_ok(const FwdArgs& a) { return rsplit3_ok(a) && rsplit3_mode() == 2 && a.W % 512 == 0; }
 
 // Per-stream device scratch for the pre-split filter panels (grown on demand; a launch on
 // a stream only ever overlaps its own stream's earlier work, which hipFree waits for).
@@ -2410,7 +2570,11 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
       hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
                          0, st, (const float*)a.w, nw, wsp);
       const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));
-      if (rsplit3_ok(a)) {
+      if (rsplit3w_ok(a)) {
+        const dim3 gw((unsigned)((long long)(M / 512) * (a.Cout / 64)));
+        if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3>), gw, dim3(512), 0, st, a, (const char*)wsp);
+        else hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0>), gw, dim3(512), 0, st, a, (const char*)wsp);
+      } else if (rsplit3_ok(a)) {
         if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
         else hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<0>), g, dim3(512), 0, st, a, (const char*)wsp);
       } else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
@@ -3946,6 +4110,7 @@ extern "C" int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, 
   const long long M = (long long)N * H * W;
   FwdArgs a{nullptr, ldx, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0};
   if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, psplit_psb(f32_pers_bn(Cout), psplit_wide()));
+  if (dtype == DG_F32 && rsplit_ok(a) && rsplit3w_ok(a)) return dg_cdiv(M, 512);
   return dg_cdiv(M, 256);
 }
 extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,

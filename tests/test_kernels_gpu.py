@@ -365,7 +365,8 @@ def test_conv_f32_split_math(dev, case):
                                               (3, 128, 256, 256, 512, "eval"), (8, 100, 130, 128, 256, "bias"),
                                               (3, 70, 90, 64, 64, "stats"), (2, 64, 256, 128, 64, "eval"),
                                               (2, 33, 40, 64, 64, "bias"), (2, 8, 256, 64, 64, "stats"),
-                                              (1, 6, 512, 128, 64, "bias"), (2, 5, 256, 64, 64, "eval")])
+                                              (1, 6, 512, 128, 64, "bias"), (2, 5, 256, 64, 64, "eval"),
+                                              (2, 4, 512, 64, 64, "stats"), (1, 3, 1024, 64, 64, "eval")])
 def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
     """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128; Cout = 64 on
     conv_fwd_rsplit_kernel, 256-pixel tiles) with
@@ -387,8 +388,9 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
         ref = (ref * st[2].double() + st[3].double()).clamp_min(0)
     elif epi == "stats":
         rows = K.query("dg_conv_stats_rows_ex", 0, N, H, W, C, C, Cout, 3, 3)
-        # tiles: 192 px at 256 channels, 384 px at 128 (conv_fwd_psplit_kernel), 256 px at 64 (rsplit)
-        tile = 192 if Cout % 256 == 0 else (384 if Cout % 128 == 0 else 256)
+        # tiles: 192 px at 256 channels, 384 px at 128 (conv_fwd_psplit_kernel), 256 px at 64 (rsplit),
+        # 512 px at 64 where W % 512 == 0 (conv_fwd_rsplit3w_kernel)
+        tile = 192 if Cout % 256 == 0 else (384 if Cout % 128 == 0 else (512 if W % 512 == 0 else 256))
         assert rows == -(-(N * H * W) // tile)
         part, r2 = K.conv_fwd_stats(K.Act(x.to(dev)), wp, Cout, 3, 1, z, bias=b.to(dev))
         assert r2 == rows
@@ -445,10 +447,12 @@ def test_conv_f32_wgrad_split3(dev, N, H, W, C, Cout, mode):
     assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, (e3, e1)
 
 
-@pytest.mark.parametrize("N,H,W,C,Cout", [(2, 7, 256, 64, 64), (1, 5, 512, 64, 128), (1, 4, 256, 256, 64)])
+@pytest.mark.parametrize("N,H,W,C,Cout", [(2, 7, 256, 64, 64), (1, 5, 512, 64, 128), (1, 4, 256, 256, 64),
+                                          (2, 3, 1024, 64, 64), (1, 6, 512, 128, 64)])
 def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
     """Cout = 64 split-math forward with the 3 taps of a kernel row on one staged strip
-    (conv_fwd_rsplit3_kernel, W % 256 == 0) and the dgrad that lands on it (64-channel dx): against
+    (conv_fwd_rsplit3_kernel, W % 256 == 0; conv_fwd_rsplit3w_kernel, W % 512 == 0) and the dgrad
+    that lands on it (64-channel dx): against
     float64 torch and against the per-tap kernel (DGVCC_RSPLIT3=0), within the f32-grade bound."""
     import os
     K = _k()
@@ -464,7 +468,7 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
     errs = {}
     old = os.environ.get("DGVCC_RSPLIT3")
     try:
-        for m in ("1", "0"):
+        for m in ("2", "1", "0"):
             os.environ["DGVCC_RSPLIT3"] = m
             e = []
             if Cout == 64:
@@ -483,5 +487,6 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
             os.environ.pop("DGVCC_RSPLIT3", None)
         else:
             os.environ["DGVCC_RSPLIT3"] = old
-    for e3, e1 in zip(errs["1"], errs["0"]):
-        assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
+    for m in ("2", "1"):  # 512-pixel all-pixel-wave form (W % 512 == 0), 256-pixel form
+        for e3, e1 in zip(errs[m], errs["0"]):
+            assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
