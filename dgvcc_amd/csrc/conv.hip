@@ -136,7 +136,7 @@ __device__ __forceinline__ void epi_stats(f4v (&acc)[TI][TJ], const bool (&valid
 // Epilogue BatchNorm-backward partial sums of the stored (bf16-rounded) gradient tile:
 // the separate pass over (g, z) of norm.hip's bn_bwd_partial, computed where g is
 // produced; z is read here at the tile's pixels (8-B loads), once.
-template <int TI, int TJ, int NPW, int BN, typename T = bf16>
+template <int TI, int TJ, int NPW, int BN, typename T = bf16, int PXT = 256>
 __device__ __forceinline__ void epi_bnbwd(f4v (&acc)[TI][TJ], const bool (&valid)[TJ], int pw, int cw, int wpx,
                                           char* lds, const FwdArgs& a, int px0, int co0, int tid, int fr, int fc) {
   float* sh = (float*)lds;  // [NPW][3][BN]
@@ -186,8 +186,8 @@ __device__ __forceinline__ void epi_bnbwd(f4v (&acc)[TI][TJ], const bool (&valid
     }
   }
   lds_barrier();
-  float* row = a.bpart + (long long)(px0 / 256) * 3 * a.Cout;
-  for (int t = tid; t < 3 * BN; t += 512) {  // the pipe kernel's 512 threads
+  float* row = a.bpart + (long long)(px0 / PXT) * 3 * a.Cout;
+  for (int t = tid; t < 3 * BN; t += 512) {  // the pipe / pre-split kernels' 512 threads
     const int k = t / BN, c = t - k * BN;
     float v = 0.f;
 #pragma unroll
@@ -1241,6 +1241,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
         for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
       }
     }
+    if constexpr (EPI == 2)  // dgrad: BatchNorm-backward partials of the layer whose gradient this is
+      epi_bnbwd<TI, TJ, NPXG, BN, float, PSB>(acc, valid, wid % NPXG, wco, wpx, epi_lds, a, cur.px0, cur.co0, tid, fr,
+                                             fc);
     if (EPI == 0 && a.part)
       epi_stats<TI, TJ, NPXG, BN>(acc, valid, wid % NPXG, wco, epi_lds, a.part + (long long)(cur.px0 / PSB) * 3 * a.Cout,
                                a.Cout, cur.co0, tid, fr, fc);
@@ -2563,6 +2566,23 @@ int launch_fwd(const FwdArgs& a, hipStream_t st) {
     }
   }
   if constexpr (!Is16<T>::value) {
+    if (a.bpart) {  // dgrad with the BN-backward partials in the epilogue: the pre-split kernel only
+      FwdArgs q = a;
+      q.bpart = nullptr;
+      if (!(psplit_ok(q) && psplit_wide())) return DG_ERR_UNSUPPORTED;
+      const long long nw = (long long)a.Cout * a.R * a.S * a.C;
+      unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
+      if (!wsp) return DG_ERR_HIP;
+      hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
+                         0, st, (const float*)a.w, nw, wsp);
+      const int bn2 = f32_pers_bn(a.Cout);
+      const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_psb(bn2)) * (a.Cout / bn2),
+                                                        persist_grid());
+      if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 2>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
+      else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 2>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
+      DG_CHECK_LAUNCH();
+      return DG_OK;
+    }
     if (rsplit_ok(a)) {  // split math, Cout = 64: both operands split once per block
       const long long nw = (long long)a.Cout * a.R * a.S * a.C;
       unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
@@ -4213,18 +4233,20 @@ extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, i
                                  int act, const float* drop, int HW, float* bpart, void* stream) {
   DG_REQUIRE(x && w && y && z && bpart && scale && shift && mean && invstd && N > 0 && H > 0 && W > 0 && C > 0 &&
              Cout > 0 && R > 0 && S > 0 && (act == 0 || act == 1) && (!drop || HW > 0));
-  DG_SUPPORTED(DG_IS16(dtype) && fwd_has_epi_stats(C, Cout, ldx, R, S));
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(dtype == DG_F32 || fwd_has_epi_stats(C, Cout, ldx, R, S));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 128 == 0);  // the pipe kernel's 128/256 tiles
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldy % 4 == 0 && ldz >= Cout && ldz % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   const long long M = (long long)N * H * W;
-  DG_SUPPORTED(fwd_ksplit(M, Cout, C, R, S) == 1);
+  DG_SUPPORTED(dtype == DG_F32 || fwd_ksplit(M, Cout, C, R, S) == 1);
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, nullptr, (char*)y, ldy, 0};
   a.bz = (const char*)z;
   a.ldbz = ldz;
   a.bsc = scale; a.bsf = shift; a.bmu = mean; a.bis = invstd; a.bdrop = drop;
   a.bact = act; a.bHW = drop ? HW : 1;
   a.bpart = bpart;
+  if (dtype == DG_F32) return launch_fwd<float>(a, (hipStream_t)stream);  // conv_fwd_psplit_kernel<.., EPI 2>
   return dtype == DG_F16 ? launch_fwd<f16>(a, (hipStream_t)stream) : launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 

@@ -151,6 +151,10 @@ def conv_dgrad(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, acc
 # the epilogue's z loads and reductions are fully exposed: +1.3 ms of dgrad per step against
 # the 0.75 ms partial pass it removes at 768x1024, A/B in DESIGN.md).
 _BNPART_OFF = __import__("os").environ.get("DGVCC_DGRAD_BNPART", "0") != "1"
+# fp32 (split math, conv_fwd_psplit_kernel EPI 2): opt-in as well; measured no faster on the fp32
+# final step (415-417 ms either way, profiles/round2f/dgrad_bnpart_f32_ab.txt): the 8 KB-per-tile z
+# reads and reductions in the persistent kernel's epilogue cost what the partial pass saved
+_BNPART_F32_OFF = __import__("os").environ.get("DGVCC_DGRAD_BNPART_F32", "0") != "1"
 
 
 def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, z: Act, stats,
@@ -159,10 +163,11 @@ def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: A
     sums of the layer whose output gradient dx is (z, stats, act, drop: that layer's);
     returns (part, rows) for bn_bwd_from_part, or None (nothing launched) when the shape is
     not served that way."""
-    if dy.dt != 1 or _BNPART_OFF or stats is None:
+    if stats is None or (dy.dt == 1 and _BNPART_OFF) or (dy.dt == 0 and _BNPART_F32_OFF) or dy.dt == 2:
         return None
     wflip = flip_weight(wp, dy.C, C, R)
-    rows = query("dg_conv_stats_rows", dy.N, dy.H, dy.W)
+    rows = (query("dg_conv_stats_rows_ex", 0, dy.N, dy.H, dy.W, dy.C, dy.ld, C, R, R) if dy.dt == 0
+            else query("dg_conv_stats_rows", dy.N, dy.H, dy.W))
     part = torch.empty((rows, 3, C), dtype=torch.float32, device=dy.buf.device)
     flops = 2.0 * dy.M * dy.C * R * R * C
     nbytes = dy.buf.element_size() * (dy.M * dy.C + wflip.numel() + 2 * dy.M * C)

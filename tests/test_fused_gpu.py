@@ -295,18 +295,20 @@ def test_wgrad9_padded_k(dev, monkeypatch, N, H, W, C, Cout):
     assert relerr(outs[0], outs[1]) < 1e-5
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("N,H,W,C,Cin_next,act,use_drop", [
-    (2, 128, 128, 256, 256, 1, False),   # 256-wide tiles (grids large enough not to split K)
-    (2, 120, 140, 128, 256, 1, True),    # 128-wide tiles, ragged last tile, Dropout2d mask
-    (1, 128, 128, 512, 512, 0, False),   # two channel tiles, no ReLU
+    (4, 128, 256, 256, 256, 1, False),   # 256-wide tiles (grids large enough not to split K / > 256 tiles)
+    (4, 120, 300, 128, 256, 1, True),    # 128-wide tiles, ragged last tile, Dropout2d mask
+    (2, 128, 256, 512, 512, 0, False),   # two channel tiles, no ReLU
 ])
-def test_dgrad_epilogue_bn_partials(dev, monkeypatch, N, H, W, C, Cin_next, act, use_drop):
-    """dg_conv_fwd_bnbwd (BN-backward partial sums in the dgrad epilogue) + dg_bn_bwd_from_part
-    against dg_conv_dgrad + dg_bn_bwd on the same inputs: gx bit-identical, dz/dgamma/dbeta
-    to f32 summation-order rounding."""
+def test_dgrad_epilogue_bn_partials(dev, monkeypatch, dtype, N, H, W, C, Cin_next, act, use_drop):
+    """dg_conv_fwd_bnbwd (BN-backward partial sums in the dgrad epilogue: the bf16 pipe kernel,
+    the fp32 pre-split kernel's EPI 2) + dg_bn_bwd_from_part against dg_conv_dgrad + dg_bn_bwd on
+    the same inputs: gx bit-identical, dz/dgamma/dbeta to f32 summation-order rounding."""
     K = _k()
     monkeypatch.setattr(K, "_BNPART_OFF", False)
-    bf = torch.bfloat16
+    monkeypatch.setattr(K, "_BNPART_F32_OFF", False)
+    bf = dtype
     g = torch.Generator().manual_seed(9)
     dz_next = torch.randn(N, H, W, Cin_next, generator=g).to(dev, bf)
     w = (torch.randn(Cin_next, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(dev)
@@ -330,6 +332,9 @@ def test_dgrad_epilogue_bn_partials(dev, monkeypatch, N, H, W, C, Cin_next, act,
     torch.cuda.synchronize()
     assert torch.equal(gx1.buf, gx0.buf)
     assert relerr(dg1, dg0) < 1e-5 and relerr(db1, db0) < 1e-5
+    if dtype == torch.float32:
+        assert relerr(dz1.buf, dz0.buf) < 1e-5
+        return
     assert relerr(dz1.buf, dz0.buf) < 1e-2  # bf16 storage: rare 1-ulp flips from the coefficients
     assert (dz1.buf.float() - dz0.buf.float()).abs().max() <= 2 * dz0.buf.float().abs().max() * 2 ** -8
 
