@@ -244,13 +244,13 @@ _EPI_STATS_OFF = __import__("os").environ.get("DGVCC_EPI_STATS", "1") == "0"
 
 
 def conv_fwd_stats(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
-                   bias: torch.Tensor | None = None):
+                   bias: torch.Tensor | None = None, k_alg=None):
     """conv_fwd with the BN statistics partials of y from the conv epilogue; returns
     (part, rows), or None (nothing launched) when the shape is served by a kernel without
-    epilogue statistics."""
+    epilogue statistics.  k_alg: algorithmic reduction length when the GEMM K is padded."""
     rows = query("dg_conv_stats_rows_ex", x.dt, x.N, x.H, x.W, x.C, x.ld, Cout, R, R)
     part = torch.empty((rows, 3, Cout), dtype=torch.float32, device=x.buf.device)
-    flops = 2.0 * x.M * x.C * R * R * Cout
+    flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * Cout
     es = x.buf.element_size()
     nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout)
     res = []
