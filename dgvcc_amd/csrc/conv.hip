@@ -3091,7 +3091,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 // 64 x 64 (x 3 taps): 4 waves of 32 x 32, two blocks per CU (the per-tap kernel's 64-wide tiles
 // were bound by the split and LDS-store work, ~30% MFMA-busy); 128 x 128: 8 waves of 64 x 32,
 // one block per CU.
-template <int BCO, int BC, int WCO, int NTH>
+template <int BCO, int BC, int WCO, int NTH, int SWP = 0>
 __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArgs a) {
   constexpr int BKP = 32, XR = BKP + 2;
   constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
@@ -3156,11 +3156,11 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       if (++sp == a.H) { sp = 0; ++sn; }
     }
   };
-  auto swrite = [&](int buf) __attribute__((always_inline)) {
+  auto swrite = [&](int buf, int part = 3) __attribute__((always_inline)) {
     char* As = smem + buf * TILE;
     char* Bs = As + 3 * PA;
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
+    for (int i = 0; i < AR * (part & 1); ++i) {
       const int idx = tid + NTH * i;
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       u2v h0, h1, h2;
@@ -3170,7 +3170,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       *(u2v*)(As + 2 * PA + o) = h2;
     }
 #pragma unroll
-    for (int i = 0; i < BR; ++i) {
+    for (int i = 0; i < BR * ((part >> 1) & 1); ++i) {
       const int idx = tid + NTH * i;
       if (idx < XR * CPRB) {
         const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
@@ -3240,7 +3240,12 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
           for (int j = 0; j < TJ; ++j)
             acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[s][i][j], 0, 0, 0);
       // one block per CU: the next step's split + LDS stores between the taps' MFMA blocks
-      if (NTH == 512 && s == 1 && kt + 1 < nkt) swrite(cur ^ 1);
+      if (NTH == 512 && kt + 1 < nkt) {
+        if (SWP == 0 && s == 1) swrite(cur ^ 1);
+        if (SWP == 1 && s == 0) swrite(cur ^ 1, 1);
+        if (SWP == 1 && s == 1) swrite(cur ^ 1, 2);
+        if (SWP == 2 && s == 0) swrite(cur ^ 1);
+      }
     }
     if (NTH != 512 && kt + 1 < nkt) swrite(cur ^ 1);  // two blocks per CU overlap each other instead
     __syncthreads();
@@ -3906,7 +3911,16 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
         slab_splits = p.splits;
         const dim3 g3((unsigned)(wgs3_tiles(a.C, a.Cout, b3) * p.splits));
         if (b3 == 64) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 256>), g3, dim3(256), 0, st, a);
-        else hipLaunchKernelGGL((conv_wgrad_split3_kernel<128, 128, 2, 512>), g3, dim3(512), 0, st, a);
+        else {
+          // placement of the next step's split + LDS stores among the taps' MFMA blocks: 0 after tap 1,
+          // 1 dY after tap 0 / X after tap 1, 2 (default) all after tap 0: wgrad 0.59 -> 0.60 of the
+          // ceiling (profiles/round2g/wgrad3_swp_ab.txt)
+          const char* e = getenv("DGVCC_WG3_SWP");
+          const int sw = e ? e[0] - '0' : 2;
+          if (sw == 1) hipLaunchKernelGGL((conv_wgrad_split3_kernel<128, 128, 2, 512, 1>), g3, dim3(512), 0, st, a);
+          else if (sw == 2) hipLaunchKernelGGL((conv_wgrad_split3_kernel<128, 128, 2, 512, 2>), g3, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_wgrad_split3_kernel<128, 128, 2, 512>), g3, dim3(512), 0, st, a);
+        }
         done = true;
       }
     }
