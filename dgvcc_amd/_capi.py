@@ -16,6 +16,8 @@ import re
 
 import torch  # noqa: F401  (must precede the dlopen of our HIP library)
 
+from .srchash import source_hash
+
 _PKG = os.path.dirname(os.path.abspath(__file__))
 HEADER = os.path.join(os.path.dirname(_PKG), "include", "dgvcc.h")
 LIB_PATH = os.path.join(_PKG, "lib", "libdgvcc_hip.so")
@@ -73,8 +75,21 @@ def lib():
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args
+        want = source_hash()
+        got = library_hash(l)
+        if want is not None and got != want:
+            raise DGError(f"{LIB_PATH} was built from other sources (library {got}, sources {want}): "
+                          "rebuild with `python -m dgvcc_amd.build`")
         _lib = l
     return _lib
+
+
+def library_hash(l=None) -> str:
+    """The source hash compiled into the library (dg_source_hash)."""
+    l = l if l is not None else lib()
+    buf = ctypes.create_string_buffer(64)
+    n = l.dg_source_hash(buf, 64)
+    return buf.value.decode() if n > 0 else ""
 
 
 def exported_symbols() -> list[str]:

@@ -15,6 +15,12 @@ import shutil
 import subprocess
 import sys
 
+try:
+    from .srchash import source_hash
+except ImportError:  # run as a script
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from dgvcc_amd.srchash import source_hash
+
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
@@ -70,6 +76,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if todo:
         with cf.ThreadPoolExecutor(jobs) as ex:
             list(ex.map(_compile, todo))
+    objs.append(_hash_object(force))
     if todo or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(o) for o in objs):
         tmp = LIB + ".tmp"
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
@@ -78,6 +85,30 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             raise RuntimeError(f"link failed:\n{r.stderr}")
         os.replace(tmp, LIB)
     return LIB
+
+
+def _hash_object(force: bool) -> str:
+    """srchash.o: `dg_source_hash` returning the content hash of the sources compiled above
+    (regenerated whenever the hash changes, so a relink follows any source edit)."""
+    h = source_hash()
+    src = os.path.join(OBJ, "srchash.cpp")
+    obj = os.path.join(OBJ, "srchash.o")
+    code = ('#include <string.h>\n'
+            f'static const char kHash[] = "{h}";\n'
+            'extern "C" int dg_source_hash(char* out, int cap) {\n'
+            '  const int n = (int)sizeof(kHash) - 1;\n'
+            '  if (!out || cap <= n) return -1;\n'
+            '  memcpy(out, kHash, n + 1);\n'
+            '  return n;\n'
+            '}\n')
+    old = open(src).read() if os.path.exists(src) else None
+    if force or old != code or not os.path.exists(obj):
+        with open(src, "w") as f:
+            f.write(code)
+        r = subprocess.run(["g++", "-O2", "-fPIC", "-c", src, "-o", obj], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"srchash compile failed:\n{r.stderr}")
+    return obj
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@
 // K-tile) and consumed by v_mfma_f32_16x16x32_bf16 (perf mode) or the exact
 // f32 v_mfma_f32_16x16x4_f32 (parity mode).  Out-of-image taps are zero-filled
 // by the buffer-load range check (voffset past num_records returns 0).
+#include <mutex>
 #include "dg_common.h"
 #include <algorithm>
 #include <cstdlib>
@@ -1734,18 +1735,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
                              co0, tid, fr, fc);
 }
 
-// wsp[co][kb][part][32] (bf16) = the exact 3-way split of the packed f32 filter w[co][kb*32 + j]
+// wsp[co][kb][part][32] (bf16) = the exact 3-way split (dg_common.h split3_pair, nearest-even
+// parts) of the packed f32 filter w[co][kb*32 + j]; two consecutive elements per thread
 __global__ void split_weight_kernel(const float* __restrict__ w, long long n, unsigned short* __restrict__ wsp) {
-  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n; o += (long long)gridDim.x * blockDim.x) {
-    const unsigned u = __float_as_uint(w[o]);
-    const float r = __uint_as_float(u) - __uint_as_float(u & 0xffff0000u);
-    const unsigned ur = __float_as_uint(r);
-    const float q = r - __uint_as_float(ur & 0xffff0000u);
-    const long long blk = o >> 5, j = o & 31;
-    unsigned short* d = wsp + blk * 96 + j;
-    d[0] = (unsigned short)(u >> 16);
-    d[32] = (unsigned short)(ur >> 16);
-    d[64] = (unsigned short)(__float_as_uint(q) >> 16);
+  const long long n2 = n >> 1;  // n = Cout*R*S*C is a multiple of 32
+  for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n2; o += (long long)gridDim.x * blockDim.x) {
+    const float2 v = *(const float2*)(w + 2 * o);
+    unsigned p0, p1, p2;
+    split3_pair(__float_as_uint(v.x), __float_as_uint(v.y), p0, p1, p2);
+    const long long e = 2 * o, blk = e >> 5, j = e & 31;
+    unsigned* d = (unsigned*)(wsp + blk * 96 + j);
+    d[0] = p0;
+    d[16] = p1;
+    d[32] = p2;
   }
 }
 
@@ -2471,15 +2473,23 @@ static bool rsplit3w_ok(const FwdArgs& a) { return rsplit3_ok(a) && rsplit3_mode
 
 // Per-stream device scratch for the pre-split filter panels (grown on demand; a launch on
 // a stream only ever overlaps its own stream's earlier work, which hipFree waits for).
+// Per-(device, stream) scratch for the pre-split filter planes.  Launches on one stream are
+// ordered, so a layer's split + conv may reuse the previous layer's buffer; torch's default
+// stream reports the same handle (0) on every device, hence the device in the key.  The table
+// is shared by every thread of the process, so it is guarded by a mutex.
 static void* split_scratch(hipStream_t st, size_t bytes) {
-  struct Ent { hipStream_t st; void* p; size_t cap; };
-  static Ent ents[8];
+  struct Ent { int dev; hipStream_t st; void* p; size_t cap; };
+  static Ent ents[32];
   static int n = 0;
+  static std::mutex mu;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
   int k = 0;
-  while (k < n && ents[k].st != st) ++k;
+  while (k < n && !(ents[k].st == st && ents[k].dev == dev)) ++k;
   if (k == n) {
-    if (n == 8) return nullptr;
-    ents[n++] = Ent{st, nullptr, 0};
+    if (n == 32) return nullptr;
+    ents[n++] = Ent{dev, st, nullptr, 0};
   }
   if (ents[k].cap < bytes) {
     if (ents[k].p && hipFree(ents[k].p) != hipSuccess) return nullptr;

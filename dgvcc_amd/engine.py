@@ -958,7 +958,7 @@ class SinglePlan(_Heads):
             else:
                 g_y = self.head_bwd(st.get("ynew", st["yden"]), st["yh"], g_h, grads)
             if self.memr is not None and st.get("v") is None:
-                dt = y.buf.dtype
+                dt = st["ynew"].buf.dtype
                 gP, dmem_a = self.memr.bwd_readout(g_y, st["P"], dt)
                 gL = Act(torch.empty_like(gP.buf))
                 K.call("dg_softmax_bwd", gP.dt, st["P"].ptr, gP.ptr, gP.M, gP.C, gL.ptr, K.stream())

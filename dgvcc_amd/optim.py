@@ -75,8 +75,8 @@ class AdamW(torch.optim.Optimizer):
         group.pop("_live_cache", None)
 
     def _gather(self, group):
-        """Gather live gradients into the flat buffer; returns the [start, end) runs of
-        parameters that have a gradient (torch.optim.AdamW skips params whose .grad
+        """Gather live gradients into the flat buffer; returns the [i0, i1) parameter-index runs
+        of parameters that have a gradient (torch.optim.AdamW skips params whose .grad
         is None: no decay, no moment update — e.g. the ISW counter's unused layer4)."""
         ps = group["params"]
         g = group["_g"]
@@ -110,8 +110,7 @@ class AdamW(torch.optim.Optimizer):
             call("dg_gather_flat", ptr(table), ptr(o), i1 - i0, g.numel(), ptr(g), stream())
             tables.append((host, table))
         group["_table"] = tables  # keep alive until the launches retire
-        offs = group["_offs"]
-        return [(offs[i0], offs[i1 - 1] + ps[i1 - 1].numel()) for i0, i1 in runs]
+        return runs
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -149,23 +148,23 @@ class AdamW(torch.optim.Optimizer):
 
     @staticmethod
     def _step_runs(group, runs):
-        """Advance the step count of every live parameter and split the live runs into
-        maximal sub-runs of equal count: one launch per (run, bias-correction step); a
-        single launch when every parameter has always had a gradient."""
+        """Advance the step count of every live parameter and split the live runs (parameter
+        index ranges [i0, i1)) into maximal sub-runs of equal count: one launch per (element
+        range, bias-correction step); a single launch when every parameter has always had a
+        gradient.  Walking indices, not element offsets, keeps zero-numel parameters (which
+        share their offset with the next parameter) attributed correctly."""
         offs, steps = group["_offs"], group["_steps"]
         out = []
-        for a, b in runs:
-            i = offs.index(a)
-            start = i
-            while i < len(steps) and offs[i] < b:
+        for i0, i1 in runs:
+            for i in range(i0, i1):
                 steps[i] += 1
-                i += 1
-            j = start
-            while j < i:
+            j = i0
+            while j < i1:
                 k = j
-                while k + 1 < i and steps[k + 1] == steps[j]:
+                while k + 1 < i1 and steps[k + 1] == steps[j]:
                     k += 1
-                out.append((offs[j], offs[k + 1], steps[j]))
+                if offs[k + 1] > offs[j]:
+                    out.append((offs[j], offs[k + 1], steps[j]))
                 j = k + 1
         return out
 

@@ -14,7 +14,9 @@
  *   - dtype: DG_F32 (parity mode, exact-f32 MFMA), DG_BF16 (perf mode, bf16
  *     storage + bf16 MFMA, f32 accumulation/statistics) or DG_F16 (fp16 storage +
  *     f16 MFMA, f32 accumulation/statistics; configs/qnrf_final.yml's precision).
- *   - the library is stateless: no globals, safe to call from any thread.
+ *   - the library holds no tensors and is safe to call from any thread; its only
+ *     state is a mutex-guarded per-(device, stream) scratch for the pre-split f32
+ *     filter planes of the split-math convolutions.
  */
 #ifndef DGVCC_H
 #define DGVCC_H
@@ -34,12 +36,17 @@ extern "C" {
 
 /* ---- library ----------------------------------------------------------- */
 int dg_version(void); /* returns DGVCC_ABI_VERSION */
+/* writes the 16-hex-digit content hash of the sources the library was built from
+ * (the csrc .hip/.h files and this header; dgvcc_amd/srchash.py) into out (cap > 16 bytes);
+ * returns its length, or -1.  The Python binding refuses a library whose hash differs
+ * from the sources beside it. */
+int dg_source_hash(char* out, int cap);
 /* test hook: 1/0 force the persistent pipelined conv forward on/off, -1 = DGVCC_PERSIST default */
 int dg_set_persist(int mode);
 /* f32 GEMM arithmetic of the DG_F32 convolutions: 0 = v_mfma_f32_16x16x4_f32;
  * 1 = exact 3-way bf16 split of both operands (x = h0 + h1 + h2), six
- * v_mfma_f32_16x16x32_bf16 products per block, f32 accumulation (f32-grade: dropped
- * terms < 2^-24 relative).  Default from DGVCC_F32_MATH (exact | split), else 1. */
+ * v_mfma_f32_16x16x32_bf16 products per block, f32 accumulation (the truncated parts
+ * drop terms up to ~2^-20 |x*y|, typically ~2^-22, one-sided; see dg_common.h).  Default from DGVCC_F32_MATH (exact | split), else 1. */
 int dg_set_f32_math(int mode);
 int dg_get_f32_math(void);
 #define DGVCC_ABI_VERSION 1

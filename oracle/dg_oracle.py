@@ -184,13 +184,16 @@ def single_forward(sd, x, training, c_gt=None, cls_thrs=0.5):
     return _up(d * c_resized, 4), c
 
 
-def memadd_forward_train(sd, img1, img2, training=True, err_thrs=0.5):
-    """DGModel_memadd.forward_train (models/models.py:159-184) with dropout p = 0."""
+def memadd_forward_train(sd, img1, img2, training=True, err_thrs=0.5, e_mask_in=None):
+    """DGModel_memadd.forward_train (models/models.py:159-184) with dropout p = 0; e_mask_in
+    (bool [B,C,h,w]) replaces the thresholded mask, as in final_forward."""
     y_cat1, _ = forward_fe(sd, img1, training)
     y_cat2, _ = forward_fe(sd, img2, training)
     y_den1 = _conv_bn_relu(y_cat1, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
     y_den2 = _conv_bn_relu(y_cat2, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
     e_mask = (torch.abs(F.instance_norm(y_den1, eps=1e-5) - F.instance_norm(y_den2, eps=1e-5)) < err_thrs).detach()
+    if e_mask_in is not None:
+        e_mask = e_mask_in.bool()
     y_new1, logits1 = forward_mem(sd, y_den1 * e_mask)
     y_new2, logits2 = forward_mem(sd, y_den2 * e_mask)
     loss_con = F.mse_loss(F.softmax(logits1, dim=1), F.softmax(logits2, dim=1))
@@ -208,7 +211,8 @@ def train_step(sd, batch, mode="simple", log_para=1000.0, lr=1e-4, weight_decay=
                c_pred_in=None):
     """One DGTrainer.train_step (trainers/dgtrainer.py:143-192, MSE loss, AdamW step 1).
     Returns (loss, outputs, grads, new_sd).  Final mode takes final_forward's threshold
-    injection (e_mask_in, c_pred_in) so a checked path is compared on its own decisions."""
+    injection (e_mask_in, c_pred_in), add mode the e_mask one, so a checked path is compared on
+    its own decisions."""
     sd = {k: v.clone() for k, v in sd.items()}
     keys = trainable_keys(sd)
     for k in keys:
@@ -225,7 +229,7 @@ def train_step(sd, batch, mode="simple", log_para=1000.0, lr=1e-4, weight_decay=
         loss = F.mse_loss(d1, gt) + F.mse_loss(d2, gt)
         outs = (d1, d2)
     elif mode == "add":  # DGModel_memadd (trainers/dgtrainer.py:166-173)
-        d1, d2, loss_con = memadd_forward_train(sd, imgs1, imgs2)
+        d1, d2, loss_con = memadd_forward_train(sd, imgs1, imgs2, e_mask_in=e_mask_in)
         loss = F.mse_loss(d1, gt) + F.mse_loss(d2, gt) + loss_con
         outs = (d1, d2, loss_con)
     elif mode == "cls":  # DGModel_cls / DGModel_memcls (trainers/dgtrainer.py:175-183)

@@ -20,6 +20,34 @@ def test_library_exports_every_header_symbol():
     assert len(protos) >= 30
 
 
+def test_library_matches_its_sources():
+    """The library carries the content hash of the sources it was built from; the binding
+    refuses one that differs, so no test can run a stale binary."""
+    from dgvcc_amd import _capi, srchash
+    assert _capi.library_hash() == srchash.source_hash()
+    assert len(srchash.source_hash()) == 16
+
+
+def test_adamw_step_runs_zero_numel_params():
+    """_step_runs walks parameter indices: a zero-numel parameter (same element offset as its
+    neighbour) neither steals nor gets the neighbour's step count."""
+    from dgvcc_amd.optim import AdamW
+    sizes = [3, 0, 4, 5, 0]
+    offs = [0]
+    for n in sizes:
+        offs.append(offs[-1] + n)
+    group = {"_offs": offs, "_steps": [0] * len(sizes)}
+    out = AdamW._step_runs(group, [(0, 3)])
+    assert group["_steps"] == [1, 1, 1, 0, 0]
+    assert out == [(0, 7, 1)]
+    out = AdamW._step_runs(group, [(1, 2), (3, 5)])  # the zero-numel param alone, then 3..4
+    assert group["_steps"] == [1, 2, 1, 1, 1]
+    assert out == [(7, 12, 1)]
+    out = AdamW._step_runs(group, [(0, 5)])
+    assert group["_steps"] == [2, 3, 2, 2, 2]
+    assert out == [(0, 3, 2), (3, 12, 2)]
+
+
 def test_invalid_arguments_rejected_without_gpu():
     from dgvcc_amd import _capi
     L = _capi.lib()

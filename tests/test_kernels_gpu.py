@@ -361,6 +361,54 @@ def test_conv_f32_split_math(dev, case):
         assert e1 < 5e-6 and e1 < 2 * e0 + 2e-7, errs
 
 
+@pytest.mark.parametrize("case,which", [((1, 32, 64, 512, 512, 3), "fd"),      # K = 4608 fwd + dgrad
+                                        ((1, 48, 64, 512, 256, 3), "fd"),
+                                        ((1, 768, 1024, 64, 64, 3), "w"),      # 786k-pixel wgrad reduction
+                                        ((4, 192, 256, 128, 128, 3), "w")])
+def test_conv_f32_split_same_sign(dev, case, which):
+    """The truncating 3-way split drops x1*y2 + x2*y1 (+ x2*y2), up to ~2^-20 |x*y| and all with
+    the sign of x*y (dg_common.h): a bias, which randn operands hide because mixed signs cancel.
+    Same-sign operands (post-ReLU activations, positive filters and output gradients) make it add
+    up coherently over the K = 4608 forward/dgrad and the 786k-pixel wgrad reduction.  Bound:
+    within 2x the exact v_mfma_f32_16x16x4_f32 path's own error on the same launch."""
+    K = _k()
+    N, H, W, C, Cout, R = case
+    pad = R // 2
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, C, H, W, generator=g).abs()
+    w = torch.rand(Cout, C, R, R, generator=g) / (C * R * R)
+    gy = torch.rand(N, Cout, H, W, generator=g)
+    xd = K.Act(to_nhwc(x).to(dev))
+    gyd = K.Act(to_nhwc(gy).to(dev))
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    if which == "fd":
+        ref_y = F.conv2d(x.double(), w.double(), padding=pad)
+        ref_dx = torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=pad)
+    else:
+        ref_dw = torch.nn.grad.conv2d_weight(x.double(), w.shape, gy.double(), padding=pad)
+    errs = {}
+    try:
+        for mode in (0, 1):
+            K.call("dg_set_f32_math", mode)
+            if which == "fd":
+                y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+                K.conv_fwd(xd, wp, Cout, R, pad, y)
+                dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+                K.conv_dgrad(gyd, wp, C, R, pad, dx)
+                torch.cuda.synchronize()
+                errs[mode] = (relerr(to_nchw(y.buf), ref_y), relerr(to_nchw(dx.buf), ref_dx))
+            else:
+                dw = torch.empty(Cout, C, R, R, device=dev)
+                K.conv_wgrad(xd, gyd, R, pad, dw)
+                torch.cuda.synchronize()
+                errs[mode] = (relerr(dw, ref_dw),)
+    finally:
+        K.call("dg_set_f32_math", 1)
+    for e0, e1 in zip(errs[0], errs[1]):
+        assert e1 < 2 * e0 + 1e-7, errs
+    print("same-sign split errors (exact, split):", errs)
+
+
 @pytest.mark.parametrize("N,H,W,C,Cout,epi", [(5, 128, 256, 64, 256, "stats"), (3, 96, 320, 128, 128, "stats"),
                                               (3, 128, 256, 256, 512, "eval"), (8, 100, 130, 128, 256, "bias"),
                                               (3, 70, 90, 64, 64, "stats"), (2, 64, 256, 128, 64, "eval"),

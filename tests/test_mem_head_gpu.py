@@ -143,13 +143,14 @@ def test_softmax_head_eval_without_probabilities(dev):
     assert _rel(ya, ref) < 1e-6
 
 
-@pytest.mark.parametrize("name", ["DGModel_final", "DGModel_memadd"])
-def test_fused_head_step_matches_materialised_readout(dev, name):
+@pytest.mark.parametrize("name,mode", [("DGModel_final", "final"), ("DGModel_memadd", "add"),
+                                       ("DGModel_mem", "base"), ("DGModel_memcls", "cls")])
+def test_fused_head_step_matches_materialised_readout(dev, name, mode):
     from oracle import dg_oracle as O
     from dgvcc_amd import engine as E
     from dgvcc_amd.models import models as MM
     kw = dict(pretrained=False, den_dropout=0.0)
-    if name == "DGModel_final":
+    if "cls" in name or name == "DGModel_final":
         kw["cls_dropout"] = 0.0
     runs = []
     for fused in (True, False):
@@ -160,7 +161,6 @@ def test_fused_head_step_matches_materialised_readout(dev, name):
             model.load_state_dict(sd0)
             model = model.to(dev).set_precision("fp32").train()
             batch = O.synthetic_batch(2, 64, 64, seed=77)
-            mode = "final" if name == "DGModel_final" else "add"
             from dgvcc_amd.trainers.dgtrainer import DGTrainer
             from dgvcc_amd.losses import MSELoss
             with tempfile.TemporaryDirectory() as td:

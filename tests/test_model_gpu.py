@@ -50,21 +50,6 @@ def _f64(sd, batch):
 GRAD_TOL = 5e-3
 
 
-def grad_sensitivity(sd0, batch, mode, eps=3e-5, **inject):
-    """How far the float64 gradients move when the input frames move by eps (relative,
-    seeded noise) -- the conditioning of this gradient w.r.t. forward perturbations of the
-    size an fp32 forward accumulates (1e-5..3e-5 relative by the decoder's last layers,
-    measured per op in tools/diag_models2.py).  Per parameter, normwise."""
-    sd64, b64 = _f64(sd0, batch)
-    _, _, g0, _ = O.train_step(sd64, b64, mode, **inject)
-    i1, i2, rest = b64
-    g = torch.Generator().manual_seed(77)
-    n1 = torch.randn(i1.shape, generator=g, dtype=torch.float64)
-    n2 = torch.randn(i2.shape, generator=g, dtype=torch.float64)
-    _, _, g1, _ = O.train_step(sd64, (i1 * (1 + eps * n1), i2 * (1 + eps * n2), rest), mode, **inject)
-    return {k: ((g1[k] - g0[k]).norm() / g0[k].norm().clamp_min(1e-300)).item() for k in g0}, g0
-
-
 def _check_grads(model, sd0, batch, mode, grads_ref32, tol=GRAD_TOL):
     """Gradients against the float64 oracle, normwise per parameter.
 
@@ -191,24 +176,138 @@ def test_final_step_fp32(dev, B, H, W):
     assert rel(dc1, outs[0]) < 1e-4 and rel(dc2, outs[1]) < 1e-4
     assert rel(c1, outs[2]) < 1e-4 and rel(c2, outs[3]) < 1e-4
     assert abs(loss_con.item() - outs[4].item()) <= 1e-4 * abs(outs[4].item())
-    plan = model._get_plans()["pair"]
-    plan.capture = {}
-    try:
-        loss = _run_step(model, "final", batch, dev)
-        cap = plan.capture
-    finally:
-        plan.capture = None
+    loss = _run_step(model, "final", batch, dev)
     assert abs(loss - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
-    # gradients on the HIP step's own threshold decisions (e_mask, class maps):
-    # the float64 oracle re-run with them injected, per parameter within max(2 x the fp32
-    # oracle's error, 3 x the measured sensitivity, 5e-3), as the ablation modes
-    inject = dict(e_mask_in=cap["emask"].permute(0, 3, 1, 2).bool().cpu(),
-                  c_pred_in=tuple(c.cpu() for c in cap["c_pred"]))
-    sens, g64 = grad_sensitivity(sd0, batch, "final", **inject)
-    mine = _grads_normrel(model, g64)
-    _, _, g32, _ = O.train_step(sd0, batch, "final", **inject)
-    ref32 = {k: ((g32[k].double() - g64[k]).norm() / g64[k].norm()).item() for k in mine}
-    bad = {k: (v, ref32[k], sens[k]) for k, v in mine.items() if v > max(2 * ref32[k], 3 * sens[k], GRAD_TOL)}
+    sd = model.state_dict()
+    for k in sd1:
+        if "running" in k:
+            assert rel(sd[k], sd1[k]) < 1e-4, k
+
+
+# End-to-end at 256x256, no sensitivity term: every parameter within E2E_GRAD_TOL, and the
+# whole gradient (all parameters concatenated) within 2x the fp32 CPU oracle's own error on the
+# same decisions.  Measured (round 3): the fp32 oracle itself is 1e-3..7.3e-3 off float64 per
+# parameter at this size (forward rounding through ReLU / max-pool near-ties and batch BN of a
+# random-init VGG16), the HIP step 5e-3..8.8e-3; the backward itself is pinned at 1e-4 given the
+# forward (test_final_step_backward_exact_given_forward: measured 1.3e-5).
+E2E_GRAD_TOL = 1e-2
+
+
+def _e2e_grads(name, mode, B, H, W, dev, **kw):
+    """One HIP train step at B x 3 x H x W, its threshold decisions (e_mask, class maps)
+    captured and injected into the float64 and fp32 oracles; returns the HIP gradients, the
+    float64 ones and the fp32 oracle's ({name: tensor} each)."""
+    model = _model(name, **kw)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    model = model.to(dev).set_precision("fp32").train()
+    batch = O.synthetic_batch(B, H, W, seed=2112)
+    plan = model._get_plans().get("pair")
+    if plan is not None:
+        plan.capture = {}
+    try:
+        _run_step(model, mode, batch, dev)
+        cap = plan.capture if plan is not None else {}
+    finally:
+        if plan is not None:
+            plan.capture = None
+    inject = {}
+    if "emask" in cap:
+        inject["e_mask_in"] = cap["emask"].permute(0, 3, 1, 2).bool().cpu()
+    if "c_pred" in cap:
+        inject["c_pred_in"] = tuple(c.cpu() for c in cap["c_pred"])
+    _, _, g64, _ = O.train_step(*_f64(sd0, batch), mode, **inject)
+    _, _, g32, _ = O.train_step(sd0, batch, mode, **inject)
+    mine = {k: (p.grad if p.grad is not None else torch.zeros_like(p)).detach().double().cpu()
+            for k, p in model.named_parameters()}
+    return mine, g64, g32
+
+
+@pytest.mark.parametrize("name,mode", [("DGModel_final", "final"), ("DGModel_memadd", "add"),
+                                       ("DGModel_base", "base"), ("DGModel_mem", "base"),
+                                       ("DGModel_cls", "cls"), ("DGModel_memcls", "cls")])
+def test_step_grads_e2e_256(dev, name, mode):
+    """End-to-end gradient parity of the train step (trainers/dgtrainer.py:143-192) at
+    2 x 3 x 256 x 256 against the float64 oracle, with the step's own e_mask / class-map
+    decisions injected and fixed bounds (E2E_GRAD_TOL above; no sensitivity term)."""
+    kw = {"den_dropout": 0.0}
+    if "cls" in name or name == "DGModel_final":
+        kw["cls_dropout"] = 0.0
+    mine, g64, g32 = _e2e_grads(name, mode, 2, 256, 256, dev, **kw)
+    keys = [k for k in g64 if not _skip_bias(k) and g64[k].norm() > 0]
+    err = {k: ((mine[k] - g64[k]).norm() / g64[k].norm()).item() for k in keys}
+    e32 = {k: ((g32[k].double() - g64[k]).norm() / g64[k].norm()).item() for k in keys}
+    cat = lambda d: torch.cat([d[k].double().reshape(-1) for k in keys])  # noqa: E731
+    ref = cat(g64)
+    glob = ((cat(mine) - ref).norm() / ref.norm()).item()
+    glob32 = ((cat(g32) - ref).norm() / ref.norm()).item()
+    worst = max(err.items(), key=lambda kv: kv[1])
+    print(name, mode, f"e2e 256: worst {worst}, fp32 oracle worst {max(e32.values()):.3e}, "
+                      f"global {glob:.3e} (fp32 oracle {glob32:.3e})")
+    bad = {k: (v, e32[k]) for k, v in err.items() if v > E2E_GRAD_TOL}
+    assert not bad, bad
+    assert glob <= max(2 * glob32, 2e-3), (glob, glob32)
+
+
+def _skip_bias(k):
+    # conv biases followed by BN: mathematically zero gradient (rounding noise in any implementation)
+    return k.endswith(".bias") and (k.startswith("enc") or ".conv." in k) and "cls_head.2" not in k
+
+
+@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (2, 128, 160)])
+def test_final_step_backward_exact_given_forward(dev, B, H, W):
+    """The whole DGModel_final train-step backward (encoder, decoder, den_dec, memory read,
+    JSD-MSE, density and class heads, both views; trainers/dgtrainer.py:184-192 on
+    models/models.py:298-335) against float64 VJPs evaluated at the HIP plans' own saved fp32
+    activations, with every ReLU, max-pool argmax, e_mask and class decision the HIP forward's
+    (tests/exact_vjp.py).  No forward rounding can move this comparison: every parameter
+    gradient within 1e-4 normwise, and the plans' input gradients too."""
+    import exact_vjp as X
+    model = _model("DGModel_final", den_dropout=0.0, cls_dropout=0.0)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    model = model.to(dev).set_precision("fp32").train()
+    i1, i2, (_pts, dm, bm) = O.synthetic_batch(B, H, W, seed=2112)
+    plans = model._get_plans()
+    fe, pair = plans["fe"], plans["pair"]
+    tA, tB, tP = {}, {}, {}
+    with torch.no_grad():
+        outA = fe.forward(i1.to(dev), torch.float32, True, tA)
+        outB = fe.forward(i2.to(dev), torch.float32, True, tB)
+        outs = pair.forward(outA[:3], outB[:3], outA[3], outB[3], bm.to(dev), 0.0, float(model.err_thrs), tP)
+    torch.cuda.synchronize()
+    hip_outs = (outs[0], outs[1], outs[2], outs[3], outs[5])
+    g64 = X.final_loss_grads(hip_outs, dm, bm)
+    # the float64 graph at the taped point (built before the HIP backward consumes the tapes)
+    P = X.Params64(model)
+    with torch.enable_grad():
+        pA = X.feature_ref(fe, tA, i1.double(), P, outA)
+        pB = X.feature_ref(fe, tB, i2.double(), P, outB)
+        ref = X.pair_ref(pair, tP, pA[:3], pB[:3], pA[3], pB[3], P)
+        for a, r in zip(hip_outs, ref):  # the last layers recomputed in float64 from HIP's inputs
+            assert rel(a.reshape(r.shape), r) < 1e-5
+        torch.autograd.backward(ref, g64)
+    g32 = [g.float().to(dev) for g in g64]
+    with torch.no_grad():
+        gin, gp = pair.backward(tP, g32[0], g32[1], g32[2], g32[3], None, g32[4])
+        _, ga = fe.backward(tA, *gin[0:3], gin[6])
+        _, gb = fe.backward(tB, *gin[3:6], gin[7])
+    torch.cuda.synchronize()
+    names = {p: n for n, p in model.named_parameters()}
+    mine = {}
+    for d in (gp, ga, gb):
+        for p, g in d.items():
+            n = names[p]
+            mine[n] = mine[n] + g.double().cpu() if n in mine else g.double().cpu()
+    ref_g = P.grads()
+    worst = {}
+    for n, r in ref_g.items():
+        if _skip_bias(n) or r.norm() == 0:
+            continue
+        assert n in mine, n
+        worst[n] = ((mine[n].reshape(r.shape) - r).norm() / r.norm()).item()
+    bad = {k: v for k, v in worst.items() if v > 1e-4}
+    print("exact-given-forward worst:", max(worst.items(), key=lambda kv: kv[1]))
     assert not bad, bad
 
 
@@ -341,11 +440,8 @@ def test_ablation_mode_steps_fp32(dev, cls_name, mode):
     """DGTrainer modes base / add / cls of the ablation configs (trainers/dgtrainer.py:157-183,
     configs/ablation/*): the HIP step's loss and outputs against the oracle (pinned to the
     reference's own step by tests/golden/train_{base_base,mem_base,memadd_add,cls_cls,
-    memcls_cls}.npz) at 1e-4; gradients against the float64 oracle, per parameter within
-    max(2 x the fp32 oracle's error, 3 x the measured gradient sensitivity, 5e-3), the
-    sensitivity being how far the float64 gradient itself moves under a 3e-5 relative
-    perturbation of the frames (grad_sensitivity): the memory read's 1024-way softmax and
-    the thresholds make some of these gradients move by percents under fp32-sized changes."""
+    memcls_cls}.npz) at 1e-4, and the BN running statistics.  The gradients of these modes are
+    checked end to end at 256x256 (test_step_grads_e2e_256) with a fixed bound."""
     kw = {"den_dropout": 0.0}
     if "cls" in cls_name:
         kw["cls_dropout"] = 0.0
@@ -373,15 +469,6 @@ def test_ablation_mode_steps_fp32(dev, cls_name, mode):
             assert rel(a, b) < 1e-4
     loss = _run_step(model, mode, batch, dev)
     assert abs(loss - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
-    sens, g64 = grad_sensitivity(sd0, batch, mode)
-    mine = _grads_normrel(model, g64)
-    ref32 = {k: ((grads_ref[k].double() - g64[k]).norm() / g64[k].norm()).item() for k in mine}
-    # memadd: one e_mask decision flipped by fp32 rounding at this 16x16 den_dec size moves a
-    # BN-parameter gradient summed over 512 pixels by ~1/sqrt(512) (as final mode, whose test
-    # uses the same floor); the math itself is pinned at 1e-5 by test_head_plans_exact_given_features
-    floor = 0.15 if mode == "add" else GRAD_TOL
-    bad = {k: (v, ref32[k], sens[k]) for k, v in mine.items() if v > max(2 * ref32[k], 3 * sens[k], floor)}
-    assert not bad, bad
     sd = model.state_dict()
     for k in sd1:
         if "running" in k:

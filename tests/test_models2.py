@@ -210,3 +210,71 @@ def test_generator_chain_backward_exact_given_forward(dev):
             g = x.grad if not layer.first else None
     worst = max(((grads[p].double() - v).norm() / v.norm().clamp_min(1e-30)).item() for p, v in ref.items())
     assert worst < 1e-4, worst
+
+
+@pytest.mark.gpu
+def test_dgnet_bf16_close(dev):
+    """configs/stb_reg_base.yml: DensityRegressorBase ('dgnet', models/models2.py:375-432) in the
+    bf16 perf precision against the reference's own float64 output (models2_DensityRegressorBase.npz,
+    2x3x64x64, train-mode BN).  Bounds as test_base_bf16_close: a random-init VGG16-BN with batch-2
+    train-mode BN at 64x64 (2x2 maps in stage3) amplifies bf16 rounding, so the count within 8%
+    and the map within 0.2 of its peak; the same frames through the fp32 HIP path are at 1e-4."""
+    d = np.load(os.path.join(G, "models2_DensityRegressorBase.npz"))
+    ref = torch.from_numpy(d["forward__out0"]).double()
+    model = _ctor("DensityRegressorBase")
+    model.load_state_dict(O.seeded_state_dict(model.state_dict()))
+    for mod in model.modules():
+        if isinstance(mod, torch.nn.Dropout2d):
+            mod.p = 0.0
+    model = model.to(dev).set_precision("bf16").train()
+    img1 = O.synthetic_batch(2, 64, 64, seed=2112)[0]
+    with torch.no_grad():
+        out = model(img1.to(dev)).double().cpu()
+    assert out.shape == ref.shape
+    assert torch.isfinite(out).all()
+    c, cr = out.sum().item(), ref.sum().item()
+    assert abs(c - cr) <= 8e-2 * abs(cr), (c, cr)
+    assert ((out - ref).abs().max() / ref.abs().max()).item() < 0.2
+
+
+@pytest.mark.gpu
+def test_dgnet_bf16_train_step_768x1024(dev):
+    """configs/stb_reg_base.yml at the metric's 768x1024 (DensityRegressorBase, DGTrainer 'simple'
+    mode, fused AdamW, batch 2) in bf16: loss finite and within 2% of the fp32 HIP path's on the
+    same weights and frames, density count within 2%, the update applied to every parameter with
+    a gradient and every parameter finite afterwards."""
+    import tempfile
+    from dgvcc_amd.losses import MSELoss
+    from dgvcc_amd.models import models2 as M2
+    from dgvcc_amd.optim import AdamW
+    from dgvcc_amd.trainers.dgtrainer import DGTrainer
+    sd0 = O.seeded_state_dict(M2.DensityRegressorBase(pretrained=False).state_dict())
+    batch = O.synthetic_batch(2, 768, 1024, seed=5)
+    res = {}
+    for prec in ("fp32", "bf16"):
+        m = M2.DensityRegressorBase(pretrained=False)
+        m.load_state_dict(sd0)
+        m.den_dropout = 0.0
+        m = m.to(dev).set_precision(prec).train()
+        with torch.no_grad():
+            cnt = m(batch[0].to(dev)).sum().item()
+        m.load_state_dict(sd0)  # the no-grad forward updated the running statistics
+        before = [p.detach().clone() for p in m.parameters()]
+        opt = AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4)
+        with tempfile.TemporaryDirectory() as td:
+            cwd = os.getcwd()
+            os.chdir(td)
+            try:
+                tr = DGTrainer(2112, "t", dev, 1000, 10000, "simple")
+                loss = tr.train_step(m, MSELoss(), opt, batch, 0)
+            finally:
+                os.chdir(cwd)
+        torch.cuda.synchronize()
+        moved = [not torch.equal(p.detach(), b) for p, b in zip(m.parameters(), before)]
+        res[prec] = (cnt, loss, moved, all(bool(torch.isfinite(p).all()) for p in m.parameters()))
+    (c32, l32, _, _), (c16, l16, moved, finite) = res["fp32"], res["bf16"]
+    assert np.isfinite(l16) and finite
+    assert abs(c16 - c32) <= 2e-2 * abs(c32), (c16, c32)
+    assert abs(l16 - l32) <= 2e-2 * abs(l32), (l16, l32)
+    assert all(moved), [n for (n, _), mv in zip(M2.DensityRegressorBase(pretrained=False).named_parameters(), moved)
+                        if not mv]
