@@ -71,7 +71,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="frames (samples) per GPU")
+    ap.add_argument("--batch", type=int, default=16, help="frames (samples) per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: this many samples per step over all ranks (per-rank batch = G / N)")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="nn.SyncBatchNorm.convert_sync_batchnorm: BN statistics over all ranks' samples")
     ap.add_argument("--mode", default="final", choices=["simple", "base", "final"])
     ap.add_argument("--model", default=None,
                     help="model class (default: DGModel_final for final mode, DGModel_base otherwise; "
@@ -266,6 +270,8 @@ def run_leg(args, precision, dev, world, rank):
     B, H, W = args.batch, args.height, args.width
     torch.manual_seed(2112)
     model, mode = build_model(args, precision, dev)
+    if args.sync_bn:  # BN over the global batch (syncbn.py; a no-op for a single rank)
+        model = torch.nn.SyncBatchNorm.convert_sync_batchnorm(model)
     if world > 1:  # identical init on every rank
         import torch.distributed as dist
         for t in model.state_dict().values():
@@ -539,6 +545,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.global_batch is not None:  # strong scaling: the global batch is fixed, split over the ranks
+        if args.global_batch % world:
+            raise SystemExit(f"bench.py: --global-batch {args.global_batch} does not split over {world} ranks")
+        args.batch = args.global_batch // world
     # DGVCC_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing one
     # GPU (local rank modulo the visible devices); the driver's runs use RCCL ("nccl").
     backend = os.environ.get("DGVCC_BENCH_BACKEND", "nccl")
@@ -575,7 +585,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(r["elapsed"] / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch is not None else "weak",
         "vs_baseline": None,
         "dtype": prec,
         "data": f"synthetic 3x{args.height}x{args.width} frames (view 2 = view 1 + 0.1 N(0,1)) + Poisson(500) "
@@ -583,6 +593,7 @@ def main():
         "config": {"workload": workload, "global_batch": args.batch * world,
                    "frames_per_gpu_step": r["frames"] // (world * args.steps),
                    "resolution": f"{args.height}x{args.width}", "parallelism": f"dp{world}",
+                   "batch_per_gpu": args.batch, "sync_bn": bool(args.sync_bn),
                    "rccl_world_size": dist_world, "backend": backend if world > 1 else None,
                    "last_loss": r["last_loss"]},
         "roofline": roofline(args, leg, r),

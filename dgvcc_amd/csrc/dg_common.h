@@ -173,12 +173,29 @@ __device__ __forceinline__ unsigned split_level2(float a, float b, float& ra, fl
   rb = b - __uint_as_float(p & 0xffff0000u);
   return p;
 }
+// DGVCC_SPLIT_RNE 0 selects the truncating split of round 2 (kept for same-box A/Bs; see above)
+#ifndef DGVCC_SPLIT_RNE
+#define DGVCC_SPLIT_RNE 1
+#endif
+#if !DGVCC_SPLIT_RNE
+__device__ __forceinline__ void split3_pair(unsigned a, unsigned b, unsigned& p0, unsigned& p1, unsigned& p2) {
+  p0 = __builtin_amdgcn_perm(b, a, 0x07060302u);
+  const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
+  const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
+  const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
+  p1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+  const float sa = ra - __uint_as_float(ua & 0xffff0000u);
+  const float sb = rb - __uint_as_float(ub & 0xffff0000u);
+  p2 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+}
+#else
 __device__ __forceinline__ void split3_pair(unsigned a, unsigned b, unsigned& p0, unsigned& p1, unsigned& p2) {
   float ra, rb, sa, sb;
   p0 = split_level2(__uint_as_float(a), __uint_as_float(b), ra, rb);
   p1 = split_level2(ra, rb, sa, sb);
   p2 = cvt_pk_bf16(sa, sb);  // exact
 }
+#endif
 // 8 f32 (x0[0..3], x1[0..3]) -> bf16 parts h0/h1/h2, element k of each part = float k
 __device__ __forceinline__ void split3_8(const u4v& x0, const u4v& x1, s8v& h0, s8v& h1, s8v& h2) {
   u4v p0, p1, p2;

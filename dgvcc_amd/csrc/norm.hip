@@ -70,7 +70,9 @@ __global__ __launch_bounds__(NT) void bn_stats_partial(const T* __restrict__ z, 
 
 // 16 channels per block, 16 lanes per channel striding over the block partials
 // (independent loads, 4 in flight per lane), then an LDS combine in double.
-template <typename T>
+// ROW = true: write this batch's (n, mean, M2) row [3][C] to save_mean instead (a SyncBatchNorm
+// rank's local statistics, merged across ranks by dg_bn_part_finalize).
+template <typename T, bool ROW = false>
 __global__ __launch_bounds__(NT) void bn_stats_finalize(const T* __restrict__ z, const float* __restrict__ part,
                                                         int nblk, int M, int C, const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float* running_mean,
@@ -106,6 +108,12 @@ __global__ __launch_bounds__(NT) void bn_stats_finalize(const T* __restrict__ z,
   double var = b / M - ms * ms;
   if (var < 0) var = 0;
   const double mean = K + ms;
+  if constexpr (ROW) {
+    save_mean[c] = (float)M;
+    save_mean[C + c] = (float)mean;
+    save_mean[2 * C + c] = (float)(var * M);
+    return;
+  }
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   save_mean[c] = (float)mean;
   save_invstd[c] = invstd;
@@ -277,6 +285,46 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ 
   if (dgamma) dgamma[c] = (float)b;
   if (dbeta) dbeta[c] = (float)a;
   if (dbias) dbias[c] = (float)(-(double)k2 * d);
+  coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
+}
+
+// Column sums of part[nblk][3][C] in double -> out[3][C] (a rank's BN-backward sums, fixed order).
+__global__ __launch_bounds__(NT) void bn_sum_rows3(const float* __restrict__ part, int nblk, int C,
+                                                   float* __restrict__ out) {
+  __shared__ double sh[3][16][17];
+  const int cl = threadIdx.x & 15, r = threadIdx.x >> 4;
+  const int c = blockIdx.x * 16 + cl;
+  double a = 0.0, b = 0.0, d = 0.0;
+  if (c < C)
+    for (int k = r; k < nblk; k += 16) {
+      const float* o = part + (long long)k * 3 * C;
+      a += o[c]; b += o[C + c]; d += o[2 * C + c];
+    }
+  sh[0][r][cl] = a; sh[1][r][cl] = b; sh[2][r][cl] = d;
+  __syncthreads();
+  if (r != 0 || c >= C) return;
+  a = 0.0; b = 0.0; d = 0.0;
+  for (int q = 0; q < 16; ++q) { a += sh[0][q][cl]; b += sh[1][q][cl]; d += sh[2][q][cl]; }
+  out[c] = (float)a; out[C + c] = (float)b; out[2 * C + c] = (float)d;
+}
+
+// SyncBatchNorm backward finalize (torch.nn.SyncBatchNorm semantics): the dz coefficients from the
+// sums over all ranks (sg = sum g', sgx = sum g' xhat over Mg pixels), dgamma / dbeta from this
+// rank's sums (data parallel then averages them with the other parameter gradients), and the conv
+// bias gradient as this rank's sum of dz: k1 sg_l - k2 sx_l - Ml k3.
+__global__ __launch_bounds__(NT) void bn_bwd_finalize_sync(const float* __restrict__ loc, const float* __restrict__ glob,
+                                                           int Ml, double Mg, int C, const float* gamma,
+                                                           const float* invstd, float* dgamma, float* dbeta,
+                                                           float* dbias, float* coef) {
+  const int c = blockIdx.x * NT + threadIdx.x;
+  if (c >= C) return;
+  const float gm = gamma ? gamma[c] : 1.f;
+  const float k1 = gm * invstd[c];
+  const float k2 = (float)(k1 * (double)glob[C + c] / Mg);
+  const float k3 = (float)(k1 * (double)glob[c] / Mg);
+  if (dgamma) dgamma[c] = loc[C + c];
+  if (dbeta) dbeta[c] = loc[c];
+  if (dbias) dbias[c] = (float)((double)k1 * loc[c] - (double)k2 * loc[2 * C + c] - (double)Ml * k3);
   coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
 }
 
@@ -765,4 +813,164 @@ extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const voi
              : dtype == DG_F16 ? bn_pool_bwd_impl<f16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
                                       shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st) : bn_pool_bwd_impl<float>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
                                        shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st);
+}
+
+// ---------------------------------------------------------------------------
+// SyncBatchNorm phases (nn.SyncBatchNorm over data-parallel ranks; models/ISW/mynn.py:8-14):
+// the host all-gathers / all-reduces the per-rank rows between them (dgvcc_amd/syncbn.py).
+// ---------------------------------------------------------------------------
+extern "C" int dg_bn_stats_row(int dtype, const void* z, int64_t ldz, int M, int C, float* row, void* workspace,
+                               void* stream) {
+  DG_REQUIRE(z && row && workspace && M > 0 && C > 0 && ldz >= C);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz));
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = bn_nblk(M);
+  const int ppb = dg_cdiv(M, nblk);
+  float* part = (float*)workspace;
+  if (dtype == DG_BF16) {
+    hipLaunchKernelGGL(bn_stats_partial<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, ppb, part);
+    hipLaunchKernelGGL((bn_stats_finalize<bf16, true>), dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, (const bf16*)z,
+                       (const float*)part, nblk, M, C, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, row, nullptr,
+                       nullptr, nullptr);
+  } else if (dtype == DG_F16) {
+    hipLaunchKernelGGL(bn_stats_partial<f16>, dim3(nblk), dim3(NT), 0, st, (const f16*)z, ldz, M, C, ppb, part);
+    hipLaunchKernelGGL((bn_stats_finalize<f16, true>), dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, (const f16*)z,
+                       (const float*)part, nblk, M, C, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, row, nullptr,
+                       nullptr, nullptr);
+  } else {
+    hipLaunchKernelGGL(bn_stats_partial<float>, dim3(nblk), dim3(NT), 0, st, (const float*)z, ldz, M, C, ppb, part);
+    hipLaunchKernelGGL((bn_stats_finalize<float, true>), dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, (const float*)z,
+                       (const float*)part, nblk, M, C, nullptr, nullptr, nullptr, nullptr, 0.f, 0.f, row, nullptr,
+                       nullptr, nullptr);
+  }
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_part_sums(const float* part, int nblk, int C, float* sums, void* stream) {
+  DG_REQUIRE(part && sums && nblk > 0 && C > 0);
+  hipLaunchKernelGGL(bn_sum_rows3, dim3(dg_cdiv(C, 16)), dim3(NT), 0, (hipStream_t)stream, part, nblk, C, sums);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_bwd_sums(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                              const float* save_mean, const float* save_invstd, const float* scale,
+                              const float* shift, int act, const float* drop, int HW, float* sums, void* workspace,
+                              void* stream) {
+  DG_REQUIRE(g && z && sums && workspace && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
+  DG_REQUIRE(!drop || HW > 0);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz));
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = bn_nblk(M);
+  const int ppb = dg_cdiv(M, nblk);
+  float* part = (float*)workspace;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_bwd_partial<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z, ldz, M,
+                       C, ppb, save_mean, save_invstd, scale, shift, act, drop, HW, part);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_bwd_partial<f16>, dim3(nblk), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z, ldz, M,
+                       C, ppb, save_mean, save_invstd, scale, shift, act, drop, HW, part);
+  else
+    hipLaunchKernelGGL(bn_bwd_partial<float>, dim3(nblk), dim3(NT), 0, st, (const float*)g, ldg, (const float*)z,
+                       ldz, M, C, ppb, save_mean, save_invstd, scale, shift, act, drop, HW, part);
+  DG_CHECK_LAUNCH();
+  return dg_bn_part_sums(part, nblk, C, sums, stream);
+}
+
+extern "C" int dg_bn_bwd_pool_sums(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
+                                   const void* z, int64_t ldz, int N, int H, int W, int C, const float* save_mean,
+                                   const float* save_invstd, const float* scale, const float* shift, int act,
+                                   const float* drop, float* sums, void* workspace, void* stream) {
+  DG_REQUIRE(gp && z && sums && workspace && save_mean && save_invstd && scale && shift);
+  DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldgp) &&
+               BN_SHAPE_OK(dtype, C, ldz) && (!gd || BN_SHAPE_OK(dtype, C, ldgd)) && C % POOL_V == 0 &&
+               NT % (C / POOL_V) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long Mp = (long long)N * (H / 2) * (W / 2);
+  const int nblk = pool_nblk(Mp);
+  const long long ppb = (Mp + nblk - 1) / nblk;
+  float* part = (float*)workspace;
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_pool_bwd_partial<bf16>, dim3(nblk), dim3(NT), 0, st, (const bf16*)gp, ldgp, (const bf16*)gd,
+                       ldgd, (const bf16*)z, ldz, H, W, Mp, C, ppb, save_mean, save_invstd, scale, shift, act, drop,
+                       H * W, part);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_pool_bwd_partial<f16>, dim3(nblk), dim3(NT), 0, st, (const f16*)gp, ldgp, (const f16*)gd,
+                       ldgd, (const f16*)z, ldz, H, W, Mp, C, ppb, save_mean, save_invstd, scale, shift, act, drop,
+                       H * W, part);
+  else
+    hipLaunchKernelGGL(bn_pool_bwd_partial<float>, dim3(nblk), dim3(NT), 0, st, (const float*)gp, ldgp,
+                       (const float*)gd, ldgd, (const float*)z, ldz, H, W, Mp, C, ppb, save_mean, save_invstd, scale,
+                       shift, act, drop, H * W, part);
+  DG_CHECK_LAUNCH();
+  return dg_bn_part_sums(part, nblk, C, sums, stream);
+}
+
+extern "C" int dg_bn_bwd_finalize_sync(const float* sums_local, const float* sums_global, int M_local,
+                                       int64_t M_global, int C, const float* gamma, const float* save_invstd,
+                                       float* dgamma, float* dbeta, float* dbias, float* coef, void* stream) {
+  DG_REQUIRE(sums_local && sums_global && save_invstd && coef && M_local > 0 && M_global >= M_local && C > 0);
+  hipLaunchKernelGGL(bn_bwd_finalize_sync, dim3(dg_cdiv(C, NT)), dim3(NT), 0, (hipStream_t)stream, sums_local,
+                     sums_global, M_local, (double)M_global, C, gamma, save_invstd, dgamma, dbeta, dbias, coef);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                                    const float* save_mean, const float* save_invstd, const float* scale,
+                                    const float* shift, int act, const float* drop, int HW, const float* coef,
+                                    void* dz, int64_t lddz, void* stream) {
+  DG_REQUIRE(g && z && dz && coef && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
+  DG_REQUIRE(!drop || HW > 0);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+                       (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
+                       (float*)dz, lddz);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+extern "C" int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
+                                         const void* z, int64_t ldz, int N, int H, int W, int C,
+                                         const float* save_mean, const float* save_invstd, const float* scale,
+                                         const float* shift, int act, const float* drop, const float* coef, void* dz,
+                                         int64_t lddz, void* stream) {
+  DG_REQUIRE(gp && z && dz && coef && save_mean && save_invstd && scale && shift);
+  DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldgp) &&
+               BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz) && (!gd || BN_SHAPE_OK(dtype, C, ldgd)) &&
+               C % POOL_V == 0 && NT % (C / POOL_V) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long Mp = (long long)N * (H / 2) * (W / 2);
+  const long long total = Mp * (C / POOL_V);
+  if (dtype == DG_BF16)
+    hipLaunchKernelGGL(bn_pool_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)gp, ldgp,
+                       (const bf16*)gd, ldgd, (const bf16*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift,
+                       act, drop, H * W, coef, (bf16*)dz, lddz);
+  else if (dtype == DG_F16)
+    hipLaunchKernelGGL(bn_pool_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)gp, ldgp,
+                       (const f16*)gd, ldgd, (const f16*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift,
+                       act, drop, H * W, coef, (f16*)dz, lddz);
+  else
+    hipLaunchKernelGGL(bn_pool_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)gp, ldgp,
+                       (const float*)gd, ldgd, (const float*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale,
+                       shift, act, drop, H * W, coef, (float*)dz, lddz);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
 }

@@ -492,7 +492,9 @@ __global__ __launch_bounds__(SNT) void stem_wgrad_reduce(const float* __restrict
 }
 
 // Merge per-block (n, mean, M2) rows [nblk][3][C] into the BN batch statistics
-// (Chan et al.; double), then the same outputs as bn_stats_finalize (norm.hip).
+// (Chan et al.; double), then the same outputs as bn_stats_finalize (norm.hip).  ROW = true:
+// write the merged (n, mean, M2) row [3][C] to save_mean instead (dg_bn_part_row).
+template <bool ROW = false>
 __global__ __launch_bounds__(SNT) void bn_part_finalize(const float* __restrict__ part, int nblk, int C,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float* running_mean,
@@ -534,6 +536,12 @@ __global__ __launch_bounds__(SNT) void bn_part_finalize(const float* __restrict_
     __syncthreads();
   }
   if (tid != 0) return;
+  if constexpr (ROW) {
+    save_mean[c] = (float)M;
+    save_mean[C + c] = (float)mean;
+    save_mean[2 * C + c] = (float)sh[0][0];
+    return;
+  }
   const double var = sh[0][0] / M;
   const float invstd = (float)(1.0 / sqrt(var + (double)eps));
   save_mean[c] = (float)mean;
@@ -679,8 +687,27 @@ extern "C" int dg_bn_part_finalize(const float* part, int nblk, int C, const flo
     part = (const float*)workspace;
     nblk = r2;
   }
-  hipLaunchKernelGGL(bn_part_finalize, dim3(C), dim3(SNT), 0, st, part, nblk, C, gamma, beta, running_mean,
+  hipLaunchKernelGGL(bn_part_finalize<false>, dim3(C), dim3(SNT), 0, st, part, nblk, C, gamma, beta, running_mean,
                      running_var, momentum, eps, save_mean, save_invstd, scale, shift);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// The merged (n, mean, M2) row [3][C] of part[nblk][3][C]: one SyncBatchNorm rank's statistics,
+// all-gathered and then finalized across ranks by dg_bn_part_finalize (nblk = world size).
+extern "C" int dg_bn_part_row(const float* part, int nblk, int C, float* row, void* workspace, void* stream) {
+  DG_REQUIRE(part && row && nblk > 0 && C > 0);
+  hipStream_t st = (hipStream_t)stream;
+  const int r2 = part_rows2(nblk);
+  if (r2) {
+    DG_REQUIRE(workspace);
+    hipLaunchKernelGGL(bn_part_merge, dim3(dg_cdiv(C, 64), r2), dim3(SNT), 0, st, part, nblk, C, (float*)workspace);
+    DG_CHECK_LAUNCH();
+    part = (const float*)workspace;
+    nblk = r2;
+  }
+  hipLaunchKernelGGL(bn_part_finalize<true>, dim3(C), dim3(SNT), 0, st, part, nblk, C, nullptr, nullptr, nullptr,
+                     nullptr, 0.f, 0.f, row, nullptr, nullptr, nullptr);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

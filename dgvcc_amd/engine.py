@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import kernels as K
+from . import syncbn as SB
 from .kernels import Act
 
 # The memory readout y_new = mem P feeds only the 1x1 density head, so the head folds through it:
@@ -126,11 +127,13 @@ class ConvLayer:
             raise ValueError("ConvLayer: pooled output shape mismatch")
         bias = self.conv.bias.detach() if self.conv.bias is not None else None
         bn = self.bn
+        # nn.SyncBatchNorm under a multi-rank process group: global batch statistics (syncbn.py)
+        pg = SB.group_of(bn) if training else None
         if stem:
             N, _, H, W = x.shape
             build = lambda: K.pack_weight(self.conv.weight.detach(), dt, cpad=3, row_len=32)  # noqa: E731
             wp = build() if training else frozen(self, ("stem", dt), (self.conv.weight,), build)
-            if _STEM_RECOMP and pool is None and drop is None and out is not None:
+            if _STEM_RECOMP and pool is None and drop is None and out is not None and pg is None:
                 # z-free stem: statistics pass, then conv recomputed with BN+ReLU applied; the
                 # backward recomputes z again (27 MACs per output vs 128 B/px per HBM pass)
                 if training:
@@ -146,7 +149,9 @@ class ConvLayer:
                 return
             z = Act(K.nhwc(N, H, W, self.Cout, dt, x.device))
             part, nblk = K.stem_fwd(x, wp, bias, z)
-            if training:
+            if pg is not None:
+                stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk)
+            elif training:
                 bn.num_batches_tracked.add_(1)
                 stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                            bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
@@ -172,10 +177,14 @@ class ConvLayer:
                 K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
         else:
             K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
-        if epi is not None:
+        if epi is not None and pg is not None:
+            stats = SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1])
+        elif epi is not None:
             bn.num_batches_tracked.add_(1)
             stats = K.bn_part_finalize(epi[0], epi[1], self.Cout, bn.weight.detach(), bn.bias.detach(),
                                        bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+        elif pg is not None:
+            stats = SB.fwd_stats(bn, pg, z=z)
         elif bn is not None:
             if training:
                 bn.num_batches_tracked.add_(1)
@@ -213,6 +222,7 @@ class ConvLayer:
         dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) \
             if self.conv.bias is not None else None
         gamma = self.bn.weight.detach() if self.bn is not None else None
+        pg = SB.group_of(self.bn)
         if isinstance(x, torch.Tensor):  # fused bf16 stem: coefficients, then BN-backward + wgrad in one pass
             dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
             bias = self.conv.bias.detach() if self.conv.bias is not None else None
@@ -220,13 +230,19 @@ class ConvLayer:
                 coef = K.stem_bwd_coef(x, wp, bias, g, gamma, stats, dgamma, dbeta, dbias)
                 K.stem_bwd(x, g, None, stats, coef, dw, wp=wp, bias=bias)
             else:
-                coef = K.bn_bwd_coef(g, z, gamma, stats, self.act, dgamma, dbeta, dbias, drop)
+                if pg is not None:
+                    coef = SB.backward(self.bn, pg, g, z, stats, self.act, None, dgamma, dbeta, dbias, drop=drop)
+                else:
+                    coef = K.bn_bwd_coef(g, z, gamma, stats, self.act, dgamma, dbeta, dbias, drop)
                 K.stem_bwd(x, g, z, stats, coef, dw)
             grads = {self.conv.weight: dw, self.bn.weight: dgamma, self.bn.bias: dbeta}
             if self.conv.bias is not None:
                 grads[self.conv.bias] = dbias
             return grads
-        if g_pool is not None:
+        if pg is not None:
+            SB.backward(self.bn, pg, g, z, stats, self.act, dz, dgamma, dbeta, dbias, drop=drop, g_pool=g_pool,
+                        part=pre[0] if pre is not None else None, nblk=pre[1] if pre is not None else 0)
+        elif g_pool is not None:
             if self.bn is None:
                 raise RuntimeError("pooled backward needs a BatchNorm layer")
             K.bn_bwd_pool(g_pool, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
@@ -347,8 +363,11 @@ class CatConvLayer(ConvLayer):
         K.call("dg_cat_combine", z.dt, z.ptr, z.ld, zs[1].ptr, zs[1].ld, zs[2].ptr, zs[2].ld, z.N, z.H, z.W,
                self.Cout, K.ptr(bias), z.ptr, z.ld, K.ptr(part), K.stream())
         bn = self.bn
+        pg = SB.group_of(bn) if training else None
         if bn is None:  # models2 den_dec: ConvBlock without BatchNorm (bias-free conv + ReLU)
             stats = frozen(self, ("ident", dev), (), lambda: _ident_stats(self.Cout, dev))
+        elif pg is not None:
+            stats = SB.fwd_stats(bn, pg, part=part, nblk=rows)
         elif training:
             bn.num_batches_tracked.add_(1)
             stats = K.bn_part_finalize(part, rows, self.Cout, bn.weight.detach(), bn.bias.detach(),
@@ -372,7 +391,11 @@ class CatConvLayer(ConvLayer):
         dbias = torch.empty(self.Cout, dtype=torch.float32, device=dev) \
             if (self.conv.bias is not None and self.bn is not None) else None
         gamma = self.bn.weight.detach() if self.bn is not None else None
-        K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta, dbias, drop)
+        pg = SB.group_of(self.bn)
+        if pg is not None:
+            SB.backward(self.bn, pg, g, z, stats, self.act, dz, dgamma, dbeta, dbias, drop=drop)
+        else:
+            K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta, dbias, drop)
         gzs = [dz]
         for part, sc in zip(x.parts[1:], CatParts.SCALES[1:]):  # U^T dz at the part's resolution
             gk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dz.buf.dtype, dev))

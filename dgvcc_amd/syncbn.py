@@ -1,0 +1,134 @@
+"""SyncBatchNorm over data-parallel ranks on the HIP BN kernels.
+
+The reference's ISW trunk normalises with `nn.SyncBatchNorm` (models/ISW/mynn.py:8-14), which
+synchronises its batch statistics as soon as a process group exists; torch's
+`nn.SyncBatchNorm.convert_sync_batchnorm(model)` opts any other model in (the DGModel_* VGG16-BN
+layers for a strong-scaled jhu_fog2snow run: the configs' batch of 16 split over the ranks with
+the BN statistics of all 16).  A BN layer takes this path when its module is an
+`nn.SyncBatchNorm` and its process group (default: WORLD) has more than one rank; otherwise the
+local kernels run unchanged.
+
+The exchange is the one torch's SyncBatchNorm does, in two small collectives per layer:
+  forward   each rank's (n, mean, M2) row [3][C] is all-gathered and merged in rank order
+            (Chan, double) by dg_bn_part_finalize -> the global statistics + running-stat update;
+  backward  each rank's (sum g', sum g' xhat, sum xhat) [3][C] is all-reduced; the dz
+            coefficients come from the global sums over all ranks' pixels, dgamma / dbeta (and
+            the conv bias) from this rank's, which the data-parallel gradient average then
+            combines like every other parameter gradient.
+Rows are f32 [3][C] (at most 6 KB per layer), so the collectives are latency, not bandwidth.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from . import kernels as K
+from ._capi import call, ptr, query, stream
+
+
+def group_of(bn) -> object | None:
+    """The process group to synchronise `bn` over, or None for a local BatchNorm."""
+    if not isinstance(bn, nn.SyncBatchNorm):
+        return None
+    if not (dist.is_available() and dist.is_initialized()):
+        return None
+    pg = bn.process_group if bn.process_group is not None else dist.group.WORLD
+    return pg if dist.get_world_size(pg) > 1 else None
+
+
+def _momentum(bn) -> float:
+    if bn.momentum is None:
+        return 1.0 / float(bn.num_batches_tracked.item())
+    return float(bn.momentum)
+
+
+def _all_gather_rows(row: torch.Tensor, pg) -> torch.Tensor:
+    w = dist.get_world_size(pg)
+    out = [torch.empty_like(row) for _ in range(w)]
+    dist.all_gather(out, row.contiguous(), group=pg)
+    return torch.stack(out)  # [world][3][C], rank order
+
+
+def finalize_rows(bn, row: torch.Tensor, pg) -> torch.Tensor:
+    """Local (n, mean, M2) row -> the global stats [4][C] (mean, invstd, scale, shift)."""
+    rows = _all_gather_rows(row, pg)
+    C = row.shape[1]
+    bn.num_batches_tracked.add_(1)
+    return K.bn_part_finalize(rows, rows.shape[0], C, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
+                              bn.running_var, _momentum(bn), bn.eps)
+
+
+def row_from_z(z: K.Act) -> torch.Tensor:
+    row = torch.empty((3, z.C), dtype=torch.float32, device=z.buf.device)
+    work = torch.empty(query("dg_bn_workspace", z.M, z.C) // 4 + 1, dtype=torch.float32, device=z.buf.device)
+    call("dg_bn_stats_row", z.dt, z.ptr, z.ld, z.M, z.C, ptr(row), ptr(work), stream())
+    return row
+
+
+def row_from_part(part: torch.Tensor, nblk: int, C: int) -> torch.Tensor:
+    row = torch.empty((3, C), dtype=torch.float32, device=part.device)
+    work = torch.empty(query("dg_bn_part_workspace", nblk, C) // 4 + 1, dtype=torch.float32, device=part.device)
+    call("dg_bn_part_row", ptr(part), nblk, C, ptr(row), ptr(work), stream())
+    return row
+
+
+def fwd_stats(bn, pg, z: K.Act | None = None, part: torch.Tensor | None = None, nblk: int = 0) -> torch.Tensor:
+    """Global batch statistics of a synchronised BN layer from this rank's z or its partial rows."""
+    row = row_from_part(part, nblk, bn.num_features) if part is not None else row_from_z(z)
+    return finalize_rows(bn, row, pg)
+
+
+def bwd_sums(g: K.Act, z: K.Act, stats, act: int, drop=None, g_pool: K.Act | None = None,
+             part: torch.Tensor | None = None, nblk: int = 0) -> torch.Tensor:
+    """This rank's BN-backward sums [3][C]: from (g, z), from the pooled gradient g_pool (+ the
+    direct g) with the argmax recomputed from z, or from dgrad-epilogue partial rows."""
+    C, dev = z.C, z.buf.device
+    sums = torch.empty((3, C), dtype=torch.float32, device=dev)
+    if part is not None:
+        call("dg_bn_part_sums", ptr(part), nblk, C, ptr(sums), stream())
+        return sums
+    if g_pool is not None:
+        work = torch.empty(query("dg_bn_workspace", z.M, C) // 4 + 1, dtype=torch.float32, device=dev)
+        call("dg_bn_bwd_pool_sums", z.dt, g_pool.ptr, g_pool.ld, g.ptr if g is not None else None,
+             g.ld if g is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, C, ptr(stats[0]), ptr(stats[1]),
+             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), ptr(sums), ptr(work), stream())
+        return sums
+    work = torch.empty(query("dg_bn_workspace", z.M, C) // 4 + 1, dtype=torch.float32, device=dev)
+    call("dg_bn_bwd_sums", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, C, ptr(stats[0]), ptr(stats[1]), ptr(stats[2]),
+         ptr(stats[3]), act, ptr(drop), z.H * z.W, ptr(sums), ptr(work), stream())
+    return sums
+
+
+def bwd_coef(bn, pg, sums: torch.Tensor, M_local: int, stats, dgamma, dbeta, dbias=None) -> torch.Tensor:
+    """All-reduce the sums; the dz coefficients [3][C] from the global ones, dgamma / dbeta / dbias
+    from this rank's.  Every rank holds the same number of pixels (as torch's SyncBatchNorm with
+    equal per-rank batches and the reference's SyncMeanCov assume)."""
+    glob = sums.clone()
+    dist.all_reduce(glob, group=pg)
+    M_global = M_local * dist.get_world_size(pg)
+    coef = torch.empty_like(sums)
+    call("dg_bn_bwd_finalize_sync", ptr(sums), ptr(glob), M_local, M_global, sums.shape[1],
+         ptr(bn.weight.detach()), ptr(stats[1]), ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), stream())
+    return coef
+
+
+def bwd_apply(g: K.Act, z: K.Act, stats, act: int, coef, dz: K.Act, drop=None, g_pool: K.Act | None = None):
+    if g_pool is not None:
+        call("dg_bn_bwd_pool_apply_coef", z.dt, g_pool.ptr, g_pool.ld, g.ptr if g is not None else None,
+             g.ld if g is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(stats[0]), ptr(stats[1]),
+             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), ptr(coef), dz.ptr, dz.ld, stream())
+    else:
+        call("dg_bn_bwd_apply_coef", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(stats[0]), ptr(stats[1]),
+             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, ptr(coef), dz.ptr, dz.ld, stream())
+
+
+def backward(bn, pg, g: K.Act | None, z: K.Act, stats, act: int, dz: K.Act | None, dgamma, dbeta, dbias=None,
+             drop=None, g_pool: K.Act | None = None, part: torch.Tensor | None = None, nblk: int = 0):
+    """The whole synchronised BN(+ReLU[+pool]) backward; returns the coefficients (dz = None:
+    coefficients only, for a fused consumer such as the stem's weight-gradient pass)."""
+    sums = bwd_sums(g, z, stats, act, drop=drop, g_pool=g_pool, part=part, nblk=nblk)
+    coef = bwd_coef(bn, pg, sums, z.M, stats, dgamma, dbeta, dbias)
+    if dz is not None:
+        bwd_apply(g, z, stats, act, coef, dz, drop=drop, g_pool=g_pool)
+    return coef

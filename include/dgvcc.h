@@ -227,6 +227,42 @@ int dg_bn_part_finalize(const float* part, int nblk, int C, const float* gamma, 
                         float* save_mean, float* save_invstd, float* scale, float* shift,
                         void* workspace, void* stream);
 
+/* ---- SyncBatchNorm phases (nn.SyncBatchNorm over data-parallel ranks; the reference's ISW
+ * Norm2d, models/ISW/mynn.py:8-14, and convert_sync_batchnorm'd DGModel_* BN layers).  The host
+ * exchanges the per-rank rows between the phases (dgvcc_amd/syncbn.py):
+ *   forward:  a rank's (n, mean, M2) row [3][C] (dg_bn_stats_row from z, or dg_bn_part_row from
+ *             epilogue partials) -> all-gather [world][3][C] -> dg_bn_part_finalize(nblk = world):
+ *             the global batch statistics and running-stat update, as one BN over the global batch;
+ *   backward: a rank's sums [3][C] = (sum g', sum g' xhat, sum xhat) (dg_bn_bwd_sums,
+ *             dg_bn_bwd_pool_sums, or dg_bn_part_sums of dgrad-epilogue partials) -> all-reduce ->
+ *             dg_bn_bwd_finalize_sync (dz coefficients from the global sums over M_global pixels;
+ *             dgamma / dbeta and the conv-bias gradient from this rank's, as torch SyncBatchNorm)
+ *             -> dg_bn_bwd_apply_coef / dg_bn_bwd_pool_apply_coef.
+ * Workspaces: dg_bn_workspace(M, C) (stats_row, bwd_sums), dg_bn_workspace(N*H*W, C)
+ * (bwd_pool_sums), dg_bn_part_workspace(nblk, C) (part_row). */
+int dg_bn_stats_row(int dtype, const void* z, int64_t ldz, int M, int C, float* row, void* workspace,
+                    void* stream);
+int dg_bn_part_row(const float* part, int nblk, int C, float* row, void* workspace, void* stream);
+int dg_bn_part_sums(const float* part, int nblk, int C, float* sums, void* stream);
+int dg_bn_bwd_sums(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                   const float* save_mean, const float* save_invstd, const float* scale, const float* shift,
+                   int act, const float* drop, int HW, float* sums, void* workspace, void* stream);
+int dg_bn_bwd_pool_sums(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd, const void* z,
+                        int64_t ldz, int N, int H, int W, int C, const float* save_mean,
+                        const float* save_invstd, const float* scale, const float* shift, int act,
+                        const float* drop, float* sums, void* workspace, void* stream);
+int dg_bn_bwd_finalize_sync(const float* sums_local, const float* sums_global, int M_local, int64_t M_global,
+                            int C, const float* gamma, const float* save_invstd, float* dgamma, float* dbeta,
+                            float* dbias, float* coef, void* stream);
+int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
+                         const float* save_mean, const float* save_invstd, const float* scale,
+                         const float* shift, int act, const float* drop, int HW, const float* coef, void* dz,
+                         int64_t lddz, void* stream);
+int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
+                              const void* z, int64_t ldz, int N, int H, int W, int C, const float* save_mean,
+                              const float* save_invstd, const float* scale, const float* shift, int act,
+                              const float* drop, const float* coef, void* dz, int64_t lddz, void* stream);
+
 /* ---- fused first layer (bf16): Conv2d(3,64,3,pad 1) of vgg16_bn.features[0]
  * (models/models.py:35-36) read straight from the NCHW f32 image (no im2col buffer).
  * dg_stem_fwd: z[N,H,W,64] (pixel stride ldz, bf16) = conv + bias, and the BN statistics

@@ -21,7 +21,10 @@ def _worker(rank, world, port, q):
         with torch.no_grad():
             lin.weight.fill_(float(rank))
         D.broadcast_module_(lin)
-        q.put((rank, flat.tolist(), float(lin.weight.sum()), D.world(), D.rank()))
+        from dgvcc_amd import syncbn as SB
+        sync_ok = (SB.group_of(torch.nn.BatchNorm2d(4)) is None
+                   and SB.group_of(torch.nn.SyncBatchNorm(4)) is dist.group.WORLD)
+        q.put((rank, flat.tolist(), float(lin.weight.sum()), D.world(), D.rank(), sync_ok))
     finally:
         dist.destroy_process_group()
 
@@ -38,7 +41,14 @@ def test_average_and_broadcast_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     expect = [i * 1.5 for i in range(10)]
-    for rank, flat, wsum, world, rk in res:
+    for rank, flat, wsum, world, rk, sync_ok in res:
+        assert sync_ok  # SyncBatchNorm layers synchronise over WORLD, BatchNorm2d stays local
         assert flat == pytest.approx(expect)
         assert wsum == 0.0  # rank 0's weights everywhere
         assert world == 2 and rk == rank
+
+
+def test_syncbn_local_without_process_group():
+    from dgvcc_amd import syncbn as SB
+    assert SB.group_of(torch.nn.SyncBatchNorm(8)) is None  # no process group: a local BatchNorm
+    assert SB.group_of(None) is None

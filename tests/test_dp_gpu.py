@@ -30,6 +30,17 @@ def test_dp_final_train_step_matches_emulation(dev):
     assert r.returncode == 0 and r.stdout.count("OK") == 2, (r.stdout[-2000:], r.stderr[-3000:])
 
 
+def test_dp_syncbn_strong_scaling(dev):
+    """Strong-scaled DP with SyncBatchNorm (tests/dp_syncbn_worker.py): rank-averaged gradients,
+    loss and BN running statistics equal the single-process full-batch step."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", f"--master-port={_port()}",
+                        os.path.join(HERE, "dp_syncbn_worker.py")],
+                       capture_output=True, text=True, timeout=300)
+    print(r.stdout[-1500:])
+    assert r.returncode == 0 and r.stdout.count("OK") == 2, (r.stdout[-2000:], r.stderr[-3000:])
+
+
 def test_bench_gpus_flag_launches_ranks(dev):
     env = dict(os.environ, DGVCC_BENCH_BACKEND="gloo")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup",
