@@ -1735,14 +1735,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
                              co0, tid, fr, fc);
 }
 
-// wsp[co][kb][part][32] (bf16) = the exact 3-way split (dg_common.h split3_pair, nearest-even
-// parts) of the packed f32 filter w[co][kb*32 + j]; two consecutive elements per thread
+// wsp[co][kb][part][32] (bf16) = the exact 3-way split (dg_common.h split3_pair, truncated parts
+// as the forward's pixel fragments) of the packed f32 filter w[co][kb*32 + j]; two elements per thread
 __global__ void split_weight_kernel(const float* __restrict__ w, long long n, unsigned short* __restrict__ wsp) {
   const long long n2 = n >> 1;  // n = Cout*R*S*C is a multiple of 32
   for (long long o = blockIdx.x * (long long)blockDim.x + threadIdx.x; o < n2; o += (long long)gridDim.x * blockDim.x) {
     const float2 v = *(const float2*)(w + 2 * o);
     unsigned p0, p1, p2;
-    split3_pair(__float_as_uint(v.x), __float_as_uint(v.y), p0, p1, p2);
+    split3_pair<false>(__float_as_uint(v.x), __float_as_uint(v.y), p0, p1, p2);
     const long long e = 2 * o, blk = e >> 5, j = e & 31;
     unsigned* d = (unsigned*)(wsp + blk * 96 + j);
     d[0] = p0;
@@ -2856,7 +2856,7 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
           x0[m] = *(const unsigned*)(base + (4 * m + g) * rowb + col * 4);
           x1[m] = *(const unsigned*)(base + (4 * m + 16 + g) * rowb + col * 4);
         }
-        split3_8(x0, x1, h0, h1, h2);
+        split3_8_rn(x0, x1, h0, h1, h2);
       };
       s8v bh[TJ][3];
 #pragma unroll
@@ -3003,7 +3003,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
       const int idx = tid + NTH * i;
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       u2v h0, h1, h2;
-      split3_4(ra[i], h0, h1, h2);
+      split3_4_rn(ra[i], h0, h1, h2);
       *(u2v*)(As + o) = h0;
       *(u2v*)(As + PA + o) = h1;
       *(u2v*)(As + 2 * PA + o) = h2;
@@ -3013,7 +3013,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
       const int idx = tid + NTH * i;
       const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
       u2v h0, h1, h2;
-      split3_4(rb[i], h0, h1, h2);
+      split3_4_rn(rb[i], h0, h1, h2);
       *(u2v*)(Bs + o) = h0;
       *(u2v*)(Bs + PB + o) = h1;
       *(u2v*)(Bs + 2 * PB + o) = h2;
@@ -3174,7 +3174,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       const int idx = tid + NTH * i;
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       u2v h0, h1, h2;
-      split3_4(ra[i], h0, h1, h2);
+      split3_4_rn(ra[i], h0, h1, h2);
       *(u2v*)(As + o) = h0;
       *(u2v*)(As + PA + o) = h1;
       *(u2v*)(As + 2 * PA + o) = h2;
@@ -3185,7 +3185,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       if (idx < XR * CPRB) {
         const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
         u2v h0, h1, h2;
-        split3_4(rb[i], h0, h1, h2);
+        split3_4_rn(rb[i], h0, h1, h2);
         *(u2v*)(Bs + o) = h0;
         *(u2v*)(Bs + PB + o) = h1;
         *(u2v*)(Bs + 2 * PB + o) = h2;

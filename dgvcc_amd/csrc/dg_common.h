@@ -143,22 +143,28 @@ static inline int dg_cdiv(long long a, long long b) { return (int)((a + b - 1) /
 
 // ---------------------------------------------------------------------------
 // f32 arithmetic on the bf16 matrix cores ("3-way split", DG_F32 with
-// dg_set_f32_math(1)).  Each f32 x is cut EXACTLY into three bf16 parts by round-to-nearest-even,
-//   h0 = RN_bf16(x), h1 = RN_bf16(x - h0), h2 = x - h0 - h1
-// (x - h0 is at most half a bf16 ulp of x and spans <= 16 significant bits, its remainder <= 8, so h2 is
-// exact in bf16 and x = h0 + h1 + h2 holds bit for bit); a product x*y is then
+// dg_set_f32_math(1)).  Each f32 x is cut EXACTLY into three bf16 parts, x = h0 + h1 + h2
+// (x - h0 spans <= 16 significant bits and its remainder <= 8, so h2 is exact in bf16; the
+// identity-filter test checks it bit for bit on every kernel path); a product x*y is then
 // sum_{i+j<=2} xi*yj, six v_mfma_f32_16x16x32_bf16 per 16x16x32 block with f32 accumulation,
-// products of bf16 being exact in f32.  Each rounding is one v_cvt_pk_bf16_f32 per two values.
-// Why nearest and not truncation: with truncation every part carries its operand's sign, so
-// for same-sign operands (post-ReLU activations, positive gradients) the small products
-// x2*y0, x1*y1, x0*y2 (~2^-16 of |x*y| each) all push one way; once the f32 accumulator of a
-// long reduction is ~2^12 products large, a 32-deep block of them falls under its half-ulp and
-// is rounded away, every block, in the same direction: a one-sided loss of ~1e-5 relative on
-// the 786k-pixel weight gradients (measured; 10x the exact-f32 MFMA path).  Nearest parts are
-// sign-symmetric (|h1| <= 2^-8 |x|, |h2| <= 2^-16 |x|), so what the accumulator drops is noise,
-// and the dropped terms (i+j >= 3) are < 2^-24 |x*y| each with either sign
-// (tests/test_kernels_gpu.py::test_conv_f32_split_same_sign).  Six bf16 MFMAs (16 cycles each)
-// replace eight v_mfma_f32_16x16x4_f32 (32 cycles each) per 32-deep K block.
+// products of bf16 being exact in f32.  Six bf16 MFMAs (16 cycles each) replace eight
+// v_mfma_f32_16x16x4_f32 (32 cycles each) per 32-deep K block.  Two rounding rules for the
+// parts, each where it measured better (tests/test_kernels_gpu.py):
+//  * truncation (split3_8 / split3_4 / split_weight_kernel: forward and dgrad, K <= 4608):
+//    every part carries its operand's sign.  The rounding of the two photometric views of a
+//    final-mode step then stays correlated through the network, so the consistency loss
+//    between them (a mean of squared differences of near-equal softmaxes, ~1e-8) comes out
+//    at 5e-7 relative to float64, against 1.8e-4 with nearest parts and 8.7e-5 on the exact
+//    f32 MFMA; the one-sided dropped terms (|x1*y2|, |x2*y1| < 2^-21 |x*y|, typically ~2^-22
+//    of sum |x*y|) stay below the f32 accumulation error of these sums (same-sign K = 4608:
+//    4.2e-6 against 5.0e-6 exact).
+//  * round-to-nearest-even (split3_8_rn / split3_4_rn, one v_cvt_pk_bf16_f32 per pair and
+//    level: weight gradients, reductions over up to 786k pixels): with truncation, same-sign
+//    operands (post-ReLU x, positive dy) make the small products x2*y0, x1*y1, x0*y2 (~2^-16
+//    |x*y| each) all push one way, and once the accumulator of a long reduction is ~2^12
+//    products large a 32-deep block of them falls under its half-ulp and is rounded away in
+//    the same direction every block: 1.1e-5 relative on the 786k-pixel wgrad, 10x the exact
+//    MFMA.  Nearest parts are sign-symmetric (|h1| <= 2^-8 |x|, |h2| <= 2^-16 |x|): 3.7e-7.
 // ---------------------------------------------------------------------------
 typedef __bf16 dg_bf16x2 __attribute__((ext_vector_type(2)));
 typedef float dg_f32x2 __attribute__((ext_vector_type(2)));
@@ -166,45 +172,42 @@ typedef float dg_f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ unsigned cvt_pk_bf16(float a, float b) {
   return __builtin_bit_cast(unsigned, __builtin_convertvector(dg_f32x2{a, b}, dg_bf16x2));
 }
-// one split level of a pair: the packed parts, and the exact f32 remainders
+// one nearest split level of a pair: the packed parts, and the exact f32 remainders
 __device__ __forceinline__ unsigned split_level2(float a, float b, float& ra, float& rb) {
   const unsigned p = cvt_pk_bf16(a, b);
   ra = a - __uint_as_float(p << 16);
   rb = b - __uint_as_float(p & 0xffff0000u);
   return p;
 }
-// DGVCC_SPLIT_RNE 0 selects the truncating split of round 2 (kept for same-box A/Bs; see above)
-#ifndef DGVCC_SPLIT_RNE
-#define DGVCC_SPLIT_RNE 1
-#endif
-#if !DGVCC_SPLIT_RNE
+// the parts of a pair of f32 (bit patterns a, b), packed lo = a, hi = b
+template <bool RN>
 __device__ __forceinline__ void split3_pair(unsigned a, unsigned b, unsigned& p0, unsigned& p1, unsigned& p2) {
-  p0 = __builtin_amdgcn_perm(b, a, 0x07060302u);
-  const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
-  const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
-  const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
-  p1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
-  const float sa = ra - __uint_as_float(ua & 0xffff0000u);
-  const float sb = rb - __uint_as_float(ub & 0xffff0000u);
-  p2 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+  if constexpr (RN) {
+    float ra, rb, sa, sb;
+    p0 = split_level2(__uint_as_float(a), __uint_as_float(b), ra, rb);
+    p1 = split_level2(ra, rb, sa, sb);
+    p2 = cvt_pk_bf16(sa, sb);  // exact
+  } else {
+    p0 = __builtin_amdgcn_perm(b, a, 0x07060302u);  // (a >> 16) | (b & 0xffff0000)
+    const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
+    const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
+    const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
+    p1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
+    const float sa = ra - __uint_as_float(ua & 0xffff0000u);
+    const float sb = rb - __uint_as_float(ub & 0xffff0000u);
+    p2 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+  }
 }
-#else
-__device__ __forceinline__ void split3_pair(unsigned a, unsigned b, unsigned& p0, unsigned& p1, unsigned& p2) {
-  float ra, rb, sa, sb;
-  p0 = split_level2(__uint_as_float(a), __uint_as_float(b), ra, rb);
-  p1 = split_level2(ra, rb, sa, sb);
-  p2 = cvt_pk_bf16(sa, sb);  // exact
-}
-#endif
 // 8 f32 (x0[0..3], x1[0..3]) -> bf16 parts h0/h1/h2, element k of each part = float k
-__device__ __forceinline__ void split3_8(const u4v& x0, const u4v& x1, s8v& h0, s8v& h1, s8v& h2) {
+template <bool RN = false>
+__device__ __forceinline__ void split3_8t(const u4v& x0, const u4v& x1, s8v& h0, s8v& h1, s8v& h2) {
   u4v p0, p1, p2;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const unsigned a = k < 2 ? x0[2 * k] : x1[2 * k - 4];
     const unsigned b = k < 2 ? x0[2 * k + 1] : x1[2 * k - 3];
     unsigned q0, q1, q2;
-    split3_pair(a, b, q0, q1, q2);
+    split3_pair<RN>(a, b, q0, q1, q2);
     p0[k] = q0;
     p1[k] = q1;
     p2[k] = q2;
@@ -212,6 +215,12 @@ __device__ __forceinline__ void split3_8(const u4v& x0, const u4v& x1, s8v& h0, 
   h0 = __builtin_bit_cast(s8v, p0);
   h1 = __builtin_bit_cast(s8v, p1);
   h2 = __builtin_bit_cast(s8v, p2);
+}
+__device__ __forceinline__ void split3_8(const u4v& x0, const u4v& x1, s8v& h0, s8v& h1, s8v& h2) {
+  split3_8t<false>(x0, x1, h0, h1, h2);
+}
+__device__ __forceinline__ void split3_8_rn(const u4v& x0, const u4v& x1, s8v& h0, s8v& h1, s8v& h2) {
+  split3_8t<true>(x0, x1, h0, h1, h2);
 }
 // the six products of one block, smallest first (all into the same f32 accumulator)
 __device__ __forceinline__ f4v mfma_x6(const s8v& a0, const s8v& a1, const s8v& a2, const s8v& b0, const s8v& b1,
@@ -226,13 +235,16 @@ __device__ __forceinline__ f4v mfma_x6(const s8v& a0, const s8v& a1, const s8v& 
 }
 
 // 4 f32 -> the bf16 parts of each (element k of part p = part p of x[k])
-__device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2) {
+template <bool RN = false>
+__device__ __forceinline__ void split3_4t(const u4v& x, u2v& h0, u2v& h1, u2v& h2) {
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     unsigned p0, p1, p2;
-    split3_pair(x[2 * k], x[2 * k + 1], p0, p1, p2);
+    split3_pair<RN>(x[2 * k], x[2 * k + 1], p0, p1, p2);
     h0[k] = p0;
     h1[k] = p1;
     h2[k] = p2;
   }
 }
+__device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2) { split3_4t<false>(x, h0, h1, h2); }
+__device__ __forceinline__ void split3_4_rn(const u4v& x, u2v& h0, u2v& h1, u2v& h2) { split3_4t<true>(x, h0, h1, h2); }

@@ -5,7 +5,8 @@ with the statistics of the whole batch as the reference's single-device run does
 the final-mode step on its half; the rank-averaged gradients, the loss average and the BN
 running statistics must equal one process running the whole batch with plain BatchNorm.  Then
 one real DGTrainer step with the fused AdamW (its flat-gradient all-reduce) leaves identical
-parameters on both ranks.  Dropouts are off so both runs see the same masks."""
+parameters on both ranks.  Dropouts are off so both runs see the same masks.  Before that, a
+single SyncBN ConvLayer (plain and max-pooled) against the whole-batch layer at 1e-5."""
 import os
 import sys
 import tempfile
@@ -53,14 +54,81 @@ def step_grads(m, batch, dev):
     return loss.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
 
 
+def layer_check(dev, rank, world, pool):
+    """One Conv3x3 + SyncBatchNorm + ReLU (+ MaxPool2d) ConvLayer (engine.py) on this rank's half of
+    a batch against the same layer with a plain BatchNorm2d on the whole batch: outputs, input
+    gradients, parameter gradients (summed over ranks: the DP average x world) and running
+    statistics within 1e-5.  No network in between, so no decision can differ."""
+    from dgvcc_amd import engine as E
+    from dgvcc_amd import kernels as K
+    g = torch.Generator().manual_seed(5)
+    N, Hh, Ww, C, Co = 4, 32, 40, 64, 128
+    x = torch.randn(N, Hh, Ww, C, generator=g)
+    gy = torch.randn(N, Hh // 2 if pool else Hh, Ww // 2 if pool else Ww, Co, generator=g)
+    conv = nn.Conv2d(C, Co, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.copy_(torch.randn(conv.weight.shape, generator=g) * 0.05)
+        conv.bias.copy_(torch.randn(Co, generator=g) * 0.1)
+
+    def run(bn_cls, xs, gs):
+        cv = nn.Conv2d(C, Co, 3, padding=1).to(dev)
+        cv.load_state_dict(conv.state_dict())
+        bn = nn.BatchNorm2d(Co)
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.5, 1.5, Co))
+            bn.bias.copy_(torch.linspace(-0.2, 0.2, Co))
+        if bn_cls is nn.SyncBatchNorm:
+            bn = nn.SyncBatchNorm.convert_sync_batchnorm(bn)
+        bn = bn.to(dev)
+        L = E.ConvLayer(cv, bn, E.ACT_RELU)
+        n, h, w = xs.shape[0], xs.shape[1], xs.shape[2]
+        tape = {}
+        xa = K.Act(xs.to(dev).contiguous())
+        if pool:
+            out = K.Act(K.nhwc(n, h // 2, w // 2, Co, torch.float32, dev))
+            L.forward(xa, None, True, tape, pool=out)
+        else:
+            out = K.Act(K.nhwc(n, h, w, Co, torch.float32, dev))
+            L.forward(xa, out, True, tape)
+        gx = K.Act(K.nhwc(n, h, w, C, torch.float32, dev))
+        ga = K.Act(gs.to(dev).contiguous())
+        grads = L.backward(tape, None, gx, g_pool=ga) if pool else L.backward(tape, ga, gx)
+        names = {cv.weight: "w", cv.bias: "b", bn.weight: "gamma", bn.bias: "beta"}
+        return (out.buf.cpu(), gx.buf.cpu(), {names[p]: v.cpu() for p, v in grads.items()},
+                (bn.running_mean.cpu(), bn.running_var.cpu()))
+
+    n = N // world
+    sl = slice(rank * n, (rank + 1) * n)
+    out, gx, grads, rs = run(nn.SyncBatchNorm, x[sl], gy[sl])
+    full_out = [torch.empty_like(out) for _ in range(world)]
+    full_gx = [torch.empty_like(gx) for _ in range(world)]
+    dist.all_gather(full_out, out)
+    dist.all_gather(full_gx, gx)
+    for v in grads.values():
+        dist.all_reduce(v)
+    fails = []
+    if rank == 0:
+        r_out, r_gx, r_grads, r_rs = run(nn.BatchNorm2d, x, gy)
+        rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+        errs = {"out": rel(torch.cat(full_out), r_out), "gx": rel(torch.cat(full_gx), r_gx),
+                "running_mean": rel(rs[0], r_rs[0]), "running_var": rel(rs[1], r_rs[1])}
+        for k in ("w", "gamma", "beta"):
+            errs["grad_" + k] = rel(grads[k], r_grads[k])
+        print(f"RANK0 layer pool={pool}: {errs}", flush=True)
+        bad = {k: v for k, v in errs.items() if v > 1e-5}
+        if bad:
+            fails.append((f"layer pool={pool}", bad))
+    return fails
+
+
 def main():
     D.init_from_env("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    fails = layer_check(dev, rank, world, False) + layer_check(dev, rank, world, True)
     sd0 = O.seeded_state_dict(DGModel_final(pretrained=False).state_dict())
     batch = O.synthetic_batch(B, H, W, seed=2112)
-    fails = []
     # strong-scaled data parallel with SyncBN: this rank's B / world samples
     m = build(dev, sd0, sync=True)
     assert sum(isinstance(x, nn.SyncBatchNorm) for x in m.modules()) == 21
@@ -84,7 +152,11 @@ def main():
             if r.norm() == 0:
                 continue
             worst[k] = ((grads[k].double() - r.double()).norm() / r.double().norm()).item()
-        bad = {k: v for k, v in worst.items() if v > 1e-4}
+        # the whole network: loss and running statistics at 1e-5; the gradients only within the
+        # spread that the near-tie ReLU / max-pool decisions of a random-init VGG16 give any two
+        # fp32 evaluations of the same step (tests/test_model_gpu.py E2E_GRAD_TOL; the BN math
+        # itself is pinned at 1e-5 by layer_check above)
+        bad = {k: v for k, v in worst.items() if v > 1.5e-2}
         if bad:
             fails.append(("grads", bad))
         rs = max(((rstats[k].double() - v.double()).abs().max() / v.double().abs().max().clamp_min(1e-30)).item()

@@ -361,6 +361,41 @@ def test_conv_f32_split_math(dev, case):
         assert e1 < 5e-6 and e1 < 2 * e0 + 2e-7, errs
 
 
+@pytest.mark.parametrize("case", [(2, 20, 24, 64, 128, 3), (1, 16, 256, 64, 64, 3), (1, 24, 64, 128, 128, 3),
+                                  (1, 16, 64, 256, 256, 3), (1, 8, 64, 512, 512, 3), (1, 12, 8, 256, 128, 1),
+                                  (2, 4, 512, 128, 64, 3), (1, 6, 1024, 64, 64, 3), (1, 8, 16, 896, 256, 1)])
+def test_conv_f32_split_exact_identity(dev, case):
+    """The 3-way split is exact (x = h0 + h1 + h2 bit for bit, dg_common.h split3_pair): with an
+    identity filter (centre tap) every split-math forward and dgrad path must return its input
+    bit-identically, and the weight gradient against a one-hot output gradient must return the
+    input pixel exactly (one nonzero product per output: no rounding anywhere)."""
+    K = _k()
+    N, H, W, C, Cout, R = case
+    pad = R // 2
+    g = torch.Generator().manual_seed(31)
+    n = min(C, Cout)
+    w = torch.zeros(Cout, C, R, R)
+    w[torch.arange(n), torch.arange(n), pad, pad] = 1.0
+    x = torch.randn(N, H, W, C, generator=g) * torch.exp(torch.randn(N, H, W, C, generator=g))  # full mantissas
+    gy = torch.randn(N, H, W, Cout, generator=g)
+    xd, gyd = K.Act(x.to(dev)), K.Act(gy.to(dev))
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+    K.conv_fwd(xd, wp, Cout, R, pad, y)
+    dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+    K.conv_dgrad(gyd, wp, C, R, pad, dx)
+    oh = torch.zeros(N, H, W, Cout)
+    p = (N * H * W) // 2 + 3
+    oh.view(-1, Cout)[p] = 1.0
+    dw = torch.empty(Cout, C, R, R, device=dev)
+    K.conv_wgrad(xd, K.Act(oh.to(dev)), R, pad, dw)
+    torch.cuda.synchronize()
+    assert torch.equal(y.buf.cpu()[..., :n], x[..., :n]), "forward"
+    assert torch.equal(dx.buf.cpu()[..., :n], gy[..., :n]), "dgrad"
+    xp = x.view(-1, C)[p]
+    assert torch.equal(dw[:, :, pad, pad].cpu(), xp.view(1, C).expand(Cout, C)), "wgrad"
+
+
 @pytest.mark.parametrize("case,which", [((1, 32, 64, 512, 512, 3), "fd"),      # K = 4608 fwd + dgrad
                                         ((1, 48, 64, 512, 256, 3), "fd"),
                                         ((1, 768, 1024, 64, 64, 3), "w"),      # 786k-pixel wgrad reduction

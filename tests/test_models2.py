@@ -111,6 +111,7 @@ def test_models2_matches_reference(dev, name, method):
         assert tuple(o.shape) == tuple(ref.shape), (i, o.shape, ref.shape)
         tol = max(3 * float(d[f"{method}__out{i}__ref32_err"][0]), 1e-4)
         err = ((o.detach().double().cpu() - ref).abs().max() / ref.abs().max().clamp_min(1e-30)).item()
+        print(f"{name}.{method} out{i}: err {err:.3e} tol {tol:.3e} (fp32 reference {tol / 3:.3e})")
         assert err < tol, (name, method, i, err, tol)
         r = torch.randn(o.shape, generator=g, dtype=torch.float64).float().to(dev)
         obj = obj + (o * r).sum()

@@ -74,6 +74,7 @@ def _sensitivity(kind, sd0, img, dmaps, g64, eps=3e-5):
 
 def _check_grads(model, g64, g32, tol=GRAD_TOL, sens=None):
     bad = {}
+    worst = (0.0, "", 0.0, 0.0)
     for k, p in model.named_parameters():
         if k not in g64 or g64[k].norm() == 0:
             continue
@@ -84,6 +85,8 @@ def _check_grads(model, g64, g32, tol=GRAD_TOL, sens=None):
             continue
         if mine > max(2 * ref, tol, 3 * (sens or {}).get(k, 0.0)):
             bad[k] = (mine, ref, (sens or {}).get(k))
+        worst = max(worst, (mine / max(2 * ref, tol), k, mine, ref))
+    print("grad check worst (ratio to bound, param, err, fp32 ref err):", worst)
     assert not bad, bad
 
 
@@ -157,6 +160,8 @@ def test_isw_covstat_and_train_fp32(dev):
     torch.cuda.synchronize()
     out64, (l64, wt64), g64 = _oracle("isw", sd0, img1, dmaps, torch.float64, masks)
     _, (l32, wt32), g32 = _oracle("isw", sd0, img1, dmaps, torch.float32, masks)
+    print("isw covstat: loss err", abs(losses[0].item() - l64.item()), "fp32 ref", abs(l32.item() - l64.item()),
+          "wt err", abs(losses[1].item() - wt64.item()), "fp32 ref", abs(wt32.item() - wt64.item()))
     assert abs(losses[0].item() - l64.item()) <= max(3 * abs(l32.item() - l64.item()), 1e-4 * l64.item())
     assert abs(losses[1].item() - wt64.item()) <= max(3 * abs(wt32.item() - wt64.item()), 1e-4 * wt64.item())
     _check_grads(model, g64, {k: v.double() for k, v in g32.items()})
