@@ -180,6 +180,8 @@ __device__ __forceinline__ unsigned split_level2(float a, float b, float& ra, fl
   return p;
 }
 // the parts of a pair of f32 (bit patterns a, b), packed lo = a, hi = b
+// (the remainders are formed as float pairs: one v_pk_add_f32 per level and pair)
+typedef unsigned dg_u32x2 __attribute__((ext_vector_type(2)));
 template <bool RN>
 __device__ __forceinline__ void split3_pair(unsigned a, unsigned b, unsigned& p0, unsigned& p1, unsigned& p2) {
   if constexpr (RN) {
@@ -188,14 +190,14 @@ __device__ __forceinline__ void split3_pair(unsigned a, unsigned b, unsigned& p0
     p1 = split_level2(ra, rb, sa, sb);
     p2 = cvt_pk_bf16(sa, sb);  // exact
   } else {
+    const dg_u32x2 x = {a, b};
     p0 = __builtin_amdgcn_perm(b, a, 0x07060302u);  // (a >> 16) | (b & 0xffff0000)
-    const float ra = __uint_as_float(a) - __uint_as_float(a & 0xffff0000u);
-    const float rb = __uint_as_float(b) - __uint_as_float(b & 0xffff0000u);
-    const unsigned ua = __float_as_uint(ra), ub = __float_as_uint(rb);
-    p1 = __builtin_amdgcn_perm(ub, ua, 0x07060302u);
-    const float sa = ra - __uint_as_float(ua & 0xffff0000u);
-    const float sb = rb - __uint_as_float(ub & 0xffff0000u);
-    p2 = __builtin_amdgcn_perm(__float_as_uint(sb), __float_as_uint(sa), 0x07060302u);
+    const dg_f32x2 r = __builtin_bit_cast(dg_f32x2, x) - __builtin_bit_cast(dg_f32x2, x & 0xffff0000u);
+    const dg_u32x2 ur = __builtin_bit_cast(dg_u32x2, r);
+    p1 = __builtin_amdgcn_perm(ur.y, ur.x, 0x07060302u);
+    const dg_f32x2 q = r - __builtin_bit_cast(dg_f32x2, ur & 0xffff0000u);
+    const dg_u32x2 uq = __builtin_bit_cast(dg_u32x2, q);
+    p2 = __builtin_amdgcn_perm(uq.y, uq.x, 0x07060302u);
   }
 }
 // 8 f32 (x0[0..3], x1[0..3]) -> bf16 parts h0/h1/h2, element k of each part = float k
