@@ -346,14 +346,15 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
 // Deterministic variant (no atomics on the map): every output pixel sums its stamp values in
 // point order, the reference's `density += gaussian_filter(pt2d)` f32 accumulation
 // (dmap_gen.py:72-79) exactly, so the map is bit-identical to the reference's and stable run
-// to run.  The points are first binned by 16x64 output tile (count -> scan -> fill; a point
-// lands in the <= 4 tiles its 15x15 stamp touches), then one 256-thread block per tile sorts
-// its bin back into point order in LDS (rank sort: bins arrive in atomic order) and each
-// thread accumulates its pixel.  Work is O(points + pixels); a tile whose bin exceeds DM_CAP
-// (an extremely dense crowd) walks all of its image's points instead, same order, same sums.
-constexpr int DMT = 16;   // tile rows
-constexpr int DMTW = 64;  // tile columns: 4 consecutive pixels per thread (one 16-B store)
-constexpr int DM_CAP = 1024;
+// to run.  Two launches: the normalized stamp once (scipy's float64 weights, two float32 passes),
+// then one 256-thread block per 32 x 64 output tile that walks its image's points in order,
+// 256 at a time: each thread tests one point's stamp against the tile, the hits are compacted in
+// point order (wave ballots + an LDS prefix over the 4 waves), and every thread adds the hits'
+// stamp values to its 2 x 4 pixels.  No binning pass, no scan, no atomics: the point list of an
+// image (8 B per point) is read once per tile from L2, the map written once with 16-B stores.
+constexpr int DFR = 32;  // tile rows    (2 per thread)
+constexpr int DFC = 64;  // tile columns (4 per thread: one 16-B store per row)
+constexpr int DSK = 64;  // stamp row stride (radius < 32 -> K <= 63)
 
 // int() truncation and numpy's negative-index wrap of gaussian_filter_density_fixed
 __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long long q, int H, int W, int& r, int& c) {
@@ -365,87 +366,7 @@ __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long lon
   return in && r >= 0 && c >= 0;
 }
 
-// pass 0 (count) / 1 (fill): bin every point into the tiles its stamp touches
-template <int PASS>
-__global__ __launch_bounds__(256) void dmap_bin_kernel(const float* __restrict__ pts, const int64_t* __restrict__ offsets,
-                                                       int H, int W, int radius, int* __restrict__ cnt,
-                                                       int* __restrict__ list) {
-  const int n = blockIdx.y;
-  const int tiles_h = (H + DMT - 1) / DMT, tiles_w = (W + DMTW - 1) / DMTW;
-  const long long T = (long long)tiles_h * tiles_w;
-  const long long p0 = offsets[n], p1 = offsets[n + 1];
-  for (long long q = p0 + blockIdx.x * 256ll + threadIdx.x; q < p1; q += (long long)gridDim.x * 256) {
-    int r, c;
-    if (!dm_point(pts, q, H, W, r, c)) continue;
-    const int tr0 = max(0, r - radius) / DMT, tr1 = min(H - 1, r + radius) / DMT;
-    const int tc0 = max(0, c - radius) / DMTW, tc1 = min(W - 1, c + radius) / DMTW;
-    for (int tr = tr0; tr <= tr1; ++tr)
-      for (int tc = tc0; tc <= tc1; ++tc) {
-        int* slot = cnt + n * T + (long long)tr * tiles_w + tc;
-        if (PASS == 0) {
-          atomicAdd(slot, 1);
-        } else {
-          list[atomicAdd(slot, 1)] = (int)(q - p0);
-        }
-      }
-  }
-}
-
-// exclusive scan of the bin counts in three parallel passes: per-1024-bin block scans
-// (start = local prefix, bsum = block total), one block scanning the block totals, then
-// start += block offset (the fill cursor cnt := start, start[total] = sum)
-constexpr int DM_SB = 1024;
-__global__ __launch_bounds__(DM_SB) void dmap_scan_blocks(const int* __restrict__ cnt, long long total,
-                                                          int* __restrict__ start, int* __restrict__ bsum) {
-  __shared__ int sh[DM_SB];
-  const int t = threadIdx.x;
-  const long long i = (long long)blockIdx.x * DM_SB + t;
-  const int v = i < total ? cnt[i] : 0;
-  sh[t] = v;
-  __syncthreads();
-  for (int o = 1; o < DM_SB; o <<= 1) {
-    const int u = t >= o ? sh[t - o] : 0;
-    __syncthreads();
-    sh[t] += u;
-    __syncthreads();
-  }
-  if (i < total) start[i] = sh[t] - v;
-  if (t == DM_SB - 1) bsum[blockIdx.x] = sh[t];
-}
-
-__global__ __launch_bounds__(DM_SB) void dmap_scan_sums(int* __restrict__ bsum, int nb, int* __restrict__ total_out) {
-  __shared__ int sh[DM_SB];
-  const int t = threadIdx.x;
-  const int seg = (nb + DM_SB - 1) / DM_SB, a = t * seg, b = min(nb, a + seg);
-  int s = 0;
-  for (int i = a; i < b; ++i) s += bsum[i];
-  sh[t] = s;
-  __syncthreads();
-  for (int o = 1; o < DM_SB; o <<= 1) {
-    const int u = t >= o ? sh[t - o] : 0;
-    __syncthreads();
-    sh[t] += u;
-    __syncthreads();
-  }
-  int run = sh[t] - s;
-  for (int i = a; i < b; ++i) {
-    const int c = bsum[i];
-    bsum[i] = run;
-    run += c;
-  }
-  if (t == DM_SB - 1) *total_out = sh[t];
-}
-
-__global__ __launch_bounds__(256) void dmap_scan_add(int* __restrict__ start, int* __restrict__ cursor, long long total,
-                                                     const int* __restrict__ boff) {
-  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const int v = start[i] + boff[i / DM_SB];
-  start[i] = v;
-  cursor[i] = v;
-}
-
-// the normalized 15x15 stamp, once per launch: scipy's two float32 passes of the f64 weights
+// the normalized K x K stamp, once per launch: scipy's two float32 passes of the f64 weights
 __global__ void dmap_stamp_kernel(float sigma, int radius, float* __restrict__ stamp) {
   __shared__ double wd[64];
   __shared__ float wf[64];
@@ -460,79 +381,72 @@ __global__ void dmap_stamp_kernel(float sigma, int radius, float* __restrict__ s
   __syncthreads();
   for (int cell = tid; cell < K * K; cell += blockDim.x) {
     const int di = cell / K, dj = cell - (cell / K) * K;
-    stamp[di * 32 + dj] = (float)((double)wf[di] * wd[dj]);
+    stamp[di * DSK + dj] = (float)((double)wf[di] * wd[dj]);
   }
 }
 
-__global__ __launch_bounds__(256) void dmap_fixed_tiled_kernel(const float* __restrict__ pts,
+__global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __restrict__ pts,
                                                                const int64_t* __restrict__ offsets, int H, int W,
                                                                int radius, const float* __restrict__ gstamp,
-                                                               const int* __restrict__ start,
-                                                               const int* __restrict__ list, float* __restrict__ dmap) {
-  __shared__ float stamp[32 * 32];
-  __shared__ int sidx[DM_CAP], prow[DM_CAP], pcol[DM_CAP];
+                                                               float* __restrict__ dmap) {
+  __shared__ float stamp[DSK * DSK];
+  __shared__ int hr[256], hc[256];
+  __shared__ int wcnt[4];
   const int K = 2 * radius + 1;
-  const int tid = threadIdx.x;
-  for (int cell = tid; cell < K * 32; cell += 256) stamp[cell] = gstamp[cell];
-  const int tiles_w = (W + DMTW - 1) / DMTW;
-  const long long T = (long long)((H + DMT - 1) / DMT) * tiles_w;
-  const int ty0 = (blockIdx.x / tiles_w) * DMT, tx0 = (blockIdx.x % tiles_w) * DMTW;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int cell = tid; cell < K * DSK; cell += 256) stamp[cell] = gstamp[cell];
+  const int tiles_w = (W + DFC - 1) / DFC;
+  const int ty0 = (blockIdx.x / tiles_w) * DFR, tx0 = (blockIdx.x % tiles_w) * DFC;
   const int n = blockIdx.y;
-  const int pr = ty0 + tid / 16, pc = tx0 + (tid % 16) * 4;  // pixels (pr, pc .. pc+3)
+  const int pr = ty0 + (tid >> 4) * 2, pc = tx0 + (tid & 15) * 4;  // pixels (pr..pr+1, pc..pc+3)
   const long long p0 = offsets[n], p1 = offsets[n + 1];
-  const long long b = n * T + blockIdx.x;
-  const int s0 = start ? start[b] : 0, m = start ? start[b + 1] - s0 : 0;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  auto add = [&](int r, int c) {
-    const int di = pr - r + radius;
-    if ((unsigned)di >= (unsigned)K) return;
+  float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  for (long long base = p0; base < p1; base += 256) {
+    const long long q = base + tid;
+    int r = 0, c = 0;
+    bool hit = false;
+    if (q < p1 && dm_point(pts, q, H, W, r, c))
+      hit = r + radius >= ty0 && r - radius < ty0 + DFR && c + radius >= tx0 && c - radius < tx0 + DFC;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) wcnt[wv] = __popcll(m);
+    __syncthreads();  // also publishes the stamp on the first pass
+    int off = 0, tot = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int dj = pc + k - c + radius;
-      if ((unsigned)dj < (unsigned)K) acc[k] += stamp[di * 32 + dj];
+    for (int w = 0; w < 4; ++w) {
+      off += w < wv ? wcnt[w] : 0;
+      tot += wcnt[w];
     }
-  };
-  if (m <= DM_CAP) {
-    for (int e = tid; e < m; e += 256) sidx[e] = list[s0 + e];
-    __syncthreads();
-    for (int e = tid; e < m; e += 256) {  // rank = position in point order (indices are unique)
-      const int v = sidx[e];
-      int rank = 0;
-      for (int j = 0; j < m; ++j) rank += sidx[j] < v;
-      int r, c;
-      dm_point(pts, p0 + v, H, W, r, c);
-      prow[rank] = r;
-      pcol[rank] = c;
+    if (hit) {
+      const int k = off + __popcll(m & ((1ull << lane) - 1ull));
+      hr[k] = r;
+      hc[k] = c;
     }
     __syncthreads();
-    for (int j = 0; j < m; ++j) add(prow[j], pcol[j]);
-  } else {  // over-full bin: walk every point of the image in order, 256 at a time
-    for (long long base = p0; base < p1; base += 256) {
-      __syncthreads();
-      const long long q = base + tid;
-      if (q < p1) {
-        int r, c;
-        const bool ok = dm_point(pts, q, H, W, r, c);
-        prow[tid] = ok ? r : -1000000;
-        pcol[tid] = ok ? c : -1000000;
-      }
-      __syncthreads();
-      const int cnt = (int)min(256ll, p1 - base);
-      for (int j = 0; j < cnt; ++j) {
-        const int r = prow[j], c = pcol[j];
-        if (r + radius < ty0 || r - radius >= ty0 + DMT || c + radius < tx0 || c - radius >= tx0 + DMTW) continue;
-        add(r, c);
+    for (int j = 0; j < tot; ++j) {  // the hits in point order
+      const int rr = hr[j], cc = hc[j];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int di = pr + a - rr + radius;
+        if ((unsigned)di >= (unsigned)K) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int dj = pc + k - cc + radius;
+          if ((unsigned)dj < (unsigned)K) acc[a][k] += stamp[di * DSK + dj];
+        }
       }
     }
+    __syncthreads();  // hr / hc / wcnt are rewritten by the next chunk
   }
-  if (pr < H) {
-    float* o = dmap + ((long long)n * H + pr) * W + pc;
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    if (pr + a >= H) continue;
+    float* o = dmap + ((long long)n * H + pr + a) * W + pc;
     if (pc + 3 < W && (W & 3) == 0) {
-      *(f4v*)o = f4v{acc[0], acc[1], acc[2], acc[3]};
+      *(f4v*)o = f4v{acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k)
-        if (pc + k < W) o[k] = acc[k];
+        if (pc + k < W) o[k] = acc[a][k];
     }
   }
 }
@@ -712,14 +626,10 @@ extern "C" int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx
   return DG_OK;
 }
 
-static int64_t dmap_tiles(int H, int W) { return (int64_t)((H + DMT - 1) / DMT) * ((W + DMTW - 1) / DMTW); }
-
-// workspace (ints): stamp [32*32 floats] | cnt/cursor [bins] | start [bins+1] | bsum [nb+1] | list
+// workspace: the stamp (DSK x DSK floats)
 extern "C" int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints) {
   if (N <= 0 || H <= 0 || W <= 0 || radius < 0 || radius >= 32 || npoints < 0) return DG_ERR_INVALID;
-  const int64_t per_axis = (2 * radius) / DMT + 2;  // tiles one stamp can touch along an axis (rows bound cols)
-  const int64_t bins = (int64_t)N * dmap_tiles(H, W), nb = (bins + DM_SB - 1) / DM_SB;
-  return (1024 + 2 * bins + 1 + nb + 1 + per_axis * per_axis * npoints) * (int64_t)sizeof(int);
+  return (int64_t)DSK * DSK * sizeof(float);
 }
 
 extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W, float sigma,
@@ -727,28 +637,13 @@ extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, 
   DG_REQUIRE(offsets && dmap && workspace && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
   DG_REQUIRE(npoints >= 0 && (npoints == 0 || points));
   hipStream_t st = (hipStream_t)stream;
-  const int64_t T = dmap_tiles(H, W), bins = (int64_t)N * T, nb = (bins + DM_SB - 1) / DM_SB;
-  DG_REQUIRE(T < (1ll << 31) && bins < (1ll << 31));
+  const int64_t T = (int64_t)((H + DFR - 1) / DFR) * ((W + DFC - 1) / DFC);
+  DG_REQUIRE(T < (1ll << 31) && N < 65536);
   float* stamp = (float*)workspace;
-  int* cnt = (int*)workspace + 1024;
-  int* start = cnt + bins;
-  int* bsum = start + bins + 1;
-  int* list = bsum + nb + 1;
   hipLaunchKernelGGL(dmap_stamp_kernel, dim3(1), dim3(256), 0, st, sigma, radius, stamp);
-  if (npoints > 0) {
-    if (hipMemsetAsync(cnt, 0, (size_t)bins * sizeof(int), st) != hipSuccess) return DG_ERR_HIP;
-    const dim3 bg((unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (npoints / N + 255) / 256)), (unsigned)N);
-    hipLaunchKernelGGL((dmap_bin_kernel<0>), bg, dim3(256), 0, st, points, offsets, H, W, radius, cnt, list);
-    hipLaunchKernelGGL(dmap_scan_blocks, dim3((unsigned)nb), dim3(DM_SB), 0, st, (const int*)cnt, (long long)bins,
-                       start, bsum);
-    hipLaunchKernelGGL(dmap_scan_sums, dim3(1), dim3(DM_SB), 0, st, bsum, (int)nb, start + bins);
-    hipLaunchKernelGGL(dmap_scan_add, dim3((unsigned)((bins + 255) / 256)), dim3(256), 0, st, start, cnt,
-                       (long long)bins, (const int*)bsum);
-    hipLaunchKernelGGL((dmap_bin_kernel<1>), bg, dim3(256), 0, st, points, offsets, H, W, radius, cnt, list);
-  }
-  const dim3 grid((unsigned)T, (unsigned)N);
-  hipLaunchKernelGGL(dmap_fixed_tiled_kernel, grid, dim3(256), 0, st, points, offsets, H, W, radius,
-                     (const float*)stamp, npoints > 0 ? (const int*)start : nullptr, (const int*)list, dmap);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(dmap_fixed_fused_kernel, dim3((unsigned)T, (unsigned)N), dim3(256), 0, st, points, offsets, H, W,
+                     radius, (const float*)stamp, dmap);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -710,7 +710,12 @@ __global__ __launch_bounds__(256) void sw_bwd_apply(const T* __restrict__ gy, lo
   }
 }
 
-inline int sw_nb(int HW) { return std::max(1, std::min(64, dg_cdiv(HW, 1024))); }
+// pixel blocks per instance of the covariance / backward partial passes: enough blocks over the
+// batch to give every CU two (the deep 48x64 layers had 3 per instance, 48 blocks in all: the
+// backward partials ran at 0.3 TB/s), each at least 64 pixels, at most 64 per instance
+inline int sw_nb(int HW, int N) {
+  return std::max(1, std::min({64, std::max(1, HW / 64), std::max(dg_cdiv(HW, 1024), dg_cdiv(512, N))}));
+}
 
 }  // namespace
 
@@ -767,7 +772,7 @@ extern "C" int64_t dg_sw_moments_size(int C) {
 }
 
 static int64_t sw_ws_core(int N, int HW, int C) {  // partials + coefficients, 8-B aligned
-  const int64_t G = C / SWC, nb = sw_nb(HW);
+  const int64_t G = C / SWC, nb = sw_nb(HW, N);
   const int64_t fwd = std::max<int64_t>(dg_instnorm_workspace(N, HW, C), 0) + (int64_t)N * C * 4 +
                       (int64_t)N * nb * G * 256 * 4;
   const int64_t bwd = (int64_t)N * nb * G * 272 * 4 + (int64_t)N * G * 528 * 4 + G * 4 * 4 +
@@ -806,7 +811,7 @@ extern "C" int dg_sw_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int
   DG_REQUIRE(x && save && moments && workspace && N > 0 && HW > 0 && C > 0);
   SW_CHECK_SHAPE(dtype, C, 0, ldx);
   hipStream_t st = (hipStream_t)stream;
-  const int G = C / SWC, nb = sw_nb(HW), ppb = dg_cdiv(HW, nb);
+  const int G = C / SWC, nb = sw_nb(HW, N), ppb = dg_cdiv(HW, nb);
   float* mu = save;  // mu_in is the first save slot
   char* w = (char*)workspace;
   const int64_t in_ws = dg_instnorm_workspace(N, HW, C);
@@ -885,7 +890,7 @@ extern "C" int dg_sw_bwd_stats(int dtype, const void* gy, int64_t ldg, const voi
   DG_REQUIRE(N > 0 && HW > 0 && C > 0 && T >= 0);
   SW_CHECK_SHAPE(dtype, C, T, ldx, ldg, act ? ldy : ldx);
   hipStream_t st = (hipStream_t)stream;
-  const int G = C / SWC, nb = sw_nb(HW), ppb = dg_cdiv(HW, nb);
+  const int G = C / SWC, nb = sw_nb(HW, N), ppb = dg_cdiv(HW, nb);
   const float* mu = save;
   float* part = (float*)workspace;
   float* coef = part + (int64_t)N * nb * G * 272;
@@ -920,7 +925,7 @@ extern "C" int dg_sw_bwd_finish(int dtype, const void* gy, int64_t ldg, const vo
   DG_REQUIRE(N > 0 && HW > 0 && C > 0);
   SW_CHECK_SHAPE(dtype, C, 0, ldx, ldg, lddx, act ? ldy : ldx);
   hipStream_t st = (hipStream_t)stream;
-  const int G = C / SWC, nb = sw_nb(HW);
+  const int G = C / SWC, nb = sw_nb(HW, N);
   const float* mu = save;
   float* part = (float*)workspace;
   float* coef = part + (int64_t)N * nb * G * 272;

@@ -562,9 +562,9 @@ int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
 int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
                   float sigma, int radius, float* dmap, void* stream);
 
-/* Deterministic dg_dmap_fixed (no atomics on the map): the points are binned by 16x64 tile,
- * each tile's bin is sorted back into point order and every pixel sums its stamp values in
- * that order, the reference's f32 accumulation order: bit-identical to
+/* Deterministic dg_dmap_fixed (no atomics on the map), two launches: the stamp, then one block
+ * per 32x64 tile walking its image's points in order (hits compacted in point order), so every
+ * pixel sums its stamp values in the reference's f32 accumulation order: bit-identical to
  * gaussian_filter_density_fixed and run to run.  dmap fully written (no memset needed).
  * npoints = offsets[N] (host value); workspace: dg_dmap_fixed_tiled_workspace bytes (points
  * may be NULL when npoints == 0). */

@@ -63,9 +63,9 @@ def test_dmap_fixed_tiled_dense_bit_exact_and_stable(dev):
 
 @pytest.mark.gpu
 def test_dmap_fixed_tiled_overfull_bin(dev):
-    """A bin above the in-LDS sort capacity (1500 points inside one 16x16 tile, plus a
-    sparse background): that tile walks the image's points in order instead; still
-    bit-identical to the oracle and run to run."""
+    """1500 points inside one 16x16 region plus a sparse background: a tile whose hits span
+    several 256-point chunks of the image's point list; still bit-identical to the oracle and
+    run to run."""
     from dgvcc_amd.utils.dmap_gen import gaussian_filter_density_fixed_batch
     rng = np.random.default_rng(9)
     H, W = 96, 128

@@ -79,6 +79,10 @@ def test_train_step_oracle(name, mode, cls_name):
         assert np.allclose(outs[0].numpy(), g["out_dc1"], rtol=1e-5, atol=1e-5)
         assert np.allclose(outs[2].numpy(), g["out_c1"], rtol=1e-5, atol=1e-6)
         assert abs(outs[4].item() - g["out_loss_con"][0]) <= 1e-5 * abs(g["out_loss_con"][0])
-    check_summary("grad__", grads, g, rtol=1e-4, atol=1e-7)
-    check_summary("post__", {k: v for k, v in sd1.items() if not k.endswith("num_batches_tracked")},
+    # conv biases right before a BatchNorm (vgg16_bn's) have mathematically zero gradients: their
+    # values are rounding noise of whichever CPU ran the reference, not a property of the oracle
+    pre_bn = {f"{s}.{i}.bias" for s, idx in O.ENC_CONVS.items() for i in idx}
+    check_summary("grad__", {k: v for k, v in grads.items() if k not in pre_bn}, g, rtol=1e-4, atol=1e-7)
+    # (and AdamW's first step moves them by lr x the sign of that noise)
+    check_summary("post__", {k: v for k, v in sd1.items() if not k.endswith("num_batches_tracked") and k not in pre_bn},
                   g, rtol=1e-5, atol=1e-7)
