@@ -421,6 +421,15 @@ class CatConvLayer(ConvLayer):
 # ---------------------------------------------------------------------------
 # VGG16-BN encoder (features[0:43]) + density decoder (models/models.py:35-87)
 # ---------------------------------------------------------------------------
+_FEATURE_PLANS = __import__("weakref").WeakSet()
+
+
+def feature_plans_of(params) -> list:
+    """The live FeaturePlans whose parameters are all in `params` (an optimizer's group)."""
+    ps = set(params)
+    return [plan for plan in list(_FEATURE_PLANS) if all(p in ps for p in plan.params())]
+
+
 class FeaturePlan:
     """forward_fe of DGModel_base: img [N,3,H,W] f32 -> (y1, y2, y3, x3) NHWC, where the
     reference's y_cat = cat[y1, up2(y2), up4(y3)] (models/models.py:84) is left to the heads'
@@ -439,6 +448,8 @@ class FeaturePlan:
         self.dec = [ConvLayer(cb.conv, cb.bn, ACT_RELU if cb.relu is not None else ACT_NONE)
                     for d in (model.dec3, model.dec2, model.dec1) for cb in d]
         self.layers = self.enc + self.dec
+        self.sink = None
+        _FEATURE_PLANS.add(self)
         for l in self.enc:
             l.scope = "enc"
         for l in self.dec:
@@ -451,6 +462,10 @@ class FeaturePlan:
         N, _, H, W = img.shape
         if H % 16 or W % 16:
             raise ValueError(f"input H,W must be multiples of 16 (got {H}x{W})")
+        # data-parallel gradient sink (dgvcc_amd.dist.OverlapReducer, attached by the optimizer):
+        # the backward hands each layer's parameter gradients to it as soon as they exist
+        if tape is not None and self.sink is not None and self.sink.active:
+            self.sink.forward_seen()
         dev = img.device
         E, D = self.enc, self.dec
         nh = lambda h, w, c: Act(K.nhwc(N, h, w, c, dt, dev))  # noqa: E731
@@ -541,7 +556,7 @@ class FeaturePlan:
                 return Act(K.nhwc(N, h, w, c, dt, dev, zero=True))
             return Act(g.to(dt).contiguous().clone())
 
-        grads = {}
+        grads = _SinkDict(self.sink)
         # decoder
         g_a17 = nh(H // 4, W // 4, 256)
         grads.update(D[5].backward(tape, own(g_y1, H // 4, W // 4, 128), g_a17, gx_bn=D[4]))
@@ -593,6 +608,18 @@ class FeaturePlan:
         g_a = nh(H, W, 64); grads.update(E[1].backward(tape, None, g_a, g_pool=g_p1))
         grads.update(E[0].backward(tape, g_a, None))
         return (), grads
+
+
+class _SinkDict(dict):
+    """The FeaturePlan backward's {param: grad}: each layer's batch passes through the plan's
+    data-parallel gradient sink first (if any), which keeps what it reduces itself."""
+
+    def __init__(self, sink):
+        super().__init__()
+        self.sink = sink
+
+    def update(self, grads):
+        super().update(self.sink.emit(grads) if self.sink is not None else grads)
 
 
 class _PlanFn(torch.autograd.Function):

@@ -10,22 +10,30 @@ update — the only collective on the hot path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
+from . import engine as E
 from . import kernels as K
-from .dist import average_flat_
+from .dist import OverlapReducer, average_flat_, world
 from .engine import invalidate_frozen
 from ._capi import call, ptr, stream
 
 
 class AdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2,
-                 amsgrad=False, allreduce=True):
+                 amsgrad=False, allreduce=True, overlap=None, bucket_mb=32.0):
         if amsgrad:
             raise ValueError("amsgrad is not supported by the fused AdamW")
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.allreduce = allreduce
+        # overlap (or DGVCC_DP_OVERLAP=1): the FeaturePlan parameters' all-reduce runs in buckets
+        # under the backward (dgvcc_amd.dist.OverlapReducer), from the second step on
+        if overlap is None:
+            overlap = os.environ.get("DGVCC_DP_OVERLAP", "0") == "1"
+        self.reducer = OverlapReducer(bucket_mb) if (overlap and allreduce) else None
         # fp16 mode: the loss was multiplied by grad_scale before backward (LossScaler); the
         # step unscales the flat gradient and skips the update when it holds inf/NaN
         self.grad_scale = None
@@ -98,8 +106,10 @@ class AdamW(torch.optim.Optimizer):
                                      device=g.device) for i0, i1 in runs]
             cache = (live, runs, dev_offs)
             group["_live_cache"] = cache
-            if not all(live):
-                g.zero_()  # dead regions stay zero (the all-reduce sums them harmlessly)
+            offs = group["_offs"]
+            for i, l in enumerate(live):  # dead regions stay zero (the all-reduce sums them harmlessly)
+                if not l and ps[i].numel():
+                    g[offs[i]:offs[i] + ps[i].numel()].zero_()
         _, runs, dev_offs = cache
         tables = []
         for (i0, i1), o in zip(runs, dev_offs):
@@ -125,9 +135,25 @@ class AdamW(torch.optim.Optimizer):
             if all(p.grad is None for p in group["params"]):
                 continue
             self._ensure_flat(group)
+            red = self.reducer if (self.reducer is not None and self.reducer.active
+                                   and self.reducer.flat is group["_g"]) else None
+            if red is not None and not red.finish():  # the FeaturePlan buckets, reduced under the backward
+                red = None
             runs = self._gather(group)
             g = group["_g"]
-            if self.allreduce:
+            if red is not None:
+                offs, ps = group["_offs"], group["params"]
+                i = 0
+                while i < len(ps):  # the maximal runs of parameters outside the buckets
+                    if ps[i] in red.slot:
+                        i += 1
+                        continue
+                    j = i
+                    while j < len(ps) and ps[j] not in red.slot:
+                        j += 1
+                    average_flat_(g[offs[i]:offs[j - 1] + ps[j - 1].numel()])
+                    i = j
+            elif self.allreduce:
                 average_flat_(g)
             if self.grad_scale is not None and self.grad_scale != 1.0:
                 flag = group.setdefault("_inf", torch.zeros(1, dtype=torch.int32, device=g.device))
@@ -144,6 +170,17 @@ class AdamW(torch.optim.Optimizer):
             for a, b, step in self._step_runs(group, runs):
                 K.adamw_step(flat[a:b], g[a:b], m[a:b], v[a:b], group["lr"], b1, b2,
                              group["eps"], group["weight_decay"], step)
+        if self.reducer is not None and world() > 1 and len(self.param_groups) == 1 and self.reducer.flat is None:
+            group = self.param_groups[0]
+            if "_g" in group:  # from the next step on: the sink of the FeaturePlan backward
+                plans = E.feature_plans_of(group["params"])
+                self.reducer.attach(group["_g"], group["params"], group["_offs"],
+                                    [p for plan in plans for p in plan.params()])
+                if self.reducer.buckets:
+                    for plan in plans:
+                        plan.sink = self.reducer
+                else:  # no FeaturePlan parameters (the ResNet trunks): the ordinary path
+                    self.reducer = None
         return loss
 
     @staticmethod

@@ -3,7 +3,8 @@ the configs/jhu_fog2snow.yml step — DGModel_final, DGTrainer 'final' mode, fus
 its flat-gradient all-reduce — run data-parallel over the ranks' halves of a 4-frame batch
 must leave exactly the parameters of a single-process emulation: each half's gradients
 computed separately (per-rank BatchNorm statistics, as DDP without SyncBN), averaged, then
-one AdamW step.  Dropouts are off so both runs see the same masks."""
+one AdamW step.  Dropouts are off so both runs see the same masks.  Then the backward-overlapped
+bucketed all-reduce equals the single collective bit for bit over three steps."""
 import os
 import sys
 import tempfile
@@ -91,6 +92,22 @@ def main():
         if worst > 1e-6:
             fails.append(("post-step params vs emulation", worst))
         print(f"RANK0 worst_rel={worst:.3e} loss_dp={loss_dp:.6f} loss_half0={losses[0]:.6f}", flush=True)
+    # backward-overlapped bucketed all-reduce (dgvcc_amd.dist.OverlapReducer, active from the second
+    # step): three steps leave exactly the parameters of the one-collective-after-backward path
+    finals = []
+    for overlap in (False, True):
+        m = build(dev, sd0)
+        opt = AdamW(m.parameters(), lr=1e-4, weight_decay=1e-4, overlap=overlap, bucket_mb=8.0)
+        for _ in range(3):
+            tr.train_step(m, MSELoss(), opt, to_dev(half(batch, rank, world), dev), 0)
+        if overlap:
+            red = opt.reducer
+            if red is None or len(red.buckets) < 3 or m._get_plans()["fe"].sink is not red:
+                fails.append("overlap reducer not attached")
+        finals.append({k: v.detach().clone() for k, v in m.named_parameters()})
+    diff = [k for k in finals[0] if not torch.equal(finals[0][k], finals[1][k])]
+    if diff:
+        fails.append(("overlapped all-reduce differs", diff[:5]))
     os.chdir(cwd)
     print(f"RANK{rank} {'OK' if not fails else 'FAIL ' + repr(fails)}", flush=True)
     dist.destroy_process_group()
