@@ -430,10 +430,47 @@ def dmap_roofline(args, dev, reps=20):
         key = "deterministic" if det else "atomic"
         out[key] = {"us_per_launch": round(us, 2), "achieved": round(nbytes / (us * 1e-6) / 1e9, 1),
                     "frac": round(nbytes / (us * 1e-6) / 1e9 / 8000.0, 4)}
-    out["kernel"] = ("dmap_stamp_kernel + dmap_fixed_fused_kernel (default, 2 launches: one block per 32x64 tile "
+    out["kernel"] = ("dmap_fixed_fused_kernel (default, 1 launch: one block per 64x64 tile "
                      "walks its image's points in order, bit-identical to the reference) / memset + dmap_fixed_kernel "
                      "(f32 atomics)")
     return out
+
+
+def bl_timing(args, dev, reps=20):
+    """sta_final's BL leg (SURVEY.md §8 config mapping): losses/bl.py BL(points, st_sizes,
+    targets, pre_density) forward + backward on the workload's frames, with the synthetic BL
+    parameters of SURVEY.md (sigma 8, background ratio 1, background row on, c_size 768,
+    stride 8: the x8 avg-pooled density on a 96 x 96 grid of the frame's 768 x 768 crop).
+    Work unit: one (row, cell) posterior term -- rows = points + one background row per image,
+    cells = G^2 -- evaluated in each of the kernel's three exp passes (statistics, counts,
+    gradient); VALU/transcendental-bound, so the line reports the rate, not an HBM fraction."""
+    from dgvcc_amd.losses.bl import BL
+    B, c_size, stride = args.batch, 768, 8
+    G = c_size // stride
+    g = torch.Generator(device="cpu").manual_seed(1001)
+    n = torch.poisson(torch.full((B,), 500.0 * c_size * c_size / (H0 * W0)), generator=g).long().clamp_min(1)
+    pts = [(torch.rand(int(k), 2, generator=g) * c_size).to(dev) for k in n]
+    tg = [torch.ones(int(k), device=dev) for k in n]
+    st = [float(c_size)] * B
+    dens = torch.rand(B, 1, G, G, generator=g).to(dev).requires_grad_(True)
+    crit = BL(8.0, c_size, stride, 1.0, True, dev)
+    for _ in range(3):
+        crit(pts, st, tg, dens).backward()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        dens.grad = None
+        loss = crit(pts, st, tg, dens)
+        loss.backward()
+    e.record()
+    torch.cuda.synchronize()
+    us = s.elapsed_time(e) * 1e3 / reps
+    terms = 3.0 * (int(n.sum()) + B) * G * G
+    return {"us_per_step": round(us, 2), "frames": B, "points": int(n.sum()), "grid": f"{G}x{G}",
+            "posterior_terms_per_s": round(terms / (us * 1e-6), 1), "bound": "valu (exp per posterior term)",
+            "loss": round(float(loss.item()), 4),
+            "note": "fwd + bwd through the autograd path (host packing of the point lists included)"}
 
 
 def cpu_baseline(args, seconds):
@@ -635,6 +672,7 @@ def main():
             out["perf_bf16"]["params_in_sync"] = rb["params_in_sync"]
     if rank == 0 and not args.trunk:
         out["dmap"] = dmap_roofline(args, dev)
+        out["bl"] = bl_timing(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.trunk:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:

@@ -584,6 +584,10 @@ constexpr int PBM = 256;   // pixels per tile
 __device__ __forceinline__ void lds_dma16(__amdgpu_buffer_rsrc_t r, const char* lds, unsigned voff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (DG_LDS void*)lds, 16, voff, 0, 0, 0);
 }
+// the same with a wave-uniform byte offset added (the instruction's scalar offset operand)
+__device__ __forceinline__ void lds_dma16s(__amdgpu_buffer_rsrc_t r, const char* lds, unsigned voff, unsigned soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (DG_LDS void*)lds, 16, voff, soff, 0, 0);
+}
 constexpr int PSTAGES = 3;
 
 // EPI selects the epilogue at compile time (each variant's registers stay out of the
@@ -1082,20 +1086,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
 #pragma unroll
   for (int i = 0; i < BI; ++i) cbytes[i] = (unsigned)(((lane & 7) ^ psw_b((((wid * BI + i) & 1) << 3) + lrow)) * 16);
   // A source offsets (bytes, K-step 0) of this wave's AI DMA pieces: piece q = plane p, rows rb*16..+15
-  unsigned aoff[AI];
-#pragma unroll
-  for (int q = 0; q < AI; ++q) {
+  // = a lane part (row (lane >> 2) of a 16-row block; the swizzle only sees row & 15) + a
+  // wave-uniform part per piece (scalar offset of the DMA), so the pieces cost one VGPR
+  const unsigned alane = (unsigned)((lane >> 2) * KT * 192 + (((lane & 3) ^ psw_a(lane >> 2)) * 16));
+  auto aoff_s = [&](int q) -> unsigned {
     const int gq = wid * AI + q;
     const int pl = gq / (BN / 16), rb = gq % (BN / 16);
-    const int row = rb * 16 + (lane >> 2);
-    const int lch = (lane & 3) ^ psw_a(row);
-    aoff[q] = (unsigned)(row * KT * 192 + pl * 64 + lch * 16);
-  }
+    return (unsigned)(rb * 16 * KT * 192 + pl * 64);
+  };
 
   struct Ctx {
     int px0, co0;
     __amdgpu_buffer_rsrc_t xr, wr;
-    int pp[BI], pq[BI], prow[BI];
+    int pp[BI], pq[BI], prow0;  // piece i's window row: prow0 + 8 i
   };
   auto setup = [&](int lin, Ctx& c) {
     const int t = xcd_remap(lin, ntile);
@@ -1109,6 +1112,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     }
     const int halo = a.pad * (a.W + 1);
     const int plo = max(0, c.px0 - halo);
+    c.prow0 = c.px0 + wid * BI * 8 + lrow - plo;
     const int phi = min(M, c.px0 + PSB + halo);
     const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 4);
     c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 4), 0, win_bytes, 0x00020000);
@@ -1118,7 +1122,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     for (int i = 0; i < BI; ++i) {
       const int m = c.px0 + (wid * BI + i) * 8 + lrow;
       const int rem = m % HW;
-      c.prow[i] = m - plo;
       c.pp[i] = (m < M) ? rem / a.W : -100000;
       c.pq[i] = rem % a.W;
     }
@@ -1129,14 +1132,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     char* As = smem + stage * STAGE;
     char* Bs = As + A_BYTES;
 #pragma unroll
-    for (int q = 0; q < AI; ++q) lds_dma16(c.wr, As + (wid * AI + q) * 1024, aoff[q] + (unsigned)(kt * 192));
+    for (int q = 0; q < AI; ++q) lds_dma16s(c.wr, As + (wid * AI + q) * 1024, alane + (unsigned)(kt * 192), aoff_s(q));
     const int dh = r - a.pad, dw = s2 - a.pad;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int hh = c.pp[i] + dh, ww = c.pq[i] + dw;
       const bool ok = (unsigned)hh < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
       const unsigned off =
-          ok ? (unsigned)(((long long)(c.prow[i] + dh * a.W + dw) * a.ldx + cb * 32) * 4) + cbytes[i] : 0xFFFFFFF0u;
+          ok ? (unsigned)(((long long)((c.prow0 + 8 * i) + dh * a.W + dw) * a.ldx + cb * 32) * 4) + cbytes[i] : 0xFFFFFFF0u;
       lds_dma16(c.xr, Bs + (wid * BI + i) * 1024, off);
     }
   };

@@ -346,15 +346,19 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
 // Deterministic variant (no atomics on the map): every output pixel sums its stamp values in
 // point order, the reference's `density += gaussian_filter(pt2d)` f32 accumulation
 // (dmap_gen.py:72-79) exactly, so the map is bit-identical to the reference's and stable run
-// to run.  Two launches: the normalized stamp once (scipy's float64 weights, two float32 passes),
-// then one 256-thread block per 32 x 64 output tile that walks its image's points in order,
-// 256 at a time: each thread tests one point's stamp against the tile, the hits are compacted in
-// point order (wave ballots + an LDS prefix over the 4 waves), and every thread adds the hits'
-// stamp values to its 2 x 4 pixels.  No binning pass, no scan, no atomics: the point list of an
-// image (8 B per point) is read once per tile from L2, the map written once with 16-B stores.
-constexpr int DFR = 32;  // tile rows    (2 per thread)
+// to run.  One launch, one 256-thread block per 64 x 64 output tile: the block first forms the
+// normalized 1-D weights (scipy's float64 kernel, dmap_gen.py's gaussian_filter) in LDS, then walks
+// its image's points in order, 256 at a time: each thread tests one point's stamp against the
+// tile, the hits are compacted in point order (wave ballots + an LDS prefix over the 4 waves), and
+// every thread adds the hits' stamp values -- (float)(wf[di] * wd[dj]), scipy's two float32 passes
+// -- to its 4 x 4 pixels.  No stamp table, no binning pass, no scan, no atomics: the point list of
+// an image (8 B per point) is read once per tile from L2, the map written once with 16-B stores.
+// Measured against the alternatives (16 frames of 768 x 1024, ~490 points each, HIP-graph
+// replay): 19.8 us here; 128 x 64 tiles (half the blocks, one CU-slot round) 27.1 us; one
+// barrier-free wave per 32 x 64 strip (ballot + lane-permute walk of every point) 24.9 us; the
+// earlier stamp-table launch + 32 x 64 tiles 20.7 us.
+constexpr int DFR = 64;  // tile rows    (4 per thread)
 constexpr int DFC = 64;  // tile columns (4 per thread: one 16-B store per row)
-constexpr int DSK = 64;  // stamp row stride (radius < 32 -> K <= 63)
 
 // int() truncation and numpy's negative-index wrap of gaussian_filter_density_fixed
 __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long long q, int H, int W, int& r, int& c) {
@@ -366,41 +370,32 @@ __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long lon
   return in && r >= 0 && c >= 0;
 }
 
-// the normalized K x K stamp, once per launch: scipy's two float32 passes of the f64 weights
-__global__ void dmap_stamp_kernel(float sigma, int radius, float* __restrict__ stamp) {
-  __shared__ double wd[64];
-  __shared__ float wf[64];
-  const int K = 2 * radius + 1, tid = threadIdx.x;
-  if (tid < K) {
-    double s = 0.0;
-    for (int i = -radius; i <= radius; ++i) s += exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
-    const int i = tid - radius;
-    wd[tid] = exp(-0.5 / ((double)sigma * sigma) * (double)(i * i)) / s;
-    wf[tid] = (float)wd[tid];
-  }
-  __syncthreads();
-  for (int cell = tid; cell < K * K; cell += blockDim.x) {
-    const int di = cell / K, dj = cell - (cell / K) * K;
-    stamp[di * DSK + dj] = (float)((double)wf[di] * wd[dj]);
-  }
-}
-
 __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __restrict__ pts,
                                                                const int64_t* __restrict__ offsets, int H, int W,
-                                                               int radius, const float* __restrict__ gstamp,
-                                                               float* __restrict__ dmap) {
-  __shared__ float stamp[DSK * DSK];
+                                                               float sigma, int radius, float* __restrict__ dmap) {
+  __shared__ double ex[64], wd[64];
+  __shared__ float wf[64];
   __shared__ int hr[256], hc[256];
   __shared__ int wcnt[4];
   const int K = 2 * radius + 1;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int cell = tid; cell < K * DSK; cell += 256) stamp[cell] = gstamp[cell];
+  if (tid < K) {
+    const int i = tid - radius;
+    ex[tid] = exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+  }
   const int tiles_w = (W + DFC - 1) / DFC;
   const int ty0 = (blockIdx.x / tiles_w) * DFR, tx0 = (blockIdx.x % tiles_w) * DFC;
   const int n = blockIdx.y;
-  const int pr = ty0 + (tid >> 4) * 2, pc = tx0 + (tid & 15) * 4;  // pixels (pr..pr+1, pc..pc+3)
+  const int pr = ty0 + (tid >> 4) * 4, pc = tx0 + (tid & 15) * 4;  // pixels (pr..pr+3, pc..pc+3)
   const long long p0 = offsets[n], p1 = offsets[n + 1];
-  float acc[2][4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  __syncthreads();
+  if (tid < K) {  // phi / phi.sum(), summed in index order
+    double s = 0.0;
+    for (int j = 0; j < K; ++j) s += ex[j];
+    wd[tid] = ex[tid] / s;
+    wf[tid] = (float)wd[tid];
+  }
+  float acc[4][4] = {};
   for (long long base = p0; base < p1; base += 256) {
     const long long q = base + tid;
     int r = 0, c = 0;
@@ -409,7 +404,7 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
       hit = r + radius >= ty0 && r - radius < ty0 + DFR && c + radius >= tx0 && c - radius < tx0 + DFC;
     const unsigned long long m = __ballot(hit);
     if (lane == 0) wcnt[wv] = __popcll(m);
-    __syncthreads();  // also publishes the stamp on the first pass
+    __syncthreads();  // also publishes the weights on the first pass
     int off = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
@@ -423,22 +418,24 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     }
     __syncthreads();
     for (int j = 0; j < tot; ++j) {  // the hits in point order
-      const int rr = hr[j], cc = hc[j];
+      const int di0 = pr - hr[j] + radius, dj0 = pc - hc[j] + radius;
+      if (di0 + 3 < 0 || di0 >= K || dj0 + 3 < 0 || dj0 >= K) continue;
 #pragma unroll
-      for (int a = 0; a < 2; ++a) {
-        const int di = pr + a - rr + radius;
+      for (int a = 0; a < 4; ++a) {
+        const int di = di0 + a;
         if ((unsigned)di >= (unsigned)K) continue;
+        const double f = (double)wf[di];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          const int dj = pc + k - cc + radius;
-          if ((unsigned)dj < (unsigned)K) acc[a][k] += stamp[di * DSK + dj];
+          const int dj = dj0 + k;
+          if ((unsigned)dj < (unsigned)K) acc[a][k] += (float)(f * wd[dj]);
         }
       }
     }
     __syncthreads();  // hr / hc / wcnt are rewritten by the next chunk
   }
 #pragma unroll
-  for (int a = 0; a < 2; ++a) {
+  for (int a = 0; a < 4; ++a) {
     if (pr + a >= H) continue;
     float* o = dmap + ((long long)n * H + pr + a) * W + pc;
     if (pc + 3 < W && (W & 3) == 0) {
@@ -626,24 +623,21 @@ extern "C" int dg_tanh_bwd(const float* y, const float* gy, int64_t n, float* gx
   return DG_OK;
 }
 
-// workspace: the stamp (DSK x DSK floats)
+// no workspace (kept in the ABI for callers that size one: 0 bytes)
 extern "C" int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints) {
   if (N <= 0 || H <= 0 || W <= 0 || radius < 0 || radius >= 32 || npoints < 0) return DG_ERR_INVALID;
-  return (int64_t)DSK * DSK * sizeof(float);
+  return 0;
 }
 
 extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W, float sigma,
                                    int radius, int64_t npoints, void* workspace, float* dmap, void* stream) {
-  DG_REQUIRE(offsets && dmap && workspace && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
+  (void)workspace;
+  DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
   DG_REQUIRE(npoints >= 0 && (npoints == 0 || points));
-  hipStream_t st = (hipStream_t)stream;
   const int64_t T = (int64_t)((H + DFR - 1) / DFR) * ((W + DFC - 1) / DFC);
   DG_REQUIRE(T < (1ll << 31) && N < 65536);
-  float* stamp = (float*)workspace;
-  hipLaunchKernelGGL(dmap_stamp_kernel, dim3(1), dim3(256), 0, st, sigma, radius, stamp);
-  DG_CHECK_LAUNCH();
-  hipLaunchKernelGGL(dmap_fixed_fused_kernel, dim3((unsigned)T, (unsigned)N), dim3(256), 0, st, points, offsets, H, W,
-                     radius, (const float*)stamp, dmap);
+  hipLaunchKernelGGL(dmap_fixed_fused_kernel, dim3((unsigned)T, (unsigned)N), dim3(256), 0, (hipStream_t)stream,
+                     points, offsets, H, W, sigma, radius, dmap);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

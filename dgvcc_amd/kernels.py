@@ -463,9 +463,9 @@ def dmap_fixed(points: torch.Tensor, offsets: torch.Tensor, N: int, H: int, W: i
         return out
     npts = points.numel() // 2
     ws = query("dg_dmap_fixed_tiled_workspace", N, H, W, int(radius), npts)
-    work = torch.empty(ws // 4 + 1, dtype=torch.int32, device=offsets.device)
-    call("dg_dmap_fixed_tiled", pp, ptr(offsets), N, H, W, float(sigma), int(radius), npts, ptr(work),
-         ptr(out), stream())
+    work = torch.empty(ws // 4, dtype=torch.int32, device=offsets.device) if ws else None
+    call("dg_dmap_fixed_tiled", pp, ptr(offsets), N, H, W, float(sigma), int(radius), npts,
+         ptr(work) if ws else None, ptr(out), stream())
     return out
 
 

@@ -5,7 +5,7 @@ The reference adds one full-frame scipy.ndimage.gaussian_filter per point
 (O(N*H*W), ~15 ms/point at 768x1024, dmap_gen.py:72-79).  Here every point is a
 15x15 stamp of scipy's two-pass float32 values, in one HIP launch per batch of images:
 
-* default (`deterministic=True`, dg_dmap_fixed_tiled): one block per 32x64 tile walks its
+* default (`deterministic=True`, dg_dmap_fixed_tiled): one block per 64x64 tile walks its
   image's points in order and sums the stamps that reach it -- the reference's f32
   accumulation order, so the map is bit-identical to the reference and run to run (the
   reference runs under torch.use_deterministic_algorithms, utils/misc.py:131);

@@ -562,12 +562,12 @@ int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count,
 int dg_dmap_fixed(const float* points, const int64_t* offsets, int N, int H, int W,
                   float sigma, int radius, float* dmap, void* stream);
 
-/* Deterministic dg_dmap_fixed (no atomics on the map), two launches: the stamp, then one block
- * per 32x64 tile walking its image's points in order (hits compacted in point order), so every
+/* Deterministic dg_dmap_fixed (no atomics on the map), one launch: one block per 64x64 tile
+ * forms the 1-D weights and walks its image's points in order (hits compacted in point order), so every
  * pixel sums its stamp values in the reference's f32 accumulation order: bit-identical to
  * gaussian_filter_density_fixed and run to run.  dmap fully written (no memset needed).
- * npoints = offsets[N] (host value); workspace: dg_dmap_fixed_tiled_workspace bytes (points
- * may be NULL when npoints == 0). */
+ * npoints = offsets[N] (host value); workspace: dg_dmap_fixed_tiled_workspace bytes (now 0:
+ * NULL is accepted; points may be NULL when npoints == 0). */
 int64_t dg_dmap_fixed_tiled_workspace(int N, int H, int W, int radius, int64_t npoints);
 int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, int N, int H, int W,
                         float sigma, int radius, int64_t npoints, void* workspace, float* dmap, void* stream);
