@@ -430,6 +430,29 @@ def dmap_roofline(args, dev, reps=20):
         key = "deterministic" if det else "atomic"
         out[key] = {"us_per_launch": round(us, 2), "achieved": round(nbytes / (us * 1e-6) / 1e9, 1),
                     "frac": round(nbytes / (us * 1e-6) / 1e9 / 8000.0, 4)}
+    # the write floor of the same map: a plain fill of the [B][H][W] f32 tensor, timed the same way
+    fill = torch.empty((B, H, W), dtype=torch.float32, device=dev)
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fill.fill_(1.0)
+        with torch.cuda.graph(graph, stream=side):
+            for _ in range(reps):
+                fill.fill_(1.0)
+    torch.cuda.current_stream().wait_stream(side)
+    graph.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    graph.replay()
+    e.record()
+    torch.cuda.synchronize()
+    us_fill = s.elapsed_time(e) * 1e3 / reps
+    del graph
+    out["fill_floor"] = {"us_per_launch": round(us_fill, 2), "achieved": round(4.0 * B * H * W / (us_fill * 1e-6) / 1e9, 1),
+                         "note": "torch fill_ of the same map (write-only floor of this launch shape)"}
+    out["deterministic"]["frac_of_fill_floor"] = round(us_fill / out["deterministic"]["us_per_launch"], 4)
     out["kernel"] = ("dmap_fixed_fused_kernel (default, 1 launch: one block per 64x64 tile "
                      "walks its image's points in order, bit-identical to the reference) / memset + dmap_fixed_kernel "
                      "(f32 atomics)")
