@@ -357,10 +357,15 @@ __global__ __launch_bounds__(NT) void dmap_adaptive_kernel(const float* __restri
 // replay): 19.8 us here; 128 x 64 tiles (half the blocks, one CU-slot round) 27.1 us; one
 // barrier-free wave per 32 x 64 strip (ballot + lane-permute walk of every point) 24.9 us; the
 // earlier stamp-table launch + 32 x 64 tiles 20.7 us.
-constexpr int DFR = 64;  // tile rows    (4 per thread)
-constexpr int DFC = 64;  // tile columns (4 per thread: one 16-B store per row)
-
 // int() truncation and numpy's negative-index wrap of gaussian_filter_density_fixed
+__device__ __forceinline__ bool dm_coords(float x, float y, int H, int W, int& r, int& c) {
+  r = (int)y;
+  c = (int)x;
+  const bool in = r < H && c < W;
+  if (r < 0) r += H;
+  if (c < 0) c += W;
+  return in && r >= 0 && c >= 0;
+}
 __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long long q, int H, int W, int& r, int& c) {
   r = (int)pts[2 * q + 1];
   c = (int)pts[2 * q];
@@ -370,6 +375,9 @@ __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long lon
   return in && r >= 0 && c >= 0;
 }
 
+// DFR x DFC tiles, 4 columns per thread (one 16-B store per row), DFC / 4 threads per row,
+// rows strided by 256 / (DFC / 4) within a thread; PF: the first chunk's point loaded before the weights
+template <int DFR, int PF, int DFC = 64>
 __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __restrict__ pts,
                                                                const int64_t* __restrict__ offsets, int H, int W,
                                                                float sigma, int radius, float* __restrict__ dmap) {
@@ -386,8 +394,14 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
   const int tiles_w = (W + DFC - 1) / DFC;
   const int ty0 = (blockIdx.x / tiles_w) * DFR, tx0 = (blockIdx.x % tiles_w) * DFC;
   const int n = blockIdx.y;
-  const int pr = ty0 + (tid >> 4) * 4, pc = tx0 + (tid & 15) * 4;  // pixels (pr..pr+3, pc..pc+3)
+  constexpr int TPR = DFC / 4, RPP = 256 / TPR, RT = DFR / RPP;
+  const int pr = ty0 + tid / TPR, pc = tx0 + (tid % TPR) * 4;  // pixels (pr + a RPP, pc..pc+3), a < RT
   const long long p0 = offsets[n], p1 = offsets[n + 1];
+  float fx = 0.f, fy = 0.f;
+  if (PF && p0 + tid < p1) {
+    fx = pts[2 * (p0 + tid)];
+    fy = pts[2 * (p0 + tid) + 1];
+  }
   __syncthreads();
   if (tid < K) {  // phi / phi.sum(), summed in index order
     double s = 0.0;
@@ -395,13 +409,24 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     wd[tid] = ex[tid] / s;
     wf[tid] = (float)wd[tid];
   }
-  float acc[4][4] = {};
+  float acc[RT][4] = {};
   for (long long base = p0; base < p1; base += 256) {
     const long long q = base + tid;
     int r = 0, c = 0;
     bool hit = false;
-    if (q < p1 && dm_point(pts, q, H, W, r, c))
+    if (PF) {
+      if (q < p1) {
+        const float x = fx, y = fy;
+        if (q + 256 < p1) {
+          fx = pts[2 * (q + 256)];
+          fy = pts[2 * (q + 256) + 1];
+        }
+        if (dm_coords(x, y, H, W, r, c))
+          hit = r + radius >= ty0 && r - radius < ty0 + DFR && c + radius >= tx0 && c - radius < tx0 + DFC;
+      }
+    } else if (q < p1 && dm_point(pts, q, H, W, r, c)) {
       hit = r + radius >= ty0 && r - radius < ty0 + DFR && c + radius >= tx0 && c - radius < tx0 + DFC;
+    }
     const unsigned long long m = __ballot(hit);
     if (lane == 0) wcnt[wv] = __popcll(m);
     __syncthreads();  // also publishes the weights on the first pass
@@ -419,10 +444,10 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     __syncthreads();
     for (int j = 0; j < tot; ++j) {  // the hits in point order
       const int di0 = pr - hr[j] + radius, dj0 = pc - hc[j] + radius;
-      if (di0 + 3 < 0 || di0 >= K || dj0 + 3 < 0 || dj0 >= K) continue;
+      if (di0 + (RT - 1) * RPP < 0 || di0 >= K || dj0 + 3 < 0 || dj0 >= K) continue;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        const int di = di0 + a;
+      for (int a = 0; a < RT; ++a) {
+        const int di = di0 + a * RPP;
         if ((unsigned)di >= (unsigned)K) continue;
         const double f = (double)wf[di];
 #pragma unroll
@@ -435,9 +460,9 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     __syncthreads();  // hr / hc / wcnt are rewritten by the next chunk
   }
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    if (pr + a >= H) continue;
-    float* o = dmap + ((long long)n * H + pr + a) * W + pc;
+  for (int a = 0; a < RT; ++a) {
+    if (pr + a * RPP >= H) continue;
+    float* o = dmap + ((long long)n * H + pr + a * RPP) * W + pc;
     if (pc + 3 < W && (W & 3) == 0) {
       *(f4v*)o = f4v{acc[a][0], acc[a][1], acc[a][2], acc[a][3]};
     } else {
@@ -634,10 +659,20 @@ extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, 
   (void)workspace;
   DG_REQUIRE(offsets && dmap && N > 0 && H > 0 && W > 0 && sigma > 0 && radius >= 0 && radius < 32);
   DG_REQUIRE(npoints >= 0 && (npoints == 0 || points));
-  const int64_t T = (int64_t)((H + DFR - 1) / DFR) * ((W + DFC - 1) / DFC);
+  // DGVCC_DMAP_TILE (A/B): "64" (default), "64p", "32", "32p" -- tile rows, p = prefetched first chunk
+  const char* e = getenv("DGVCC_DMAP_TILE");
+  const bool wide = e && e[0] == 'w';  // "w": 16 x 256 tiles (1-KB row segments per wave store)
+  const int rows = wide ? 16 : (e && e[0] == '3') ? 32 : 64, cols = wide ? 256 : 64;
+  const bool pf = e && e[1] && e[2] == 'p';
+  const int64_t T = (int64_t)((H + rows - 1) / rows) * ((W + cols - 1) / cols);
   DG_REQUIRE(T < (1ll << 31) && N < 65536);
-  hipLaunchKernelGGL(dmap_fixed_fused_kernel, dim3((unsigned)T, (unsigned)N), dim3(256), 0, (hipStream_t)stream,
-                     points, offsets, H, W, sigma, radius, dmap);
+  const dim3 grid((unsigned)T, (unsigned)N);
+  hipStream_t st = (hipStream_t)stream;
+  if (wide) hipLaunchKernelGGL((dmap_fixed_fused_kernel<16, 0, 256>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
+  else if (rows == 32 && pf) hipLaunchKernelGGL((dmap_fixed_fused_kernel<32, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
+  else if (rows == 32) hipLaunchKernelGGL((dmap_fixed_fused_kernel<32, 0>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
+  else if (pf) hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
+  else hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 0>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
