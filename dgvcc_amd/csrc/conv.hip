@@ -780,7 +780,32 @@ constexpr int PERS_BIAS_MAX = 1024;  // Cout limit of the persistent forward (LD
 // SPL = 1 (T = float only): the f32 GEMM on the bf16 matrix cores through the exact 3-way
 // split (dg_common.h split3_8): one 32-channel K-step is one 16x16x32 block, the lane's 8
 // k values being its chunks fc and 4 + fc of the 128-B row for both operands.
-template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0>
+// Tap validity of the B (pixel) DMA pieces of a persistent conv tile, for the incremental
+// addressing (INC): the image-bounds test of tap (r, s) is separable, so each piece keeps 6 bits,
+// rows r = 0..2 at bits 0..2 and columns s = 0..2 at bits 3..5, five pieces per 32-bit word
+// (R, S <= 3).  Tap (r, s) of piece i is inside the image iff both of need(r, s) << 6 (i % 5) are set.
+template <int BI>
+struct TapMask {
+  unsigned w[(BI + 4) / 5];
+};
+template <int BI>
+__device__ __forceinline__ void tapmask_set(TapMask<BI>& t, int i, int pp, int pq, const FwdArgs& a) {
+  if (i % 5 == 0) t.w[i / 5] = 0;
+  unsigned b = 0;
+  for (int r = 0; r < a.R; ++r) b |= ((unsigned)(pp + r - a.pad) < (unsigned)a.H) ? 1u << r : 0u;
+  for (int s2 = 0; s2 < a.S; ++s2) b |= ((unsigned)(pq + s2 - a.pad) < (unsigned)a.W) ? 8u << s2 : 0u;
+  t.w[i / 5] |= b << (6 * (i % 5));
+}
+__device__ __forceinline__ unsigned tap_need(int r, int s2) { return (1u << r) | (8u << s2); }
+template <int BI>
+__device__ __forceinline__ bool tapmask_ok(const TapMask<BI>& t, int i, unsigned need) {
+  const unsigned nd = need << (6 * (i % 5));
+  return (t.w[i / 5] & nd) == nd;
+}
+
+// INC: incremental DMA addressing as in conv_fwd_psplit_kernel (DGVCC_PERS_INC=0 restores the per-K-step
+// recomputation)
+template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0, int INC = 1>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   constexpr int ES = (int)sizeof(T);  // element bytes: a K-step row is 128 B (64 x 16-bit or 32 x f32)
   constexpr int BK = 128 / ES;
@@ -825,6 +850,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
     int px0, co0;
     __amdgpu_buffer_rsrc_t xr, wr;
     int pp[BI], pq[BI], prow[BI];
+    unsigned bofs;        // INC: piece 0's window byte offset (piece i: + 8 i rows)
+    TapMask<BI> tm;       // INC: the pieces' in-image taps
   };
   auto setup = [&](int lin, Ctx& c) {
     const int t = xcd_remap(lin, ntile);
@@ -844,9 +871,53 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       c.prow[i] = m - plo;
       c.pp[i] = (m < M) ? rem / a.W : -100000;
       c.pq[i] = rem % a.W;
+      if constexpr (INC) {
+        if (i == 0) c.bofs = (unsigned)((long long)c.prow[0] * a.ldx * ES) + cbytes;
+        tapmask_set<BI>(c.tm, i, c.pp[i], c.pq[i], a);
+      }
     }
   };
   const int RS = a.R * a.S;
+  // INC: the K-step of the next DMA issue as three digits, fastest first: (s, r, cb) in the
+  // channel-block-major order (a.korder), (cb, s, r) in the tap-major one
+  const bool ko = a.korder != 0;
+  const int L0 = ko ? a.S : CB, L1 = ko ? a.R : a.S;
+  int d0 = 0, d1 = 0, d2 = 0;
+  auto issue_inc = [&](const Ctx& c, unsigned stage) {
+    const int is = ko ? d0 : d1, ir = ko ? d1 : d2, icb = ko ? d2 : d0;
+    const int rs = ir * a.S + is;
+    char* As = smem + stage * STAGE;
+    char* Bs = As + BN * 128;
+    const unsigned kofs = (unsigned)((rs * a.C + icb * BK) * ES);
+#pragma unroll
+    for (int i = 0; i < AI; ++i) lds_dma16(c.wr, As + (wid * AI + i) * 1024, aoff[i] + kofs);
+    const unsigned toff = (unsigned)((((ir - a.pad) * a.W + (is - a.pad)) * a.ldx + icb * BK) * ES);
+    const unsigned need = tap_need(ir, is);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      lds_dma16(c.xr, Bs + (wid * BI + i) * 1024,
+                tapmask_ok<BI>(c.tm, i, need) ? c.bofs + (toff + (unsigned)(i * 8 * a.ldx * ES)) : 0xFFFFFFF0u);
+    d0 += 1;
+    if (d0 == L0) {
+      d0 = 0;
+      d1 += 1;
+      if (d1 == L1) {
+        d1 = 0;
+        d2 += 1;
+      }
+    }
+  };
+  // the step PF ahead of consumed step t, possibly the next tile's
+  auto issue_ahead = [&](const Ctx& c, const Ctx& n, int t, bool hn, unsigned stage) {
+    const int u = t + PF;
+    if constexpr (INC) {
+      if (u < KT) issue_inc(c, stage);
+      else if (hn) {
+        if (u == KT) d0 = d1 = d2 = 0;
+        issue_inc(n, stage);
+      }
+    }
+  };
   auto issue = [&](const Ctx& c, int kt, int stage) {
     const int rs = a.korder ? kt % RS : kt / CB, cb = a.korder ? kt / RS : kt - rs * CB;
     const int r = rs / a.S, s2 = rs - r * a.S;
@@ -883,9 +954,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   if (has_next) setup(lin + G, nxt);
   const int wpx = (wid & 3) * 64, wco = (wid >> 2) * (BN / 2);
   const int fr = lane & 15, fc = lane >> 4;
-  int gs = 0;  // K-steps issued/consumed across all tiles of this block
-  issue(cur, 0, 0);
-  if (PF > 1) issue(cur, 1, 1);
+  unsigned gs = 0;  // K-steps issued/consumed across all tiles of this block
+  if constexpr (INC) {
+    issue_inc(cur, 0);
+    if (PF > 1) issue_inc(cur, 1);
+  } else {
+    issue(cur, 0, 0);
+    if (PF > 1) issue(cur, 1, 1);
+  }
   bool first_tile = true;
   while (true) {
     f4v acc[TI][TJ];
@@ -917,7 +993,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
         }
         // A fragments one row block ahead of their MFMAs (all TI at once spill at BN = 256)
         u4v a0 = *(const u4v*)(As + swz(wco + fr, fc)), a1 = *(const u4v*)(As + swz(wco + fr, 4 + fc));
-        {  // the step PF ahead (its stage was last read before this step's barrier)
+        if constexpr (INC) issue_ahead(cur, nxt, t, has_next, (gs + PF) % STG);
+        else {  // the step PF ahead (its stage was last read before this step's barrier)
           const int u = t + PF;
           if (u < KT) issue(cur, u, (gs + PF) % STG);
           else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
@@ -959,9 +1036,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
           for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
         __builtin_amdgcn_s_setprio(0);
         if (ks == 0) {  // the step PF ahead, possibly the next tile's
-          const int u = t + PF;
-          if (u < KT) issue(cur, u, (gs + PF) % STG);
-          else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+          if constexpr (INC) issue_ahead(cur, nxt, t, has_next, (gs + PF) % STG);
+          else {
+            const int u = t + PF;
+            if (u < KT) issue(cur, u, (gs + PF) % STG);
+            else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+          }
         }
       }
     }
@@ -1057,7 +1137,33 @@ static bool psplit_wide() {  // DGVCC_PSPLIT_WIDE=0: BN = 128 on 192-pixel tiles
   const char* e = getenv("DGVCC_PSPLIT_WIDE");
   return !(e && e[0] == '0');
 }
-template <int BN, int STG, int EPI = 0, int WIDE = 1>
+static bool pers_inc() {  // DGVCC_PERS_INC=0: the persistent 16-bit forward with per-K-step addressing (A/B)
+  const char* e = getenv("DGVCC_PERS_INC");
+  return !(e && e[0] == '0');
+}
+// the incremental addressing's tap masks hold R, S <= 3
+static bool inc_shape_ok(const FwdArgs& a) { return a.R <= 3 && a.S <= 3; }
+static int psplit_skew() {  // DGVCC_PSPLIT_SKEW=0|4|5: one-barrier schedule / skewed split after row block 4 / 5
+  const char* e = getenv("DGVCC_PSPLIT_SKEW");
+  return e ? (e[0] == '4' ? 4 : e[0] == '5' ? 5 : 0) : 0;
+}
+static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA addressing (read per launch: A/B)
+  const char* e = getenv("DGVCC_PSPLIT_INC");
+  return !(e && e[0] == '0');
+}
+// INC = 1: the DMA of each K-step is addressed incrementally.  The issue cursor (r, s, cb) steps
+// through the K order without divisions, and each B piece keeps its tile-constant window byte
+// offset plus a bit mask of the taps that stay inside the image (bit r * S + s), so a K-step's
+// B offsets are one scalar tap/channel offset added per piece.  INC = 0 (DGVCC_PSPLIT_INC=0)
+// recomputes kt -> (rs, cb) and each piece's bounds check and offset at every K-step: ~130
+// scalar and ~30 vector instructions in front of the split on every wave.
+// SKEW = 1 (INC, STG = 2): the B fragments of K-step t + 1 are read and split while K-step t's
+// last TI - MID row blocks of MFMAs run (their VALU fills the MFMA issue gaps), instead of in front
+// of step t + 1's first MFMA where both waves of a SIMD split at once with the matrix pipe idle.
+// Two barriers per K-step: after row block MID - 1 (every wave's DMA of step t + 1 has landed) and
+// after the last block (stage t is free: the DMA of step t + 2 goes there), so a DMA has MID / TI of
+// a K-step to land instead of a whole one.  DGVCC_PSPLIT_SKEW=0: the one-barrier schedule.
+template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int SKEW = 0, int MID = 4>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   constexpr int PSB = psplit_psb(BN, WIDE);
   constexpr int NCOG = (BN == 128 && WIDE) ? 1 : 2;  // channel groups of waves
@@ -1106,7 +1212,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   struct Ctx {
     int px0, co0;
     __amdgpu_buffer_rsrc_t xr, wr;
-    int pp[BI], pq[BI], prow0;  // piece i's window row: prow0 + 8 i
+    int pp[BI], pq[BI], prow0;  // INC = 0: piece i's window row: prow0 + 8 i
+    unsigned bofs;        // INC = 1: window byte offset of piece 0's row (piece i: + 8 i rows + its chunk)
+    TapMask<BI> tm;       // INC = 1: the pieces' in-image taps
   };
   auto setup = [&](int lin, Ctx& c) {
     const int t = xcd_remap(lin, ntile);
@@ -1132,9 +1240,45 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       const int rem = m % HW;
       c.pp[i] = (m < M) ? rem / a.W : -100000;
       c.pq[i] = rem % a.W;
+      if constexpr (INC) {
+        if (i == 0) c.bofs = (unsigned)((long long)c.prow0 * a.ldx * 4);
+        tapmask_set<BI>(c.tm, i, c.pp[i], c.pq[i], a);
+      }
     }
   };
   const int RS = a.R * a.S;
+  // INC = 1: K-step of the next DMA issue as three digits, fastest first, advanced without
+  // divisions: (s, r, cb) in the channel-block-major order (a.korder), (cb, s, r) in the tap-major one
+  const bool ko = a.korder != 0;
+  const int L0 = ko ? a.S : CB, L1 = ko ? a.R : a.S;
+  int d0 = 0, d1 = 0, d2 = 0;
+  auto advance = [&]() {
+    d0 += 1;
+    if (d0 == L0) {
+      d0 = 0;
+      d1 += 1;
+      if (d1 == L1) {
+        d1 = 0;
+        d2 += 1;
+      }
+    }
+  };
+  auto issue_inc = [&](const Ctx& c, unsigned stage) {
+    const int is = ko ? d0 : d1, ir = ko ? d1 : d2, icb = ko ? d2 : d0;
+    const int rs = ir * a.S + is;
+    char* As = smem + stage * STAGE;
+    char* Bs = As + A_BYTES;
+#pragma unroll
+    for (int q = 0; q < AI; ++q)
+      lds_dma16s(c.wr, As + (wid * AI + q) * 1024, alane + (unsigned)((rs * CB + icb) * 192), aoff_s(q));
+    const unsigned toff = (unsigned)((((ir - a.pad) * a.W + (is - a.pad)) * a.ldx + icb * 32) * 4);
+    const unsigned need = tap_need(ir, is);
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      lds_dma16(c.xr, Bs + (wid * BI + i) * 1024,
+                tapmask_ok<BI>(c.tm, i, need) ? c.bofs + cbytes[i] + (toff + (unsigned)(i * 8 * a.ldx * 4)) : 0xFFFFFFF0u);
+    advance();
+  };
   auto issue = [&](const Ctx& c, int kt, int stage) {
     const int rs = a.korder ? kt % RS : kt / CB, cb = a.korder ? kt / RS : kt - rs * CB;
     const int r = rs / a.S, s2 = rs - r * a.S;
@@ -1171,9 +1315,43 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   if (has_next) setup(lin + G, nxt);
   const int wpx = (wid % NPXG) * (PSB / NPXG), wco = (wid / NPXG) * (BN / NCOG);
   const int fr = lane & 15, fc = lane >> 4;
-  int gs = 0;
-  issue(cur, 0, 0);
-  if (PF > 1) issue(cur, 1, 1);
+  unsigned gs = 0;
+  if constexpr (INC) {
+    issue_inc(cur, 0);
+    if (PF > 1) issue_inc(cur, 1);
+  } else {
+    issue(cur, 0, 0);
+    if (PF > 1) issue(cur, 1, 1);
+  }
+  static_assert(!SKEW || (INC && STG == 2 && MID > 0 && MID < TI), "SKEW needs INC, 2 stages, 0 < MID < TI");
+  // SKEW: the split B fragments of the step about to run (carried across steps and tiles)
+  s8v bhs[SKEW ? TJ : 1][3];
+  auto bread = [&](const char* Bs, u4v (&r0)[TJ], u4v (&r1)[TJ]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      r0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc));
+      r1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc + 1));
+    }
+  };
+  // SKEW: the DMA of the step two ahead of consumed step t (t + 2 - KT of the next tile past the end)
+  auto issue_skew = [&](int t, bool hn) {
+    const int u = t + 2;
+    if (u < KT) issue_inc(cur, gs % STG);
+    else if (hn) {
+      if (u == KT) d0 = d1 = d2 = 0;
+      issue_inc(nxt, gs % STG);
+    }
+  };
+  if constexpr (SKEW) {  // step 0 landed and split, step 1 in flight
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    u4v r0[TJ], r1[TJ];
+    bread(smem + A_BYTES, r0, r1);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) split3_8(r0[j], r1[j], bhs[j][0], bhs[j][1], bhs[j][2]);
+    if (1 < KT) issue_inc(cur, 1);
+  }
   bool first_tile = true;
   while (true) {
     f4v acc[TI][TJ];
@@ -1181,6 +1359,57 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (SKEW) {
+      for (int t = 0; t < KT; ++t, ++gs) {
+        const bool more = t + 1 < KT || has_next;  // is there a step after this one
+        const char* As = smem + (gs % STG) * STAGE;
+        const char* Bn = smem + ((gs + 1) % STG) * STAGE + A_BYTES;
+        auto aread = [&](int i, s8v (&ah)[3]) __attribute__((always_inline)) {
+          const int row = wco + 16 * i + fr;
+          const int off = row * AROWB + ((fc ^ psw_a(row)) << 4);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) ah[pl] = *(const s8v*)(As + pl * BN * AROWB + off);
+        };
+        s8v ah[3];
+        aread(0, ah);
+        u4v r0[TJ], r1[TJ];
+        s8v bhn[TJ][3];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          if (i == MID && more) {  // every wave's DMA of the next step has landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+            bread(Bn, r0, r1);
+          }
+          s8v an[3];
+          if (i + 1 < TI) aread(i + 1, an);
+          __builtin_amdgcn_s_setprio(1);
+          constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bhs[j][PB[q]], acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+          if (more && i >= MID && i - MID < TJ) {
+            const int j = i - MID;
+            split3_8(r0[j], r1[j], bhn[j][0], bhn[j][1], bhn[j][2]);
+          }
+          if (i + 1 < TI) { ah[0] = an[0]; ah[1] = an[1]; ah[2] = an[2]; }
+        }
+        if (more) {
+#pragma unroll
+          for (int j = TI - MID; j < TJ; ++j) split3_8(r0[j], r1[j], bhn[j][0], bhn[j][1], bhn[j][2]);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();  // every wave is done with this step's stage
+          asm volatile("" ::: "memory");
+          issue_skew(t, has_next);
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) { bhs[j][0] = bhn[j][0]; bhs[j][1] = bhn[j][1]; bhs[j][2] = bhn[j][2]; }
+        }
+      }
+    } else
     for (int t = 0; t < KT; ++t, ++gs) {
       const bool more = t + 1 < KT || has_next;
       if (PF > 1 && more && (t > 0 || first_tile)) {
@@ -1211,8 +1440,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       aread(0, ah);
       {
         const int u = t + PF;
-        if (u < KT) issue(cur, u, (gs + PF) % STG);
-        else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+        if constexpr (INC) {
+          if (u < KT) issue_inc(cur, (gs + PF) % STG);
+          else if (has_next) {
+            if (u == KT) d0 = d1 = d2 = 0;
+            issue_inc(nxt, (gs + PF) % STG);
+          }
+        } else {
+          if (u < KT) issue(cur, u, (gs + PF) % STG);
+          else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
+        }
       }
       s8v bh[TJ][3];
 #pragma unroll
@@ -2538,7 +2775,7 @@ static void* split_scratch(hipStream_t st, size_t bytes) {
 // the shapes the f32 persistent forward serves (and so the f32 shapes with epilogue statistics):
 // more tiles than CUs, > PF K-steps per tile, no split-K / BN-backward epilogue
 static bool f32_pers_ok(const FwdArgs& a) {
-  if (!(use_f32_persist() && use_persist() && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 && a.ldx % 4 == 0 &&
+  if (!(use_f32_persist() && use_persist() && inc_shape_ok(a) && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 && a.ldx % 4 == 0 &&
         a.Cout % 64 == 0 && a.Cout <= PERS_BIAS_MAX && a.R * a.S * (a.C / 32) > 2 &&
         (long long)a.Cout * a.R * a.S * a.C * 4 < (1ll << 31)))
     return false;
@@ -2600,7 +2837,7 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
         if (tap3_bk(true) == 32) hipLaunchKernelGGL((conv_fwd_tap3n_kernel<1, T>), dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((conv_fwd_tap3_kernel<1, T>), dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
-      } else if (use_persist() && !a.bpart && var == 2 && a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX &&
+      } else if (use_persist() && !a.bpart && var == 2 && inc_shape_ok(a) && a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX &&
                  (long long)np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64))) >
                      2 * 256) {
         const int bn = a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64);
@@ -2611,7 +2848,11 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
         } else {
-          if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
+          if (!pers_inc()) {  // A/B: per-K-step recomputed DMA addressing
+            if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
+            else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
+            else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
+          } else if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
           else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
         }
@@ -2696,15 +2937,25 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           const char* e = getenv("DGVCC_PSPLIT_ORDER");
           ap.tile_order = (e && e[0] == '1') ? 1 : 0;
         }
-        if (a.escale) {
-          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
-          else if (wide) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
-          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 3, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
-        } else {
-          if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
-          else if (wide) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
-          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, 0, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);
-        }
+        const bool inc = psplit_inc();
+        const int skew = inc ? psplit_skew() : 0;
+#define PSPLIT_LAUNCH(EPI_)                                                                                    \
+  do {                                                                                                         \
+    if (bn2 == 256) {                                                                                          \
+      if (skew == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else if (skew == 5) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 1, 5>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 0>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+    } else if (wide) {                                                                                         \
+      if (skew == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else if (skew == 5) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 1, 5>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 0>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+    } else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, EPI_, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);  \
+  } while (0)
+        if (a.escale) PSPLIT_LAUNCH(3);
+        else PSPLIT_LAUNCH(0);
+#undef PSPLIT_LAUNCH
       } else if (f32_split()) F32_PERS(1);
       else F32_PERS(0);
 #undef F32_PERS
@@ -3604,7 +3855,11 @@ constexpr int W9_XROWS = 72;
 // conv_fwd_pipe_kernel (A/B in one call: wgrad 881 -> 949 TF/s, 15.1 -> 14.0 ms per step).
 // Measured and dropped: setprio alone (no change), priority without the moved issue (-0.7%),
 // the issue split over two points of the substep loop (777 TF/s).
-template <int BCO, int WT = 0, int PADK = 0, int SCH = 0, typename T = bf16>
+// INC (W % 64 == 0 path): the DMA addressing of a K-step is incremental: the step's row
+// coordinates (n, p, q0) advance by 64 pixels without divisions, and each of the wave's <= 6
+// pieces keeps its lane-constant byte offset (and X row), so a piece costs one scalar-offset add
+// and, for X, a column test.  INC = 0 (DGVCC_WG9_INC=0) recomputes every piece each K-step.
+template <int BCO, int WT = 0, int PADK = 0, int SCH = 0, typename T = bf16, int INC = 1>
 __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   constexpr int BKP = 64, BC = 64;
   constexpr int RA = BCO * 2, RX = BC * 2;                    // bytes per LDS row
@@ -3678,9 +3933,65 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
     } \
   } while (0)
 
+  // INC: the wave's pieces k (instruction ii = wid + 8 k): lane-constant source offsets, X rows
+  constexpr int KMAX = (N_INST + 7) / 8;
+  constexpr int KA = A_INST / 8;  // pieces 0 .. KA-1 of every wave are dY rows (A_INST % 8 == 0)
+  static_assert(A_INST % 8 == 0, "dY pieces must be whole rounds of the 8 waves");
+  unsigned loff[KMAX];
+  int xrow[KMAX], xdh[KMAX];
+  if constexpr (INC && !PADK) {
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+      const int ii = wid + 8 * k;
+      if (k < KA) {
+        const int row = ii * RPIA + lane / CPRA;
+        const int ch = (lane % CPRA) ^ wg_swz<CPRA>(row);
+        loff[k] = (unsigned)(((long long)row * a.lddy + co0 + ch * 8) * 2);
+        xrow[k] = 0;
+        xdh[k] = 0;
+      } else {
+        const int jj = ii - A_INST;
+        const int dhi = jj / 9, sub = jj - dhi * 9;
+        const int row = sub * 8 + (lane >> 3);
+        const int ch = (lane & 7) ^ wg_swz<CPRX>(row);
+        loff[k] = (unsigned)(((long long)(row - 4) * a.ldx + c0 + ch * 8) * 2);
+        xrow[k] = row - 4;
+        xdh[k] = dhi;
+      }
+    }
+  }
+  // INC: image coordinates of the next issued K-step's first pixel (kbeg + issued * 64)
+  int in_ = kbeg / HW, ipr = (kbeg - in_ * HW) / a.W, iq0 = kbeg - in_ * HW - ipr * a.W, ipx = kbeg;
+#define W9_ISSUE_INC(stage_) \
+  do { \
+    char* As = smem + (stage_) * STAGE; \
+    char* Xs = As + A_BYTES; \
+    const unsigned aso = (unsigned)((long long)(ipx - kbeg) * a.lddy * 2); \
+    const long long xb = (long long)in_ * HW + (long long)ipr * a.W + iq0 - xlo; \
+    _Pragma("unroll") for (int k = 0; k < KMAX; ++k) { \
+      const int ii = wid + 8 * k; \
+      if (k < KA) { \
+        lds_dma16(dyr, As + ii * 1024, loff[k] + aso); \
+      } else if (ii < N_INST) { \
+        const int h = ipr + xdh[k] - 1; \
+        const bool ok = (unsigned)h < (unsigned)a.H && (unsigned)(iq0 + xrow[k]) < (unsigned)a.W; \
+        const unsigned xso = (unsigned)((xb + (long long)(xdh[k] - 1) * a.W) * a.ldx * 2); \
+        lds_dma16(xr, Xs + xdh[k] * X_BYTES + (ii - A_INST - xdh[k] * 9) * 1024, \
+                  ok ? loff[k] + xso : 0xFFFFFFF0u); \
+      } \
+    } \
+    ipx += BKP; \
+    iq0 += BKP; \
+    if (iq0 == a.W) { \
+      iq0 = 0; \
+      if (++ipr == a.H) { ipr = 0; ++in_; } \
+    } \
+  } while (0)
+
 #define W9_ISSUE(kt_, stage_) \
   do { \
     if constexpr (PADK) { W9_ISSUE_PAD(kt_, stage_); break; } \
+    if constexpr (INC) { W9_ISSUE_INC(stage_); break; } \
     const int px0 = kbeg + (kt_) * BKP; \
     const int n = px0 / HW, rem = px0 - n * HW; \
     const int pr = rem / a.W, q0 = rem - pr * a.W; \
@@ -3782,6 +4093,7 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   }
 #undef W9_ISSUE
 #undef W9_ISSUE_PAD
+#undef W9_ISSUE_INC
 
   const long long ldk = 9ll * a.C;
   float* out = a.slab + ((long long)split * (KH ? 2 : 1) + kh) * a.Cout * ldk;
@@ -3798,6 +4110,11 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
           out[co * ldk + tp * a.C + c] = acc[tp][i][j][rr];
         }
       }
+}
+
+static bool wg9_inc() {  // DGVCC_WG9_INC=0: per-K-step recomputed DMA addressing (read per launch: A/B)
+  const char* e = getenv("DGVCC_WG9_INC");
+  return !(e && e[0] == '0');
 }
 
 static int wg9_sched() {
@@ -3925,12 +4242,17 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
       const bool kh2 = b9 == 64 && sch == 2 && wg9_khalf();
       if (kh2) slab_splits = 2 * a.splits;  // one slab split per k-half
       if (w9) {
-        if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2, T>), g9, dim3(512), 0, st, a);
-        else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 0, T>), g9, dim3(512), 0, st, a);
-        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 0, 0, T>), g9, dim3(512), 0, st, a);
-        else if (kh2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 0, 2, T>), g9, dim3(512), 0, st, a);
-        else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 2, T>), g9, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 0, T>), g9, dim3(512), 0, st, a);
+        const bool inc = wg9_inc();
+        if (b9 == 128 && wg9_wide() && sch == 2) {
+          if (inc) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2, T>), g9, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2, T, 0>), g9, dim3(512), 0, st, a);
+        } else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 0, T, 0>), g9, dim3(512), 0, st, a);
+        else if (b9 == 128) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 0, 0, 0, T, 0>), g9, dim3(512), 0, st, a);
+        else if (kh2) {
+          if (inc) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 0, 2, T>), g9, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 2, 0, 2, T, 0>), g9, dim3(512), 0, st, a);
+        } else if (sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 2, T, 0>), g9, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad9_kernel<64, 0, 0, 0, T, 0>), g9, dim3(512), 0, st, a);
       } else {
         if (b9 == 128 && wg9_wide() && sch == 2) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1, 2, T>), g9, dim3(512), 0, st, a);
         else if (b9 == 128 && wg9_wide()) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 1, 0, T>), g9, dim3(512), 0, st, a);
