@@ -1143,10 +1143,6 @@ static bool pers_inc() {  // DGVCC_PERS_INC=0: the persistent 16-bit forward wit
 }
 // the incremental addressing's tap masks hold R, S <= 3
 static bool inc_shape_ok(const FwdArgs& a) { return a.R <= 3 && a.S <= 3; }
-static int psplit_skew() {  // DGVCC_PSPLIT_SKEW=0|4|5: one-barrier schedule / skewed split after row block 4 / 5
-  const char* e = getenv("DGVCC_PSPLIT_SKEW");
-  return e ? (e[0] == '4' ? 4 : e[0] == '5' ? 5 : 0) : 0;
-}
 static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA addressing (read per launch: A/B)
   const char* e = getenv("DGVCC_PSPLIT_INC");
   return !(e && e[0] == '0');
@@ -1157,13 +1153,7 @@ static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA add
 // B offsets are one scalar tap/channel offset added per piece.  INC = 0 (DGVCC_PSPLIT_INC=0)
 // recomputes kt -> (rs, cb) and each piece's bounds check and offset at every K-step: ~130
 // scalar and ~30 vector instructions in front of the split on every wave.
-// SKEW = 1 (INC, STG = 2): the B fragments of K-step t + 1 are read and split while K-step t's
-// last TI - MID row blocks of MFMAs run (their VALU fills the MFMA issue gaps), instead of in front
-// of step t + 1's first MFMA where both waves of a SIMD split at once with the matrix pipe idle.
-// Two barriers per K-step: after row block MID - 1 (every wave's DMA of step t + 1 has landed) and
-// after the last block (stage t is free: the DMA of step t + 2 goes there), so a DMA has MID / TI of
-// a K-step to land instead of a whole one.  DGVCC_PSPLIT_SKEW=0: the one-barrier schedule.
-template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int SKEW = 0, int MID = 4>
+template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   constexpr int PSB = psplit_psb(BN, WIDE);
   constexpr int NCOG = (BN == 128 && WIDE) ? 1 : 2;  // channel groups of waves
@@ -1323,35 +1313,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     issue(cur, 0, 0);
     if (PF > 1) issue(cur, 1, 1);
   }
-  static_assert(!SKEW || (INC && STG == 2 && MID > 0 && MID < TI), "SKEW needs INC, 2 stages, 0 < MID < TI");
-  // SKEW: the split B fragments of the step about to run (carried across steps and tiles)
-  s8v bhs[SKEW ? TJ : 1][3];
-  auto bread = [&](const char* Bs, u4v (&r0)[TJ], u4v (&r1)[TJ]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      r0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc));
-      r1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc + 1));
-    }
-  };
-  // SKEW: the DMA of the step two ahead of consumed step t (t + 2 - KT of the next tile past the end)
-  auto issue_skew = [&](int t, bool hn) {
-    const int u = t + 2;
-    if (u < KT) issue_inc(cur, gs % STG);
-    else if (hn) {
-      if (u == KT) d0 = d1 = d2 = 0;
-      issue_inc(nxt, gs % STG);
-    }
-  };
-  if constexpr (SKEW) {  // step 0 landed and split, step 1 in flight
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    u4v r0[TJ], r1[TJ];
-    bread(smem + A_BYTES, r0, r1);
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) split3_8(r0[j], r1[j], bhs[j][0], bhs[j][1], bhs[j][2]);
-    if (1 < KT) issue_inc(cur, 1);
-  }
   bool first_tile = true;
   while (true) {
     f4v acc[TI][TJ];
@@ -1359,57 +1320,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
-    if constexpr (SKEW) {
-      for (int t = 0; t < KT; ++t, ++gs) {
-        const bool more = t + 1 < KT || has_next;  // is there a step after this one
-        const char* As = smem + (gs % STG) * STAGE;
-        const char* Bn = smem + ((gs + 1) % STG) * STAGE + A_BYTES;
-        auto aread = [&](int i, s8v (&ah)[3]) __attribute__((always_inline)) {
-          const int row = wco + 16 * i + fr;
-          const int off = row * AROWB + ((fc ^ psw_a(row)) << 4);
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl) ah[pl] = *(const s8v*)(As + pl * BN * AROWB + off);
-        };
-        s8v ah[3];
-        aread(0, ah);
-        u4v r0[TJ], r1[TJ];
-        s8v bhn[TJ][3];
-#pragma unroll
-        for (int i = 0; i < TI; ++i) {
-          if (i == MID && more) {  // every wave's DMA of the next step has landed
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
-            asm volatile("" ::: "memory");
-            bread(Bn, r0, r1);
-          }
-          s8v an[3];
-          if (i + 1 < TI) aread(i + 1, an);
-          __builtin_amdgcn_s_setprio(1);
-          constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-          for (int q = 0; q < 6; ++q)
-#pragma unroll
-            for (int j = 0; j < TJ; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bhs[j][PB[q]], acc[i][j], 0, 0, 0);
-          __builtin_amdgcn_s_setprio(0);
-          if (more && i >= MID && i - MID < TJ) {
-            const int j = i - MID;
-            split3_8(r0[j], r1[j], bhn[j][0], bhn[j][1], bhn[j][2]);
-          }
-          if (i + 1 < TI) { ah[0] = an[0]; ah[1] = an[1]; ah[2] = an[2]; }
-        }
-        if (more) {
-#pragma unroll
-          for (int j = TI - MID; j < TJ; ++j) split3_8(r0[j], r1[j], bhn[j][0], bhn[j][1], bhn[j][2]);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();  // every wave is done with this step's stage
-          asm volatile("" ::: "memory");
-          issue_skew(t, has_next);
-#pragma unroll
-          for (int j = 0; j < TJ; ++j) { bhs[j][0] = bhn[j][0]; bhs[j][1] = bhn[j][1]; bhs[j][2] = bhn[j][2]; }
-        }
-      }
-    } else
     for (int t = 0; t < KT; ++t, ++gs) {
       const bool more = t + 1 < KT || has_next;
       if (PF > 1 && more && (t > 0 || first_tile)) {
@@ -2938,18 +2848,13 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           ap.tile_order = (e && e[0] == '1') ? 1 : 0;
         }
         const bool inc = psplit_inc();
-        const int skew = inc ? psplit_skew() : 0;
 #define PSPLIT_LAUNCH(EPI_)                                                                                    \
   do {                                                                                                         \
     if (bn2 == 256) {                                                                                          \
-      if (skew == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc); \
-      else if (skew == 5) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 1, 5>), dim3(g2), dim3(512), 0, st, ap, wspc); \
-      else if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
       else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 0>), dim3(g2), dim3(512), 0, st, ap, wspc); \
     } else if (wide) {                                                                                         \
-      if (skew == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc); \
-      else if (skew == 5) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 1, 5>), dim3(g2), dim3(512), 0, st, ap, wspc); \
-      else if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
       else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 0>), dim3(g2), dim3(512), 0, st, ap, wspc); \
     } else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, EPI_, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);  \
   } while (0)
