@@ -72,6 +72,76 @@ __global__ void in_stats_finalize(const T* __restrict__ x, long long ldx, int N,
   invstd[i] = (float)(1.0 / sqrt(var + (double)eps));
 }
 
+// V consecutive per-(instance, channel) floats (16-B aligned: C % 4 == 0, c0 % V == 0); 1 when absent
+template <int V>
+__device__ __forceinline__ void ld_nc(const float* a, long long off, float (&o)[V]) {
+  if (!a) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = 1.f;
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < V; e += 4) {
+    const f4v t = *(const f4v*)(a + off + e);
+    o[e] = t[0]; o[e + 1] = t[1]; o[e + 2] = t[2]; o[e + 3] = t[3];
+  }
+}
+
+// The elementwise e_mask passes walk (pixel, V-channel chunk) items.  When the chunks of a pixel
+// divide the block (NT % (C / V) == 0, e.g. the 512-channel x3) every thread keeps one chunk, so
+// the item -> (pixel, channel) split is one division per block instead of two 64-bit divisions per
+// item; the per-(instance, channel) statistics come in as 16-B loads and the V mask bytes as one
+// store.
+template <int V>
+struct EwWalk {
+  long long p, pstride, total;
+  int c0, tpp;
+  bool fixed;
+  __device__ __forceinline__ EwWalk(long long M, int C) {
+    tpp = C / V;
+    total = M * tpp;
+    fixed = NT % tpp == 0;
+    const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+    if (fixed) {
+      c0 = (int)(threadIdx.x % tpp) * V;
+      p = blockIdx.x * (long long)(NT / tpp) + threadIdx.x / tpp;
+      pstride = (long long)gridDim.x * (NT / tpp);
+    } else {
+      p = gt;  // item index
+      pstride = (long long)gridDim.x * NT;
+      c0 = 0;
+    }
+  }
+  __device__ __forceinline__ bool next(long long M, long long& px, int& ch) {
+    if (fixed) {
+      if (p >= M) return false;
+      px = p;
+      ch = c0;
+    } else {
+      if (p >= total) return false;
+      px = p / tpp;
+      ch = (int)(p % tpp) * V;
+    }
+    p += pstride;
+    return true;
+  }
+};
+
+template <int V>
+__device__ __forceinline__ void st_mask(unsigned char* m, const unsigned char (&mk)[V]) {
+  if constexpr (V == 8) {
+    unsigned long long w = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w |= (unsigned long long)mk[e] << (8 * e);
+    *(unsigned long long*)m = w;
+  } else {
+    unsigned w = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) w |= (unsigned)mk[e] << (8 * e);
+    *(unsigned*)m = w;
+  }
+}
+
 // m_v = y_v * e * drop_v ; e = |(y1-mu1)*is1 - (y2-mu2)*is2| < thr  (stored as 0/1 bytes)
 template <typename T>
 __global__ __launch_bounds__(NT) void emask_fwd_kernel(const T* __restrict__ y1, const T* __restrict__ y2, long long ld,
@@ -80,30 +150,34 @@ __global__ __launch_bounds__(NT) void emask_fwd_kernel(const T* __restrict__ y1,
                                                        const float* drop1, const float* drop2, T* __restrict__ m1,
                                                        T* __restrict__ m2, unsigned char* __restrict__ mask) {
   constexpr int V = 16 / (int)sizeof(T);
-  const int tpp = C / V;
-  const long long total = (long long)N * HW * tpp;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const long long p = i / tpp;
-    const int c0 = (int)(i % tpp) * V;
-    const int n = (int)(p / HW);
-    float a[V], b[V];
+  const long long M = (long long)N * HW;
+  EwWalk<V> w(M, C);
+  long long p;
+  int c0;
+  while (w.next(M, p, c0)) {
+    const long long nc = (M < (1ll << 31) ? (long long)((unsigned)p / (unsigned)HW) : p / HW) * C + c0;
+    float a[V], b[V], ma[V], sa[V], mb[V], sb[V], da[V], db[V];
     ldv(y1 + p * ld + c0, a);
     ldv(y2 + p * ld + c0, b);
+    ld_nc<V>(mu1, nc, ma);
+    ld_nc<V>(is1, nc, sa);
+    ld_nc<V>(mu2, nc, mb);
+    ld_nc<V>(is2, nc, sb);
+    ld_nc<V>(drop1, nc, da);
+    ld_nc<V>(drop2, nc, db);
     unsigned char mk[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int nc = n * C + c0 + e;
-      const float ia = (a[e] - mu1[nc]) * is1[nc];
-      const float ib = (b[e] - mu2[nc]) * is2[nc];
+      const float ia = (a[e] - ma[e]) * sa[e];
+      const float ib = (b[e] - mb[e]) * sb[e];
       const bool keep = fabsf(ia - ib) < thr;
       mk[e] = keep ? 1 : 0;
-      a[e] = keep ? a[e] * (drop1 ? drop1[nc] : 1.f) : 0.f;
-      b[e] = keep ? b[e] * (drop2 ? drop2[nc] : 1.f) : 0.f;
+      a[e] = keep ? a[e] * da[e] : 0.f;
+      b[e] = keep ? b[e] * db[e] : 0.f;
     }
     stv(m1 + p * C + c0, a);
     stv(m2 + p * C + c0, b);
-#pragma unroll
-    for (int e = 0; e < V; ++e) mask[p * C + c0 + e] = mk[e];
+    st_mask<V>(mask + p * C + c0, mk);
   }
 }
 
@@ -114,21 +188,25 @@ __global__ __launch_bounds__(NT) void emask_bwd_kernel(const T* __restrict__ gm1
                                                        const float* drop1, const float* drop2, T* __restrict__ gy1,
                                                        T* __restrict__ gy2, long long ldgy) {
   constexpr int V = 16 / (int)sizeof(T);
-  const int tpp = C / V;
-  const long long total = (long long)N * HW * tpp;
-  for (long long i = blockIdx.x * (long long)NT + threadIdx.x; i < total; i += (long long)gridDim.x * NT) {
-    const long long p = i / tpp;
-    const int c0 = (int)(i % tpp) * V;
-    const int n = (int)(p / HW);
-    float a[V], b[V];
+  const long long M = (long long)N * HW;
+  EwWalk<V> w(M, C);
+  long long p;
+  int c0;
+  while (w.next(M, p, c0)) {
+    const long long nc = (M < (1ll << 31) ? (long long)((unsigned)p / (unsigned)HW) : p / HW) * C + c0;
+    float a[V], b[V], da[V], db[V];
     ldv(gm1 + p * C + c0, a);
     ldv(gm2 + p * C + c0, b);
+    ld_nc<V>(drop1, nc, da);
+    ld_nc<V>(drop2, nc, db);
+    unsigned long long mw;
+    if constexpr (V == 8) mw = *(const unsigned long long*)(mask + p * C + c0);
+    else mw = *(const unsigned*)(mask + p * C + c0);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const int nc = n * C + c0 + e;
-      const float k = mask[p * C + c0 + e] ? 1.f : 0.f;
-      a[e] *= k * (drop1 ? drop1[nc] : 1.f);
-      b[e] *= k * (drop2 ? drop2[nc] : 1.f);
+      const float k = ((mw >> (8 * e)) & 0xff) ? 1.f : 0.f;
+      a[e] *= k * da[e];
+      b[e] *= k * db[e];
     }
     stv(gy1 + p * ldgy + c0, a);
     stv(gy2 + p * ldgy + c0, b);
