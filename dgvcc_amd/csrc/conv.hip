@@ -1153,9 +1153,14 @@ static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA add
 // B offsets are one scalar tap/channel offset added per piece.  INC = 0 (DGVCC_PSPLIT_INC=0)
 // recomputes kt -> (rs, cb) and each piece's bounds check and offset at every K-step: ~130
 // scalar and ~30 vector instructions in front of the split on every wave.
-template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1>
+// TALL = 1 (BN = 256, EPI 0): 256-pixel tiles, each wave 128 channels x 64 pixels (TJ = 4), so every
+// filter fragment read and every staged filter byte feeds 4 pixel blocks instead of 3.  The two
+// 80-KB stages fill the LDS; the epilogue's statistics scratch and this tile's bias live in the
+// stage the last K-step consumed (free until the next tile's second K-step issues its DMA there).
+template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
-  constexpr int PSB = psplit_psb(BN, WIDE);
+  static_assert(!TALL || (BN == 256 && EPI == 0 && STG == 2 && INC), "TALL: 256-channel training forward only");
+  constexpr int PSB = TALL ? 256 : psplit_psb(BN, WIDE);
   constexpr int NCOG = (BN == 128 && WIDE) ? 1 : 2;  // channel groups of waves
   constexpr int NPXG = 8 / NCOG;                   // pixel groups of waves
   constexpr int AROWB = 64;                        // bytes per A plane row (32 bf16)
@@ -1167,7 +1172,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   constexpr int PF = STG - 1;
   constexpr int EPI_B = NPXG * 3 * BN * 4;
   static_assert(AI * 8 * 1024 == A_BYTES, "A tile must split evenly over the 8 waves");
-  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B + PERS_BIAS_MAX * 4];
+  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + (TALL ? 0 : EPI_B + PERS_BIAS_MAX * 4)];
+  static_assert(!TALL || EPI_B + BN * 4 <= STAGE, "TALL epilogue scratch must fit in a stage");
   char* epi_lds = smem + STG * STAGE;
   float* bbuf = (float*)(epi_lds + EPI_B);
   constexpr int E3_MAX = (EPI_B + PERS_BIAS_MAX * 4) / 12;
@@ -1296,7 +1302,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       escl[c] = a.escale[c];
       eshf[c] = a.eshift[c];
     }
-  } else if (a.bias) {
+  } else if (a.bias && !TALL) {
     for (int c = tid; c < a.Cout; c += 512) bbuf[c] = a.bias[c];
   }
   Ctx cur, nxt;
@@ -1380,6 +1386,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       }
     }
     first_tile = false;
+    if constexpr (TALL) {  // the consumed stage becomes the epilogue scratch: this tile's bias, statistics
+      epi_lds = smem + ((gs - 1) % STG) * STAGE;
+      bbuf = (float*)(epi_lds + EPI_B) - cur.co0;  // indexed by absolute channel
+      lds_barrier();  // every wave is done reading the stage
+      if (a.bias && tid < BN) bbuf[cur.co0 + tid] = a.bias[cur.co0 + tid];
+      lds_barrier();
+    }
     float* y = (float*)a.y;
     bool valid[TJ];
 #pragma unroll
@@ -2634,6 +2647,25 @@ static bool psplit_ok(const FwdArgs& a) {
          (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
 }
 
+// DGVCC_PSPLIT_TALL=0: never the 256-pixel pre-split tiles; 1 (default): where they quantise onto the
+// CUs no worse than the 192-pixel ones; 2: always (256-channel training forwards/dgrads)
+static int psplit_tall_mode() {
+  const char* e = getenv("DGVCC_PSPLIT_TALL");
+  return e ? e[0] - '0' : 1;
+}
+// the 256-pixel form for this launch: 256 output channels, no eval epilogue, and (mode 1) whole
+// rounds of 256-pixel tiles costing no more than the 192-pixel ones at ~5% less time per pixel
+static bool psplit_tall(const FwdArgs& a) {
+  const int mode = psplit_tall_mode();
+  if (mode == 0 || f32_pers_bn(a.Cout) != 256 || a.escale || a.bpart || !psplit_inc()) return false;
+  if (mode == 2) return true;
+  const long long M = (long long)a.N * a.H * a.W, nco = a.Cout / 256, G = persist_grid();
+  const long long r256 = dg_cdiv(dg_cdiv(M, 256) * nco, G), r192 = dg_cdiv(dg_cdiv(M, PSB) * nco, G);
+  return (double)r256 * 256 * 0.95 < (double)r192 * PSB;
+}
+// pixels per tile of the pre-split launch (and so rows of its epilogue statistics)
+static int psplit_tile_px(const FwdArgs& a) { return psplit_tall(a) ? 256 : psplit_psb(f32_pers_bn(a.Cout), psplit_wide()); }
+
 // f32 split-math shapes served by conv_fwd_rsplit_kernel (64-wide channel tiles)
 static bool rsplit_ok(const FwdArgs& a) {
   return use_psplit() && f32_split() && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 && a.ldx % 4 == 0 &&
@@ -2839,7 +2871,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
                            0, st, (const float*)a.w, nw, wsp);
         const int bn2 = f32_pers_bn(a.Cout);
         const bool wide = psplit_wide();
-        const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_psb(bn2, wide)) * (a.Cout / bn2),
+        const bool tall = psplit_tall(a);
+        const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_tile_px(a)) * (a.Cout / bn2),
                                                           persist_grid());
         const char* wspc = (const char*)wsp;
         FwdArgs ap = a;
@@ -2859,6 +2892,7 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
     } else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, EPI_, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);  \
   } while (0)
         if (a.escale) PSPLIT_LAUNCH(3);
+        else if (tall) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
         else PSPLIT_LAUNCH(0);
 #undef PSPLIT_LAUNCH
       } else if (f32_split()) F32_PERS(1);
@@ -4428,8 +4462,15 @@ extern "C" int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, 
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
   const long long M = (long long)N * H * W;
   FwdArgs a{nullptr, ldx, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0};
-  if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, psplit_psb(f32_pers_bn(Cout), psplit_wide()));
+  if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, psplit_tile_px(a));
   if (dtype == DG_F32 && rsplit_ok(a) && rsplit3w_ok(a)) return dg_cdiv(M, 512);
+  return dg_cdiv(M, 256);
+}
+extern "C" int64_t dg_conv_bnpart_rows_ex(int dtype, int N, int H, int W, int C, int64_t ldx, int Cout, int R, int S) {
+  if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
+  const long long M = (long long)N * H * W;
+  FwdArgs a{nullptr, ldx, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0};
+  if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, psplit_psb(f32_pers_bn(Cout), psplit_wide()));
   return dg_cdiv(M, 256);
 }
 extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,

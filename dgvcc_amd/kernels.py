@@ -166,7 +166,7 @@ def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: A
     if stats is None or (dy.dt == 1 and _BNPART_OFF) or (dy.dt == 0 and _BNPART_F32_OFF) or dy.dt == 2:
         return None
     wflip = flip_weight(wp, dy.C, C, R)
-    rows = (query("dg_conv_stats_rows_ex", 0, dy.N, dy.H, dy.W, dy.C, dy.ld, C, R, R) if dy.dt == 0
+    rows = (query("dg_conv_bnpart_rows_ex", 0, dy.N, dy.H, dy.W, dy.C, dy.ld, C, R, R) if dy.dt == 0
             else query("dg_conv_stats_rows", dy.N, dy.H, dy.W))
     part = torch.empty((rows, 3, C), dtype=torch.float32, device=dy.buf.device)
     flops = 2.0 * dy.M * dy.C * R * R * C

@@ -75,8 +75,13 @@ int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int H, int W, 
  * serves the shape; the caller then runs dg_conv_fwd + dg_bn_fwd_train. */
 int64_t dg_conv_stats_rows(int N, int H, int W);
 /* rows of (n, mean, M2) BN partials a dg_conv_fwd_ex launch of this shape writes: one per
- * tile of 256 output pixels, or of 192 on the pre-split f32 kernel (DG_F32, split math) */
+ * tile of 256 output pixels; on the pre-split f32 kernel (DG_F32, split math) one per tile of
+ * 192 pixels, or of 256 where the 256-channel launch takes 256-pixel tiles (DGVCC_PSPLIT_TALL) */
 int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, int64_t ldx, int Cout, int R, int S);
+/* rows of the BN-backward partials part[rows][3][C] that dg_conv_fwd_bnbwd writes for an
+ * output-gradient shape (N, H, W, C = the gradient's channels) and Cout = the consumer's input
+ * channels (the dgrad-epilogue launches never take the 256-pixel tiles) */
+int64_t dg_conv_bnpart_rows_ex(int dtype, int N, int H, int W, int C, int64_t ldx, int Cout, int R, int S);
 int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                       const void* w, int Cout, int R, int S, int pad, const float* bias,
                       void* y, int64_t ldy, float* part, void* stream);

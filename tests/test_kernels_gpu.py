@@ -450,12 +450,17 @@ def test_conv_f32_split_same_sign(dev, case, which):
                                               (2, 33, 40, 64, 64, "bias"), (2, 8, 256, 64, 64, "stats"),
                                               (1, 6, 512, 128, 64, "bias"), (2, 5, 256, 64, 64, "eval"),
                                               (2, 4, 512, 64, 64, "stats"), (1, 3, 1024, 64, 64, "eval")])
-def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
+@pytest.mark.parametrize("tall", ["0", "2"])
+def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi, tall, monkeypatch):
     """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128; Cout = 64 on
     conv_fwd_rsplit_kernel, 256-pixel tiles) with
     bias + epilogue BN statistics (rows per 192-pixel tile: dg_conv_stats_rows_ex), the eval-BN
     epilogue and a ragged last tile, against float64: y within 5e-6, the merged (n, mean, M2)
-    rows equal to the statistics of the stored y."""
+    rows equal to the statistics of the stored y.  tall = "2": the 256-channel training launches on
+    256-pixel tiles (DGVCC_PSPLIT_TALL, epilogue scratch and bias in the consumed stage)."""
+    if tall == "2" and (Cout % 256 or epi == "eval"):
+        pytest.skip("256-pixel tiles serve 256-channel training launches only")
+    monkeypatch.setenv("DGVCC_PSPLIT_TALL", tall)
     K = _k()
     g = torch.Generator().manual_seed(14)
     x = torch.randn(N, H, W, C, generator=g)
@@ -473,7 +478,8 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi):
         rows = K.query("dg_conv_stats_rows_ex", 0, N, H, W, C, C, Cout, 3, 3)
         # tiles: 192 px at 256 channels, 384 px at 128 (conv_fwd_psplit_kernel), 256 px at 64 (rsplit),
         # 512 px at 64 where W % 512 == 0 (conv_fwd_rsplit3w_kernel)
-        tile = 192 if Cout % 256 == 0 else (384 if Cout % 128 == 0 else (512 if W % 512 == 0 else 256))
+        tile = (256 if tall == "2" else 192) if Cout % 256 == 0 else (384 if Cout % 128 == 0 else
+                                                                      (512 if W % 512 == 0 else 256))
         assert rows == -(-(N * H * W) // tile)
         part, r2 = K.conv_fwd_stats(K.Act(x.to(dev)), wp, Cout, 3, 1, z, bias=b.to(dev))
         assert r2 == rows
