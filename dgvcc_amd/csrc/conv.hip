@@ -805,16 +805,23 @@ __device__ __forceinline__ bool tapmask_ok(const TapMask<BI>& t, int i, unsigned
 
 // INC: incremental DMA addressing as in conv_fwd_psplit_kernel (DGVCC_PERS_INC=0 restores the per-K-step
 // recomputation)
-template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0, int INC = 1>
+// WIDE (16-bit, BN = 128): 384-pixel tiles with the 8 waves all on pixels, each 128 channels x 48
+// pixels (the 256-channel kernel's per-wave filter reuse; 1.5x the MFMAs per barrier of the 2 x 4
+// layout of 64 x 64 wave tiles), two stages of (16 + 48) KB (DGVCC_PERS_WIDE=0: the 2 x 4 layout).
+template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0, int INC = 1, int WIDE = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
+  static_assert(!WIDE || (BN == 128 && SPL == 0 && STG == 2), "WIDE: the 16-bit 128-channel kernel");
+  constexpr int PB = WIDE ? 384 : PBM;   // pixels per tile
+  constexpr int NPXG = WIDE ? 8 : 4;     // pixel groups of waves
+  constexpr int NCOG = 8 / NPXG;         // channel groups of waves
   constexpr int ES = (int)sizeof(T);  // element bytes: a K-step row is 128 B (64 x 16-bit or 32 x f32)
   constexpr int BK = 128 / ES;
   constexpr int AI = BN / 64;
-  constexpr int BI = PBM / 64;
-  constexpr int TI = BN / 32, TJ = 4;
-  constexpr int STAGE = (BN + PBM) * 128;
+  constexpr int BI = PB / 64;
+  constexpr int TI = BN / NCOG / 16, TJ = PB / NPXG / 16;
+  constexpr int STAGE = (BN + PB) * 128;
   constexpr int PF = STG - 1;
-  constexpr int EPI_B = 4 * 3 * BN * 4;  // epi_stats scratch [4][3][BN] f32
+  constexpr int EPI_B = NPXG * 3 * BN * 4;  // epi_stats scratch [NPXG][3][BN] f32
   __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + EPI_B + PERS_BIAS_MAX * 4];
   char* epi_lds = smem + STG * STAGE;
   // bias staged in LDS once per block: a global load per use in the epilogue makes the
@@ -832,7 +839,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   const int HW = a.H * a.W;
   const int M = a.N * HW;
   const int nco = a.Cout / BN;
-  const int ntile = (M + PBM - 1) / PBM * nco;
+  const int ntile = (M + PB - 1) / PB * nco;
   const int G = gridDim.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -856,10 +863,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   auto setup = [&](int lin, Ctx& c) {
     const int t = xcd_remap(lin, ntile);
     c.co0 = (t % nco) * BN;
-    c.px0 = (t / nco) * PBM;
+    c.px0 = (t / nco) * PB;
     const int halo = a.pad * (a.W + 1);
     const int plo = max(0, c.px0 - halo);
-    const int phi = min(M, c.px0 + PBM + halo);
+    const int phi = min(M, c.px0 + PB + halo);
     const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * ES);
     c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * ES), 0, win_bytes, 0x00020000);
     c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.w + (long long)c.co0 * ldw * ES), 0, (unsigned)(BN * ldw * ES),
@@ -952,7 +959,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   setup(lin, cur);
   bool has_next = lin + G < ntile;
   if (has_next) setup(lin + G, nxt);
-  const int wpx = (wid & 3) * 64, wco = (wid >> 2) * (BN / 2);
+  const int wpx = (wid % NPXG) * (PB / NPXG), wco = (wid / NPXG) * (BN / NCOG);
   const int fr = lane & 15, fc = lane >> 4;
   unsigned gs = 0;  // K-steps issued/consumed across all tiles of this block
   if constexpr (INC) {
@@ -1090,7 +1097,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       }
     }
     if (EPI == 0 && a.part)
-      epi_stats<TI, TJ, 4, BN>(acc, valid, wid & 3, wco, epi_lds, a.part + (long long)(cur.px0 / PBM) * 3 * a.Cout,
+      epi_stats<TI, TJ, NPXG, BN>(acc, valid, wid % NPXG, wco, epi_lds, a.part + (long long)(cur.px0 / PB) * 3 * a.Cout,
                                a.Cout, cur.co0, tid, fr, fc);
     if (!has_next) break;
     cur = nxt;
@@ -2733,6 +2740,23 @@ static int conv_korder() {  // DGVCC_CONV_KORDER=0/1 (read per launch: same-proc
 template <typename T>
 int launch_fwd_impl(const FwdArgs& a, hipStream_t st);
 
+static bool pers_wide_on() {  // DGVCC_PERS_WIDE=0: the 16-bit 128-channel persistent forward on 2 x 4 waves
+  const char* e = getenv("DGVCC_PERS_WIDE");
+  return !(e && e[0] == '0');
+}
+// the 16-bit forward takes conv_fwd_pers_kernel<128, .., WIDE = 1> (384-pixel tiles): the same
+// conditions as launch_fwd_impl's persistent branch at BN = 128, no split-K / BN-backward epilogue
+static bool pers16_wide(const FwdArgs& a) {
+  if (!(pers_wide_on() && use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
+        !(short_k_reg() && a.R * a.S * (a.C / 64) <= 2) && (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31) &&
+        a.ksplit <= 1 && !a.bpart && use_persist() && pipe_var() == 2 && inc_shape_ok(a) &&
+        a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX))
+    return false;
+  if (!(a.Cout % 128 == 0 && !(a.Cout % 256 == 0 && pipe_wide()))) return false;  // BN = 128
+  const long long M = (long long)a.N * a.H * a.W;
+  return (long long)dg_cdiv(M, PBM) * (a.Cout / 128) > 2 * 256;
+}
+
 template <typename T>
 int launch_fwd(const FwdArgs& a0, hipStream_t st) {
   FwdArgs a = a0;
@@ -2789,6 +2813,9 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 3, T>), dim3(g), dim3(512), 0, st, a);
           else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
+        } else if (bn == 128 && pers16_wide(a)) {
+          const unsigned gw = (unsigned)std::min<long long>((long long)dg_cdiv(M, 384) * (a.Cout / 128), persist_grid());
+          hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1>), dim3(gw), dim3(512), 0, st, a);
         } else {
           if (!pers_inc()) {  // A/B: per-K-step recomputed DMA addressing
             if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
@@ -4464,6 +4491,7 @@ extern "C" int64_t dg_conv_stats_rows_ex(int dtype, int N, int H, int W, int C, 
   FwdArgs a{nullptr, ldx, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0};
   if (dtype == DG_F32 && psplit_ok(a)) return dg_cdiv(M, psplit_tile_px(a));
   if (dtype == DG_F32 && rsplit_ok(a) && rsplit3w_ok(a)) return dg_cdiv(M, 512);
+  if (DG_IS16(dtype) && pers16_wide(a)) return dg_cdiv(M, 384);
   return dg_cdiv(M, 256);
 }
 extern "C" int64_t dg_conv_bnpart_rows_ex(int dtype, int N, int H, int W, int C, int64_t ldx, int Cout, int R, int S) {
