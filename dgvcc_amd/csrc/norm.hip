@@ -197,7 +197,7 @@ __device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* 
 }
 
 template <typename T>
-__global__ __launch_bounds__(NT) void bn_bwd_partial(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
+__global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_partial(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
                                                      long long ldz, int M, int C, int ppb, const float* mean,
                                                      const float* invstd, const float* scale, const float* shift,
                                                      int act, const float* drop, int HW, float* __restrict__ part) {
@@ -215,15 +215,40 @@ __global__ __launch_bounds__(NT) void bn_bwd_partial(const T* __restrict__ g, lo
   if (pl < rows) {
     ChanParams<V> cp;
     cp.load(c0, scale, shift, mean, invstd);
-    for (int p = p0 + pl; p < p1; p += rows) {
-      float gv[V], zv[V];
-      bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
+    if constexpr (V == 8) {
+      // 16-bit: sum g' z and z in the loop and centre once per thread afterwards
+      // (sum g' xhat = (sum g' z - mu sum g') is, sum xhat = (sum z - n mu) is), so mean / invstd
+      // are not held across the loop (92 -> <= 72 VGPRs: 7 waves per SIMD instead of 5); the
+      // per-thread sums run over a few hundred pixels, far inside f32 for 16-bit operands
+      int cnt = 0;
+      for (int p = p0 + pl; p < p1; p += rows) {
+        float gv[V], zv[V];
+        bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          sg[e] += gv[e];
+          sgx[e] = fmaf(gv[e], zv[e], sgx[e]);
+          sx[e] += zv[e];
+        }
+        ++cnt;
+      }
 #pragma unroll
       for (int e = 0; e < V; ++e) {
-        const float xh = (zv[e] - cp.mu[e]) * cp.is[e];
-        sg[e] += gv[e];
-        sgx[e] = fmaf(gv[e], xh, sgx[e]);
-        sx[e] += xh;
+        const float mu = mean ? mean[c0 + e] : 0.f, is = invstd ? invstd[c0 + e] : 1.f;
+        sgx[e] = (sgx[e] - mu * sg[e]) * is;
+        sx[e] = (sx[e] - (float)cnt * mu) * is;
+      }
+    } else {
+      for (int p = p0 + pl; p < p1; p += rows) {
+        float gv[V], zv[V];
+        bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const float xh = (zv[e] - cp.mu[e]) * cp.is[e];
+          sg[e] += gv[e];
+          sgx[e] = fmaf(gv[e], xh, sgx[e]);
+          sx[e] += xh;
+        }
       }
     }
 #pragma unroll
@@ -329,7 +354,7 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_sync(const float* __restri
 }
 
 template <typename T>
-__global__ __launch_bounds__(NT) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
+__global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
                                                    long long ldz, int M, int C, const float* mean, const float* invstd,
                                                    const float* scale, const float* shift, int act, const float* drop,
                                                    int HW, const float* __restrict__ coef, T* __restrict__ dz,
@@ -344,13 +369,29 @@ __global__ __launch_bounds__(NT) void bn_bwd_apply(const T* __restrict__ g, long
   float k1[V], k2[V], k3[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) { k1[e] = coef[c0 + e]; k2[e] = coef[C + c0 + e]; k3[e] = coef[2 * C + c0 + e]; }
+  if constexpr (V == 8) {
+    // 16-bit: dz = k1 g' - (k2 is) z + (k2 is mu - k3), with k1 = gamma * invstd = the forward's
+    // scale (every finalizer forms both as that one product; identity when unnormalised), so 4
+    // per-channel values stay in registers instead of 7 (90 -> 64 VGPRs: 8 waves per SIMD
+    // instead of 5).  The result is rounded to 16 bits; the f32 reassociation is far below that.
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const float A = k2[e] * cp.is[e];
+      k3[e] = A * cp.mu[e] - k3[e];
+      k2[e] = A;
+    }
+  }
   for (long long p = gt / tpp; p < M; p += pstride) {
     float gv[V], zv[V];
     bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      const float xh = (zv[e] - cp.mu[e]) * cp.is[e];
-      gv[e] = k1[e] * gv[e] - k2[e] * xh - k3[e];
+      if constexpr (V == 8) {
+        gv[e] = fmaf(cp.sc[e], gv[e], fmaf(-k2[e], zv[e], k3[e]));
+      } else {
+        const float xh = (zv[e] - cp.mu[e]) * cp.is[e];
+        gv[e] = k1[e] * gv[e] - k2[e] * xh - k3[e];
+      }
     }
     stv(dz + p * lddz + c0, gv);
   }
