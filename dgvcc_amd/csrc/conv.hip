@@ -2955,6 +2955,7 @@ struct WgArgs {
   int stride, P, Q;    // output grid of dy (stride 1: P = H, Q = W)
   int whole_x;         // 1: descriptor over the whole x (strided convs)
   int pad_ok = 0;      // 1: the plan may be the padded 9-tap kernel's (dg_conv_wgrad)
+  int band = 0;        // > 0: the 9-tap wgrad walks its K-steps in bands of this many image rows
 };
 
 template <typename T> struct WgCfg;
@@ -3928,6 +3929,10 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
   }
   // INC: image coordinates of the next issued K-step's first pixel (kbeg + issued * 64)
   int in_ = kbeg / HW, ipr = (kbeg - in_ * HW) / a.W, iq0 = kbeg - in_ * HW - ipr * a.W, ipx = kbeg;
+  // a.band: the K-steps walk bands of a.band image rows column block by column block, so two of a
+  // step's three X strips are the previous step's (L2-hot) instead of a whole row of steps back;
+  // the band's first row and the row within it
+  int bn_ = in_, bpr = ipr, bri = 0;
 #define W9_ISSUE_INC(stage_) \
   do { \
     char* As = smem + (stage_) * STAGE; \
@@ -3946,11 +3951,26 @@ __global__ __launch_bounds__(512, 1) void conv_wgrad9_kernel(WgArgs a) {
                   ok ? loff[k] + xso : 0xFFFFFFF0u); \
       } \
     } \
-    ipx += BKP; \
-    iq0 += BKP; \
-    if (iq0 == a.W) { \
-      iq0 = 0; \
-      if (++ipr == a.H) { ipr = 0; ++in_; } \
+    if (a.band) { /* down the band's rows, then the next 64-pixel column block of the band */ \
+      if (++bri == a.band) { \
+        bri = 0; \
+        iq0 += BKP; \
+        if (iq0 == a.W) { \
+          iq0 = 0; \
+          bpr += a.band; \
+          while (bpr >= a.H) { bpr -= a.H; ++bn_; } \
+        } \
+        in_ = bn_; \
+        ipr = bpr; \
+      } else if (++ipr == a.H) { ipr = 0; ++in_; } \
+      ipx = (int)(((long long)in_ * a.H + ipr) * a.W + iq0); \
+    } else { \
+      ipx += BKP; \
+      iq0 += BKP; \
+      if (iq0 == a.W) { \
+        iq0 = 0; \
+        if (++ipr == a.H) { ipr = 0; ++in_; } \
+      } \
     } \
   } while (0)
 
@@ -4128,7 +4148,15 @@ static bool wg9p_ok(int N, int H, int W, int C, int Cout, int R, int S, int pad,
 // whole rounds of one block per CU (tail efficiency >= 90% where possible), starting from
 // one round: every extra round doubles the f32 slab written and re-read by the reduce.
 // units: the K index space (pixels, or padded cells for the PADK variant).
-static WgPlan wg9_plan(long long units, int C, int Cout) {
+// DGVCC_WG9_BAND=0: row-major K-steps; B: bands of B rows (read per call: A/B).  Default 8 on the
+// 64-input-channel layers, the HBM-bound ones (`profiles/round3d/ab_wgrad9_band*.txt`: 64 -> 64 at
+// 768x1024 +5.4%, the wider layers within +-1%)
+static int wg9_band(int C) {
+  const char* e = getenv("DGVCC_WG9_BAND");
+  return e ? std::max(0, atoi(e)) : (C == 64 ? 8 : 0);
+}
+// quantum: K-steps per split rounded up to a multiple of it (whole bands of rows per split)
+static WgPlan wg9_plan(long long units, int C, int Cout, long long quantum = 1) {
   const long long steps = (units + 63) / 64;
   const int bco = Cout % 128 == 0 ? 128 : 64;
   const long long tiles = (long long)(Cout / bco) * (C / 64);
@@ -4148,8 +4176,14 @@ static WgPlan wg9_plan(long long units, int C, int Cout) {
     if (eff >= 0.9) break;
   }
   long long sps = (steps + best - 1) / best;  // K-steps per split
+  if (quantum > 1) sps = (sps + quantum - 1) / quantum * quantum;
   const long long splits = (steps + sps - 1) / sps;
   return WgPlan{(int)splits, (int)(sps * 64)};
+}
+// the band height the 9-tap wgrad of this (W % 64 == 0) shape walks in, or 0
+static int wg9_band_of(int N, int H, int W, int C) {
+  const int b = wg9_band(C);
+  return (b > 1 && b <= H && ((long long)N * H) % b == 0) ? b : 0;
 }
 
 // ld* < 0: the shape-only plan of the workspace query (assumes the padded 9-tap kernel is
@@ -4158,8 +4192,10 @@ template <typename T>
 WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S, long long ldx = -1, long long lddy = -1,
                bool pad_ok = false) {  // H, W: output grid
   constexpr int BKP = WgCfg<T>::BKP;
-  if (Is16<T>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2))
-    return wg9_plan((long long)N * H * W, C, Cout);
+  if (Is16<T>::value && wg9_ok(C, Cout, R, S, W, (R - 1) / 2)) {
+    const int b = wg9_band_of(N, H, W, C);
+    return wg9_plan((long long)N * H * W, C, Cout, b ? (long long)b * W / 64 : 1);
+  }
   if (Is16<T>::value && pad_ok &&
       wg9p_ok(N, H, W, C, Cout, R, S, (R - 1) / 2, ldx < 0 ? C : ldx, lddy < 0 ? Cout : lddy))
     return wg9_plan((long long)N * (H + 2) * (W + 2), C, Cout);
@@ -4209,6 +4245,10 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
       if (kh2) slab_splits = 2 * a.splits;  // one slab split per k-half
       if (w9) {
         const bool inc = wg9_inc();
+        {
+          const int b = wg9_band_of(a.N, a.H, a.W, a.C);
+          a.band = (inc && b && a.pps % ((long long)b * a.W) == 0) ? b : 0;
+        }
         if (b9 == 128 && wg9_wide() && sch == 2) {
           if (inc) hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2, T>), g9, dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_wgrad9_kernel<128, 1, 0, 2, T, 0>), g9, dim3(512), 0, st, a);
