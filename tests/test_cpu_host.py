@@ -69,6 +69,28 @@ def test_wgrad_workspace_plan():
     assert L.dg_conv_wgrad_workspace(1, 0, 48, 64, 512, 512, 3, 3) == -1
 
 
+def test_conv_tile_layout_queries(monkeypatch):
+    """Rows of epilogue BN partials per conv launch follow the tile layout the launch will use
+    (host logic, no GPU): the 256-channel f32 pre-split forward on 256-pixel tiles where they
+    quantise onto the 256 CUs no worse than 192-pixel ones (DGVCC_PSPLIT_TALL), the dgrad-epilogue
+    partials always on 192-pixel tiles, the 16-bit 128-channel persistent forward on 384-pixel
+    tiles (DGVCC_PERS_WIDE)."""
+    from dgvcc_amd import _capi
+    L = _capi.lib()
+    rows = lambda dt, N, H, W, C, Co: L.dg_conv_stats_rows_ex(dt, N, H, W, C, C, Co, 3, 3)  # noqa: E731
+    M = 16 * 192 * 256
+    assert rows(0, 16, 192, 256, 256, 256) == M // 256            # 12 rounds of 256 px < 16 of 192 px
+    assert rows(0, 16, 48, 64, 512, 512) == 16 * 48 * 64 // 192   # 1/16 scale: 2 rounds either way
+    assert L.dg_conv_bnpart_rows_ex(0, 16, 192, 256, 256, 256, 256, 3, 3) == M // 192
+    assert rows(1, 16, 384, 512, 128, 128) == 16 * 384 * 512 // 384
+    monkeypatch.setenv("DGVCC_PSPLIT_TALL", "0")
+    monkeypatch.setenv("DGVCC_PERS_WIDE", "0")
+    assert rows(0, 16, 192, 256, 256, 256) == M // 192
+    assert rows(1, 16, 384, 512, 128, 128) == 16 * 384 * 512 // 256
+    monkeypatch.setenv("DGVCC_PSPLIT_TALL", "2")
+    assert rows(0, 16, 48, 64, 512, 512) == 16 * 48 * 64 // 256
+
+
 def test_call_raises_on_error():
     from dgvcc_amd import _capi
     with pytest.raises(_capi.DGError):
