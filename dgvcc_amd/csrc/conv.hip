@@ -3367,14 +3367,19 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 // 64 x 64 (x 3 taps): 4 waves of 32 x 32, two blocks per CU (the per-tap kernel's 64-wide tiles
 // were bound by the split and LDS-store work, ~30% MFMA-busy); 128 x 128: 8 waves of 64 x 32,
 // one block per CU.
-template <int BCO, int BC, int WCO, int NTH, int SWP = 0>
+// NR = 3 (the 64-channel layers, 8 waves of 32 x 16 x 9 taps): a block owns all three kernel rows,
+// staging the dY rows once and the three X strips of image rows p - 1, p, p + 1 per K-step, instead
+// of three blocks (one per kernel row) each staging and splitting the same dY rows: 33% less split
+// and staging work per MFMA (DGVCC_WGRAD_SPLIT9=0: the 64 x 64 x 3-tap blocks).
+template <int BCO, int BC, int WCO, int NTH, int SWP = 0, int NR = 1>
 __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArgs a) {
+  static_assert(NR == 1 || NR == 3, "one kernel row per block, or all three");
   constexpr int BKP = 32, XR = BKP + 2;
   constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
   constexpr int PA = BKP * ROWA, PB = XR * ROWB;           // bytes per plane
-  constexpr int TILE = 3 * (PA + PB);
+  constexpr int TILE = 3 * (PA + NR * PB);
   constexpr int CPRA = BCO / 4, CPRB = BC / 4;             // 16-B f32 chunks per pixel row
-  constexpr int AR = BKP * CPRA / NTH, BR = (XR * CPRB + NTH - 1) / NTH;
+  constexpr int AR = BKP * CPRA / NTH, BR = (NR * XR * CPRB + NTH - 1) / NTH;
   constexpr int WC = NTH / 64 / WCO;
   constexpr int TI = BCO / WCO / 16, TJ = BC / WC / 16;
   static_assert(AR * NTH == BKP * CPRA && TI >= 1 && TJ >= 1, "tile / block mismatch");
@@ -3383,13 +3388,13 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
   const int HW = a.H * a.W;
   const int M = a.N * HW;
   const int nco = a.Cout / BCO, ncb = a.C / BC;
-  const int tiles = nco * ncb * 3;
+  const int tiles = nco * ncb * (NR == 3 ? 1 : 3);
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int split = bid / tiles;
   int t = bid - split * tiles;
   const int cot = t % nco; t /= nco;
   const int cbt = t % ncb;
-  const int r = t / ncb;
+  const int r = NR == 3 ? 0 : t / ncb;  // kernel row (NR = 1)
   const int co0 = cot * BCO, c0 = cbt * BC;
   const int dh = r - 1;
   const int kbeg = split * a.pps;
@@ -3416,13 +3421,14 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       const int row = idx / CPRA, ch = idx % CPRA;
       ra[i] = bload(dyr, (unsigned)(((long long)(k0 + row - kbeg) * a.lddy + co0 + ch * 4) * 4));
     }
-    const int h = sp + dh;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int idx = tid + NTH * i;
-      const int row = idx / CPRB, ch = idx % CPRB;
+      const int strip = NR == 3 ? idx / (XR * CPRB) : 0, sidx = idx - strip * (XR * CPRB);
+      const int h = sp + (NR == 3 ? strip - 1 : dh);
+      const int row = sidx / CPRB, ch = sidx % CPRB;
       const int ww = sq - 1 + row;
-      const bool ok = idx < XR * CPRB && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
+      const bool ok = idx < NR * XR * CPRB && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
       const long long pin = (long long)sn * HW + (long long)h * a.W + ww - xlo;
       rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + c0 + ch * 4) * 4) : 0xFFFFFFF0u);
     }
@@ -3448,8 +3454,9 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
 #pragma unroll
     for (int i = 0; i < BR * ((part >> 1) & 1); ++i) {
       const int idx = tid + NTH * i;
-      if (idx < XR * CPRB) {
-        const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
+      if (idx < NR * XR * CPRB) {
+        const int strip = NR == 3 ? idx / (XR * CPRB) : 0, sidx = idx - strip * (XR * CPRB);
+        const int o = strip * 3 * PB + (sidx / CPRB) * ROWB + (sidx % CPRB) * 8;
         u2v h0, h1, h2;
         split3_4_rn(rb[i], h0, h1, h2);
         *(u2v*)(Bs + o) = h0;
@@ -3459,9 +3466,9 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
     }
   };
 
-  f4v acc[3][TI][TJ];
+  f4v acc[3 * NR][TI][TJ];
 #pragma unroll
-  for (int s = 0; s < 3; ++s)
+  for (int s = 0; s < 3 * NR; ++s)
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -3494,14 +3501,15 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       }
     }
 #pragma unroll
-    for (int s = 0; s < 3; ++s) {
+    for (int rs = 0; rs < 3 * NR; ++rs) {
+      const int s = rs % 3;
       s8v bh[TJ][3];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int col = (wc + 16 * j + 4 * p4) * 2;
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl) {
-          const char* b = Bs + pl * PB;
+          const char* b = Bs + (rs / 3) * 3 * PB + pl * PB;
           s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + (r1 + s) * ROWB + col));
           s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + (r2 + s) * ROWB + col));
           bh[j][pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -3514,13 +3522,13 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
         for (int i = 0; i < TI; ++i)
 #pragma unroll
           for (int j = 0; j < TJ; ++j)
-            acc[s][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[s][i][j], 0, 0, 0);
+            acc[rs][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[rs][i][j], 0, 0, 0);
       // one block per CU: the next step's split + LDS stores between the taps' MFMA blocks
       if (NTH == 512 && kt + 1 < nkt) {
-        if (SWP == 0 && s == 1) swrite(cur ^ 1);
-        if (SWP == 1 && s == 0) swrite(cur ^ 1, 1);
-        if (SWP == 1 && s == 1) swrite(cur ^ 1, 2);
-        if (SWP == 2 && s == 0) swrite(cur ^ 1);
+        if (SWP == 0 && rs == 1) swrite(cur ^ 1);
+        if (SWP == 1 && rs == 0) swrite(cur ^ 1, 1);
+        if (SWP == 1 && rs == 1) swrite(cur ^ 1, 2);
+        if (SWP == 2 && rs == 0) swrite(cur ^ 1);
       }
     }
     if (NTH != 512 && kt + 1 < nkt) swrite(cur ^ 1);  // two blocks per CU overlap each other instead
@@ -3530,7 +3538,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
   const long long ldk = 9ll * a.C;
   float* out = a.slab + (long long)split * a.Cout * ldk;
 #pragma unroll
-  for (int s = 0; s < 3; ++s)
+  for (int s = 0; s < 3 * NR; ++s)
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -3596,6 +3604,13 @@ static int wgs3_tile(int C, int Cout, int R, int S, int W) {
 }
 static bool wgs3_shape_ok(int C, int Cout, int R, int S, int W) { return wgs3_tile(C, Cout, R, S, W) != 0; }
 static long long wgs3_tiles(int C, int Cout, int b) { return (long long)(Cout / b) * (C / b) * 3; }
+// the 64-tile layers on the 9-tap (all three kernel rows per block) form: DGVCC_WGRAD_SPLIT9=0 off
+static bool wgs9_on(int b3) {
+  if (b3 != 64) return false;
+  const char* e = getenv("DGVCC_WGRAD_SPLIT9");
+  return !(e && e[0] == '0');
+}
+static long long wgs9_tiles(int C, int Cout) { return (long long)(Cout / 64) * (C / 64); }
 static long long wgs3_slots(int b) { return b == 64 ? 512 : 256; }
 
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int Cout, int C, int RS,
@@ -4289,14 +4304,16 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
   } else if constexpr (!Is16<T>::value) {
     const long long M3 = (long long)a.N * a.P * a.Q;
     const int b3 = wgs3_tile(a.C, a.Cout, a.R, a.S, a.W);
+    const bool nr3 = wgs9_on(b3);
     if (f32_split() && a.stride == 1 && !a.whole_x && a.pad == 1 && b3) {
-      const WgPlan p = wgs_plan(M3, wgs3_tiles(a.C, a.Cout, b3), wgs3_slots(b3));
+      const WgPlan p = nr3 ? wgs_plan(M3, wgs9_tiles(a.C, a.Cout), 256) : wgs_plan(M3, wgs3_tiles(a.C, a.Cout, b3), wgs3_slots(b3));
       if ((long long)(p.pps + 2 * (a.W + 1)) * std::max(a.ldx, a.lddy) * 4 < (1ll << 31)) {
         a.splits = p.splits;
         a.pps = p.pps;
         slab_splits = p.splits;
-        const dim3 g3((unsigned)(wgs3_tiles(a.C, a.Cout, b3) * p.splits));
-        if (b3 == 64) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 256>), g3, dim3(256), 0, st, a);
+        const dim3 g3((unsigned)((nr3 ? wgs9_tiles(a.C, a.Cout) : wgs3_tiles(a.C, a.Cout, b3)) * p.splits));
+        if (nr3) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 512, 2, 3>), g3, dim3(512), 0, st, a);
+        else if (b3 == 64) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 256>), g3, dim3(256), 0, st, a);
         else {
           // placement of the next step's split + LDS stores among the taps' MFMA blocks: 0 after tap 1,
           // 1 dY after tap 0 / X after tap 1, 2 (default) all after tap 0: wgrad 0.59 -> 0.60 of the
@@ -4712,6 +4729,8 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
     const int b3 = wgs3_tile(C, Cout, R, S, W);
     const WgPlan q3 = wgs_plan((long long)N * H * W, wgs3_tiles(C, Cout, b3), wgs3_slots(b3));
     if (q3.splits > q.splits) q = q3;
+    const WgPlan q9 = wgs_plan((long long)N * H * W, wgs9_tiles(C, Cout), 256);
+    if (wgs9_on(b3) && q9.splits > q.splits) q = q9;
   }
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
   return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
