@@ -275,6 +275,134 @@ __global__ __launch_bounds__(SNT, 2) void stem_fwd_kernel(const float* __restric
   }
 }
 
+// fp32 first layer forward: exact f32 FMAs on the VALU (27 MACs per output; 0.1 TFLOP per 16
+// frames at 768x1024 is below the VALU's ~1 ms, and an MFMA split would need 6 products per
+// f32 product), replacing the generic route's [N*H*W][64] f32 im2col buffer, its K = 64
+// GEMM and the separate BN statistics pass over z.  Wave-independent 64-pixel row segments,
+// lane = pixel: the 27 taps are loaded straight from the NCHW image (prefetched a segment
+// ahead), the filter wk[27][64] is wave-uniform (scalar loads), the 64 channel results go
+// through the wave's LDS tile [64 px][64 co] (16-B chunks XOR-swizzled by pixel) so the z
+// stores are 1-KB wave writes, and the statistics read the tile back with lane = channel
+// (shifted sums, then the Chan merge of stem_fwd_kernel's epilogue: same part rows).
+constexpr int F32_TILE = 64 * 16;  // f4v chunks per wave tile (16 KB)
+
+__global__ __launch_bounds__(SNT, 2) void stem_fwd_f32_kernel(const float* __restrict__ img, int H, int W,
+                                                              const float* __restrict__ wk,
+                                                              const float* __restrict__ bias, float* __restrict__ z,
+                                                              long long ldz, long long nseg, float* __restrict__ part) {
+  __shared__ f4v tile[4 * F32_TILE];
+  __shared__ float sh[4][3][SCO];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  f4v* O = tile + wid * F32_TILE;
+  const int spr = W / 64;
+  // bias in the store / statistics phases, where lanes own channels
+  const int cq = lane >> 2, ci = lane & 3;
+  const f4v b4 = bias ? *(const f4v*)(bias + 4 * (lane & 15)) : f4v{0.f, 0.f, 0.f, 0.f};
+  const float b1 = bias ? bias[lane] : 0.f;
+  float xv[27];
+  auto gload = [&](long long seg) {
+    const int row_id = (int)(seg / spr);  // n*H + p
+    const int q = (int)(seg - (long long)row_id * spr) * 64 + lane;
+    const int n = row_id / H, p = row_id - n * H;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int pr = p + r - 1;
+        const bool rok = (unsigned)pr < (unsigned)H;
+        const float* src = img + ((long long)(n * 3 + c) * H + (rok ? pr : 0)) * W + q;
+        const int e = (c * 3 + r) * 3;
+        xv[e] = (rok && q >= 1) ? src[-1] : 0.f;
+        xv[e + 1] = rok ? src[0] : 0.f;
+        xv[e + 2] = (rok && q + 1 < W) ? src[1] : 0.f;
+      }
+  };
+  float Ksh = 0.f, S1 = 0.f, S2 = 0.f;
+  long long nloc = 0;
+  long long seg = (long long)blockIdx.x * 4 + wid;
+  const long long sstride = (long long)gridDim.x * 4;
+  if (seg < nseg) gload(seg);
+  for (; seg < nseg; seg += sstride) {
+    lds_fence();  // the previous segment's tile reads are done before it is overwritten
+    // 16 channels per pass (rolled): 16 accumulators, the pass's filter slice [27][16] is
+    // wave-uniform and arrives through scalar loads one 16-float row per tap
+#pragma unroll 1
+    for (int cc = 0; cc < 4; ++cc) {
+      const float* w = wk + 16 * cc;
+      float acc[16];
+#pragma unroll
+      for (int co = 0; co < 16; ++co) acc[co] = 0.f;
+      // one tap's 16 weights in flight ahead of its FMAs; the opaque address keeps the compiler
+      // from hoisting all 432 scalar loads of the pass (which spills the SGPR file)
+      float wc[16], wn[16];
+#pragma unroll
+      for (int co = 0; co < 16; ++co) wc[co] = w[co];
+#pragma unroll
+      for (int k = 0; k < 27; ++k) {
+        if (k + 1 < 27) {
+          int off = (k + 1) * SCO;
+          asm volatile("" : "+s"(off));  // opaque offset: the load cannot move above this tap
+#pragma unroll
+          for (int co = 0; co < 16; ++co) wn[co] = w[off + co];
+        }
+        const float xk = xv[k];
+#pragma unroll
+        for (int co = 0; co < 16; ++co) acc[co] = fmaf(xk, wc[co], acc[co]);
+#pragma unroll
+        for (int co = 0; co < 16; ++co) wc[co] = wn[co];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        O[lane * 16 + ((4 * cc + j) ^ (lane & 15))] = f4v{acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]};
+    }
+    if (seg + sstride < nseg) gload(seg + sstride);
+    lds_fence();
+    const long long m0 = seg * 64;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int row = 4 * u + (lane >> 4), ch = lane & 15;
+      const f4v v = O[row * 16 + (ch ^ (row & 15))];
+      *(f4v*)(z + (m0 + row) * ldz + 4 * ch) = f4v{v[0] + b4[0], v[1] + b4[1], v[2] + b4[2], v[3] + b4[3]};
+    }
+    // statistics of the stored values (the same fp32 add), lane = channel
+    const float* Of = (const float*)O;
+    if (nloc == 0) Ksh = Of[cq * 4 + ci] + b1;  // pixel 0: chunk cq ^ 0
+#pragma unroll 8
+    for (int px = 0; px < 64; ++px) {
+      const float d = (Of[(px * 16 + (cq ^ (px & 15))) * 4 + ci] + b1) - Ksh;
+      S1 += d;
+      S2 = fmaf(d, d, S2);
+    }
+    nloc += 64;
+  }
+  {
+    const float nn = (float)nloc;
+    sh[wid][0][lane] = nn;
+    sh[wid][1][lane] = nloc ? Ksh + S1 / nn : 0.f;
+    sh[wid][2][lane] = nloc ? fmaxf(S2 - S1 * S1 / nn, 0.f) : 0.f;
+  }
+  __syncthreads();
+  if (threadIdx.x < SCO) {  // Chan merge of the 4 waves
+    const int c = threadIdx.x;
+    float n = 0.f, mean = 0.f, m2 = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const float nb = sh[w][0][c];
+      if (nb == 0.f) continue;
+      const float mb = sh[w][1][c];
+      const float nt = n + nb;
+      const float d = mb - mean;
+      mean += d * (nb / nt);
+      m2 += sh[w][2][c] + d * d * (n * nb / nt);
+      n = nt;
+    }
+    float* o = part + (long long)blockIdx.x * 3 * SCO;
+    o[c] = n;
+    o[SCO + c] = mean;
+    o[2 * SCO + c] = m2;
+  }
+}
+
 // Backward, wave-independent 32-pixel row segments: dW[co][k] = sum_px dz[px][co] col[px][k].
 // Per wave LDS: dz tile [32 px][64 co] bf16 (128-B rows, read transposed) and the
 // transposed im2col tile colT[32 k][32 px] bf16 (64-B rows; rows 27..31 stay zero).
@@ -617,6 +745,18 @@ extern "C" int dg_stem_fwd(const float* img, int N, int H, int W, const void* wp
   const long long nseg = (long long)N * H * (W / 64);
   hipLaunchKernelGGL(stem_fwd_kernel<0>, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
                      (const bf16*)wpack, bias, (bf16*)z, (long long)ldz, nseg, part, StemBn{});
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// fp32: wk = the filter as [k = (c*3 + r)*3 + s][64] f32, z f32 NHWC (same part rows).
+extern "C" int dg_stem_fwd_f32(const float* img, int N, int H, int W, const float* wk, const float* bias, float* z,
+                               int64_t ldz, float* part, void* stream) {
+  DG_REQUIRE(img && wk && z && part && N > 0 && H > 0 && W > 0 && ldz >= SCO);
+  DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldz % 4 == 0);
+  const long long nseg = (long long)N * H * (W / 64);
+  hipLaunchKernelGGL(stem_fwd_f32_kernel, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
+                     wk, bias, z, (long long)ldz, nseg, part);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -36,6 +36,8 @@ ACT_NONE, ACT_RELU = 0, 1
 _FROZEN_GEN = [0]
 _EVAL_FUSE = __import__("os").environ.get("DGVCC_EVAL_FUSE", "1") != "0"
 _STEM_RECOMP = __import__("os").environ.get("DGVCC_STEM_RECOMP", "1") != "0"
+# fp32 first layer straight from the image (dg_stem_fwd_f32); 0 = im2col + GEMM + statistics pass
+_STEM_F32 = __import__("os").environ.get("DGVCC_STEM_F32", "1") != "0"
 
 
 def invalidate_frozen():
@@ -103,8 +105,10 @@ class ConvLayer:
         return K.pack_weight(w, dt)
 
     def stem_ok(self, dt) -> bool:
-        """bf16 first layer with BN + ReLU: fused conv/statistics and BN-backward/wgrad kernels."""
-        return (self.first and dt == torch.bfloat16 and self.bn is not None and self.act == ACT_RELU
+        """bf16 first layer with BN + ReLU: fused conv/statistics and BN-backward/wgrad kernels;
+        fp32: conv + BN statistics from the image (the backward re-forms the im2col for its wgrad)."""
+        ok_dt = dt == torch.bfloat16 or (dt == torch.float32 and _STEM_F32)
+        return (self.first and ok_dt and self.bn is not None and self.act == ACT_RELU
                 and self.Cin == 3 and self.Cout == 64 and self.R == 3)
 
     @staticmethod
@@ -129,6 +133,23 @@ class ConvLayer:
         bn = self.bn
         # nn.SyncBatchNorm under a multi-rank process group: global batch statistics (syncbn.py)
         pg = SB.group_of(bn) if training else None
+        if stem and dt == torch.float32:
+            wk = (K.stem_weight_f32(self.conv.weight) if training else
+                  frozen(self, ("stem32", dt), (self.conv.weight,), lambda: K.stem_weight_f32(self.conv.weight)))
+            z = Act(K.nhwc(x.shape[0], x.shape[2], x.shape[3], self.Cout, dt, x.device))
+            part, nblk = K.stem_fwd_f32(x, wk, bias, z)
+            if pg is not None:
+                stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk)
+            elif training:
+                bn.num_batches_tracked.add_(1)
+                stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
+                                           bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+            else:
+                stats = bn_eval_cached(self, bn)
+            self._apply(z, stats, out, drop, pool)
+            if tape is not None:
+                tape[self] = (x, z, stats, None, drop, training)
+            return
         if stem:
             N, _, H, W = x.shape
             build = lambda: K.pack_weight(self.conv.weight.detach(), dt, cpad=3, row_len=32)  # noqa: E731
@@ -223,6 +244,8 @@ class ConvLayer:
             if self.conv.bias is not None else None
         gamma = self.bn.weight.detach() if self.bn is not None else None
         pg = SB.group_of(self.bn)
+        if isinstance(x, torch.Tensor) and z is not None and z.buf.dtype == torch.float32:
+            x = Act(K.im2col_c3(x, torch.float32))  # fp32 stem: the generic BN backward + im2col wgrad
         if isinstance(x, torch.Tensor):  # fused bf16 stem: coefficients, then BN-backward + wgrad in one pass
             dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
             bias = self.conv.bias.detach() if self.conv.bias is not None else None

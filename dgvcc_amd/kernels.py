@@ -229,6 +229,26 @@ def stem_fwd(img: torch.Tensor, wp: torch.Tensor, bias: torch.Tensor | None, z: 
     return part, rows
 
 
+def stem_weight_f32(w: torch.Tensor) -> torch.Tensor:
+    """[64][3][3][3] torch filter -> the f32 [27][64] layout of dg_stem_fwd_f32 (k = (c*3+r)*3+s)."""
+    return w.detach().float().permute(1, 2, 3, 0).reshape(27, w.shape[0]).contiguous()
+
+
+def stem_fwd_f32(img: torch.Tensor, wk: torch.Tensor, bias: torch.Tensor | None, z: Act) -> tuple:
+    """fp32 first layer: z = conv3x3(img NCHW f32, 3->64) + bias (exact f32 FMAs), plus BN partials."""
+    N, _, H, W = img.shape
+    if wk.shape != (27, 64) or wk.dtype != torch.float32 or z.buf.dtype != torch.float32 or z.C != 64 \
+            or (z.N, z.H, z.W) != (N, H, W):
+        raise ValueError("stem_fwd_f32: operand shapes/dtypes")
+    rows = query("dg_stem_part_rows", N, H, W)
+    part = torch.empty((rows, 3, 64), dtype=torch.float32, device=img.device)
+    flops = 2.0 * N * H * W * 27 * 64
+    nbytes = 4.0 * img.numel() + 4.0 * N * H * W * 64
+    _timed("stem", flops, lambda: call("dg_stem_fwd_f32", ptr(img), N, H, W, ptr(wk), ptr(bias), z.ptr, z.ld,
+                                       ptr(part), stream()), nbytes)
+    return part, rows
+
+
 def bn_part_finalize(part: torch.Tensor, nblk: int, C: int, gamma, beta, running_mean, running_var,
                      momentum, eps):
     stats = torch.empty((4, C), dtype=torch.float32, device=part.device)

@@ -279,6 +279,11 @@ int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp, const voi
 int64_t dg_stem_part_rows(int N, int H, int W);
 int dg_stem_fwd(const float* img, int N, int H, int W, const void* wpack, const float* bias,
                 void* z, int64_t ldz, float* part, void* stream);
+/* dg_stem_fwd_f32: the fp32 first layer forward (exact f32 FMAs): z f32 (pixel stride ldz,
+ * ldz % 4 == 0) = conv + bias and the same BN partials; wk: f32 [27][64], k = (c*3+r)*3+s
+ * (torch weight [co][c][r][s] permuted to [c][r][s][co]).  W % 64 == 0. */
+int dg_stem_fwd_f32(const float* img, int N, int H, int W, const float* wk, const float* bias,
+                    float* z, int64_t ldz, float* part, void* stream);
 int64_t dg_stem_bwd_workspace(int N, int H, int W);
 int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
                 int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,

@@ -28,6 +28,39 @@ def relerr(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 32, 64), (1, 16, 256), (3, 5, 64), (2, 128, 1024)])
+def test_stem_fwd_f32(dev, N, H, W):
+    """fp32 first layer (dg_stem_fwd_f32, exact f32 FMAs) vs the float64 conv, and its BN
+    partials vs float64 statistics of the stored z; (2, 128, 1024): several segments per wave."""
+    K = _k()
+    g = torch.Generator().manual_seed(3)
+    img = torch.randn(N, 3, H, W, generator=g)
+    w = torch.randn(64, 3, 3, 3, generator=g) / 27 ** 0.5
+    b = torch.randn(64, generator=g) * 0.1 + 2.0  # |mean| >> std: exercises the shifted statistics
+    gam = torch.rand(64, generator=g) + 0.5
+    bet = torch.randn(64, generator=g) * 0.1
+    imgd, wd, bd = img.to(dev), w.to(dev), b.to(dev)
+    z = K.Act(K.nhwc(N, H, W, 64, torch.float32, dev))
+    z.buf.fill_(float("nan"))  # every output must be written
+    part, nblk = K.stem_fwd_f32(imgd, K.stem_weight_f32(wd), bd, z)
+    rm, rv = torch.zeros(64, device=dev), torch.ones(64, device=dev)
+    stats = K.bn_part_finalize(part, nblk, 64, gam.to(dev), bet.to(dev), rm, rv, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    ref = F.conv2d(img.double(), w.double(), b.double(), padding=1)
+    assert torch.isfinite(z.buf).all()
+    assert relerr(z.buf.permute(0, 3, 1, 2), ref) < 2e-6
+    zf = z.buf.double().cpu().reshape(-1, 64)
+    assert relerr(stats[0], zf.mean(0)) < 1e-6
+    assert relerr(stats[1], 1.0 / (zf.var(0, unbiased=False) + 1e-5).sqrt()) < 1e-5
+    assert relerr(rv, 0.9 + 0.1 * zf.var(0, unbiased=True)) < 1e-5
+    # the generic route (im2col + split-math GEMM + statistics pass) agrees to its own accuracy
+    col = K.Act(K.im2col_c3(imgd, torch.float32))
+    z0 = K.Act(K.nhwc(N, H, W, 64, torch.float32, dev))
+    K.conv_fwd(col, K.pack_weight(wd, torch.float32, cpad=3, row_len=64), 64, 1, 0, z0, bias=bd)
+    torch.cuda.synchronize()
+    assert relerr(z.buf, z0.buf) < 1e-5
+
+
 @pytest.mark.parametrize("N,H,W", [(2, 32, 64), (2, 8, 128), (1, 16, 256), (3, 5, 64)])
 def test_stem_fwd_bwd(dev, N, H, W):
     K = _k()
