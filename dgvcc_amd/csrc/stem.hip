@@ -589,6 +589,120 @@ __global__ __launch_bounds__(SNT, 2) void stem_bwd_kernel(
   for (int e = threadIdx.x; e < SCO * SK; e += SNT) o[e] = red[e];
 }
 
+// fp32 backward of the first layer: dz = BN/ReLU backward of (g, z) (bn_bwd_apply's arithmetic)
+// and dW[co][k] = sum_px dz[px][co] col[px][k] on v_mfma_f32_16x16x4_f32 (exact f32 products),
+// without the dz tensor or the im2col buffer in HBM.  Wave-independent 32-pixel row segments;
+// per wave LDS: dz [32 px][64 co] f32 (row stride 80 floats: the 4 pixel rows of an A read hit
+// distinct banks) and colT [32 k][32 px] f32 (stride 36: the 16 k rows x 4 pixels of a B read
+// hit distinct banks; rows 27..31 zero).  The next segment's g, z and taps are loaded while
+// this one's MFMAs run.  Output: one slab row [64][32] per block (stem_wgrad_reduce order
+// k = (r*3+s)*3+c), combined over the 4 waves in a fixed order.
+constexpr int F_DZS = 80, F_CTS = 36;
+constexpr int F_BW = (32 * F_DZS + 32 * F_CTS) * 4;
+
+__global__ __launch_bounds__(SNT, 2) void stem_bwd_f32_kernel(
+    const float* __restrict__ img, int H, int W, const float* __restrict__ g, long long ldg,
+    const float* __restrict__ z, long long ldz, const float* __restrict__ mean, const float* __restrict__ invstd,
+    const float* __restrict__ scale, const float* __restrict__ shift, const float* __restrict__ coef, long long nseg,
+    float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * F_BW];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* DZ = (float*)(smem + wid * F_BW);
+  float* CT = DZ + 32 * F_DZS;
+  const int spr = W / 32;
+  const int c0 = (lane & 15) * 4;  // this lane's 4 channels in the dz phase
+  float sc[4], sf[4], mu[4], is[4], k1[4], k2[4], k3[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; mu[e] = mean[c0 + e]; is[e] = invstd[c0 + e];
+    k1[e] = coef[c0 + e]; k2[e] = coef[SCO + c0 + e]; k3[e] = coef[2 * SCO + c0 + e];
+  }
+  const int half = lane >> 5, xq = lane & 31;
+  for (int r = 27 + half; r < 32; r += 2) CT[r * F_CTS + xq] = 0.f;
+  f4v gr[8], zr[8];
+  float cv[14];
+  auto gload = [&](long long seg) {
+    const int row_id = (int)(seg / spr);
+    const int q0 = (int)(seg - (long long)row_id * spr) * 32;
+    const int n = row_id / H, p = row_id - n * H;
+    const long long m0 = (long long)row_id * W + q0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const long long m = m0 + (lane >> 4) + 4 * u;
+      gr[u] = *(const f4v*)(g + m * ldg + c0);
+      zr[u] = *(const f4v*)(z + m * ldz + c0);
+    }
+#pragma unroll
+    for (int i = 0; i < 14; ++i) {
+      const int k = 2 * i + half;
+      const int t = k / 3, c = k - 3 * t, r = t / 3, s2 = t - 3 * r;
+      const int pr = p + r - 1, qq = q0 + xq + s2 - 1;
+      const bool in = k < 27 && (unsigned)pr < (unsigned)H && (unsigned)qq < (unsigned)W;
+      cv[i] = in ? img[((long long)(n * 3 + c) * H + pr) * W + qq] : 0.f;
+    }
+  };
+  f4v acc[4][2];
+#pragma unroll
+  for (int cf = 0; cf < 4; ++cf) acc[cf][0] = acc[cf][1] = f4v{0.f, 0.f, 0.f, 0.f};
+  const int mrow = lane & 15, kq = lane >> 4;  // MFMA operand roles: A[m][k], B[k][n]
+  long long seg = (long long)blockIdx.x * 4 + wid;
+  const long long sstride = (long long)gridDim.x * 4;
+  if (seg < nseg) gload(seg);
+  for (; seg < nseg; seg += sstride) {
+    lds_fence();  // the previous segment's fragment reads are done before the tiles are overwritten
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      float dz[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // bn_bwd_load + bn_bwd_apply of norm.hip (act = relu, no dropout)
+        float gv = gr[u][e];
+        const float zv = zr[u][e];
+        if (!(fmaf(zv, sc[e], sf[e]) > 0.f)) gv = 0.f;
+        const float xh = (zv - mu[e]) * is[e];
+        dz[e] = k1[e] * gv - k2[e] * xh - k3[e];
+      }
+      *(f4v*)(DZ + ((lane >> 4) + 4 * u) * F_DZS + c0) = f4v{dz[0], dz[1], dz[2], dz[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 14; ++i)
+      if (2 * i + half < 27) CT[(2 * i + half) * F_CTS + xq] = cv[i];
+    if (seg + sstride < nseg) gload(seg + sstride);
+    lds_fence();
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {  // 4 pixels per MFMA k-step
+      const int px = 4 * s + kq;
+      float bv[2];
+#pragma unroll
+      for (int kf = 0; kf < 2; ++kf) bv[kf] = CT[(16 * kf + mrow) * F_CTS + px];
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf) {
+        const float av = DZ[px * F_DZS + 16 * cf + mrow];
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf) acc[cf][kf] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv[kf], acc[cf][kf], 0, 0, 0);
+      }
+    }
+  }
+  // combine the 4 waves in a fixed order (deterministic), then one slab row per block
+  __syncthreads();
+  float* red = (float*)smem;  // [64 co][32 k]
+  for (int w = 0; w < 4; ++w) {
+    if (wid == w) {
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf)
+#pragma unroll
+        for (int kf = 0; kf < 2; ++kf)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float* d = red + (16 * cf + 4 * kq + i) * SK + 16 * kf + mrow;
+            *d = (w == 0 ? 0.f : *d) + acc[cf][kf][i];
+          }
+    }
+    __syncthreads();
+  }
+  float* o = slab + (long long)blockIdx.x * SCO * SK;
+  for (int e = threadIdx.x; e < SCO * SK; e += SNT) o[e] = red[e];
+}
+
 // out[rb][c] = sum of rows [rb*rpb, (rb+1)*rpb) of in[rows][cols]; grid (cols/256, ceil(rows/rpb)).
 __global__ __launch_bounds__(SNT) void colsum_rows_kernel(const float* __restrict__ in, int rows, int cols, int rpb,
                                                           float* __restrict__ out) {
@@ -860,6 +974,32 @@ extern "C" int64_t dg_stem_bwd_workspace(int N, int H, int W) {
 
 // z == NULL: z is recomputed from img with the packed filters wpack (+ bias), as dg_stem_stats
 // / dg_stem_apply do, instead of read from HBM.
+// fp32: g, z f32 (pixel strides ldg, ldz % 4 == 0); same workspace, reduction and dw layout.
+extern "C" int dg_stem_bwd_f32(const float* img, int N, int H, int W, const float* g, int64_t ldg, const float* z,
+                               int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
+                               const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,
+                               int accumulate, void* stream) {
+  DG_REQUIRE(img && g && z && save_mean && save_invstd && scale && shift && coef && dw && workspace);
+  DG_REQUIRE(N > 0 && H > 0 && W > 0 && ldg >= SCO && ldz >= SCO);
+  DG_SUPPORTED(W % 32 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldg % 4 == 0 && ldz % 4 == 0);
+  const long long nseg = (long long)N * H * (W / 32);
+  const int grid = stem_bwd_grid(nseg);
+  const int nred = dg_cdiv(grid, STEM_RPB);
+  DG_REQUIRE(ws_bytes >= ((int64_t)grid + nred) * SCO * SK * 4);
+  hipStream_t st = (hipStream_t)stream;
+  float* slab = (float*)workspace;
+  float* slab2 = slab + (long long)grid * SCO * SK;
+  hipLaunchKernelGGL(stem_bwd_f32_kernel, dim3(grid), dim3(SNT), 0, st, img, H, W, g, (long long)ldg, z,
+                     (long long)ldz, save_mean, save_invstd, scale, shift, coef, nseg, slab);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3(SCO * SK / SNT, nred), dim3(SNT), 0, st, (const float*)slab, grid,
+                     SCO * SK, STEM_RPB, slab2);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(stem_wgrad_reduce, dim3(SCO), dim3(SNT), 0, st, (const float*)slab2, nred, dw, accumulate);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
 extern "C" int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
                            int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
                            const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,

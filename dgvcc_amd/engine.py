@@ -38,6 +38,8 @@ _EVAL_FUSE = __import__("os").environ.get("DGVCC_EVAL_FUSE", "1") != "0"
 _STEM_RECOMP = __import__("os").environ.get("DGVCC_STEM_RECOMP", "1") != "0"
 # fp32 first layer straight from the image (dg_stem_fwd_f32); 0 = im2col + GEMM + statistics pass
 _STEM_F32 = __import__("os").environ.get("DGVCC_STEM_F32", "1") != "0"
+# its backward: dz and the wgrad on f32 MFMA in one pass (dg_stem_bwd_f32); 0 = BN backward + im2col wgrad
+_STEM_BWD_F32 = __import__("os").environ.get("DGVCC_STEM_BWD_F32", "1") != "0"
 
 
 def invalidate_frozen():
@@ -245,7 +247,17 @@ class ConvLayer:
         gamma = self.bn.weight.detach() if self.bn is not None else None
         pg = SB.group_of(self.bn)
         if isinstance(x, torch.Tensor) and z is not None and z.buf.dtype == torch.float32:
-            x = Act(K.im2col_c3(x, torch.float32))  # fp32 stem: the generic BN backward + im2col wgrad
+            if (_STEM_BWD_F32 and pg is None and drop is None and g is not None and g_pool is None
+                    and pre is None and x.shape[3] % 32 == 0):
+                # fp32 stem: BN-backward coefficients, then dz and the conv1_1 wgrad in one pass
+                coef = K.bn_bwd_coef(g, z, gamma, stats, self.act, dgamma, dbeta, dbias, drop)
+                dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
+                K.stem_bwd_f32(x, g, z, stats, coef, dw)
+                grads = {self.conv.weight: dw, self.bn.weight: dgamma, self.bn.bias: dbeta}
+                if self.conv.bias is not None:
+                    grads[self.conv.bias] = dbias
+                return grads
+            x = Act(K.im2col_c3(x, torch.float32))  # the generic BN backward + im2col wgrad
         if isinstance(x, torch.Tensor):  # fused bf16 stem: coefficients, then BN-backward + wgrad in one pass
             dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
             bias = self.conv.bias.detach() if self.conv.bias is not None else None

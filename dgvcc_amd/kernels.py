@@ -249,6 +249,21 @@ def stem_fwd_f32(img: torch.Tensor, wk: torch.Tensor, bias: torch.Tensor | None,
     return part, rows
 
 
+def stem_bwd_f32(img: torch.Tensor, g: Act, z: Act, stats, coef, dw: torch.Tensor, accumulate=False):
+    """fp32 first-layer backward: conv1_1 weight gradient from (g, z) and the BN-backward coef."""
+    N, _, H, W = img.shape
+    if g.buf.dtype != torch.float32 or z.buf.dtype != torch.float32 or (z.N, z.H, z.W, z.C) != (N, H, W, 64) \
+            or (g.N, g.H, g.W, g.C) != (N, H, W, 64) or dw.shape != (64, 3, 3, 3):
+        raise ValueError("stem_bwd_f32: operand shapes/dtypes")
+    ws = query("dg_stem_bwd_workspace", N, H, W)
+    work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=img.device)
+    flops = 2.0 * N * H * W * 27 * 64
+    nbytes = 4.0 * g.M * g.C * 2 + 4.0 * img.numel()
+    _timed("stem_wgrad", flops, lambda: call("dg_stem_bwd_f32", ptr(img), N, H, W, g.ptr, g.ld, z.ptr, z.ld,
+                                             ptr(stats[0]), ptr(stats[1]), ptr(stats[2]), ptr(stats[3]),
+                                             ptr(coef), ptr(dw), ptr(work), ws, int(accumulate), stream()), nbytes)
+
+
 def bn_part_finalize(part: torch.Tensor, nblk: int, C: int, gamma, beta, running_mean, running_var,
                      momentum, eps):
     stats = torch.empty((4, C), dtype=torch.float32, device=part.device)

@@ -284,6 +284,13 @@ int dg_stem_fwd(const float* img, int N, int H, int W, const void* wpack, const 
  * (torch weight [co][c][r][s] permuted to [c][r][s][co]).  W % 64 == 0. */
 int dg_stem_fwd_f32(const float* img, int N, int H, int W, const float* wk, const float* bias,
                     float* z, int64_t ldz, float* part, void* stream);
+/* dg_stem_bwd_f32: fp32 counterpart of dg_stem_bwd with z stored (g, z f32, ldg/ldz % 4 == 0,
+ * W % 32 == 0; dg_stem_bwd_workspace bytes): dW [64][3][3][3] f32 on f32 MFMA, dz and the im2col
+ * never materialised. */
+int dg_stem_bwd_f32(const float* img, int N, int H, int W, const float* g, int64_t ldg, const float* z,
+                    int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,
+                    const float* shift, const float* coef, float* dw, void* workspace, int64_t ws_bytes,
+                    int accumulate, void* stream);
 int64_t dg_stem_bwd_workspace(int N, int H, int W);
 int dg_stem_bwd(const float* img, int N, int H, int W, const void* g, int64_t ldg, const void* z,
                 int64_t ldz, const float* save_mean, const float* save_invstd, const float* scale,

@@ -60,6 +60,28 @@ def test_stem_fwd_f32(dev, N, H, W):
     torch.cuda.synchronize()
     assert relerr(z.buf, z0.buf) < 1e-5
 
+    # backward (dg_stem_bwd_f32): dz and the wgrad in one pass vs the materialised dz route
+    gy = torch.randn(N, H, W, 64, generator=g)
+    g_act = K.Act(gy.to(dev))
+    dgam, dbet, dbias = (torch.empty(64, device=dev) for _ in range(3))
+    coef = K.bn_bwd_coef(g_act, z, gam.to(dev), stats, 1, dgam, dbet, dbias)
+    dw = torch.full((64, 3, 3, 3), float("nan"), device=dev)
+    K.stem_bwd_f32(imgd, g_act, z, stats, coef, dw)
+    dz0 = K.Act(K.nhwc(N, H, W, 64, torch.float32, dev))
+    dgam0, dbet0, dbias0 = (torch.empty(64, device=dev) for _ in range(3))
+    K.bn_bwd(g_act, z, gam.to(dev), stats, 1, dz0, dgam0, dbet0, dbias0)
+    torch.cuda.synchronize()
+    assert torch.equal(dgam, dgam0) and torch.equal(dbet, dbet0) and torch.equal(dbias, dbias0)
+    dz64 = dz0.buf.double().cpu().permute(0, 3, 1, 2)
+    wref = torch.nn.grad.conv2d_weight(img.double(), (64, 3, 3, 3), dz64, padding=1)
+    assert torch.isfinite(dw).all()
+    assert relerr(dw, wref) < 1e-5
+    # accumulate = 1 adds into dw
+    dw2 = dw.clone()
+    K.stem_bwd_f32(imgd, g_act, z, stats, coef, dw2, accumulate=True)
+    torch.cuda.synchronize()
+    assert relerr(dw2, 2 * wref) < 1e-5
+
 
 @pytest.mark.parametrize("N,H,W", [(2, 32, 64), (2, 8, 128), (1, 16, 256), (3, 5, 64)])
 def test_stem_fwd_bwd(dev, N, H, W):
