@@ -343,6 +343,9 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_sync(const float* __restri
                                                            float* dbias, float* coef) {
   const int c = blockIdx.x * NT + threadIdx.x;
   if (c >= C) return;
+  // Mg <= 0: the pixel count over all ranks is the all-reduced fourth row (hi + lo parts, each
+  // exact in f32), so ranks holding different batch sizes share one count, as in the forward
+  if (Mg <= 0.0) Mg = (double)glob[3 * C] + (double)glob[3 * C + 1];
   const float gm = gamma ? gamma[c] : 1.f;
   const float k1 = gm * invstd[c];
   const float k2 = (float)(k1 * (double)glob[C + c] / Mg);
@@ -955,7 +958,9 @@ extern "C" int dg_bn_bwd_pool_sums(int dtype, const void* gp, int64_t ldgp, cons
 extern "C" int dg_bn_bwd_finalize_sync(const float* sums_local, const float* sums_global, int M_local,
                                        int64_t M_global, int C, const float* gamma, const float* save_invstd,
                                        float* dgamma, float* dbeta, float* dbias, float* coef, void* stream) {
-  DG_REQUIRE(sums_local && sums_global && save_invstd && coef && M_local > 0 && M_global >= M_local && C > 0);
+  DG_REQUIRE(sums_local && sums_global && save_invstd && coef && M_local > 0 && C > 0);
+  DG_REQUIRE(M_global <= 0 || M_global >= M_local);  // <= 0: read from sums_global's fourth row (C >= 2)
+  DG_REQUIRE(M_global > 0 || C >= 2);
   hipLaunchKernelGGL(bn_bwd_finalize_sync, dim3(dg_cdiv(C, NT)), dim3(NT), 0, (hipStream_t)stream, sums_local,
                      sums_global, M_local, (double)M_global, C, gamma, save_invstd, dgamma, dbeta, dbias, coef);
   DG_CHECK_LAUNCH();

@@ -75,7 +75,12 @@ class OverlapReducer:
     its own stream, so it runs under the remaining layers' backward kernels).  The optimizer step
     then waits for the buckets, averages them, and all-reduces only the parameters outside the
     FeaturePlan (the heads, the memory) as before.  Buckets are contiguous in the flat buffer
-    and ~`bucket_mb` MB, so the all-reduces are few, large and ring-friendly over xGMI."""
+    and ~`bucket_mb` MB, so the all-reduces are few, large and ring-friendly over xGMI.
+
+    One optimizer step = every taped FeaturePlan forward of the step followed by its backward:
+    gradient accumulation over micro-batches (several backwards per step) is not supported with
+    overlap=True, and a delivery into a bucket whose all-reduce is already in flight raises
+    before anything is written (it would race RCCL on that slice)."""
 
     def __init__(self, bucket_mb: float = 32.0):
         self.bucket_bytes = int(bucket_mb * (1 << 20))
@@ -111,6 +116,7 @@ class OverlapReducer:
         self.nfwd = 0
         self.count = {}
         self.left = [bk[2] for bk in self.buckets]
+        self.launched = [False] * len(self.buckets)
         self.handles = []
 
     @property
@@ -132,6 +138,10 @@ class OverlapReducer:
                 continue
             view = self.flat[sl[0]:sl[1]]
             k = self.count.get(p, 0)
+            b = self.bucket_of[p]
+            if self.launched[b] or k >= self.nfwd:
+                raise RuntimeError("OverlapReducer: more FeaturePlan backwards than taped forwards this step "
+                                   "(gradient accumulation is not supported with overlap=True)")
             if k == 0:
                 view.copy_(g.reshape(-1))
                 if p.grad is None or p.grad.data_ptr() != view.data_ptr():
@@ -140,12 +150,21 @@ class OverlapReducer:
                 view.add_(g.reshape(-1))
             self.count[p] = k + 1
             if k + 1 == self.nfwd:
-                b = self.bucket_of[p]
                 self.left[b] -= 1
                 if self.left[b] == 0:
                     a, e, _ = self.buckets[b]
+                    self.launched[b] = True
                     self.handles.append((a, e, dist.all_reduce(self.flat[a:e], async_op=True)))
         return rest
+
+    def detach(self) -> None:
+        """The optimizer re-created its flat buffer: settle what is in flight on the old one (its
+        slices, which p.grad views, then hold rank averages) and forget it until re-attached."""
+        for a, e, h in self.handles:
+            h.wait()
+            self.flat[a:e].div_(world())
+        self.flat = None
+        self.reset()
 
     def finish(self) -> bool:
         """Wait for the buckets and average them.  False when no FeaturePlan ran this step (its

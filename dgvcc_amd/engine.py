@@ -141,7 +141,7 @@ class ConvLayer:
             z = Act(K.nhwc(x.shape[0], x.shape[2], x.shape[3], self.Cout, dt, x.device))
             part, nblk = K.stem_fwd_f32(x, wk, bias, z)
             if pg is not None:
-                stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk)
+                stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk, M=z.M)
             elif training:
                 bn.num_batches_tracked.add_(1)
                 stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
@@ -173,7 +173,7 @@ class ConvLayer:
             z = Act(K.nhwc(N, H, W, self.Cout, dt, x.device))
             part, nblk = K.stem_fwd(x, wp, bias, z)
             if pg is not None:
-                stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk)
+                stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk, M=z.M)
             elif training:
                 bn.num_batches_tracked.add_(1)
                 stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
@@ -201,7 +201,7 @@ class ConvLayer:
         else:
             K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
         if epi is not None and pg is not None:
-            stats = SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1])
+            stats = SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1], M=z.M)
         elif epi is not None:
             bn.num_batches_tracked.add_(1)
             stats = K.bn_part_finalize(epi[0], epi[1], self.Cout, bn.weight.detach(), bn.bias.detach(),
@@ -402,7 +402,7 @@ class CatConvLayer(ConvLayer):
         if bn is None:  # models2 den_dec: ConvBlock without BatchNorm (bias-free conv + ReLU)
             stats = frozen(self, ("ident", dev), (), lambda: _ident_stats(self.Cout, dev))
         elif pg is not None:
-            stats = SB.fwd_stats(bn, pg, part=part, nblk=rows)
+            stats = SB.fwd_stats(bn, pg, part=part, nblk=rows, M=z.M)
         elif training:
             bn.num_batches_tracked.add_(1)
             stats = K.bn_part_finalize(part, rows, self.Cout, bn.weight.detach(), bn.bias.detach(),
@@ -1085,6 +1085,10 @@ class PairPlan(_Heads):
         # forward (e_mask as uint8 NHWC [N,h,w,C]; the thresholded class maps), so a checker
         # can be run on the same decisions (bench.py's full-frame final-mode parity)
         self.capture = None
+        # the converse: a dict {"emask": uint8 [N,h,w,C], "c_pred": (c1, c2) 0/1 [N,1,h/4,w/4]}
+        # whose decisions the next forward uses instead of its own (a strong-scaled DP rank run on
+        # a single-process run's decisions, tests/dp_syncbn_worker.py); consumed by that forward
+        self.inject = None
 
     def forward(self, ycat1, ycat2, x3_1, x3_2, c_gt, p_drop, err_thrs, tape=None):
         """ycat1/2: (y1, y2, y3) NHWC parts or materialised NHWC y_cat tensors."""
@@ -1117,6 +1121,17 @@ class PairPlan(_Heads):
         K.call("dg_emask_fwd", y1.dt, y1.ptr, y2.ptr, y1.ld, N, HW, C, K.ptr(stats[0]), K.ptr(stats[1]),
                K.ptr(stats[2]), K.ptr(stats[3]), float(err_thrs), K.ptr(d1), K.ptr(d2), m1.ptr, m2.ptr,
                K.ptr(mask), K.stream())
+        inject, self.inject = self.inject, None
+        if self.capture is not None:
+            self.capture["emask"] = mask.view(N, h, w, C).clone()
+        if inject is not None and "emask" in inject:
+            # injected decisions: m_v = y_v * e * drop_v is exactly dg_emask_bwd's product
+            em = inject["emask"]
+            if tuple(em.shape) != (N, h, w, C) or em.dtype != torch.uint8 or y1.ld != C:
+                raise ValueError(f"PairPlan.inject: e_mask must be uint8 {(N, h, w, C)}, got {tuple(em.shape)}")
+            mask.copy_(em.reshape(-1))
+            K.call("dg_emask_bwd", y1.dt, y1.ptr, y2.ptr, N, HW, C, K.ptr(mask), K.ptr(d1), K.ptr(d2), m1.ptr,
+                   m2.ptr, C, K.stream())
         # memory read, both views, + consistency loss
         memT_s, mem_p, scale = self.memr.packs(dt)
         L1 = self.memr.logits(m1, memT_s, dt)
@@ -1155,11 +1170,7 @@ class PairPlan(_Heads):
             p1, p2 = torch.empty_like(yh1), torch.empty_like(yh2)
             K.call("dg_mul_f32", K.ptr(yh1), K.ptr(cres1), yh1.numel(), K.ptr(p1), K.stream())
             K.call("dg_mul_f32", K.ptr(yh2), K.ptr(cres2), yh2.numel(), K.ptr(p2), K.stream())
-            loss_err = torch.empty((), dtype=torch.float32, device=dev)
-            ws = K.query("dg_in_l1_workspace", N, HW, C)
-            work3 = torch.empty(ws // 4 + 1, dtype=torch.float32, device=dev)
-            K.call("dg_in_l1_fwd", y1.dt, y1.ptr, y2.ptr, y1.ld, N, HW, C, K.ptr(stats[0]), K.ptr(stats[1]),
-                   K.ptr(stats[2]), K.ptr(stats[3]), K.ptr(loss_err), K.ptr(work3), K.stream())
+            loss_err = self._in_l1(y1, y2, stats, N, HW, C)
             st.update(cres1=cres1, cres2=cres2, sub=sub, stats=stats, y1=y1, y2=y2)
             outs = (_up4(p1, N, h, w), _up4(p2, N, h, w), c1.view(N, 1, h // 4, w // 4),
                     c2.view(N, 1, h // 4, w // 4), loss_con, loss_err)
@@ -1169,23 +1180,42 @@ class PairPlan(_Heads):
             cres = torch.empty((N, h, w), dtype=torch.float32, device=dev)
             cerr = torch.empty((N, h, w), dtype=torch.float32, device=dev)
             cg = c_gt.float().contiguous() if c_gt is not None else None
-            K.call("dg_cls_combine", K.ptr(c1), K.ptr(c2), K.ptr(cg), N, h // 4, w // 4, 4,
-                   float(self.model.cls_thrs), K.ptr(cres), K.ptr(cerr), K.stream())
+            thr = float(self.model.cls_thrs)
+            cd1, cd2 = c1, c2
+            if inject is not None and "c_pred" in inject:
+                # injected class decisions as 0/1 maps: (1 >= thr) and (0 < thr) for thr in (0, 1]
+                if not 0.0 < thr <= 1.0:
+                    raise ValueError("PairPlan.inject: class decisions need 0 < cls_thrs <= 1")
+                cd1, cd2 = (t.to(device=dev, dtype=torch.float32).reshape(c1.shape).contiguous()
+                            for t in inject["c_pred"])
+            K.call("dg_cls_combine", K.ptr(cd1), K.ptr(cd2), K.ptr(cg), N, h // 4, w // 4, 4,
+                   thr, K.ptr(cres), K.ptr(cerr), K.stream())
             p1, p2 = torch.empty_like(yh1), torch.empty_like(yh2)
             K.call("dg_mul_f32", K.ptr(yh1), K.ptr(cres), yh1.numel(), K.ptr(p1), K.stream())
             K.call("dg_mul_f32", K.ptr(yh2), K.ptr(cres), yh2.numel(), K.ptr(p2), K.stream())
             st.update(cres=cres, sub=sub)
             outs = (_up4(p1, N, h, w), _up4(p2, N, h, w), c1.view(N, 1, h // 4, w // 4),
                     c2.view(N, 1, h // 4, w // 4), _up4(cerr, N, h, w), loss_con)
+            if getattr(self.model, "has_err_loss", False):
+                # loss_err = F.l1_loss(IN(y_den1), IN(y_den2)) (models/models.py:303-311)
+                outs = outs + (self._in_l1(y1, y2, stats, N, HW, C),)
+                st.update(stats=stats, y1=y1, y2=y2)
             if self.capture is not None:
-                thr = float(self.model.cls_thrs)
                 self.capture.update(c_pred=((c1 >= thr).float().view(N, 1, h // 4, w // 4),
                                             (c2 >= thr).float().view(N, 1, h // 4, w // 4)))
-        if self.capture is not None:
-            self.capture["emask"] = mask.view(N, h, w, C)
         if tape is not None:
             tape[self] = st
         return outs
+
+    @staticmethod
+    def _in_l1(y1: Act, y2: Act, stats, N, HW, C):
+        """mean |IN(y1) - IN(y2)| from the instance-norm statistics already formed for e_mask."""
+        dev = y1.buf.device
+        loss_err = torch.empty((), dtype=torch.float32, device=dev)
+        work = torch.empty(K.query("dg_in_l1_workspace", N, HW, C) // 4 + 1, dtype=torch.float32, device=dev)
+        K.call("dg_in_l1_fwd", y1.dt, y1.ptr, y2.ptr, y1.ld, N, HW, C, K.ptr(stats[0]), K.ptr(stats[1]),
+               K.ptr(stats[2]), K.ptr(stats[3]), K.ptr(loss_err), K.ptr(work), K.stream())
+        return loss_err
 
     def backward(self, tape, *gouts):
         st = tape.pop(self)
@@ -1198,8 +1228,9 @@ class PairPlan(_Heads):
             g_c1 = g_c2 = None
         elif self.variant == "M":
             g_d1, g_d2, g_c1, g_c2, g_con, g_err = gouts
-        else:
-            g_d1, g_d2, g_c1, g_c2, _g_cerr, g_con = gouts
+        else:  # (+ loss_err's gradient when the forward ran with has_err_loss)
+            g_d1, g_d2, g_c1, g_c2, _g_cerr, g_con = gouts[:6]
+            g_err = gouts[6] if len(gouts) > 6 else None
         dt = st["m1"].buf.dtype
         dev = st["m1"].buf.device
         C = self.den.Cout

@@ -383,9 +383,12 @@ class DGModel_final(_PairMixin, DGModel_memcls):
             ConvBlock(512 + 256 + 128, self.mem_dim, kernel_size=1, padding=0, bn=True))
 
     def forward_train(self, img1, img2, c_gt=None):
-        if self.has_err_loss:
-            raise NotImplementedError("has_err_loss=True (L1 between instance norms) is not on the HIP path")
+        """(dc1, dc2, c1, c2, c_err, loss_con, loss_err); loss_err = F.l1_loss(IN(y_den1), IN(y_den2))
+        when has_err_loss, else 0 (models/models.py:298-335)."""
         if c_gt is None:
             raise ValueError("DGModel_final.forward_train needs c_gt (the block map)")
-        dc1, dc2, c1, c2, c_err, loss_con = self._pair(img1, img2, c_gt)
+        outs = self._pair(img1, img2, c_gt)
+        if self.has_err_loss:
+            return tuple(outs)
+        dc1, dc2, c1, c2, c_err, loss_con = outs
         return dc1, dc2, c1, c2, c_err, loss_con, 0

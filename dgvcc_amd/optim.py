@@ -135,6 +135,10 @@ class AdamW(torch.optim.Optimizer):
             if all(p.grad is None for p in group["params"]):
                 continue
             self._ensure_flat(group)
+            if self.reducer is not None and self.reducer.flat is not None and self.reducer.flat is not group["_g"]:
+                # the flat buffer was re-created (re-homed parameters): drain the reducer and
+                # re-attach it to the new buffer after this step (its sinks keep pointing at it)
+                self.reducer.detach()
             red = self.reducer if (self.reducer is not None and self.reducer.active
                                    and self.reducer.flat is group["_g"]) else None
             if red is not None and not red.finish():  # the FeaturePlan buckets, reduced under the backward

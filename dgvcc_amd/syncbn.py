@@ -59,7 +59,14 @@ def finalize_rows(bn, row: torch.Tensor, pg) -> torch.Tensor:
                               bn.running_var, _momentum(bn), bn.eps)
 
 
+# the (n, mean, M2) rows carry the pixel count in f32: exact below 2^24 pixels per rank
+# (16 frames at 768 x 1024 is 12.6M)
+_ROW_MAX_M = 1 << 24
+
+
 def row_from_z(z: K.Act) -> torch.Tensor:
+    if z.M >= _ROW_MAX_M:
+        raise ValueError(f"SyncBatchNorm: {z.M} pixels per rank exceed the f32-exact row count 2^24")
     row = torch.empty((3, z.C), dtype=torch.float32, device=z.buf.device)
     work = torch.empty(query("dg_bn_workspace", z.M, z.C) // 4 + 1, dtype=torch.float32, device=z.buf.device)
     call("dg_bn_stats_row", z.dt, z.ptr, z.ld, z.M, z.C, ptr(row), ptr(work), stream())
@@ -73,18 +80,33 @@ def row_from_part(part: torch.Tensor, nblk: int, C: int) -> torch.Tensor:
     return row
 
 
-def fwd_stats(bn, pg, z: K.Act | None = None, part: torch.Tensor | None = None, nblk: int = 0) -> torch.Tensor:
-    """Global batch statistics of a synchronised BN layer from this rank's z or its partial rows."""
+def fwd_stats(bn, pg, z: K.Act | None = None, part: torch.Tensor | None = None, nblk: int = 0,
+              M: int = 0) -> torch.Tensor:
+    """Global batch statistics of a synchronised BN layer from this rank's z or its partial rows
+    (M: the pixels those rows cover)."""
+    if part is not None and M >= _ROW_MAX_M:
+        raise ValueError(f"SyncBatchNorm: {M} pixels per rank exceed the f32-exact row count 2^24")
     row = row_from_part(part, nblk, bn.num_features) if part is not None else row_from_z(z)
     return finalize_rows(bn, row, pg)
 
 
+def _count_row(sums: torch.Tensor, M: int):
+    """Row 3 of the sums: this rank's pixel count as hi + lo parts, each exact in f32, so the
+    all-reduced row carries the global count even when the ranks' batches differ."""
+    lo = M % 4096
+    sums[3].zero_()
+    sums[3, 0] = float(M - lo)
+    sums[3, 1] = float(lo)
+
+
 def bwd_sums(g: K.Act, z: K.Act, stats, act: int, drop=None, g_pool: K.Act | None = None,
              part: torch.Tensor | None = None, nblk: int = 0) -> torch.Tensor:
-    """This rank's BN-backward sums [3][C]: from (g, z), from the pooled gradient g_pool (+ the
-    direct g) with the argmax recomputed from z, or from dgrad-epilogue partial rows."""
+    """This rank's BN-backward sums [4][C]: (sum g', sum g' xhat, sum xhat) from (g, z), from the
+    pooled gradient g_pool (+ the direct g) with the argmax recomputed from z, or from
+    dgrad-epilogue partial rows; row 3 the pixel count (_count_row)."""
     C, dev = z.C, z.buf.device
-    sums = torch.empty((3, C), dtype=torch.float32, device=dev)
+    sums = torch.empty((4, C), dtype=torch.float32, device=dev)
+    _count_row(sums, z.M)
     if part is not None:
         call("dg_bn_part_sums", ptr(part), nblk, C, ptr(sums), stream())
         return sums
@@ -101,14 +123,14 @@ def bwd_sums(g: K.Act, z: K.Act, stats, act: int, drop=None, g_pool: K.Act | Non
 
 
 def bwd_coef(bn, pg, sums: torch.Tensor, M_local: int, stats, dgamma, dbeta, dbias=None) -> torch.Tensor:
-    """All-reduce the sums; the dz coefficients [3][C] from the global ones, dgamma / dbeta / dbias
-    from this rank's.  Every rank holds the same number of pixels (as torch's SyncBatchNorm with
-    equal per-rank batches and the reference's SyncMeanCov assume)."""
+    """All-reduce the sums [4][C]; the dz coefficients [3][C] from the global ones over the
+    global pixel count (the all-reduced row 3: ranks may hold different batch sizes, as torch's
+    SyncBatchNorm allows), dgamma / dbeta / dbias from this rank's."""
     glob = sums.clone()
     dist.all_reduce(glob, group=pg)
-    M_global = M_local * dist.get_world_size(pg)
-    coef = torch.empty_like(sums)
-    call("dg_bn_bwd_finalize_sync", ptr(sums), ptr(glob), M_local, M_global, sums.shape[1],
+    C = sums.shape[1]
+    coef = torch.empty((3, C), dtype=torch.float32, device=sums.device)
+    call("dg_bn_bwd_finalize_sync", ptr(sums), ptr(glob), M_local, -1, C,
          ptr(bn.weight.detach()), ptr(stats[1]), ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), stream())
     return coef
 

@@ -22,6 +22,7 @@ import torch.nn as nn
 
 from . import dist as D
 from . import kernels as K
+from . import syncbn as SB
 from .engine import ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_cached, frozen
 from .kernels import Act
 
@@ -68,12 +69,32 @@ class TConv:
 
 
 def bn_stats(z: Act, bn: nn.BatchNorm2d, training: bool) -> torch.Tensor:
-    """[4, C]: mean, invstd, scale, shift (train: batch stats + running update)."""
+    """[4, C]: mean, invstd, scale, shift (train: batch stats + running update).  An
+    nn.SyncBatchNorm under a multi-rank process group (the ISW trunk's Norm2d when cfg.MODEL.BNFUNC
+    is SyncBatchNorm, models/ISW/mynn.py:8-14) normalises with the whole batch's statistics."""
     if training:
+        pg = SB.group_of(bn)
+        if pg is not None:
+            return SB.fwd_stats(bn, pg, z=z)
         bn.num_batches_tracked.add_(1)
         return K.bn_fwd_train(z, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                               bn.running_var, _bn_momentum(bn), bn.eps)
     return bn_eval_cached(bn, bn)
+
+
+def bn_backward(bn: nn.BatchNorm2d, g: Act, z: Act, st, act: int, dz: Act, grads: dict):
+    """dz of a training-mode BatchNorm (+ ReLU) from g; dgamma / dbeta accumulated into grads
+    (the synchronised backward under a process group, as bn_stats' forward)."""
+    C, dev = z.C, z.buf.device
+    dgam = torch.empty(C, dtype=torch.float32, device=dev)
+    dbet = torch.empty(C, dtype=torch.float32, device=dev)
+    pg = SB.group_of(bn)
+    if pg is not None:
+        SB.backward(bn, pg, g, z, st, act, dz, dgam, dbet)
+    else:
+        K.bn_bwd(g, z, bn.weight.detach(), st, act, dz, dgam, dbet)
+    _acc(grads, bn.weight, dgam)
+    _acc(grads, bn.bias, dbet)
 
 
 def _identity_stats(C, dev):
@@ -129,11 +150,7 @@ class Norm:
         dev = z.buf.device
         C = z.C
         if self.kind == "bn":
-            dgam = torch.empty(C, dtype=torch.float32, device=dev)
-            dbet = torch.empty(C, dtype=torch.float32, device=dev)
-            K.bn_bwd(g, z, self.m.weight.detach(), st, act, dz, dgam, dbet)
-            _acc(grads, self.m.weight, dgam)
-            _acc(grads, self.m.bias, dbet)
+            bn_backward(self.m, g, z, st, act, dz, grads)
         elif self.kind in ("in", "iw"):
             if act:
                 K.relu_bwd(g, y, g)
@@ -242,20 +259,11 @@ class Block:
             else:
                 g_s = Act(torch.empty_like(s.buf))
                 self.post.backward(g_out, s, out, t["sst"], ACT_RELU, g_s, grads)
-        C3 = self.c3.Cout
         g_z3 = Act(torch.empty_like(t["z3"].buf))
-        dgam = torch.empty(C3, dtype=torch.float32, device=dev)
-        dbet = torch.empty(C3, dtype=torch.float32, device=dev)
-        K.bn_bwd(g_s, t["z3"], self.bn3.weight.detach(), t["st3"], ACT_NONE, g_z3, dgam, dbet)
-        _acc(grads, self.bn3.weight, dgam)
-        _acc(grads, self.bn3.bias, dbet)
+        bn_backward(self.bn3, g_s, t["z3"], t["st3"], ACT_NONE, g_z3, grads)
         if self.cd is not None:
             g_zd = Act(torch.empty_like(t["zd"].buf))
-            dgd = torch.empty(C3, dtype=torch.float32, device=dev)
-            dbd = torch.empty(C3, dtype=torch.float32, device=dev)
-            K.bn_bwd(g_s, t["zd"], self.bnd.weight.detach(), t["std"], ACT_NONE, g_zd, dgd, dbd)
-            _acc(grads, self.bnd.weight, dgd)
-            _acc(grads, self.bnd.bias, dbd)
+            bn_backward(self.bnd, g_s, t["zd"], t["std"], ACT_NONE, g_zd, grads)
             gx = Act(K.nhwc(x.N, x.H, x.W, x.C, dt, dev))
             _acc(grads, self.cd.conv.weight, self.cd.bwd(x, g_zd, wpd, gx))
         else:
@@ -267,11 +275,7 @@ class Block:
         g_a1 = Act(torch.empty_like(t["a1"].buf))
         _acc(grads, self.c2.conv.weight, self.c2.bwd(t["a1"], g_z2, wp2, g_a1))
         g_z1 = Act(torch.empty_like(t["z1"].buf))
-        dg1 = torch.empty(self.c1.Cout, dtype=torch.float32, device=dev)
-        db1 = torch.empty(self.c1.Cout, dtype=torch.float32, device=dev)
-        K.bn_bwd(g_a1, t["z1"], self.bn1.weight.detach(), t["st1"], ACT_RELU, g_z1, dg1, db1)
-        _acc(grads, self.bn1.weight, dg1)
-        _acc(grads, self.bn1.bias, db1)
+        bn_backward(self.bn1, g_a1, t["z1"], t["st1"], ACT_RELU, g_z1, grads)
         _acc(grads, self.c1.conv.weight, self.c1.bwd(x, g_z1, wp1, gx, accumulate=True))
         return gx
 

@@ -240,7 +240,9 @@ int dg_bn_part_finalize(const float* part, int nblk, int C, const float* gamma, 
  *             the global batch statistics and running-stat update, as one BN over the global batch;
  *   backward: a rank's sums [3][C] = (sum g', sum g' xhat, sum xhat) (dg_bn_bwd_sums,
  *             dg_bn_bwd_pool_sums, or dg_bn_part_sums of dgrad-epilogue partials) -> all-reduce ->
- *             dg_bn_bwd_finalize_sync (dz coefficients from the global sums over M_global pixels;
+ *             dg_bn_bwd_finalize_sync (dz coefficients from the global sums over M_global pixels, or,
+ *             with M_global <= 0, over the count all-reduced as a fourth row of the sums [4][C]:
+ *             sums[3][0] + sums[3][1], hi and lo parts of this rank's pixel count;
  *             dgamma / dbeta and the conv-bias gradient from this rank's, as torch SyncBatchNorm)
  *             -> dg_bn_bwd_apply_coef / dg_bn_bwd_pool_apply_coef.
  * Workspaces: dg_bn_workspace(M, C) (stats_row, bwd_sums), dg_bn_workspace(N*H*W, C)

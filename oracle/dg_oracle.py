@@ -132,6 +132,8 @@ def final_forward(sd, img1, img2, c_gt, training=True, err_thrs=0.5, cls_thrs=0.
     y_in2 = F.instance_norm(y_den2, eps=1e-5)
     e_y = torch.abs(y_in1 - y_in2)
     e_mask = (e_y < err_thrs).clone().detach()
+    if info is not None:  # has_err_loss=True: loss_err = F.l1_loss(y_in1, y_in2) (models/models.py:311)
+        info["loss_err"] = F.l1_loss(y_in1, y_in2)
     if e_mask_in is not None:
         flip = e_mask_in.bool() != e_mask
         if info is not None:
@@ -200,6 +202,21 @@ def memadd_forward_train(sd, img1, img2, training=True, err_thrs=0.5, e_mask_in=
     d1 = _up(F.relu(F.conv2d(y_new1, sd["den_head.0.conv.weight"])), 4)
     d2 = _up(F.relu(F.conv2d(y_new2, sd["den_head.0.conv.weight"])), 4)
     return d1, d2, loss_con
+
+
+def err_loss_grads(sd, batch):
+    """DGModel_final(has_err_loss=True).forward_train's loss_err (models/models.py:303-311) and
+    the gradients of loss_err alone with respect to every trainable entry (dropouts off)."""
+    sd = {k: v.clone() for k, v in sd.items()}
+    keys = trainable_keys(sd)
+    for k in keys:
+        sd[k].requires_grad_(True)
+    imgs1, imgs2, (_points, _dmaps, bmaps) = batch
+    info = {}
+    final_forward(sd, imgs1, imgs2, bmaps, info=info)
+    loss_err = info["loss_err"]
+    grads = torch.autograd.grad(loss_err, [sd[k] for k in keys], allow_unused=True)
+    return loss_err.detach(), {k: (g if g is not None else torch.zeros_like(sd[k])) for k, g in zip(keys, grads)}
 
 
 def trainable_keys(sd):

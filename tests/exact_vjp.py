@@ -208,17 +208,23 @@ def pair_ref(pair: E.PairPlan, tp: dict, parts1, parts2, x31, x32, P: Params64):
     c1 = _cls_head(pair, s["sub"], "c1", x31, P)
     c2 = _cls_head(pair, s["sub"], "c2", x32, P)
     cres = s["cres"].double().cpu().view(N, 1, h, w)
-    return up(d1 * cres, 4), up(d2 * cres, 4), c1, c2, loss_con
+    outs = (up(d1 * cres, 4), up(d2 * cres, 4), c1, c2, loss_con)
+    if "y1" in s:  # has_err_loss: loss_err = F.l1_loss(IN(y_den1), IN(y_den2)) (models/models.py:303-311)
+        outs = outs + (F.l1_loss(F.instance_norm(yd1, eps=1e-5), F.instance_norm(yd2, eps=1e-5)),)
+    return outs
 
 
 def final_loss_grads(outs, gt, bmaps, log_para=1000.0):
     """Upstream gradients of DGTrainer's final-mode loss (trainers/dgtrainer.py:184-192:
     MSE(dc, gt*log_para) x2 + 10 BCE(c, bmap) x2 + 10 loss_con) at the given outputs,
-    float64, as torch's MSELoss / binary_cross_entropy define them."""
+    float64, as torch's MSELoss / binary_cross_entropy define them (+ loss_err, weight 1, when
+    the outputs carry it: the has_err_loss objective)."""
     leaves = [o.detach().double().cpu().requires_grad_(True) for o in outs]
-    dc1, dc2, c1, c2, lc = leaves
+    dc1, dc2, c1, c2, lc = leaves[:5]
     g = gt.double().cpu() * log_para
     b = bmaps.double().cpu()
     loss = (F.mse_loss(dc1, g) + F.mse_loss(dc2, g)
             + 10 * (F.binary_cross_entropy(c1, b) + F.binary_cross_entropy(c2, b)) + 10 * lc)
+    if len(leaves) > 5:
+        loss = loss + leaves[5]
     return torch.autograd.grad(loss, leaves)

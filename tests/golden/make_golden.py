@@ -114,6 +114,25 @@ def gen_train(name, model_cls, kwargs, mode, B=2, H=64, W=64):
     np.savez_compressed(os.path.join(HERE, f"train_{name}.npz"), **out)
 
 
+def gen_final_err(B=2, H=64, W=64):
+    """DGModel_final(has_err_loss=True).forward_train (models/models.py:298-335): its loss_err =
+    F.l1_loss(IN(y_den1), IN(y_den2)) and the parameter gradients of loss_err alone, every
+    dropout off, seeded weights and batch -> train_final_err.npz."""
+    rm = import_ref("models.models")
+    model = rm.DGModel_final(pretrained=False, den_dropout=0.0, cls_dropout=0.0, has_err_loss=True)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    model.train()
+    imgs1, imgs2, (_pts, _dmaps, bmaps) = O.synthetic_batch(B, H, W, seed=2112)
+    dc1, dc2, c1, c2, c_err, loss_con, loss_err = model.forward_train(imgs1, imgs2, bmaps)
+    loss_err.backward()
+    grads = {k: p.grad if p.grad is not None else torch.zeros_like(p) for k, p in model.named_parameters()}
+    out = {"shape": np.array([B, H, W]), "out_loss_err": np.array([loss_err.item()], np.float64),
+           "out_loss_con": np.array([loss_con.item()], np.float64), "out_dc1": dc1.detach().numpy()}
+    summarize("grad__", grads, out)
+    np.savez_compressed(os.path.join(HERE, "train_final_err.npz"), **out)
+
+
 
 
 # ---------------------------------------------------------------------------
@@ -405,6 +424,8 @@ if __name__ == "__main__":
         gen_train("simple_base", "DGModel_base", {"den_dropout": 0.0}, "simple")
     if "final" in which:
         gen_train("final", "DGModel_final", {"den_dropout": 0.0, "cls_dropout": 0.0}, "final")
+    if "final_err" in which:
+        gen_final_err()
     # DGTrainer modes of the ablation configs (configs/ablation/*: base/mem -> 'base',
     # memadd -> 'add', cls/memcls -> 'cls'); every dropout off
     for key, cls_name, kw, mode in [("base_base", "DGModel_base", {"den_dropout": 0.0}, "base"),

@@ -259,16 +259,18 @@ def _skip_bias(k):
     return k.endswith(".bias") and (k.startswith("enc") or ".conv." in k) and "cls_head.2" not in k
 
 
-@pytest.mark.parametrize("B,H,W", [(2, 64, 64), (2, 128, 160)])
-def test_final_step_backward_exact_given_forward(dev, B, H, W):
+@pytest.mark.parametrize("B,H,W,err", [(2, 64, 64, False), (2, 128, 160, False), (4, 128, 128, False),
+                                       (2, 64, 64, True)])
+def test_final_step_backward_exact_given_forward(dev, B, H, W, err):
     """The whole DGModel_final train-step backward (encoder, decoder, den_dec, memory read,
     JSD-MSE, density and class heads, both views; trainers/dgtrainer.py:184-192 on
     models/models.py:298-335) against float64 VJPs evaluated at the HIP plans' own saved fp32
     activations, with every ReLU, max-pool argmax, e_mask and class decision the HIP forward's
     (tests/exact_vjp.py).  No forward rounding can move this comparison: every parameter
-    gradient within 1e-4 normwise, and the plans' input gradients too."""
+    gradient within 1e-4 normwise, and the plans' input gradients too.  err: has_err_loss=True,
+    the objective + loss_err = L1(IN(y_den1), IN(y_den2)) (models/models.py:303-311)."""
     import exact_vjp as X
-    model = _model("DGModel_final", den_dropout=0.0, cls_dropout=0.0)
+    model = _model("DGModel_final", den_dropout=0.0, cls_dropout=0.0, has_err_loss=err)
     sd0 = O.seeded_state_dict(model.state_dict())
     model.load_state_dict(sd0)
     model = model.to(dev).set_precision("fp32").train()
@@ -281,7 +283,8 @@ def test_final_step_backward_exact_given_forward(dev, B, H, W):
         outB = fe.forward(i2.to(dev), torch.float32, True, tB)
         outs = pair.forward(outA[:3], outB[:3], outA[3], outB[3], bm.to(dev), 0.0, float(model.err_thrs), tP)
     torch.cuda.synchronize()
-    hip_outs = (outs[0], outs[1], outs[2], outs[3], outs[5])
+    hip_outs = (outs[0], outs[1], outs[2], outs[3], outs[5]) + ((outs[6],) if err else ())
+    assert len(outs) == (7 if err else 6)
     g64 = X.final_loss_grads(hip_outs, dm, bm)
     # the float64 graph at the taped point (built before the HIP backward consumes the tapes)
     P = X.Params64(model)
@@ -294,7 +297,7 @@ def test_final_step_backward_exact_given_forward(dev, B, H, W):
         torch.autograd.backward(ref, g64)
     g32 = [g.float().to(dev) for g in g64]
     with torch.no_grad():
-        gin, gp = pair.backward(tP, g32[0], g32[1], g32[2], g32[3], None, g32[4])
+        gin, gp = pair.backward(tP, g32[0], g32[1], g32[2], g32[3], None, g32[4], *g32[5:])
         _, ga = fe.backward(tA, *gin[0:3], gin[6])
         _, gb = fe.backward(tB, *gin[3:6], gin[7])
     torch.cuda.synchronize()

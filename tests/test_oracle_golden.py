@@ -86,3 +86,18 @@ def test_train_step_oracle(name, mode, cls_name):
     # (and AdamW's first step moves them by lr x the sign of that noise)
     check_summary("post__", {k: v for k, v in sd1.items() if not k.endswith("num_batches_tracked") and k not in pre_bn},
                   g, rtol=1e-5, atol=1e-7)
+
+
+def test_final_err_loss_oracle():
+    """DGModel_final(has_err_loss=True): loss_err = F.l1_loss(IN(y_den1), IN(y_den2)) and the
+    gradients of loss_err alone (models/models.py:303-311) against train_final_err.npz, which
+    tests/golden/make_golden.py (gen_final_err) produced by running the reference."""
+    g = load("train_final_err.npz")
+    B, H, W = (int(v) for v in g["shape"])
+    sd0 = O.seeded_state_dict(state_template("DGModel_final"))
+    batch = O.synthetic_batch(B, H, W, seed=2112)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    loss_err, grads = O.err_loss_grads(sd0, batch)
+    assert abs(loss_err.item() - g["out_loss_err"][0]) <= 1e-6 * abs(g["out_loss_err"][0])
+    pre_bn = {f"{s}.{i}.bias" for s, idx in O.ENC_CONVS.items() for i in idx}
+    check_summary("grad__", {k: v for k, v in grads.items() if k not in pre_bn}, g, rtol=1e-4, atol=1e-7)
