@@ -50,6 +50,10 @@ struct FwdArgs {
   // CB blocks of the tap, when 32 tiles per XCD of windows no longer fit the 4-MB L2: on the
   // 512 -> 512 f32 layer HBM fetch 9.1 -> 2.7 GB per launch, L2 hit rate 85 -> 95%)
   int korder = 0;
+  // f32 split math: caller-owned room for the pre-split filter planes (3 bf16 planes of the
+  // Cout*R*S*C filter, dg_conv_fwd_workspace); null / too small: kernels that split per wave
+  char* wsplit = nullptr;
+  long long wsplit_bytes = 0;
 };
 
 __device__ __forceinline__ void epi_affine(float v[4], const FwdArgs& a, int co) {
@@ -2690,35 +2694,19 @@ static bool rsplit3_ok(const FwdArgs& a) {
 }
 static bool rsplit3w_ok(const FwdArgs& a) { return rsplit3_ok(a) && rsplit3_mode() == 2 && a.W % 512 == 0; }
 
-// Per-stream device scratch for the pre-split filter panels (grown on demand; a launch on
-// a stream only ever overlaps its own stream's earlier work, which hipFree waits for).
-// Per-(device, stream) scratch for the pre-split filter planes.  Launches on one stream are
-// ordered, so a layer's split + conv may reuse the previous layer's buffer; torch's default
-// stream reports the same handle (0) on every device, hence the device in the key.  The table
-// is shared by every thread of the process, so it is guarded by a mutex.
-static void* split_scratch(hipStream_t st, size_t bytes) {
-  struct Ent { int dev; hipStream_t st; void* p; size_t cap; };
-  static Ent ents[32];
-  static int n = 0;
-  static std::mutex mu;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  int k = 0;
-  while (k < n && !(ents[k].st == st && ents[k].dev == dev)) ++k;
-  if (k == n) {
-    if (n == 32) return nullptr;
-    ents[n++] = Ent{dev, st, nullptr, 0};
-  }
-  if (ents[k].cap < bytes) {
-    if (ents[k].p && hipFree(ents[k].p) != hipSuccess) return nullptr;
-    ents[k].p = nullptr;
-    ents[k].cap = 0;
-    const size_t cap = std::max(bytes, (size_t)16 << 20);
-    if (hipMalloc(&ents[k].p, cap) != hipSuccess) return nullptr;
-    ents[k].cap = cap;
-  }
-  return ents[k].p;
+// The pre-split filter planes of a split-math f32 launch: split_weight_kernel writes them into
+// the caller's workspace (dg_conv_fwd_workspace) ahead of the conv on the same stream; null
+// when the caller passed no room for them (the launch then takes a kernel that splits per wave).
+static const unsigned short* presplit(const FwdArgs& a, hipStream_t st) {
+  const long long nw = (long long)a.Cout * a.R * a.S * a.C;
+  if (!a.wsplit || a.wsplit_bytes < nw * 6) return nullptr;
+  unsigned short* wsp = (unsigned short*)a.wsplit;
+  hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256), 0,
+                     st, (const float*)a.w, nw, wsp);
+  return wsp;
+}
+static bool has_split_room(const FwdArgs& a) {
+  return a.wsplit && a.wsplit_bytes >= (long long)a.Cout * a.R * a.S * a.C * 6;
 }
 
 // the shapes the f32 persistent forward serves (and so the f32 shapes with epilogue statistics):
@@ -2837,12 +2825,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
     if (a.bpart) {  // dgrad with the BN-backward partials in the epilogue: the pre-split kernel only
       FwdArgs q = a;
       q.bpart = nullptr;
-      if (!(psplit_ok(q) && psplit_wide())) return DG_ERR_UNSUPPORTED;
-      const long long nw = (long long)a.Cout * a.R * a.S * a.C;
-      unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
-      if (!wsp) return DG_ERR_HIP;
-      hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
-                         0, st, (const float*)a.w, nw, wsp);
+      if (!(psplit_ok(q) && psplit_wide() && has_split_room(a))) return DG_ERR_UNSUPPORTED;
+      const unsigned short* wsp = presplit(a, st);
       const int bn2 = f32_pers_bn(a.Cout);
       const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_psb(bn2)) * (a.Cout / bn2),
                                                         persist_grid());
@@ -2851,12 +2835,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
       DG_CHECK_LAUNCH();
       return DG_OK;
     }
-    if (rsplit_ok(a)) {  // split math, Cout = 64: both operands split once per block
-      const long long nw = (long long)a.Cout * a.R * a.S * a.C;
-      unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
-      if (!wsp) return DG_ERR_HIP;
-      hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
-                         0, st, (const float*)a.w, nw, wsp);
+    if (rsplit_ok(a) && has_split_room(a)) {  // split math, Cout = 64: both operands split once per block
+      const unsigned short* wsp = presplit(a, st);
       const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));
       if (rsplit3w_ok(a)) {
         const dim3 gw((unsigned)((long long)(M / 512) * (a.Cout / 64)));
@@ -2890,12 +2870,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, SPL_>), dim3(g), dim3(512), 0, st, a); \
         } \
       } while (0)
-      if (f32_split() && psplit_ok(a)) {
-        const long long nw = (long long)a.Cout * a.R * a.S * a.C;
-        unsigned short* wsp = (unsigned short*)split_scratch(st, (size_t)nw * 6);
-        if (!wsp) return DG_ERR_HIP;
-        hipLaunchKernelGGL(split_weight_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(nw, 256), 4096)), dim3(256),
-                           0, st, (const float*)a.w, nw, wsp);
+      if (f32_split() && psplit_ok(a) && has_split_room(a)) {
+        const unsigned short* wsp = presplit(a, st);
         const int bn2 = f32_pers_bn(a.Cout);
         const bool wide = psplit_wide();
         const bool tall = psplit_tall(a);
@@ -4578,6 +4554,7 @@ extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, i
 extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
   const long long M = (long long)N * H * W;
+  if (dtype == DG_F32) return ((long long)Cout * R * S * C * 6 + 255) / 256 * 256;  // pre-split filter planes
   if (!DG_IS16(dtype) || !fwd_has_epi_stats(C, Cout, C, R, S)) return 0;
   const int ks = fwd_ksplit(M, Cout, C, R, S);
   return ks > 1 ? (int64_t)ks * M * Cout * 4 : 0;
@@ -4595,7 +4572,13 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   DG_REQUIRE(ldx >= C && ldy >= Cout && ldx % 8 == 0 && ldy % 4 == 0);
   DG_SUPPORTED((long long)(128 + 2 * pad * (W + 1)) * ldx * 4 < (1ll << 31));
   FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, R, S, pad, bias, (char*)y, ldy, accumulate, part};
-  if (part) DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S) : (f32_pers_ok(a) || rsplit_ok(a)));
+  if (dtype == DG_F32) {
+    a.wsplit = (char*)workspace;
+    a.wsplit_bytes = workspace ? ws_bytes : 0;
+  }
+  if (part)
+    DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S)
+                                : (f32_pers_ok(a) || (rsplit_ok(a) && has_split_room(a))));
   {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
      // runs dg_conv_fwd + the statistics pass instead
     FwdArgs q = a;
@@ -4640,6 +4623,10 @@ extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N,
   a.escale = scale;
   a.eshift = shift;
   a.eact = act;
+  if (dtype == DG_F32) {
+    a.wsplit = (char*)workspace;
+    a.wsplit_bytes = workspace ? ws_bytes : 0;
+  }
   if (DG_IS16(dtype) && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
     const long long M = (long long)N * H * W;
     const int ks = fwd_ksplit(M, Cout, C, R, S);
@@ -4655,7 +4642,8 @@ extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N,
 extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                                  int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
                                  const float* scale, const float* shift, const float* mean, const float* invstd,
-                                 int act, const float* drop, int HW, float* bpart, void* stream) {
+                                 int act, const float* drop, int HW, float* bpart, void* workspace, int64_t ws_bytes,
+                                 void* stream) {
   DG_REQUIRE(x && w && y && z && bpart && scale && shift && mean && invstd && N > 0 && H > 0 && W > 0 && C > 0 &&
              Cout > 0 && R > 0 && S > 0 && (act == 0 || act == 1) && (!drop || HW > 0));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
@@ -4671,7 +4659,11 @@ extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, i
   a.bsc = scale; a.bsf = shift; a.bmu = mean; a.bis = invstd; a.bdrop = drop;
   a.bact = act; a.bHW = drop ? HW : 1;
   a.bpart = bpart;
-  if (dtype == DG_F32) return launch_fwd<float>(a, (hipStream_t)stream);  // conv_fwd_psplit_kernel<.., EPI 2>
+  if (dtype == DG_F32) {  // conv_fwd_psplit_kernel<.., EPI 2> on the caller's pre-split planes
+    a.wsplit = (char*)workspace;
+    a.wsplit_bytes = workspace ? ws_bytes : 0;
+    return launch_fwd<float>(a, (hipStream_t)stream);
+  }
   return dtype == DG_F16 ? launch_fwd<f16>(a, (hipStream_t)stream) : launch_fwd<bf16>(a, (hipStream_t)stream);
 }
 

@@ -125,7 +125,9 @@ _FWD_WS: dict = {}
 
 
 def _fwd_workspace(x: Act, Cout: int, R: int):
-    """Split-K partials for small-grid forward/dgrad shapes (deep layers at small batch)."""
+    """Split-K partials for small-grid 16-bit forward/dgrad shapes (deep layers at small batch);
+    f32: the pre-split filter planes of the split-math kernels (caller-owned, from torch's
+    caching allocator, stream-ordered like every other buffer)."""
     key = (x.dt, x.N, x.H, x.W, x.C, Cout, R)
     ws = _FWD_WS.get(key)
     if ws is None:
@@ -169,6 +171,7 @@ def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: A
     rows = (query("dg_conv_bnpart_rows_ex", 0, dy.N, dy.H, dy.W, dy.C, dy.ld, C, R, R) if dy.dt == 0
             else query("dg_conv_stats_rows", dy.N, dy.H, dy.W))
     part = torch.empty((rows, 3, C), dtype=torch.float32, device=dy.buf.device)
+    ws, work = _fwd_workspace(dy, C, R)
     flops = 2.0 * dy.M * dy.C * R * R * C
     nbytes = dy.buf.element_size() * (dy.M * dy.C + wflip.numel() + 2 * dy.M * C)
     res = []
@@ -176,7 +179,8 @@ def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: A
     def launch():
         res.append(lib_call_status("dg_conv_fwd_bnbwd", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W, dy.C, ptr(wflip), C,
                                    R, R, R - 1 - pad, dx.ptr, dx.ld, z.ptr, z.ld, ptr(stats[2]), ptr(stats[3]),
-                                   ptr(stats[0]), ptr(stats[1]), act, ptr(drop), z.H * z.W, ptr(part), stream()))
+                                   ptr(stats[0]), ptr(stats[1]), act, ptr(drop), z.H * z.W, ptr(part), ptr(work),
+                                   ws, stream()))
 
     _timed("dgrad", flops, launch, nbytes)
     if res[0] == -2:

@@ -14,9 +14,9 @@
  *   - dtype: DG_F32 (parity mode, exact-f32 MFMA), DG_BF16 (perf mode, bf16
  *     storage + bf16 MFMA, f32 accumulation/statistics) or DG_F16 (fp16 storage +
  *     f16 MFMA, f32 accumulation/statistics; configs/qnrf_final.yml's precision).
- *   - the library holds no tensors and is safe to call from any thread; its only
- *     state is a mutex-guarded per-(device, stream) scratch for the pre-split f32
- *     filter planes of the split-math convolutions.
+ *   - the library holds no tensors and no device memory and is safe to call from any
+ *     thread; the pre-split f32 filter planes of the split-math convolutions live in
+ *     the caller's workspace (dg_conv_fwd_workspace).
  */
 #ifndef DGVCC_H
 #define DGVCC_H
@@ -85,8 +85,12 @@ int64_t dg_conv_bnpart_rows_ex(int dtype, int N, int H, int W, int C, int64_t ld
 int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                       const void* w, int Cout, int R, int S, int pad, const float* bias,
                       void* y, int64_t ldy, float* part, void* stream);
-/* Split-K workspace (bytes, 0 = none needed) for the bf16 forward of a shape whose tile
- * grid cannot fill the GPU (deep layers at small batch). */
+/* Workspace (bytes, 0 = none needed) of dg_conv_fwd_ex / dg_conv_fwd_bn_eval /
+ * dg_conv_fwd_bnbwd: 16-bit, the split-K partials of a shape whose tile grid cannot fill the
+ * GPU (deep layers at small batch); DG_F32, the pre-split filter planes of the split-math
+ * kernels (Cout*R*S*C*6 bytes).  With less (or none, as dg_conv_fwd passes) an f32 launch
+ * takes a kernel that splits the filter per wave, and the statistics row counts of
+ * dg_conv_stats_rows_ex assume the full workspace. */
 int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S);
 /* dg_conv_fwd + dg_conv_fwd_stats in one entry: part may be NULL; with a workspace of
  * dg_conv_fwd_workspace bytes the K loop is split over blocks and reduced deterministically
@@ -111,7 +115,8 @@ int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N, int H, int
 int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                       int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
                       const float* scale, const float* shift, const float* mean, const float* invstd,
-                      int act, const float* drop, int HW, float* bpart, void* stream);
+                      int act, const float* drop, int HW, float* bpart, void* workspace, int64_t ws_bytes,
+                      void* stream);
 
 /* wflip[C][R][S][Cout] = w[Cout][R-1-r][S-1-s][C] (packed filters of dtype). */
 int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream);

@@ -69,6 +69,23 @@ def test_wgrad_workspace_plan():
     assert L.dg_conv_wgrad_workspace(1, 0, 48, 64, 512, 512, 3, 3) == -1
 
 
+def test_f32_presplit_workspace_is_caller_owned():
+    """The split-math f32 convolutions' pre-split filter planes (3 bf16 planes of the filter) are
+    part of the caller's dg_conv_fwd_workspace: the library allocates no device memory."""
+    import os
+    from dgvcc_amd import _capi
+    L = _capi.lib()
+    for C, Co, R in ((512, 512, 3), (64, 64, 3), (896, 256, 1)):
+        ws = L.dg_conv_fwd_workspace(0, 16, 48, 64, C, Co, R, R)
+        assert ws >= Co * R * R * C * 6 and ws % 256 == 0, (C, Co, R, ws)
+    assert L.dg_conv_fwd_workspace(0, 0, 48, 64, 64, 64, 3, 3) == -1
+    csrc = os.path.join(os.path.dirname(_capi.HEADER), "..", "dgvcc_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".h")):
+            src = open(os.path.join(csrc, f)).read()
+            assert "hipMalloc" not in src and "hipFree" not in src, f
+
+
 def test_conv_tile_layout_queries(monkeypatch):
     """Rows of epilogue BN partials per conv launch follow the tile layout the launch will use
     (host logic, no GPU): the 256-channel f32 pre-split forward on 256-pixel tiles where they
