@@ -545,7 +545,7 @@ def density_parity(sd, batch, loss_ref, outs_ref, mode):
     the number of decisions that differ is reported; the loss is compared as is."""
     from dgvcc_amd import kernels as K
     try:
-        res = _density_parity_once(sd, batch, loss_ref, outs_ref, mode)
+        res = _density_parity_once(sd, batch, loss_ref, outs_ref, mode, grads=True)
         K.call("dg_set_f32_math", 0)
         ex = _density_parity_once(sd, batch, loss_ref, outs_ref, mode)
     finally:
@@ -555,7 +555,10 @@ def density_parity(sd, batch, loss_ref, outs_ref, mode):
     return res
 
 
-def _density_parity_once(sd, batch, loss_ref, outs_ref, mode):
+def _density_parity_once(sd, batch, loss_ref, outs_ref, mode, grads=False):
+    """grads (final mode): also the train step's backward, HIP against the oracle's step on the
+    HIP decisions: per-parameter normwise gradient errors and each loss term's relative error
+    (the whole loss is dominated by the MSE x 1000 term at random init, so it alone is no check)."""
     from oracle import dg_oracle as O
     from dgvcc_amd.models.models import DGModel_base, DGModel_final
     from dgvcc_amd.losses import mse_loss
@@ -569,27 +572,53 @@ def _density_parity_once(sd, batch, loss_ref, outs_ref, mode):
     model.load_state_dict(sd)
     model = model.to(dev).set_precision("fp32").train()
     res = {"precision": "fp32", "frame": "1x3x%dx%d" % tuple(img1.shape[-2:]), "tolerance_rel": 1e-4}
-    with torch.no_grad():
+    with torch.set_grad_enabled(grads and mode == "final"):
         if mode == "final":
             plan = model._get_plans()["pair"]
             plan.capture = {}
             gb = bmaps.to(dev)
             dc1, dc2, c1, c2, _, loss_con, _ = model.forward_train(img1.to(dev), img2.to(dev), gb)
             gt = dmaps.to(dev)
-            loss = (mse_loss(dc1, gt, 1000.0) + mse_loss(dc2, gt, 1000.0)
-                    + 10 * (binary_cross_entropy(c1, gb) + binary_cross_entropy(c2, gb)) + 10 * loss_con)
+            terms = (mse_loss(dc1, gt, 1000.0) + mse_loss(dc2, gt, 1000.0),
+                     binary_cross_entropy(c1, gb) + binary_cross_entropy(c2, gb), loss_con)
+            loss = terms[0] + 10 * terms[1] + 10 * terms[2]
+            if grads:
+                loss.backward()
             cap = plan.capture
             plan.capture = None
             em = cap["emask"].permute(0, 3, 1, 2).bool().cpu()
             cp = tuple(c.cpu() for c in cap["c_pred"])
             info = {}
             sd2 = {k: v.clone() for k, v in sd.items()}
-            r1, r2, *_ = O.final_forward(sd2, img1, img2, bmaps, e_mask_in=em, c_pred_in=cp, info=info)
+            with torch.no_grad():
+                r1, r2, rc1, rc2, _, rcon, _ = O.final_forward(sd2, img1, img2, bmaps, e_mask_in=em, c_pred_in=cp,
+                                                               info=info)
+            rt = (torch.nn.functional.mse_loss(r1, dmaps * 1000.0) + torch.nn.functional.mse_loss(r2, dmaps * 1000.0),
+                  torch.nn.functional.binary_cross_entropy(rc1, bmaps)
+                  + torch.nn.functional.binary_cross_entropy(rc2, bmaps), rcon)
+            res["loss_terms_rel"] = {k: float(abs(a.item() - b.item()) / abs(b.item()))
+                                     for k, a, b in zip(("mse", "bce", "jsd_mse"), terms, rt)}
             pairs = [(dc1, r1), (dc2, r2)]
             res.update({k: v for k, v in info.items()})
             res["note"] = ("oracle re-run on the HIP path's e_mask / class-map decisions; flips = decisions "
                            "within fp32 rounding of the threshold")
             res["loss_rel_uninjected"] = float(abs(loss.item() - loss_ref.item()) / abs(loss_ref.item()))
+            if grads:
+                _, _, g_ref, _ = O.train_step(sd, batch, "final", e_mask_in=em, c_pred_in=cp)
+                err, num, den = {}, 0.0, 0.0
+                for k, p in model.named_parameters():
+                    if (k.endswith(".bias") and (k.startswith("enc") or ".conv." in k)) or g_ref[k].norm() == 0:
+                        continue  # pre-BN conv biases: mathematically zero gradient
+                    d = p.grad.detach().double().cpu() - g_ref[k].double()
+                    err[k] = float(d.norm() / g_ref[k].double().norm())
+                    num += float(d.norm() ** 2)
+                    den += float(g_ref[k].double().norm() ** 2)
+                worst = max(err.items(), key=lambda kv: kv[1])
+                res["grad_parity"] = {"worst_param": worst[0], "worst_normwise_rel": worst[1],
+                                      "global_normwise_rel": (num / den) ** 0.5, "params": len(err),
+                                      "note": "HIP fp32 step backward against the fp32 oracle's step on the HIP "
+                                              "decisions; ReLU / max-pool branches are each side's own, so the "
+                                              "residual is their fp32 spread (tests/test_model_gpu.py E2E_GRAD_TOL)"}
         else:
             d = model(img1.to(dev))
             loss = mse_loss(d, dmaps.to(dev), 1000.0)

@@ -116,14 +116,15 @@ def cls_pred_map(c, thrs=0.5):
 
 
 def final_forward(sd, img1, img2, c_gt, training=True, err_thrs=0.5, cls_thrs=0.5,
-                  drop1=None, drop2=None, e_mask_in=None, c_pred_in=None, info=None):
+                  drop1=None, drop2=None, e_mask_in=None, c_pred_in=None, info=None, err=None):
     """DGModel_final.forward_train (models/models.py:298-335); drop* = dropout2d masks.
 
     Threshold injection for full-frame parity (SURVEY.md §7 "threshold discontinuities"):
     e_mask_in (bool [B,C,h,w]) replaces the |IN1-IN2| < err_thrs mask and c_pred_in
     ((c_r1, c_r2) 0/1 maps [B,1,h/4,w/4]) the thresholded class maps, so that a checked
     path whose fp32 rounding flips a few near-threshold decisions is compared on the same
-    decisions; `info` (a dict) receives how many decisions the injection changed."""
+    decisions; `info` (a dict) receives how many decisions the injection changed, `err` (a dict)
+    the has_err_loss term loss_err (with its autograd graph)."""
     y_cat1, x3_1 = forward_fe(sd, img1, training)
     y_cat2, x3_2 = forward_fe(sd, img2, training)
     y_den1 = _conv_bn_relu(y_cat1, sd, "den_dec.0.conv", "den_dec.0.bn", training, pad=0)
@@ -132,8 +133,8 @@ def final_forward(sd, img1, img2, c_gt, training=True, err_thrs=0.5, cls_thrs=0.
     y_in2 = F.instance_norm(y_den2, eps=1e-5)
     e_y = torch.abs(y_in1 - y_in2)
     e_mask = (e_y < err_thrs).clone().detach()
-    if info is not None:  # has_err_loss=True: loss_err = F.l1_loss(y_in1, y_in2) (models/models.py:311)
-        info["loss_err"] = F.l1_loss(y_in1, y_in2)
+    if err is not None:  # has_err_loss=True: loss_err = F.l1_loss(y_in1, y_in2) (models/models.py:311)
+        err["loss_err"] = F.l1_loss(y_in1, y_in2)
     if e_mask_in is not None:
         flip = e_mask_in.bool() != e_mask
         if info is not None:
@@ -212,9 +213,9 @@ def err_loss_grads(sd, batch):
     for k in keys:
         sd[k].requires_grad_(True)
     imgs1, imgs2, (_points, _dmaps, bmaps) = batch
-    info = {}
-    final_forward(sd, imgs1, imgs2, bmaps, info=info)
-    loss_err = info["loss_err"]
+    err = {}
+    final_forward(sd, imgs1, imgs2, bmaps, err=err)
+    loss_err = err["loss_err"]
     grads = torch.autograd.grad(loss_err, [sd[k] for k in keys], allow_unused=True)
     return loss_err.detach(), {k: (g if g is not None else torch.zeros_like(sd[k])) for k, g in zip(keys, grads)}
 
