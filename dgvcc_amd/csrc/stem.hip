@@ -17,6 +17,7 @@
 //            (the first layer has no input gradient).
 #include "dg_common.h"
 #include <algorithm>
+#include <cstdlib>
 
 extern "C" int dg_bn_bwd_finalize_part(const float* part, int nblk, int M, int C, const float* gamma,
                                        const float* save_invstd, float* dgamma, float* dbeta, float* dbias,
@@ -842,6 +843,15 @@ __global__ __launch_bounds__(SNT) void bn_part_merge(const float* __restrict__ p
 inline int part_rows2(int nblk) { return nblk > 1024 ? dg_cdiv(nblk, PMG) : 0; }
 
 inline int stem_fwd_grid(long long nseg) { return (int)std::max(1LL, std::min(512LL, (nseg + 3) / 4)); }
+// the apply pass (MODE 2) writes no statistics rows, so its grid is free of the 512-row layout:
+// at 114 VGPRs four 256-thread blocks fit per CU (4 waves per SIMD instead of 2), which a
+// streaming pass with one 1-KB store per pixel group needs to keep enough bytes in flight
+// (DGVCC_STEM_APPLY_BPC = blocks per CU, default 4; 2 restores the statistics passes' grid)
+inline int stem_apply_grid(long long nseg) {
+  const char* e = getenv("DGVCC_STEM_APPLY_BPC");
+  const long long bpc = e ? std::max(1, atoi(e)) : 4;
+  return (int)std::max(1LL, std::min(256LL * bpc, (nseg + 3) / 4));
+}
 inline int stem_bwd_grid(long long nseg) { return (int)std::max(1LL, std::min(512LL, (nseg + 3) / 4)); }
 constexpr int STEM_RPB = 32;  // slab rows per first-stage reduce block
 
@@ -895,7 +905,7 @@ extern "C" int dg_stem_apply(const float* img, int N, int H, int W, const void* 
   DG_SUPPORTED(W % 64 == 0 && (long long)N * 3 * H * W < (1LL << 31) && ldy % 8 == 0);
   const long long nseg = (long long)N * H * (W / 64);
   StemBn bn{scale, shift, nullptr, nullptr, nullptr, 0};
-  hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(stem_fwd_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
+  hipLaunchKernelGGL(stem_fwd_kernel<2>, dim3(stem_apply_grid(nseg)), dim3(SNT), 0, (hipStream_t)stream, img, H, W,
                      (const bf16*)wpack, bias, (bf16*)y, (long long)ldy, nseg, (float*)nullptr, bn);
   DG_CHECK_LAUNCH();
   return DG_OK;
