@@ -2611,10 +2611,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
   }
 }
 
-// output rows per persistent 3-tap tile (DGVCC_TAP3P_ROWS=1|2; 2 needs H even)
+// output rows per persistent 3-tap tile (DGVCC_TAP3P_ROWS=1|2|3; ROWS must divide H): ROWS output
+// rows share ROWS + 2 strips, so each barrier-separated strip feeds more MFMAs (4 rows spill)
 static int tap3p_rows() {
   const char* e = getenv("DGVCC_TAP3P_ROWS");
-  return (e && e[0] == '1') ? 1 : 2;
+  return (e && e[0] == '1') ? 1 : (e && e[0] == '3') ? 3 : 2;
 }
 
 static bool use_tap3p() {
@@ -2781,7 +2782,9 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
       } else if (a.Cout == 64 && a.R == 3 && a.S == 3 && a.pad == 1 && a.W % 256 == 0 && use_tap3()) {
         if (a.C == 64 && !a.bpart && use_tap3p()) {
           const unsigned g = (unsigned)std::min<long long>(M / 256, persist_grid());
-          if (a.H % 2 == 0 && tap3p_rows() == 2)
+          if (a.H % 3 == 0 && tap3p_rows() == 3)
+            hipLaunchKernelGGL((conv_fwd_tap3p_kernel<3, T>), dim3((unsigned)std::min<long long>(M / 768, g)), dim3(512), 0, st, a);
+          else if (a.H % 2 == 0 && tap3p_rows() >= 2)
             hipLaunchKernelGGL((conv_fwd_tap3p_kernel<2, T>), dim3((unsigned)std::min<long long>(M / 512, g)), dim3(512), 0, st, a);
           else
             hipLaunchKernelGGL((conv_fwd_tap3p_kernel<1, T>), dim3(g), dim3(512), 0, st, a);

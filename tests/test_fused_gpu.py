@@ -495,13 +495,14 @@ def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
 
 
 @pytest.mark.parametrize("N,H,W,acc", [(2, 16, 256, False), (5, 128, 256, True), (3, 40, 512, False),
-                                       (1, 15, 256, True)])
+                                       (1, 15, 256, True), (3, 48, 256, False)])
 def test_tap3_persistent_matches(dev, monkeypatch, N, H, W, acc):
     """C = Cout = 64 row-aligned 3x3 (enc1.3 and its dgrad): the persistent resident-filter
     kernel (conv_fwd_tap3p_kernel; grids below and above one block per CU) against the
     one-tile-per-block 3-tap kernel: bit-identical forward (+accumulate), BN statistics
-    partials, eval-BN epilogue and dgrad (same K order per output row) with one or two output
-    rows per tile, and within bf16 rounding of float64."""
+    partials, eval-BN epilogue and dgrad (same K order per output row) with one, two or three
+    output rows per tile (rows not dividing H fall back to fewer), and within bf16 rounding of
+    float64."""
     K = _k()
     bf = torch.bfloat16
     g = torch.Generator().manual_seed(14)
@@ -514,7 +515,7 @@ def test_tap3_persistent_matches(dev, monkeypatch, N, H, W, acc):
     st = K.bn_eval_stats(gam, bet, torch.randn(64, device=dev) * 0.1, torch.rand(64, device=dev) + 0.5, 1e-5)
     wp = K.pack_weight(w, bf)
     outs = []
-    for p, rows in (("0", "2"), ("1", "1"), ("1", "2")):  # 2 output rows per tile need H even
+    for p, rows in (("0", "2"), ("1", "1"), ("1", "2"), ("1", "3")):  # ROWS rows per tile need H % ROWS == 0
         monkeypatch.setenv("DGVCC_TAP3P", p)
         monkeypatch.setenv("DGVCC_TAP3P_ROWS", rows)
         y = K.Act(y0.clone())
