@@ -2110,6 +2110,7 @@ static bool use_f32_persist() {
 }
 static int f32_pers_bn(int Cout);
 static bool f32_pers_ok(const FwdArgs& a);
+static bool f32_pers_shape_ok(const FwdArgs& a);
 
 // f32 GEMM arithmetic: 0 = v_mfma_f32_16x16x4_f32, 1 = the exact 3-way bf16 split on
 // v_mfma_f32_16x16x32_bf16 (dg_common.h split3_8; f32-grade).
@@ -2653,10 +2654,23 @@ static bool use_psplit() {
   return !(e && e[0] == '0');
 }
 
+static int psplit_tile_px(const FwdArgs& a);
+// DGVCC_PSPLIT_MIN_TILES: fewest pre-split tiles a launch may have (default 128: half the CUs busy
+// at split-math rates still beats the exact-f32 register-staged kernel, tools/ab_psplit_small.py);
+// 0 = the persistent forward's own bound (more 256-pixel tiles than CUs)
+static int psplit_min_tiles() {
+  const char* e = getenv("DGVCC_PSPLIT_MIN_TILES");
+  return e ? atoi(e) : 128;
+}
 // f32 split-math shapes served by conv_fwd_psplit_kernel (filter panel pre-split per launch)
 static bool psplit_ok(const FwdArgs& a) {
-  return use_psplit() && f32_split() && f32_pers_ok(a) && f32_pers_bn(a.Cout) >= 128 &&
-         (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31);
+  if (!(use_psplit() && f32_split() && f32_pers_shape_ok(a) && f32_pers_bn(a.Cout) >= 128 &&
+        (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31)))
+    return false;
+  const int mt = psplit_min_tiles();
+  if (mt <= 0) return f32_pers_ok(a);
+  const long long M = (long long)a.N * a.H * a.W;
+  return (long long)dg_cdiv(M, psplit_tile_px(a)) * (a.Cout / f32_pers_bn(a.Cout)) >= mt;
 }
 
 // DGVCC_PSPLIT_TALL=0: never the 256-pixel pre-split tiles; 1 (default): where they quantise onto the
@@ -2712,11 +2726,13 @@ static bool has_split_room(const FwdArgs& a) {
 
 // the shapes the f32 persistent forward serves (and so the f32 shapes with epilogue statistics):
 // more tiles than CUs, > PF K-steps per tile, no split-K / BN-backward epilogue
+static bool f32_pers_shape_ok(const FwdArgs& a) {
+  return use_f32_persist() && use_persist() && inc_shape_ok(a) && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 &&
+         a.ldx % 4 == 0 && a.Cout % 64 == 0 && a.Cout <= PERS_BIAS_MAX && a.R * a.S * (a.C / 32) > 2 &&
+         (long long)a.Cout * a.R * a.S * a.C * 4 < (1ll << 31);
+}
 static bool f32_pers_ok(const FwdArgs& a) {
-  if (!(use_f32_persist() && use_persist() && inc_shape_ok(a) && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 && a.ldx % 4 == 0 &&
-        a.Cout % 64 == 0 && a.Cout <= PERS_BIAS_MAX && a.R * a.S * (a.C / 32) > 2 &&
-        (long long)a.Cout * a.R * a.S * a.C * 4 < (1ll << 31)))
-    return false;
+  if (!f32_pers_shape_ok(a)) return false;
   const long long M = (long long)a.N * a.H * a.W;
   return (long long)dg_cdiv(M, PBM) * (a.Cout / f32_pers_bn(a.Cout)) > 256;
 }
@@ -2856,7 +2872,7 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
     // f32: the persistent LDS-DMA pipeline with 128-B (32-channel) K-steps; each K-step is 4x
     // the MFMA work of a 16-bit one (v_mfma_f32_16x16x4_f32), so the 2-stage 256-wide ring
     // hides the DMA latency comfortably.  Epilogue BN statistics (a.part) as in 16-bit.
-    if (f32_pers_ok(a)) {
+    if (f32_pers_ok(a) || (psplit_ok(a) && has_split_room(a))) {
       const int np = dg_cdiv(M, PBM);
       const int bn = f32_pers_bn(a.Cout);
       const long long tiles = (long long)np * (a.Cout / bn);
@@ -4581,7 +4597,7 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   }
   if (part)
     DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S)
-                                : (f32_pers_ok(a) || (rsplit_ok(a) && has_split_room(a))));
+                                : (f32_pers_ok(a) || ((rsplit_ok(a) || psplit_ok(a)) && has_split_room(a))));
   {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
      // runs dg_conv_fwd + the statistics pass instead
     FwdArgs q = a;

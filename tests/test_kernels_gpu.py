@@ -449,7 +449,9 @@ def test_conv_f32_split_same_sign(dev, case, which):
                                               (3, 70, 90, 64, 64, "stats"), (2, 64, 256, 128, 64, "eval"),
                                               (2, 33, 40, 64, 64, "bias"), (2, 8, 256, 64, 64, "stats"),
                                               (1, 6, 512, 128, 64, "bias"), (2, 5, 256, 64, 64, "eval"),
-                                              (2, 4, 512, 64, 64, "stats"), (1, 3, 1024, 64, 64, "eval")])
+                                              (2, 4, 512, 64, 64, "stats"), (1, 3, 1024, 64, 64, "eval"),
+                                              (16, 48, 64, 256, 256, "stats"), (2, 96, 128, 128, 256, "bias"),
+                                              (16, 48, 64, 512, 256, "eval")])
 @pytest.mark.parametrize("tall", ["0", "2"])
 def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi, tall, monkeypatch):
     """Pre-split-filter f32 forward (conv_fwd_psplit_kernel, 192-pixel tiles, BN = 256 / 128; Cout = 64 on
@@ -457,7 +459,9 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi, tall, monkeypatch
     bias + epilogue BN statistics (rows per 192-pixel tile: dg_conv_stats_rows_ex), the eval-BN
     epilogue and a ragged last tile, against float64: y within 5e-6, the merged (n, mean, M2)
     rows equal to the statistics of the stored y.  tall = "2": the 256-channel training launches on
-    256-pixel tiles (DGVCC_PSPLIT_TALL, epilogue scratch and bias in the consumed stage)."""
+    256-pixel tiles (DGVCC_PSPLIT_TALL, epilogue scratch and bias in the consumed stage).  The last three
+    shapes have 128..256 pre-split tiles (fewer than the CUs: DGVCC_PSPLIT_MIN_TILES, the ISW trunk's
+    layer3 at 48 x 64), served before round 4 by the exact-f32 register-staged kernel."""
     if tall == "2" and (Cout % 256 or epi == "eval"):
         pytest.skip("256-pixel tiles serve 256-channel training launches only")
     monkeypatch.setenv("DGVCC_PSPLIT_TALL", tall)
