@@ -127,6 +127,19 @@ __global__ __launch_bounds__(NT) void bn_stats_finalize(const T* __restrict__ z,
   }
 }
 
+// per-channel parameter row r[c0 .. c0+V) (NULL: dflt) with 16-byte loads (c0 % 4 == 0 and
+// the rows start 16-byte aligned)
+template <int V>
+__device__ __forceinline__ void ld_chan_row(const float* r, int c0, float dflt, float v[V]) {
+  if (r) {
+#pragma unroll
+    for (int e = 0; e < V; e += 4) ld4(r + c0 + e, v + e);
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = dflt;
+  }
+}
+
 // The grid stride (gridDim*NT) is a multiple of tpp = C/V (a power of two <= NT),
 // so each thread keeps one channel chunk: per-channel parameters live in registers.
 template <typename T>
@@ -140,8 +153,8 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
   const int c0 = (int)(gt % tpp) * V;
   const long long pstride = (long long)gridDim.x * NT / tpp;
   float sc[V], sf[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
+  ld_chan_row<V>(scale, c0, 1.f, sc);
+  ld_chan_row<V>(shift, c0, 0.f, sf);
   for (long long p = gt / tpp; p < M; p += pstride) {
     float v[V];
     ldv(z + p * ldz + c0, v);
@@ -166,24 +179,22 @@ struct ChanParams {
   float sc[V], sf[V], mu[V], is[V];
   __device__ __forceinline__ void load(int c0, const float* scale, const float* shift, const float* mean,
                                        const float* invstd) {
-#pragma unroll
-    for (int e = 0; e < V; ++e) {  // NULL = identity (conv + activation without normalisation)
-      sc[e] = scale ? scale[c0 + e] : 1.f;
-      sf[e] = shift ? shift[c0 + e] : 0.f;
-      mu[e] = mean ? mean[c0 + e] : 0.f;
-      is[e] = invstd ? invstd[c0 + e] : 1.f;
-    }
+    // NULL = identity (conv + activation without normalisation)
+    ldrow(scale, c0, 1.f, sc);
+    ldrow(shift, c0, 0.f, sf);
+    ldrow(mean, c0, 0.f, mu);
+    ldrow(invstd, c0, 1.f, is);
+  }
+  static __device__ __forceinline__ void ldrow(const float* r, int c0, float dflt, float v[V]) {
+    ld_chan_row<V>(r, c0, dflt, v);
   }
 };
 
 // masked upstream gradient: g * drop, zeroed where the ReLU was inactive
 // (relu mask recomputed from z exactly as the forward: fmaf(z, scale, shift) > 0)
-template <typename T, int V>
-__device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* z, long long ldz, long long p, int c0,
-                                            int C, const ChanParams<V>& cp, int act, const float* drop, int HW,
-                                            float gv[], float zv[]) {
-  ldv(g + p * ldg + c0, gv);
-  ldv(z + p * ldz + c0, zv);
+template <int V>
+__device__ __forceinline__ void bn_bwd_mask(long long p, int c0, int C, const ChanParams<V>& cp, int act,
+                                            const float* drop, int HW, float gv[], const float zv[]) {
   if (drop) {
     const float* d = drop + (p / HW) * C + c0;
 #pragma unroll
@@ -194,6 +205,36 @@ __device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* 
     for (int e = 0; e < V; ++e)
       if (!(fmaf(zv[e], cp.sc[e], cp.sf[e]) > 0.f)) gv[e] = 0.f;
   }
+}
+template <int V, bool DROP, bool ACT>
+__device__ __forceinline__ void bn_mask_t(long long p, int c0, int C, const ChanParams<V>& cp, const float* drop,
+                                          int HW, float gv[], const float zv[]) {
+  if constexpr (DROP) {
+    const float* d = drop + (p / HW) * C + c0;
+#pragma unroll
+    for (int e = 0; e < V; ++e) gv[e] *= d[e];
+  }
+  if constexpr (ACT) {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      if (!(fmaf(zv[e], cp.sc[e], cp.sf[e]) > 0.f)) gv[e] = 0.f;
+  }
+}
+template <typename T, int V>
+__device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* z, long long ldz, long long p, int c0,
+                                            int C, const ChanParams<V>& cp, int act, const float* drop, int HW,
+                                            float gv[], float zv[]) {
+  ldv(g + p * ldg + c0, gv);
+  ldv(z + p * ldz + c0, zv);
+  bn_bwd_mask<V>(p, c0, C, cp, act, drop, HW, gv, zv);
+}
+
+// DGVCC_EW_UNROLL=2: the channel-stationary elementwise passes handle two pixels per loop trip
+// with all four loads issued before the first use; 1 (default): one pixel per trip
+// (tools/bench_bn.py: two per trip is 2-7% slower at 94 VGPRs / 5 waves)
+inline int ew_unroll() {  // read per launch: same-process A/B (tools/bench_bn.py)
+  const char* e = getenv("DGVCC_EW_UNROLL");
+  return e && e[0] == '2' ? 2 : 1;
 }
 
 template <typename T>
@@ -356,8 +397,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_sync(const float* __restri
   coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
+template <typename T, int U = 1>
+__global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
                                                    long long ldz, int M, int C, const float* mean, const float* invstd,
                                                    const float* scale, const float* shift, int act, const float* drop,
                                                    int HW, const float* __restrict__ coef, T* __restrict__ dz,
@@ -370,8 +411,9 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_apply(const
   ChanParams<V> cp;
   cp.load(c0, scale, shift, mean, invstd);
   float k1[V], k2[V], k3[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) { k1[e] = coef[c0 + e]; k2[e] = coef[C + c0 + e]; k3[e] = coef[2 * C + c0 + e]; }
+  ChanParams<V>::ldrow(coef, c0, 0.f, k1);
+  ChanParams<V>::ldrow(coef + C, c0, 0.f, k2);
+  ChanParams<V>::ldrow(coef + 2 * C, c0, 0.f, k3);
   if constexpr (V == 8) {
     // 16-bit: dz = k1 g' - (k2 is) z + (k2 is mu - k3), with k1 = gamma * invstd = the forward's
     // scale (every finalizer forms both as that one product; identity when unnormalised), so 4
@@ -384,9 +426,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_apply(const
       k2[e] = A;
     }
   }
-  for (long long p = gt / tpp; p < M; p += pstride) {
-    float gv[V], zv[V];
-    bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
+  auto f = [&](float gv[], const float zv[]) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       if constexpr (V == 8) {
@@ -396,7 +436,49 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_apply(const
         gv[e] = k1[e] * gv[e] - k2[e] * xh - k3[e];
       }
     }
-    stv(dz + p * lddz + c0, gv);
+  };
+  // dropout / ReLU as compile-time flags: straight-line loop bodies (no loads behind branches)
+  auto run = [&](auto drop_t, auto act_t) {
+    constexpr bool DROP = decltype(drop_t)::value, ACT = decltype(act_t)::value;
+    long long p = gt / tpp;
+    if constexpr (U == 2) {
+      for (; p + pstride < M; p += 2 * pstride) {
+        const long long q = p + pstride;
+        float g0[V], z0[V], g1[V], z1[V];
+        ldv(g + p * ldg + c0, g0);
+        ldv(z + p * ldz + c0, z0);
+        ldv(g + q * ldg + c0, g1);
+        ldv(z + q * ldz + c0, z1);
+        bn_mask_t<V, DROP, ACT>(p, c0, C, cp, drop, HW, g0, z0);
+        bn_mask_t<V, DROP, ACT>(q, c0, C, cp, drop, HW, g1, z1);
+        f(g0, z0);
+        f(g1, z1);
+        stv(dz + p * lddz + c0, g0);
+        stv(dz + q * lddz + c0, g1);
+      }
+    }
+    for (; p < M; p += pstride) {
+      float gv[V], zv[V];
+      ldv(g + p * ldg + c0, gv);
+      ldv(z + p * ldz + c0, zv);
+      bn_mask_t<V, DROP, ACT>(p, c0, C, cp, drop, HW, gv, zv);
+      f(gv, zv);
+      stv(dz + p * lddz + c0, gv);
+    }
+  };
+  if constexpr (U == 1) {  // the round-3 loop (runtime dropout / ReLU flags)
+    for (long long p = gt / tpp; p < M; p += pstride) {
+      float gv[V], zv[V];
+      bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
+      f(gv, zv);
+      stv(dz + p * lddz + c0, gv);
+    }
+  } else if (drop) {
+    if (act == 1) run(std::true_type{}, std::true_type{});
+    else run(std::true_type{}, std::false_type{});
+  } else {
+    if (act == 1) run(std::false_type{}, std::true_type{});
+    else run(std::false_type{}, std::false_type{});
   }
 }
 
@@ -622,6 +704,18 @@ inline int ew_grid(long long n) {
   long long g = (n + NT - 1) / NT;
   return (int)std::max<long long>(1, std::min<long long>(g, 8192));
 }
+// Grid of the channel-stationary passes (bn_apply_kernel, bn_bwd_apply): each thread loads its
+// channel chunk's parameters once, so fewer, longer-lived threads amortise that prologue.
+// DGVCC_EW_GRID (read per launch: tools/bench_bn.py) caps the blocks.
+inline int cs_grid(long long n) {
+  // tools/bench_bn.py (profiles/round4a/bn_grid): 16384 blocks where that leaves every thread >= 2
+  // chunks, else 2048 blocks (each thread then walks several chunks per parameter prologue:
+  // bf16 1024-channel layer3 BN backward 4.2 -> 5.5 TB/s)
+  const char* e = getenv("DGVCC_EW_GRID");
+  const long long g = (n + NT - 1) / NT;
+  if (e) return (int)std::max<long long>(1, std::min<long long>(g, std::max(64, atoi(e))));
+  return (int)(g >= 2 * 16384 ? 16384 : std::min<long long>(g, 2048));
+}
 
 template <typename T>
 int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, const float* beta, float* rm, float* rv,
@@ -654,7 +748,7 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
   DG_CHECK_LAUNCH();
   if (!dz) return DG_OK;  // coefficients only (a fused consumer applies them)
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
-  hipLaunchKernelGGL(bn_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
+  hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<T, 2> : bn_bwd_apply<T, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
                      mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -697,13 +791,13 @@ extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, 
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
+    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
                        shift, act, drop, HW, (bf16*)y, ldy);
   else if (dtype == DG_F16)
-    hipLaunchKernelGGL(bn_apply_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
+    hipLaunchKernelGGL(bn_apply_kernel<f16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
                        shift, act, drop, HW, (f16*)y, ldy);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
+    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
                        scale, shift, act, drop, HW, (float*)y, ldy);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -744,15 +838,15 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
   DG_CHECK_LAUNCH();
   if (dtype == DG_BF16) {
     const long long total = (long long)M * (C / 8);
-    hipLaunchKernelGGL(bn_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
   } else if (dtype == DG_F16) {
     const long long total = (long long)M * (C / 8);
-    hipLaunchKernelGGL(bn_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz);
   } else {
     const long long total = (long long)M * (C / 4);
-    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
                        (float*)dz, lddz);
   }
@@ -978,13 +1072,13 @@ extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
   else if (dtype == DG_F16)
-    hipLaunchKernelGGL(bn_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz);
   else
-    hipLaunchKernelGGL(bn_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
                        (float*)dz, lddz);
   DG_CHECK_LAUNCH();
