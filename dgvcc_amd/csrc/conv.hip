@@ -2110,7 +2110,7 @@ static bool use_f32_persist() {
 }
 static int f32_pers_bn(int Cout);
 static bool f32_pers_ok(const FwdArgs& a);
-static bool f32_pers_shape_ok(const FwdArgs& a);
+static bool f32_pers_shape_ok(const FwdArgs& a, int kmin);
 
 // f32 GEMM arithmetic: 0 = v_mfma_f32_16x16x4_f32, 1 = the exact 3-way bf16 split on
 // v_mfma_f32_16x16x32_bf16 (dg_common.h split3_8; f32-grade).
@@ -2663,8 +2663,14 @@ static int psplit_min_tiles() {
   return e ? atoi(e) : 128;
 }
 // f32 split-math shapes served by conv_fwd_psplit_kernel (filter panel pre-split per launch)
+// DGVCC_PSPLIT_SHORTK=0: not for launches of 2 K-steps per tile (the trunks' 1x1 convs from 64
+// channels, which then take the exact-f32 register-staged kernel)
+static bool psplit_shortk() {
+  const char* e = getenv("DGVCC_PSPLIT_SHORTK");
+  return !(e && e[0] == '0');
+}
 static bool psplit_ok(const FwdArgs& a) {
-  if (!(use_psplit() && f32_split() && f32_pers_shape_ok(a) && f32_pers_bn(a.Cout) >= 128 &&
+  if (!(use_psplit() && f32_split() && f32_pers_shape_ok(a, psplit_shortk() ? 2 : 3) && f32_pers_bn(a.Cout) >= 128 &&
         (long long)a.Cout * a.R * a.S * a.C * 6 < (1ll << 31)))
     return false;
   const int mt = psplit_min_tiles();
@@ -2726,13 +2732,15 @@ static bool has_split_room(const FwdArgs& a) {
 
 // the shapes the f32 persistent forward serves (and so the f32 shapes with epilogue statistics):
 // more tiles than CUs, > PF K-steps per tile, no split-K / BN-backward epilogue
-static bool f32_pers_shape_ok(const FwdArgs& a) {
+// kmin: fewest 32-channel K-steps per tile (the exact / per-wave-split persistent forward prefetches
+// two K-steps of a tile in its prologue and needs > 2; the pre-split one needs >= its stage count - 1)
+static bool f32_pers_shape_ok(const FwdArgs& a, int kmin) {
   return use_f32_persist() && use_persist() && inc_shape_ok(a) && a.ksplit <= 1 && !a.bpart && a.C % 32 == 0 &&
-         a.ldx % 4 == 0 && a.Cout % 64 == 0 && a.Cout <= PERS_BIAS_MAX && a.R * a.S * (a.C / 32) > 2 &&
+         a.ldx % 4 == 0 && a.Cout % 64 == 0 && a.Cout <= PERS_BIAS_MAX && a.R * a.S * (a.C / 32) >= kmin &&
          (long long)a.Cout * a.R * a.S * a.C * 4 < (1ll << 31);
 }
 static bool f32_pers_ok(const FwdArgs& a) {
-  if (!f32_pers_shape_ok(a)) return false;
+  if (!f32_pers_shape_ok(a, 3)) return false;
   const long long M = (long long)a.N * a.H * a.W;
   return (long long)dg_cdiv(M, PBM) * (a.Cout / f32_pers_bn(a.Cout)) > 256;
 }

@@ -529,8 +529,8 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
   const int c0 = (int)(gt % tpp) * V;
   const long long pstride = (long long)gridDim.x * NT / tpp;
   float sc[V], sf[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) { sc[e] = scale[c0 + e]; sf[e] = shift[c0 + e]; }
+  ld_chan_row<V>(scale, c0, 1.f, sc);
+  ld_chan_row<V>(shift, c0, 0.f, sf);
   for (long long pp = gt / tpp; pp < Mp; pp += pstride) {
     long long pos[4];
     pool_window(pp, H, W, pos);
@@ -681,8 +681,9 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
   ChanParams<V> cp;
   cp.load(c0, scale, shift, mean, invstd);
   float k1[V], k2[V], k3[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) { k1[e] = coef[c0 + e]; k2[e] = coef[C + c0 + e]; k3[e] = coef[2 * C + c0 + e]; }
+  ld_chan_row<V>(coef, c0, 0.f, k1);
+  ld_chan_row<V>(coef + C, c0, 0.f, k2);
+  ld_chan_row<V>(coef + 2 * C, c0, 0.f, k3);
   for (long long pp = gt / tpp; pp < Mp; pp += pstride) {
     long long pos[4];
     pool_window(pp, H, W, pos);

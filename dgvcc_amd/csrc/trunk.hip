@@ -162,9 +162,14 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
   const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
   float ga[V], be[V], m[V], s[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) {
-    ga[e] = gamma ? gamma[c0 + e] : 1.f;
-    be[e] = gamma ? beta[c0 + e] : 0.f;
+  for (int e = 0; e < V; e += 4) {  // 16-byte parameter loads (c0 % 4 == 0, rows 16-byte aligned)
+    if (gamma) {
+      ld4(gamma + c0 + e, ga + e);
+      ld4(beta + c0 + e, be + e);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { ga[e + k] = 1.f; be[e + k] = 0.f; }
+    }
   }
   int cur = -1;
   for (int p = gt / tpp; p < M; p += pstride) {
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
     if (n != cur) {
       cur = n;
 #pragma unroll
-      for (int e = 0; e < V; ++e) { m[e] = mu[n * C + c0 + e]; s[e] = is[n * C + c0 + e]; }
+      for (int e = 0; e < V; e += 4) { ld4(mu + n * C + c0 + e, m + e); ld4(is + n * C + c0 + e, s + e); }
     }
     float v[V];
     ldv(x + p * ldx + c0, v);
@@ -206,7 +211,7 @@ __global__ __launch_bounds__(NT) void in_bwd_partial(const T* __restrict__ g, lo
   if (pl < rows) {
     float m[V], s[V];
 #pragma unroll
-    for (int e = 0; e < V; ++e) { m[e] = mu[n * C + c0 + e]; s[e] = is[n * C + c0 + e]; }
+    for (int e = 0; e < V; e += 4) { ld4(mu + n * C + c0 + e, m + e); ld4(is + n * C + c0 + e, s + e); }
     for (int p = p0 + pl; p < p1; p += rows) {
       const long long pp = (long long)n * HW + p;
       float gv[V], xv[V];
@@ -288,12 +293,16 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
     const int n = p / HW;
     if (n != cur) {
       cur = n;
+      // 16-byte loads: (n C + c0) % 4 == 0, so the (k1, k2, k3) triples of the chunk start
+      // 48-byte aligned
+      const int nc = n * C + c0;
+      float t[3 * V];
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        const int nc = n * C + c0 + e;
-        m[e] = mu[nc]; s[e] = is[nc];
-        k1[e] = coef[nc * 3]; k2[e] = coef[nc * 3 + 1]; k3[e] = coef[nc * 3 + 2];
-      }
+      for (int e = 0; e < V; e += 4) { ld4(mu + nc + e, m + e); ld4(is + nc + e, s + e); }
+#pragma unroll
+      for (int q = 0; q < 3 * V; q += 4) ld4(coef + (long long)nc * 3 + q, t + q);
+#pragma unroll
+      for (int e = 0; e < V; ++e) { k1[e] = t[3 * e]; k2[e] = t[3 * e + 1]; k3[e] = t[3 * e + 2]; }
     }
     float gv[V], xv[V], o[V];
     ldv(g + p * ldg + c0, gv);

@@ -503,6 +503,47 @@ def test_conv_f32_psplit_epilogues(dev, N, H, W, C, Cout, epi, tall, monkeypatch
         assert relerr(gm, yd.mean(0)) < 1e-5 and relerr(var, yd.var(0, unbiased=False)) < 1e-5
 
 
+@pytest.mark.parametrize("N,H,W,C,Cout", [(16, 48, 64, 64, 256), (4, 96, 128, 64, 256), (4, 100, 130, 64, 128),
+                                         (16, 48, 64, 32, 256)])
+def test_conv_f32_psplit_short_k(dev, N, H, W, C, Cout, monkeypatch):
+    """1x1 f32 convs from 64 (or 32) channels -- one or two 32-channel K-steps per tile, the
+    trunks' bottleneck expansions -- on the pre-split kernel (DGVCC_PSPLIT_SHORTK, default on) with
+    bias and epilogue statistics against float64, and against the exact-f32 kernel the switch
+    restores: y within 5e-6, the (n, mean, M2) rows equal to the statistics of the stored y.
+    C = 32 (a single K-step) stays on the exact kernel (the pre-split pipeline needs >= 2)."""
+    K = _k()
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, H, W, C, generator=g)
+    w = torch.randn(Cout, C, 1, 1, generator=g) / C ** 0.5
+    b = torch.randn(Cout, generator=g)
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double()).permute(0, 2, 3, 1)
+    ys = []
+    for sk in ("1", "0"):
+        monkeypatch.setenv("DGVCC_PSPLIT_SHORTK", sk)
+        z = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+        res = K.conv_fwd_stats(K.Act(x.to(dev)), wp, Cout, 1, 0, z, bias=b.to(dev))
+        if res is None:  # served by a kernel without epilogue statistics: nothing was launched
+            K.conv_fwd(K.Act(x.to(dev)), wp, Cout, 1, 0, z, bias=b.to(dev))
+        torch.cuda.synchronize()
+        y = z.buf.cpu()
+        assert relerr(y, ref) < 5e-6
+        ys.append(y)
+        if sk == "1" and C == 64:
+            rows = K.query("dg_conv_stats_rows_ex", 0, N, H, W, C, C, Cout, 1, 1)
+            assert res is not None and res[1] == rows == -(-(N * H * W) // (192 if Cout == 256 else 384))
+        if res is not None:
+            p = res[0].double().cpu()
+            n, mean, m2 = p[:, 0], p[:, 1], p[:, 2]
+            tot = n.sum(0)
+            gm = (n * mean).sum(0) / tot
+            var = (m2 + n * (mean - gm) ** 2).sum(0) / tot
+            yd = y.double().reshape(-1, Cout)
+            assert torch.equal(tot, torch.full_like(tot, N * H * W))
+            assert relerr(gm, yd.mean(0)) < 1e-5 and relerr(var, yd.var(0, unbiased=False)) < 1e-5
+    assert relerr(ys[0], ys[1]) < 5e-6
+
+
 @pytest.mark.parametrize("N,H,W,C,Cout,mode", [(2, 9, 64, 64, 64, "1"), (3, 17, 96, 64, 128, "1"),
                                                (2, 40, 32, 128, 64, "1"), (1, 48, 160, 256, 128, "2"),
                                                (4, 5, 128, 64, 64, "1"), (2, 11, 96, 128, 256, "3"),
