@@ -56,6 +56,13 @@ struct FwdArgs {
   long long wsplit_bytes = 0;
 };
 
+// EPI_ACC_NOTE -- conv epilogues: y += old y (accumulate) runs as a pass of its own ahead of the
+// stores, acc = (acc + bias) + y_old with the loads issued together, and the store loop adds the
+// bias only when not accumulating (the same float operations in the same order).  With the y load
+// inside the store loop behind the runtime `accumulate` branch, the compiler drained vmcnt to 0 in
+// front of every store, so each store waited for the previous ones (and for the next tile's DMA in
+// the persistent kernels); the store loop now holds no global loads and its stores issue back to
+// back.  (Bias values come from registers or LDS for the same reason.)
 __device__ __forceinline__ void epi_affine(float v[4], const FwdArgs& a, int co) {
   if (!a.escale) return;
   const f4v sc = *(const f4v*)(a.escale + co), sf = *(const f4v*)(a.eshift + co);
@@ -335,8 +342,36 @@ _Pragma("unroll") \
 #undef FWD_GLOAD
 #undef FWD_SWRITE
 
-  // Epilogue: lane holds pixel column fr, 4 consecutive output channels.
+  // Epilogue: lane holds pixel column fr, 4 consecutive output channels.  Bias, accumulate and
+  // the eval-BN affine (all global loads) in a pass of their own ahead of the stores, so the store
+  // loop holds no global loads (EPI_ACC_NOTE)
   T* y = (T*)a.y;
+  const bool pre = a.bias || a.accumulate || a.escale;
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      const T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco + 16 * i + 4 * fc;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (a.bias) {
+          const float4 b = *(const float4*)(a.bias + co);
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
+          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+        }
+        epi_affine(v, a, co);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
@@ -345,17 +380,7 @@ _Pragma("unroll") \
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const float4 b = *(const float4*)(a.bias + co);
-        v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-      }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-      }
-      epi_affine(v, a, co);
+      const float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       st4(yrow + co, v);
     }
   }
@@ -506,28 +531,51 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
 #undef GEN_GLOAD
 #undef GEN_SWRITE
   T* y = (T*)a.y;
+  // bias read once and y += old y in a pass of its own, ahead of the stores (EPI_ACC_NOTE)
+  f4v bv[TI];
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int px = px0 + wpx + 16 * j + fr;
-    if (px >= M) continue;
+  for (int i = 0; i < TI; ++i)
+    bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  auto out_row = [&](int px) -> T* {
     long long orow = px;
     if (par) {  // class pixel -> dX pixel (n, stride*i + pa, stride*j + pb)
       const int n = px / PQ, rem = px - n * PQ, i = rem / Qc, jj = rem - i * Qc;
       orow = ((long long)n * a.P + i * a.stride + a.pa) * a.Q + jj * a.stride + a.pb;
     }
-    T* yrow = y + orow * a.ldy;
+    return y + orow * a.ldy;
+  };
+  if (a.accumulate) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      const T* yrow = out_row(px);
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco + 16 * i + 4 * fc;
+        float o[4];
+        ld4(yrow + co, o);
+        if (a.bias) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += bv[i][r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int px = px0 + wpx + 16 * j + fr;
+    if (px >= M) continue;
+    T* yrow = out_row(px);
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
+      if (a.bias && !a.accumulate) {
+        const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-      }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       st4(yrow + co, v);
     }
@@ -741,6 +789,27 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      const T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco + 16 * i + 4 * fc;
+        float o[4];
+        ld4(yrow + co, o);
+        if (a.bias) {
+          const f4v b = bv[i];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
@@ -751,14 +820,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
+      if (a.bias && !a.accumulate) {
         const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-      }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
@@ -1060,6 +1124,29 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
     // epilogue of the current tile (the next tile's first DMAs are in flight)
     T* y = (T*)a.y;
     bool valid[TJ];
+    // y += old y ahead of the stores (EPI_ACC_NOTE)
+    if (a.accumulate) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int px = cur.px0 + wpx + 16 * j + fr;
+        if (px >= M) continue;
+        const T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int co = cur.co0 + wco + 16 * i + 4 * fc;
+          float o[4];
+          ld4(yrow + co, o);
+          if (e3_lds) {
+            const f4v b = *(const f4v*)(ebias + co);
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+          } else if (a.bias) {
+            const f4v b = *(const f4v*)(bbuf + co);
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+          }
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = cur.px0 + wpx + 16 * j + fr;
@@ -1070,17 +1157,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       for (int i = 0; i < TI; ++i) {
         const int co = cur.co0 + wco + 16 * i + 4 * fc;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (e3_lds) {
+        if (a.accumulate) {
+        } else if (e3_lds) {
           const f4v b = *(const f4v*)(ebias + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         } else if (a.bias) {
           const f4v b = *(const f4v*)(bbuf + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-        }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
         }
         if constexpr (EPI == 3) {
           if (e3_lds) {  // same fmaf / ReLU as epi_affine on the same f32 value
@@ -1097,7 +1180,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
         }
         st4(yrow + co, v);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);
       }
     }
     if (EPI == 0 && a.part)
@@ -1406,6 +1489,29 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     }
     float* y = (float*)a.y;
     bool valid[TJ];
+    // y += old y ahead of the stores (EPI_ACC_NOTE)
+    if (a.accumulate) {
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int px = cur.px0 + wpx + 16 * j + fr;
+        if (px >= M) continue;
+        const float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int co = cur.co0 + wco + 16 * i + 4 * fc;
+          float o[4];
+          ld4(yrow + co, o);
+          if (e3_lds) {
+            const f4v b = *(const f4v*)(ebias + co);
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+          } else if (a.bias) {
+            const f4v b = *(const f4v*)(bbuf + co);
+            for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+          }
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = cur.px0 + wpx + 16 * j + fr;
@@ -1416,20 +1522,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       for (int i = 0; i < TI; ++i) {
         const int co = cur.co0 + wco + 16 * i + 4 * fc;
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-        if (e3_lds) {
+        if (a.accumulate) {
+        } else if (e3_lds) {
           const f4v b = *(const f4v*)(ebias + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         } else if (a.bias) {
           const f4v b = *(const f4v*)(bbuf + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-        }
         if constexpr (EPI == 3) {
-          if (e3_lds) {
+          if (e3_lds) {  // same fmaf / ReLU as epi_affine on the same f32 value
             const f4v sc = *(const f4v*)(escl + co), sf = *(const f4v*)(eshf + co);
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1591,6 +1693,31 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
 
   float* y = (float*)a.y;
   bool valid[TJ];
+  f4v bv[TI];  // bias read once, ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+    bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      const float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco + 16 * i + 4 * fc;
+        float o[4];
+        ld4(yrow + co, o);
+        if (a.bias) {
+          const f4v b = *(const f4v*)(a.bias + co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
@@ -1601,14 +1728,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
+      if (a.bias && !a.accumulate) {
+        const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-      }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
@@ -1754,6 +1876,31 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
 
   float* y = (float*)a.y;
   bool valid[TJ];
+  f4v bv[TI];  // bias read once, ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+    bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      const float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco + 16 * i + 4 * fc;
+        float o[4];
+        ld4(yrow + co, o);
+        if (a.bias) {
+          const f4v b = *(const f4v*)(a.bias + co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
@@ -1764,14 +1911,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
+      if (a.bias && !a.accumulate) {
+        const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-      }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
@@ -1909,6 +2051,31 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
 
   float* y = (float*)a.y;
   bool valid[TJ];
+  f4v bv[TI];  // bias read once, ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+    bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = px0 + wpx + 16 * j + fr;
+      if (px >= M) continue;
+      const float* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = co0 + wco + 16 * i + 4 * fc;
+        float o[4];
+        ld4(yrow + co, o);
+        if (a.bias) {
+          const f4v b = *(const f4v*)(a.bias + co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = px0 + wpx + 16 * j + fr;
@@ -1919,14 +2086,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const f4v b = *(const f4v*)(a.bias + co);
+      if (a.bias && !a.accumulate) {
+        const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-      }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
       }
       if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
@@ -2193,6 +2355,34 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = (!PADK && a.bias) ? *(const f4v*)(a.bias + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  // accumulate, the eval-BN affine and (PADK) the per-use bias load run in a pass of their own
+  // ahead of the stores, so the store loop holds no global loads (EPI_ACC_NOTE)
+  const bool pre = a.accumulate || a.escale || (PADK && a.bias);
+  if (pre) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int px = PADK ? unpad(px0 + wpx + 16 * j + fr) : px0 + wpx + 16 * j + fr;
+      if (px < 0) continue;
+      const T* yrow = y + (long long)px * a.ldy;
+#pragma unroll
+      for (int i = 0; i < TI; ++i) {
+        const int co = 16 * i + 4 * fc;
+        float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+        if (a.bias) {
+          const f4v b = PADK ? *(const f4v*)(a.bias + co) : bv[i];
+          v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
+        }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
+          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
+        }
+        epi_affine(v, a, co);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+      }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int px = PADK ? unpad(px0 + wpx + 16 * j + fr) : px0 + wpx + 16 * j + fr;
@@ -2203,16 +2393,10 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
     for (int i = 0; i < TI; ++i) {
       const int co = 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias) {
-        const f4v b = PADK ? *(const f4v*)(a.bias + co) : bv[i];
+      if (!PADK && a.bias && !pre) {
+        const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
-      if (a.accumulate) {
-        float o[4];
-        ld4(yrow + co, o);
-        v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-      }
-      epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
@@ -2569,6 +2753,25 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
 #pragma unroll
     for (int r = 0; r < ROWS; ++r) {
     const int opx0 = cur.px0 + r * a.W;
+    if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const T* yrow = y + (long long)(opx0 + wpx + 16 * j + fr) * a.ldy;
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {
+          const int co = wco + 16 * i + 4 * fc;
+          float o[4];
+          ld4(yrow + co, o);
+          if (a.bias) {
+            const f4v b = *(const f4v*)(ebuf + co);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc[r][i][j][e] += b[e];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[r][i][j][e] += o[e];
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       valid[j] = true;
@@ -2577,14 +2780,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_tap3p_kernel(FwdArgs a) {
       for (int i = 0; i < TI; ++i) {
         const int co = wco + 16 * i + 4 * fc;
         float v[4] = {acc[r][i][j][0], acc[r][i][j][1], acc[r][i][j][2], acc[r][i][j][3]};
-        if (a.bias) {
+        if (a.bias && !a.accumulate) {
           const f4v b = *(const f4v*)(ebuf + co);
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
-        }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
         }
         if (a.escale) {  // as epi_affine
           const f4v sc = *(const f4v*)(ebuf + BN + co), sf = *(const f4v*)(ebuf + 2 * BN + co);
@@ -2759,11 +2957,19 @@ static bool pers_wide_on() {  // DGVCC_PERS_WIDE=0: the 16-bit 128-channel persi
 }
 // the 16-bit forward takes conv_fwd_pers_kernel<128, .., WIDE = 1> (384-pixel tiles): the same
 // conditions as launch_fwd_impl's persistent branch at BN = 128, no split-K / BN-backward epilogue
+// DGVCC_PERS_SHORTK=0: the 16-bit persistent forward only for > 2 K-steps per tile (round 3); default:
+// down to the pipeline depth (1 K-step on the 2-stage kernels, 2 on the 3-stage ones), so the
+// trunks' 1x1 convs from 64 / 128 channels run persistent too (read per launch: A/B)
+static bool pers16_shortk() {
+  const char* e = getenv("DGVCC_PERS_SHORTK");
+  return !(e && e[0] == '0');
+}
+static int pers16_kmin(int stg) { return pers16_shortk() ? stg - 1 : 3; }
 static bool pers16_wide(const FwdArgs& a) {
   if (!(pers_wide_on() && use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
         !(short_k_reg() && a.R * a.S * (a.C / 64) <= 2) && (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31) &&
         a.ksplit <= 1 && !a.bpart && use_persist() && pipe_var() == 2 && inc_shape_ok(a) &&
-        a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX))
+        a.R * a.S * (a.C / 64) >= pers16_kmin(2) && a.Cout <= PERS_BIAS_MAX))
     return false;
   if (!(a.Cout % 128 == 0 && !(a.Cout % 256 == 0 && pipe_wide()))) return false;  // BN = 128
   const long long M = (long long)a.N * a.H * a.W;
@@ -2818,7 +3024,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
         const long long U = (long long)a.N * (a.H + 2) * (a.W + 2);
         if (tap3_bk(true) == 32) hipLaunchKernelGGL((conv_fwd_tap3n_kernel<1, T>), dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
         else hipLaunchKernelGGL((conv_fwd_tap3_kernel<1, T>), dim3((unsigned)dg_cdiv(U, 256)), dim3(256), 0, st, a);
-      } else if (use_persist() && !a.bpart && var == 2 && inc_shape_ok(a) && a.R * a.S * (a.C / 64) > 2 && a.Cout <= PERS_BIAS_MAX &&
+      } else if (use_persist() && !a.bpart && var == 2 && inc_shape_ok(a) &&
+                 a.R * a.S * (a.C / 64) >= pers16_kmin(a.Cout % 256 == 0 && pipe_wide() ? 2 : 3) && a.Cout <= PERS_BIAS_MAX &&
                  (long long)np * (a.Cout / (a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64))) >
                      2 * 256) {
         const int bn = a.Cout % 256 == 0 && pipe_wide() ? 256 : (a.Cout % 128 == 0 ? 128 : 64);
