@@ -25,7 +25,8 @@ if len(sys.argv) > 7 and sys.argv[7] == "small":
               (48, 64, 256, 128, 16, 3), (40, 64, 256, 256, 16, 3), (32, 48, 512, 256, 16, 3),
               (24, 32, 1024, 512, 16, 3)]
 if len(sys.argv) > 7 and sys.argv[7] == "shortk":  # 1x1 from 64 channels (two 32-channel K-steps)
-    shapes = [(192, 256, 64, 256, 16, 1), (96, 128, 64, 256, 16, 1), (384, 512, 64, 128, 16, 1)]
+    shapes = [(192, 256, 64, 256, 16, 1), (96, 128, 64, 256, 16, 1), (384, 512, 64, 128, 16, 1),
+              (96, 128, 128, 512, 16, 1), (48, 64, 256, 1024, 16, 1)]
 dev = "cuda"
 K.call("dg_set_f32_math", 1)
 tot = {a: 0.0 for a in arms}
