@@ -789,7 +789,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
-  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+  if (a.accumulate || EPI == 3) {  // old y, bias and the eval-BN affine ahead of the stores (EPI_ACC_NOTE)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = px0 + wpx + 16 * j + fr;
@@ -798,15 +798,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int co = co0 + wco + 16 * i + 4 * fc;
-        float o[4];
-        ld4(yrow + co, o);
         if (a.bias) {
           const f4v b = bv[i];
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+        if constexpr (EPI == 3) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          epi_affine(v, a, co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+        }
       }
     }
   }
@@ -820,11 +828,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias && !a.accumulate) {
+      if (a.bias && !a.accumulate && EPI != 3) {
         const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
-      if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
@@ -1697,7 +1704,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
-  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+  if (a.accumulate || EPI == 3) {  // old y, bias and the eval-BN affine ahead of the stores (EPI_ACC_NOTE)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = px0 + wpx + 16 * j + fr;
@@ -1706,15 +1713,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int co = co0 + wco + 16 * i + 4 * fc;
-        float o[4];
-        ld4(yrow + co, o);
         if (a.bias) {
           const f4v b = *(const f4v*)(a.bias + co);
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+        if constexpr (EPI == 3) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          epi_affine(v, a, co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+        }
       }
     }
   }
@@ -1728,11 +1743,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias && !a.accumulate) {
+      if (a.bias && !a.accumulate && EPI != 3) {
         const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
-      if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
@@ -1880,7 +1894,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
-  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+  if (a.accumulate || EPI == 3) {  // old y, bias and the eval-BN affine ahead of the stores (EPI_ACC_NOTE)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = px0 + wpx + 16 * j + fr;
@@ -1889,15 +1903,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int co = co0 + wco + 16 * i + 4 * fc;
-        float o[4];
-        ld4(yrow + co, o);
         if (a.bias) {
           const f4v b = *(const f4v*)(a.bias + co);
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+        if constexpr (EPI == 3) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          epi_affine(v, a, co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+        }
       }
     }
   }
@@ -1911,11 +1933,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias && !a.accumulate) {
+      if (a.bias && !a.accumulate && EPI != 3) {
         const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
-      if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
@@ -2055,7 +2076,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
-  if (a.accumulate) {  // y += old y ahead of the stores (EPI_ACC_NOTE)
+  if (a.accumulate || EPI == 3) {  // old y, bias and the eval-BN affine ahead of the stores (EPI_ACC_NOTE)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int px = px0 + wpx + 16 * j + fr;
@@ -2064,15 +2085,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int co = co0 + wco + 16 * i + 4 * fc;
-        float o[4];
-        ld4(yrow + co, o);
         if (a.bias) {
           const f4v b = *(const f4v*)(a.bias + co);
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
+        if (a.accumulate) {
+          float o[4];
+          ld4(yrow + co, o);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+        }
+        if constexpr (EPI == 3) {
+          float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+          epi_affine(v, a, co);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
+        }
       }
     }
   }
@@ -2086,11 +2115,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (a.bias && !a.accumulate) {
+      if (a.bias && !a.accumulate && EPI != 3) {
         const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
-      if constexpr (EPI == 3) epi_affine(v, a, co);
       st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
