@@ -2993,15 +2993,32 @@ static bool pers16_shortk() {
   return !(e && e[0] == '0');
 }
 static int pers16_kmin(int stg) { return pers16_shortk() ? stg - 1 : 3; }
+// DGVCC_PERS_WIDE_SMALL=0: 256-channel launches of <= 2 rounds of tiles stay on the pipe kernel
+// (read per launch: A/B)
+static bool pers_wide_small() {
+  const char* e = getenv("DGVCC_PERS_WIDE_SMALL");
+  return !(e && e[0] == '0');
+}
 static bool pers16_wide(const FwdArgs& a) {
   if (!(pers_wide_on() && use_pipe() && a.C % 64 == 0 && a.ldx % 8 == 0 &&
         !(short_k_reg() && a.R * a.S * (a.C / 64) <= 2) && (long long)a.Cout * a.R * a.S * a.C * 2 < (1ll << 31) &&
         a.ksplit <= 1 && !a.bpart && use_persist() && pipe_var() == 2 && inc_shape_ok(a) &&
         a.R * a.S * (a.C / 64) >= pers16_kmin(2) && a.Cout <= PERS_BIAS_MAX))
     return false;
-  if (!(a.Cout % 128 == 0 && !(a.Cout % 256 == 0 && pipe_wide()))) return false;  // BN = 128
+  if (a.Cout % 128 != 0) return false;
   const long long M = (long long)a.N * a.H * a.W;
-  return (long long)dg_cdiv(M, PBM) * (a.Cout / 128) > 2 * 256;
+  if (!(a.Cout % 256 == 0 && pipe_wide())) return (long long)dg_cdiv(M, PBM) * (a.Cout / 128) > 2 * 256;  // BN = 128
+  // 256-channel launches too small for the 256-channel persistent forward (<= 2 rounds of 256 x 256
+  // tiles, which then ran one tile per block on the pipe kernel: 384 tiles = 1.5 rounds at 1/16
+  // resolution): the 384 x 128 tiles where they cost fewer tile-areas of rounds (+10% for the
+  // narrower tile's lower rate)
+  // (grids small enough for split-K keep it: dg_conv_fwd_ex splits their K loop when given a
+  // workspace, and the statistics rows must not depend on whether one was given)
+  if (!pers_wide_small() || fwd_ksplit(M, a.Cout, a.C, a.R, a.S) > 1) return false;
+  const long long t256 = (long long)dg_cdiv(M, PBM) * (a.Cout / 256);
+  if (t256 > 2 * 256) return false;
+  const long long tw = (long long)dg_cdiv(M, 384) * (a.Cout / 128), G = persist_grid();
+  return (double)dg_cdiv(tw, G) * 384 * 128 * 1.1 < (double)dg_cdiv(t256, G) * 256 * 256;
 }
 
 template <typename T>
@@ -3075,6 +3092,9 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
         }
+      } else if (epi == 0 && pers16_wide(a)) {  // small 256-channel grids on 384 x 128 persistent tiles
+        const unsigned gw = (unsigned)std::min<long long>((long long)dg_cdiv(M, 384) * (a.Cout / 128), persist_grid());
+        hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1>), dim3(gw), dim3(512), 0, st, a);
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
       else PIPE_LAUNCH(64, 3, np * (a.Cout / 64));

@@ -226,6 +226,7 @@ def test_bn_relu_pool_fused(dev, dtype, with_y, with_gd, C, H, W):
     (1, 8, 256, 64, 64),      # fused 3-tap kernel
     (3, 256, 512, 64, 64),    # fused 3-tap, 1536 partial rows: two-stage merge
     (1, 12, 12, 512, 1024),   # several co tiles
+    (16, 48, 64, 256, 512),   # 384 256-channel tiles: persistent 384 x 128 tiles (DGVCC_PERS_WIDE_SMALL)
 ])
 def test_conv_epilogue_bn_stats(dev, N, H, W, C, Cout):
     """dg_conv_fwd_stats (statistics in the conv epilogue) + dg_bn_part_finalize against

@@ -2,7 +2,7 @@
 DGVCC_CONV_KORDER) on the sta_final layer shapes, f32 split math (the pre-split kernel serves
 forward- and dgrad-shaped launches alike), interleaved rounds, min over rounds.  Prints the max
 abs difference between the two arms' outputs (0 when the switch only changes scheduling).
-usage: ab_conv_env.py VAR A B [reps] [dtype] [fwd|wgrad] [sta|small|shortk]
+usage: ab_conv_env.py VAR A B [reps] [dtype] [fwd|wgrad] [sta|small|small16|shortk]
 (small: launches of 96..256 pre-split tiles -- the ISW trunk's layer3 at 48 x 64 and the sta cls_head
 -- for DGVCC_PSPLIT_MIN_TILES)"""
 import os
@@ -24,6 +24,9 @@ if len(sys.argv) > 7 and sys.argv[7] == "small":
     shapes = [(48, 64, 1024, 256, 16, 1), (48, 64, 256, 256, 16, 3), (48, 64, 512, 256, 16, 3),
               (48, 64, 256, 128, 16, 3), (40, 64, 256, 256, 16, 3), (32, 48, 512, 256, 16, 3),
               (24, 32, 1024, 512, 16, 3)]
+if len(sys.argv) > 7 and sys.argv[7] == "small16":  # 256-channel grids of <= 2 rounds (DGVCC_PERS_WIDE_SMALL)
+    shapes = [(48, 64, 512, 512, 16, 3), (48, 64, 256, 512, 16, 3), (48, 64, 512, 256, 16, 3), (48, 64, 1024, 256, 16, 1),
+              (96, 128, 512, 256, 4, 3)]
 if len(sys.argv) > 7 and sys.argv[7] == "shortk":  # 1x1 from 64 channels (two 32-channel K-steps)
     shapes = [(192, 256, 64, 256, 16, 1), (96, 128, 64, 256, 16, 1), (384, 512, 64, 128, 16, 1),
               (96, 128, 128, 512, 16, 1), (48, 64, 256, 1024, 16, 1)]
