@@ -425,7 +425,10 @@ __device__ __forceinline__ bool gen_src(const GenArgs& a, int n, int p, int q, i
   return true;
 }
 
-template <typename T, int BCO, int BPX>
+// SPL = 1 (T = float): the f32 GEMM on the bf16 matrix cores through the exact 3-way split of both
+// operands per wave (dg_common.h split3_8; conv_fwd_pers_kernel SPL = 1): one 32-channel K-step is
+// one 16x16x32 block, the lane's 8 k values being chunks fc and 4 + fc of the 128-B rows
+template <typename T, int BCO, int BPX, int SPL = 0>
 __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
   constexpr int EPC = 16 / (int)sizeof(T);
   constexpr int BK = 128 / (int)sizeof(T);
@@ -512,18 +515,42 @@ __global__ __launch_bounds__(NT, 2) void conv_gen_kernel(GenArgs a) {
     if (t + 1 < KT) GEN_GLOAD(t + 1);
     const char* As = smem + cur * TILE_BYTES;
     const char* Bs = As + BCO * 128;
+    if constexpr (SPL) {
+      static_assert(!Is16<T>::value, "split path is for f32 operands");
+      s8v bh[TJ][3];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int ch = 4 * ks + fc;
-      u4v af[TI], bfr[TJ];
+      for (int j = 0; j < TJ; ++j) {
+        const u4v b0 = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, fc));
+        const u4v b1 = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, 4 + fc));
+        split3_8(b0, b1, bh[j][0], bh[j][1], bh[j][2]);
+      }
 #pragma unroll
-      for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+      for (int i = 0; i < TI; ++i) {
+        const u4v a0 = *(const u4v*)(As + swz(wco + 16 * i + fr, fc));
+        const u4v a1 = *(const u4v*)(As + swz(wco + 16 * i + fr, 4 + fc));
+        s8v ah[3];
+        split3_8(a0, a1, ah[0], ah[1], ah[2]);
+        constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
+        for (int q = 0; q < 6; ++q)
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
+      }
+    } else {
 #pragma unroll
-        for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+      for (int ks = 0; ks < 2; ++ks) {
+        const int ch = 4 * ks + fc;
+        u4v af[TI], bfr[TJ];
+#pragma unroll
+        for (int i = 0; i < TI; ++i) af[i] = *(const u4v*)(As + swz(wco + 16 * i + fr, ch));
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) bfr[j] = *(const u4v*)(Bs + swz(wpx + 16 * j + fr, ch));
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) mfma_frag<T>(acc[i][j], af[i], bfr[j]);
+      }
     }
     if (t + 1 < KT) GEN_SWRITE(cur ^ 1);
     __syncthreads();
@@ -587,8 +614,18 @@ static bool gen_parity() {  // DGVCC_GEN_PARITY=0: strided dgrad as one transpos
   return !(e && e[0] == '0');
 }
 
+static bool f32_split();
+// DGVCC_GEN_SPLIT=0: f32 strided / general convs on v_mfma_f32_16x16x4_f32 also under the split
+// math (read per launch: A/B)
+static bool gen_split() {
+  const char* e = getenv("DGVCC_GEN_SPLIT");
+  return !(e && e[0] == '0');
+}
+
 template <typename T>
 int launch_gen(const GenArgs& a0, hipStream_t st) {
+  bool spl = false;
+  if constexpr (!Is16<T>::value) spl = f32_split() && gen_split();
   const int ncls = (a0.mode == 1 && a0.stride > 1 && gen_parity()) ? a0.stride * a0.stride : 1;
   for (int c = 0; c < ncls; ++c) {
     GenArgs a = a0;
@@ -601,7 +638,12 @@ int launch_gen(const GenArgs& a0, hipStream_t st) {
       if (M == 0) continue;
     }
     const int npx = dg_cdiv(M, 128);
-    if (a.Cout % 128 == 0)
+    if (spl) {
+      if (a.Cout % 128 == 0)
+        hipLaunchKernelGGL((conv_gen_kernel<T, 128, 128, !Is16<T>::value>), dim3(npx * (a.Cout / 128)), dim3(NT), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv_gen_kernel<T, 64, 128, !Is16<T>::value>), dim3(npx * (a.Cout / 64)), dim3(NT), 0, st, a);
+    } else if (a.Cout % 128 == 0)
       hipLaunchKernelGGL((conv_gen_kernel<T, 128, 128>), dim3(npx * (a.Cout / 128)), dim3(NT), 0, st, a);
     else
       hipLaunchKernelGGL((conv_gen_kernel<T, 64, 128>), dim3(npx * (a.Cout / 64)), dim3(NT), 0, st, a);

@@ -63,12 +63,13 @@ def _oracle(kind, sd0, img, dmaps, dtype, masks=None):
     return out.detach().double(), loss, grads
 
 
-def _sensitivity(kind, sd0, img, dmaps, g64, eps=3e-5):
+def _sensitivity(kind, sd0, img, dmaps, g64, eps=3e-5, masks=None):
     """Normwise change of each float64 gradient when the frames move by eps (relative,
     seeded noise): the conditioning of that gradient against forward perturbations of the
-    size fp32 arithmetic makes (see tests/test_model_gpu.py::grad_sensitivity)."""
+    size fp32 arithmetic makes (see tests/test_model_gpu.py::grad_sensitivity).  masks: the
+    ISW sensitive-covariance masks, held fixed."""
     noise = torch.randn(img.shape, generator=torch.Generator().manual_seed(77), dtype=torch.float64)
-    _, _, g1 = _oracle(kind, sd0, img.double() * (1 + eps * noise), dmaps, torch.float64)
+    _, _, g1 = _oracle(kind, sd0, img.double() * (1 + eps * noise), dmaps, torch.float64, masks)
     return {k: ((g1[k] - g64[k]).norm() / g64[k].norm().clamp_min(1e-300)).item() for k in g64}
 
 
@@ -164,7 +165,10 @@ def test_isw_covstat_and_train_fp32(dev):
           "wt err", abs(losses[1].item() - wt64.item()), "fp32 ref", abs(wt32.item() - wt64.item()))
     assert abs(losses[0].item() - l64.item()) <= max(3 * abs(l32.item() - l64.item()), 1e-4 * l64.item())
     assert abs(losses[1].item() - wt64.item()) <= max(3 * abs(wt32.item() - wt64.item()), 1e-4 * wt64.item())
-    _check_grads(model, g64, {k: v.double() for k, v in g32.items()})
+    sens = _sensitivity("isw", sd0, img1, dmaps, g64, masks=masks)
+    print("isw sensitivity, largest:", sorted(sens.items(), key=lambda kv: -kv[1])[:3],
+          "layer3.5.bn3.weight:", sens.get("layer3.5.bn3.weight"))
+    _check_grads(model, g64, {k: v.double() for k, v in g32.items()}, sens=sens)
 
 
 def test_isw_trainer_step(dev):
