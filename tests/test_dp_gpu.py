@@ -52,3 +52,13 @@ def test_bench_gpus_flag_launches_ranks(dev):
     out = json.loads(line[0])
     assert out["n_gpus"] == 2 and out["config"]["rccl_world_size"] == 2, out
     assert out["params_in_sync"] is True, out
+
+
+def test_rccl_backend_executes(dev):
+    """The DP path's collectives through RCCL (backend "nccl") on one rank (tests/rccl_worker.py)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+                        "--master-addr", "127.0.0.1", f"--master-port={_port()}",
+                        os.path.join(HERE, "rccl_worker.py")],
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and "OK rccl" in r.stdout, (r.stdout[-2000:], r.stderr[-3000:])
