@@ -82,6 +82,27 @@ def bn_stats(z: Act, bn: nn.BatchNorm2d, training: bool) -> torch.Tensor:
     return bn_eval_cached(bn, bn)
 
 
+_EPI_STATS_OFF = __import__("os").environ.get("DGVCC_TRUNK_EPI_STATS", "1") == "0"
+
+
+def conv_bn_stats(tc: "TConv", x: Act, wp, z: Act, bn: nn.BatchNorm2d, training: bool) -> torch.Tensor:
+    """z = conv(x) and bn_stats(z) in one: in training the statistics come from the conv
+    epilogue where the kernel serving the shape writes them (stride-1 'same' convs, as
+    engine.ConvLayer does for the VGG encoder), which saves the statistics pass's full read of z;
+    else the conv, then bn_stats.  DGVCC_TRUNK_EPI_STATS=0: always the separate pass (A/B)."""
+    if training and tc.same and not _EPI_STATS_OFF:
+        epi = K.conv_fwd_stats(x, wp, tc.Cout, tc.R, tc.pad, z)
+        if epi is not None:
+            pg = SB.group_of(bn)
+            if pg is not None:
+                return SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1], M=z.M)
+            bn.num_batches_tracked.add_(1)
+            return K.bn_part_finalize(epi[0], epi[1], tc.Cout, bn.weight.detach(), bn.bias.detach(),
+                                      bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
+    tc.fwd(x, wp, z)
+    return bn_stats(z, bn, training)
+
+
 def bn_backward(bn: nn.BatchNorm2d, g: Act, z: Act, st, act: int, dz: Act, grads: dict):
     """dz of a training-mode BatchNorm (+ ReLU) from g; dgamma / dbeta accumulated into grads
     (the synchronised backward under a process group, as bn_stats' forward)."""
@@ -206,19 +227,25 @@ class Block:
         N = x.N
         nh = lambda h, w, c: Act(K.nhwc(N, h, w, c, dt, dev))  # noqa: E731
         wp1, wp2, wp3 = self.c1.pack(dt, training), self.c2.pack(dt, training), self.c3.pack(dt, training)
-        z1 = nh(x.H, x.W, self.c1.Cout); self.c1.fwd(x, wp1, z1)
-        st1 = bn_stats(z1, self.bn1, training)
+        z1 = nh(x.H, x.W, self.c1.Cout)
+        st1 = conv_bn_stats(self.c1, x, wp1, z1, self.bn1, training)
         a1 = nh(x.H, x.W, self.c1.Cout); K.bn_apply(z1, st1, ACT_RELU, a1)
         P, Q = self.c2.out_hw(x.H, x.W)
-        z2 = nh(P, Q, self.c2.Cout); self.c2.fwd(a1, wp2, z2)
-        a2 = nh(P, Q, self.c2.Cout); st2 = self.n2.forward(z2, a2, training, ACT_RELU)
-        z3 = nh(P, Q, self.c3.Cout); self.c3.fwd(a2, wp3, z3)
-        st3 = bn_stats(z3, self.bn3, training)
+        z2 = nh(P, Q, self.c2.Cout)
+        a2 = nh(P, Q, self.c2.Cout)
+        if self.n2.kind == "bn":  # Norm.forward's BN branch with the conv-epilogue statistics
+            st2 = conv_bn_stats(self.c2, a1, wp2, z2, self.n2.m, training)
+            K.bn_apply(z2, st2, ACT_RELU, a2)
+        else:
+            self.c2.fwd(a1, wp2, z2)
+            st2 = self.n2.forward(z2, a2, training, ACT_RELU)
+        z3 = nh(P, Q, self.c3.Cout)
+        st3 = conv_bn_stats(self.c3, a2, wp3, z3, self.bn3, training)
         wpd = zd = std = None
         if self.cd is not None:
             wpd = self.cd.pack(dt, training)
-            zd = nh(P, Q, self.cd.Cout); self.cd.fwd(x, wpd, zd)
-            std = bn_stats(zd, self.bnd, training)
+            zd = nh(P, Q, self.cd.Cout)
+            std = conv_bn_stats(self.cd, x, wpd, zd, self.bnd, training)
         out = nh(P, Q, self.c3.Cout)
         s = sst = w = None
         if self.post is None:
