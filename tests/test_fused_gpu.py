@@ -495,6 +495,32 @@ def test_persistent_conv_matches(dev, monkeypatch, N, H, W, C, Cout, stats):
         assert torch.equal(outs[0][1], outs[1][1])
 
 
+@pytest.mark.parametrize("N,H,W,C,Cout", [(4, 192, 256, 64, 256), (8, 96, 128, 128, 512)])
+def test_persistent_short_k_1x1(dev, monkeypatch, N, H, W, C, Cout):
+    """bf16 1x1 convs of one or two 64-channel K-steps (the trunks' bottleneck expansions) on the
+    persistent forward (DGVCC_PERS_SHORTK, default) against the one-tile-per-block pipe kernel
+    they ran on before: bit-identical outputs and statistics partials (same K order per tile),
+    and the outputs against float64."""
+    K = _k()
+    bf = torch.bfloat16
+    g = torch.Generator().manual_seed(17)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, bf)
+    w = (torch.randn(Cout, C, 1, 1, generator=g) / C ** 0.5).to(dev)
+    b = torch.randn(Cout, generator=g).to(dev)
+    wp = K.pack_weight(w, bf)
+    outs = []
+    for sk in ("1", "0"):
+        monkeypatch.setenv("DGVCC_PERS_SHORTK", sk)
+        z = K.Act(K.nhwc(N, H, W, Cout, bf, dev))
+        res = K.conv_fwd_stats(K.Act(x), wp, Cout, 1, 0, z, bias=b)
+        assert res is not None
+        outs.append((z.buf.clone(), res[0].clone()))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    ref = F.conv2d(x.double().permute(0, 3, 1, 2), w.double(), b.double()).permute(0, 2, 3, 1)
+    assert relerr(outs[0][0], ref) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,acc", [(2, 16, 256, False), (5, 128, 256, True), (3, 40, 512, False),
                                        (1, 15, 256, True), (3, 48, 256, False)])
 def test_tap3_persistent_matches(dev, monkeypatch, N, H, W, acc):
