@@ -260,6 +260,58 @@ class BnPartCase:
         return {"ga": ga.buf, "gx": gx.buf}, {**gA, **gb}
 
 
+class TrunkBlockCase:
+    """One ResNet-50 Bottleneck of the trunk plans (dgvcc_amd/trunk.py Block: conv1 1x1 + BN + ReLU,
+    conv2 3x3/stride + BN + ReLU, conv3 1x1 + BN, downsample 1x1/stride + BN, join + ReLU) with every
+    BN a SyncBatchNorm -- the ISW trunk's Norm2d (models/ISW/mynn.py:8-14).  stride 1: the
+    statistics come from the conv epilogues' partial rows (trunk.conv_bn_stats -> SB.fwd_stats(part));
+    stride 2: conv2 and the downsample take the statistics pass over z (SB.fwd_stats(z))."""
+
+    def __init__(self, stride, N=4, H=128, W=128, C=64, mid=64, Co=256):
+        self.stride, self.C, self.mid, self.Co = stride, C, mid, Co
+        g = torch.Generator().manual_seed(29 + stride)
+        self.x = torch.relu(torch.randn(N, H, W, C, generator=g))
+        self.gy = torch.randn(N, H // stride, W // stride, Co, generator=g)
+
+    def build(self, sync, dev):
+        from dgvcc_amd import trunk as T
+
+        def conv(C, Co, R, st, seed):
+            cv = nn.Conv2d(C, Co, R, stride=st, padding=R // 2, bias=False)
+            with torch.no_grad():
+                cv.weight.copy_(torch.randn(cv.weight.shape, generator=torch.Generator().manual_seed(seed))
+                                * (2.0 / (C * R * R)) ** 0.5)
+            return cv.to(dev)
+        c1, c2, c3 = conv(self.C, self.mid, 1, 1, 31), conv(self.mid, self.mid, 3, self.stride, 37), conv(self.mid, self.Co, 1, 1, 41)
+        cd = conv(self.C, self.Co, 1, self.stride, 43)
+        b1, b2, b3, bd = (_bn(c, sync, dev) for c in (self.mid, self.mid, self.Co, self.Co))
+        blk = T.Block(c1, b1, c2, T.Norm("bn", b2), c3, b3, cd, bd)
+        names = {c1.weight: "w1", c2.weight: "w2", c3.weight: "w3", cd.weight: "wd"}
+        for k, b in (("1", b1), ("2", b2), ("3", b3), ("d", bd)):
+            names[b.weight] = "gamma" + k
+            names[b.bias] = "beta" + k
+        rs = {"rm3": b3.running_mean, "rv3": b3.running_var, "rmd": bd.running_mean, "rvd": bd.running_var,
+              "rm2": b2.running_mean, "rv2": b2.running_var}
+        return [blk], names, rs
+
+    def forward(self, layers, xs, dev):
+        blk, = layers
+        tape = {}
+        out = blk.forward(K.Act(xs.to(dev).contiguous()), True, tape, [])
+        return tape, {"out": out.buf}
+
+    def gather(self, G, tape, layers, layers_s):
+        t = tape[layers[0]]
+        gt = {k: (G.act(v) if isinstance(v, K.Act) else v) for k, v in t.items()}  # stats / packed weights: global
+        return {layers_s[0]: gt}
+
+    def backward(self, layers, tape, gs, dev):
+        blk, = layers
+        grads = {}
+        gx = blk.backward(tape, K.Act(gs.to(dev).contiguous().clone()), grads)
+        return {"gx": gx.buf}, grads
+
+
 def layer_check(name, case, dev, rank, world):
     """The case's layers with SyncBatchNorm on this rank's part against the same layers with a
     plain BatchNorm2d: forward on the whole batch (outputs, running statistics), backward on the
@@ -464,7 +516,8 @@ def main():
     for name, case in (("conv", ConvCase(False)), ("conv+pool", ConvCase(True)),
                        ("conv cls_head 8x8", ConvCase(False, 4, 8, 8, 512, 256)),
                        ("conv dec3 8x8", ConvCase(False, 4, 8, 8, 512, 1024)),
-                       ("cat", CatCase()), ("dgrad-bnpart", BnPartCase())):
+                       ("cat", CatCase()), ("dgrad-bnpart", BnPartCase()),
+                       ("trunk block", TrunkBlockCase(1)), ("trunk block stride 2", TrunkBlockCase(2))):
         fails += layer_check(name, case, dev, rank, world)
     f, sd0, batch = whole_step(dev, rank, world)
     fails += f
