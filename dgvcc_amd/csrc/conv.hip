@@ -54,6 +54,10 @@ struct FwdArgs {
   // Cout*R*S*C filter, dg_conv_fwd_workspace); null / too small: kernels that split per wave
   char* wsplit = nullptr;
   long long wsplit_bytes = 0;
+  // dg_conv_fwd_acc_relu (accumulating 1x1 dgrad whose output is the gradient of a ReLU output):
+  // the ReLU output, same dtype / rows as y; the accumulated value is zeroed where it is <= 0
+  const char* rmask = nullptr;
+  long long ldrm = 0;
 };
 
 // EPI_ACC_NOTE -- conv epilogues: y += old y (accumulate) runs as a pass of its own ahead of the
@@ -71,6 +75,24 @@ __device__ __forceinline__ void epi_affine(float v[4], const FwdArgs& a, int co)
     float t = fmaf(v[r], sc[r], sf[r]);
     if (a.eact == 1) t = t > 0.f ? t : 0.f;
     v[r] = t;
+  }
+}
+
+// y += old y of the accumulate prepass (EPI_ACC_NOTE).  With a.rmask the sum is zeroed where the
+// ReLU output at (px, co) is <= 0 -- relu_bwd_kernel's rule, applied by the launch that produces
+// the gradient instead of by a pass of its own over it (dg_conv_fwd_acc_relu)
+template <typename T, typename V>
+__device__ __forceinline__ void add_old_y(V& v, const T* yrow, const FwdArgs& a, long long px, int co) {
+  float o[4];
+  ld4(yrow + co, o);
+  if (a.rmask) {
+    float m[4];
+    ld4((const T*)a.rmask + px * a.ldrm + co, m);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = m[r] > 0.f ? v[r] + o[r] : 0.f;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += o[r];
   }
 }
 
@@ -361,11 +383,7 @@ _Pragma("unroll") \
           const float4 b = *(const float4*)(a.bias + co);
           v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-        }
+        if (a.accumulate) add_old_y(v, yrow, a, px, co);
         epi_affine(v, a, co);
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
@@ -845,12 +863,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
-        }
+        if (a.accumulate) add_old_y(acc[i][j], yrow, a, px, co);
         if constexpr (EPI == 3) {
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           epi_affine(v, a, co);
@@ -1183,8 +1196,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           const int co = cur.co0 + wco + 16 * i + 4 * fc;
-          float o[4];
-          ld4(yrow + co, o);
           if (e3_lds) {
             const f4v b = *(const f4v*)(ebias + co);
             for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
@@ -1192,7 +1203,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
             const f4v b = *(const f4v*)(bbuf + co);
             for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
           }
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+          add_old_y(acc[i][j], yrow, a, px, co);
         }
       }
     }
@@ -1548,8 +1559,6 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           const int co = cur.co0 + wco + 16 * i + 4 * fc;
-          float o[4];
-          ld4(yrow + co, o);
           if (e3_lds) {
             const f4v b = *(const f4v*)(ebias + co);
             for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
@@ -1557,7 +1566,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
             const f4v b = *(const f4v*)(bbuf + co);
             for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
           }
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
+          add_old_y(acc[i][j], yrow, a, px, co);
         }
       }
     }
@@ -1760,12 +1769,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
-        }
+        if (a.accumulate) add_old_y(acc[i][j], yrow, a, px, co);
         if constexpr (EPI == 3) {
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           epi_affine(v, a, co);
@@ -1950,12 +1954,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
-        }
+        if (a.accumulate) add_old_y(acc[i][j], yrow, a, px, co);
         if constexpr (EPI == 3) {
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           epi_affine(v, a, co);
@@ -2132,12 +2131,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
 #pragma unroll
           for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += o[r];
-        }
+        if (a.accumulate) add_old_y(acc[i][j], yrow, a, px, co);
         if constexpr (EPI == 3) {
           float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
           epi_affine(v, a, co);
@@ -2442,11 +2436,7 @@ __device__ __forceinline__ void tap3_epilogue(f4v (&acc)[TI][TJ], const FwdArgs&
           const f4v b = PADK ? *(const f4v*)(a.bias + co) : bv[i];
           v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
         }
-        if (a.accumulate) {
-          float o[4];
-          ld4(yrow + co, o);
-          v[0] += o[0]; v[1] += o[1]; v[2] += o[2]; v[3] += o[3];
-        }
+        if (a.accumulate) add_old_y(v, yrow, a, px, co);
         epi_affine(v, a, co);
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[i][j][r] = v[r];
@@ -4917,6 +4907,36 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
       a.ksplit = ks;
       a.kpart = (float*)workspace;
     }
+  }
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : dtype == DG_F16 ? launch_fwd<f16>(a, st) : launch_fwd<float>(a, st);
+}
+
+// y = (relu_out > 0) ? conv(x, w) + y : 0 -- the accumulating dgrad of a 1x1 conv whose input is
+// the ReLU output relu_out (a bottleneck's conv1 on the previous block's output), with that ReLU's
+// backward folded into the epilogue (dg_conv_fwd_ex with accumulate = 1 followed by dg_relu_bwd
+// on y, bit for bit, without the extra pass over y).  w: the flipped filter (dg_flip_weight).
+// DG_ERR_UNSUPPORTED (nothing launched) for the split-K shapes dg_conv_fwd_ex would split with
+// this workspace: the caller runs the two launches.
+extern "C" int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
+                                    const void* w, int Cout, const void* relu_out, int64_t ldr, void* y,
+                                    int64_t ldy, void* workspace, int64_t ws_bytes, void* stream) {
+  DG_REQUIRE(x && w && y && relu_out && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0);
+  DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
+  DG_SUPPORTED(Cout % 64 == 0 && (DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0)));
+  DG_REQUIRE(ldx >= C && ldy >= Cout && ldr >= Cout && ldx % 8 == 0 && ldy % 4 == 0 && ldr % 4 == 0);
+  DG_SUPPORTED((long long)128 * ldx * 4 < (1ll << 31));
+  FwdArgs a{(const char*)x, ldx, N, H, W, C, (const char*)w, Cout, 1, 1, 0, nullptr, (char*)y, ldy, 1, nullptr};
+  a.rmask = (const char*)relu_out;
+  a.ldrm = ldr;
+  if (dtype == DG_F32) {
+    a.wsplit = (char*)workspace;
+    a.wsplit_bytes = workspace ? ws_bytes : 0;
+  }
+  if (DG_IS16(dtype) && workspace && fwd_has_epi_stats(C, Cout, ldx, 1, 1)) {
+    const long long M = (long long)N * H * W;
+    const int ks = fwd_ksplit(M, Cout, C, 1, 1);
+    if (ks > 1 && ws_bytes >= (int64_t)ks * M * Cout * 4) return DG_ERR_UNSUPPORTED;
   }
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : dtype == DG_F16 ? launch_fwd<f16>(a, st) : launch_fwd<float>(a, st);

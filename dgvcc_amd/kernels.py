@@ -149,6 +149,25 @@ def conv_dgrad(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, acc
     conv_fwd(dy, wflip, C, R, R - 1 - pad, dx, accumulate=accumulate, kind="dgrad")
 
 
+def conv_dgrad_acc_relu(dy: Act, wp: torch.Tensor, C: int, dx: Act, relu_out: Act) -> bool:
+    """dx = (relu_out > 0) ? dx + dgrad_1x1(dy) : 0 in one launch (the ReLU backward of relu_out
+    folded into the accumulating dgrad's epilogue, dg_conv_fwd_acc_relu).  False (nothing
+    launched) for the shapes that launch does not serve: the caller runs conv_dgrad + relu_bwd."""
+    wflip = flip_weight(wp, dy.C, C, 1)
+    ws, work = _fwd_workspace(dy, C, 1)
+    flops = 2.0 * dy.M * dy.C * C
+    nbytes = dy.buf.element_size() * (dy.M * dy.C + wflip.numel() + 3 * dy.M * C)
+    res = []
+    _timed("dgrad", flops, lambda: res.append(lib_call_status(
+        "dg_conv_fwd_acc_relu", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W, dy.C, ptr(wflip), C, relu_out.ptr,
+        relu_out.ld, dx.ptr, dx.ld, ptr(work), ws, stream())), nbytes)
+    if res[0] == -2:
+        return False
+    if res[0] != 0:
+        raise DGError(f"dg_conv_fwd_acc_relu failed with status {res[0]}")
+    return True
+
+
 # Opt-in: measured slower on MI355X (the pipelined conv runs one 128-KB-LDS block per CU, so
 # the epilogue's z loads and reductions are fully exposed: +1.3 ms of dgrad per step against
 # the 0.75 ms partial pass it removes at 768x1024, A/B in DESIGN.md).

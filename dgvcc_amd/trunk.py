@@ -27,6 +27,9 @@ from .engine import ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_c
 from .kernels import Act
 
 STEM_KPAD = 192  # 7*7*3 = 147 taps, padded to a multiple of 64 for the MFMA K loop
+# DGVCC_TRUNK_RELU_FOLD=0: the block output ReLU's backward as its own pass (relu_bwd) instead of
+# in the next block's conv1 dgrad epilogue (A/B; bit-identical either way)
+_RELU_FOLD = __import__("os").environ.get("DGVCC_TRUNK_RELU_FOLD", "1") != "0"
 
 
 class TConv:
@@ -54,17 +57,28 @@ class TConv:
         else:
             K.conv2d_fwd(x, wp, self.Cout, self.R, self.stride, self.pad, y)
 
-    def bwd(self, x: Act, dz: Act, wp, dx: Act | None, accumulate=False) -> torch.Tensor:
+    def bwd(self, x: Act, dz: Act, wp, dx: Act | None, accumulate=False, relu_out: Act | None = None) -> torch.Tensor:
+        """relu_out (with accumulate): dx also gets the backward of the ReLU whose output is
+        relu_out, dx = (relu_out > 0) ? dx + dgrad : 0 -- in the dgrad epilogue for the 1x1
+        convs (dg_conv_fwd_acc_relu), else a relu_bwd pass after the dgrad."""
         dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
         if self.same:
             K.conv_wgrad(x, dz, self.R, self.pad, dw)
-            if dx is not None:
-                K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, dx, accumulate=accumulate)
         else:
             K.conv2d_wgrad(x, dz, self.R, self.stride, self.pad, dw)
-            if dx is not None:
-                wt = K.pack_weight_t(wp, self.Cout, self.Cin, self.R, self.R)
-                K.conv2d_dgrad(dz, wt, self.R, self.stride, self.pad, dx, accumulate=accumulate)
+        if dx is None:
+            return dw
+        if relu_out is not None:
+            assert accumulate
+            if self.same and self.R == 1 and K.conv_dgrad_acc_relu(dz, wp, self.Cin, dx, relu_out):
+                return dw
+        if self.same:
+            K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, dx, accumulate=accumulate)
+        else:
+            wt = K.pack_weight_t(wp, self.Cout, self.Cin, self.R, self.R)
+            K.conv2d_dgrad(dz, wt, self.R, self.stride, self.pad, dx, accumulate=accumulate)
+        if relu_out is not None:
+            K.relu_bwd(dx, relu_out, dx)
         return dw
 
 
@@ -265,20 +279,25 @@ class Block:
                               a2=a2, z3=z3, st3=st3, zd=zd, std=std, s=s, sst=sst, w=w, out=out)
         return out
 
-    def backward(self, tape: dict, g_out: Act, grads: dict, g_w=None) -> Act:
+    def backward(self, tape: dict, g_out: Act, grads: dict, g_w=None, g_masked=False, relu_x=False) -> Act:
         """g_out: dL/d(block output) (consumed / overwritten).  g_w(gt) -> None: adds the
-        whitening-loss gradient dL/dw into gt (ISW).  Returns dL/dx."""
+        whitening-loss gradient dL/dw into gt (ISW).  Returns dL/dx.
+        g_masked: g_out already carries the output ReLU's backward (the next block folded it
+        into its conv1 dgrad); relu_x: x is the previous block's ReLU output, whose backward
+        this block folds into its conv1 dgrad epilogue (the returned dL/dx is then masked)."""
         t = tape.pop(self)
         x, out = t["x"], t["out"]
         wp1, wp2, wp3, wpd = t["wp"]
         dev, dt = x.buf.device, x.buf.dtype
         if self.post is None:
-            K.relu_bwd(g_out, out, g_out)
+            if not g_masked:
+                K.relu_bwd(g_out, out, g_out)
             g_s = g_out
         else:
             s = t["s"]
             if self.post.kind == "iw":
-                K.relu_bwd(g_out, out, g_out)
+                if not g_masked:
+                    K.relu_bwd(g_out, out, g_out)
                 if g_w is not None:
                     g_w(g_out)
                 g_s = Act(torch.empty_like(s.buf))
@@ -303,7 +322,10 @@ class Block:
         _acc(grads, self.c2.conv.weight, self.c2.bwd(t["a1"], g_z2, wp2, g_a1))
         g_z1 = Act(torch.empty_like(t["z1"].buf))
         bn_backward(self.bn1, g_a1, t["z1"], t["st1"], ACT_RELU, g_z1, grads)
-        _acc(grads, self.c1.conv.weight, self.c1.bwd(x, g_z1, wp1, gx, accumulate=True))
+        if relu_x:
+            _acc(grads, self.c1.conv.weight, self.c1.bwd(x, g_z1, wp1, gx, accumulate=True, relu_out=x))
+        else:
+            _acc(grads, self.c1.conv.weight, self.c1.bwd(x, g_z1, wp1, gx, accumulate=True))
         return gx
 
 
@@ -421,11 +443,18 @@ class CounterPlan:
             ws, frs, masks = iw
             for w_, fr, (mask, ns) in zip(ws, frs, masks):
                 hooks[id(w_)] = _iw_grad_hook(w_, fr, mask, ns, 1.0 / len(ws), g_wt)
-        for blk in reversed(self.blocks):
+        masked = False
+        for k in reversed(range(len(self.blocks))):
+            blk = self.blocks[k]
             wkey = None
             if blk.post is not None and blk.post.kind == "iw":
                 wkey = id(tape[blk]["w"])
-            g_x = blk.backward(tape, g_x, grads, hooks.get(wkey))
+            # the previous block's output ReLU backward folded into this block's conv1 dgrad
+            # (its x is that output); IN-post blocks recompute the mask in their IN backward
+            prev = self.blocks[k - 1] if k > 0 else None
+            fold = _RELU_FOLD and prev is not None and (prev.post is None or prev.post.kind == "iw")
+            g_x = blk.backward(tape, g_x, grads, hooks.get(wkey), g_masked=masked, relu_x=fold)
+            masked = fold
         # maxpool, stem
         y0 = s["y0"]
         g_y0 = Act(torch.empty_like(y0.buf))

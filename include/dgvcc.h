@@ -98,6 +98,16 @@ int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, i
 int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                    int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                    int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream);
+/* y = (relu_out > 0) ? conv1x1(x, w) + y : 0: the accumulating dgrad of a bottleneck's conv1 (w
+ * flipped, dg_flip_weight) whose input relu_out is the previous block's ReLU output
+ * (models/SW/backbones/resnet.py:77 Bottleneck.forward's final relu, autograd's ReLU backward),
+ * so that ReLU's backward needs no pass of its own; equals dg_conv_fwd_ex(accumulate = 1)
+ * followed by dg_relu_bwd on y bit for bit.  relu_out: y's dtype and rows (ldr elements).
+ * Workspace as dg_conv_fwd_ex; DG_ERR_UNSUPPORTED (nothing launched) for the 16-bit shapes that
+ * launch splits over K with this workspace. */
+int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                         int Cout, const void* relu_out, int64_t ldr, void* y, int64_t ldy, void* workspace,
+                         int64_t ws_bytes, void* stream);
 /* Eval-mode Conv + BatchNorm(running stats) [+ ReLU]: y = act((conv(x) + bias) * scale + shift)
  * with scale = gamma/sqrt(running_var+eps), shift = beta - running_mean*scale applied in the conv
  * epilogue (z never stored);

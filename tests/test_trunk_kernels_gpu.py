@@ -350,3 +350,41 @@ def test_sync_switch_whiten_two_ranks(dev):
                         os.path.join(here, "sync_sw_worker.py")],
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and r.stdout.count("OK") == 2, (r.stdout[-2000:], r.stderr[-3000:])
+
+
+ACC_RELU_CASES = [
+    # N, H, W, planes (dgrad input channels), C (dgrad output channels = the ReLU output's)
+    (2, 48, 64, 64, 256),    # layer1 conv1 dgrad
+    (2, 24, 32, 128, 512),   # layer2
+    (2, 12, 16, 256, 1024),  # layer3 (16-bit split-K grid: the two-launch fallback)
+    (4, 96, 128, 64, 256),   # persistent grids
+    (2, 48, 64, 256, 64),    # 64 output channels
+    (1, 5, 7, 64, 128),      # ragged pixel tail
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("case", ACC_RELU_CASES)
+def test_conv_dgrad_acc_relu(dev, dtype, case):
+    """dg_conv_fwd_acc_relu == accumulating 1x1 dgrad followed by relu_bwd, bit for bit (the
+    mask applied to the same rounded sum), including exact zeros in the ReLU output."""
+    K = _k()
+    N, H, W, Cp, C = case
+    g = torch.Generator().manual_seed(11)
+    dy = K.Act(torch.randn(N, H, W, Cp, generator=g).to(dev, dtype))
+    wp = K.pack_weight((torch.randn(Cp, C, 1, 1, generator=g) / Cp ** 0.5).to(dev), dtype)
+    ro = K.Act(torch.relu(torch.randn(N, H, W, C, generator=g)).to(dev, dtype))
+    base = torch.randn(N, H, W, C, generator=g).to(dev, dtype)
+    d1 = K.Act(base.clone())
+    K.conv_dgrad(dy, wp, C, 1, 0, d1, accumulate=True)
+    K.relu_bwd(d1, ro, d1)
+    d2 = K.Act(base.clone())
+    fused = K.conv_dgrad_acc_relu(dy, wp, C, d2, ro)
+    if not fused:
+        K.conv_dgrad(dy, wp, C, 1, 0, d2, accumulate=True)
+        K.relu_bwd(d2, ro, d2)
+    torch.cuda.synchronize()
+    if dtype == torch.float32:
+        assert fused
+    assert (d2.buf[ro.buf <= 0] == 0).all()
+    assert torch.equal(d1.buf, d2.buf)

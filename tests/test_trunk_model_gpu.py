@@ -254,3 +254,40 @@ def test_counter_bf16_close(dev, kind):
 
     ours, torch16 = err(out), err(t16)
     assert ours[0] <= 3 * torch16[0] + 1e-3 and ours[1] <= 3 * torch16[1] + 1e-2, (ours, torch16)
+
+
+def _train_grads(model, kind, sd0, batch, dev):
+    img1, img2, (_, dmaps, _) = batch
+    model.load_state_dict(sd0)
+    model.zero_grad(set_to_none=True)
+    if kind == "isw":
+        model.eval()
+        with torch.no_grad():
+            model([img1.to(dev), img2.to(dev)], cal_covstat=True)
+        model.set_mask_matrix()
+        model.train()
+        losses = model(img1.to(dev), gts=dmaps.to(dev), apply_wtloss=True)
+        (losses[0] + 0.6 * losses[1]).sum().backward()
+    else:
+        from dgvcc_amd.losses import mse_loss
+        model.train()
+        mse_loss(model(img1.to(dev)), dmaps.to(dev), 1000.0).backward()
+    torch.cuda.synchronize()
+    return {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("kind", ["ibn", "sw", "isw"])
+def test_relu_fold_bit_identical(dev, kind, precision, monkeypatch):
+    """The block-output ReLU backward folded into the next block's conv1 dgrad epilogue
+    (dg_conv_fwd_acc_relu, trunk._RELU_FOLD) leaves every parameter gradient bit-identical to
+    the separate relu_bwd pass (1x1 dgrad + accumulate, then the mask: the same rounding)."""
+    from dgvcc_amd import trunk
+    model, sd0, batch = _setup(kind, dev, B=2, H=96, W=128, precision=precision)
+    monkeypatch.setattr(trunk, "_RELU_FOLD", False)
+    ref = _train_grads(model, kind, sd0, batch, dev)
+    monkeypatch.setattr(trunk, "_RELU_FOLD", True)
+    got = _train_grads(model, kind, sd0, batch, dev)
+    assert ref.keys() == got.keys() and len(ref) > 100
+    bad = [k for k in ref if not torch.equal(ref[k], got[k])]
+    assert not bad, bad[:5]
