@@ -4754,6 +4754,56 @@ __global__ void im2col_c3_ex_kernel(const float* __restrict__ img, int N, int H,
   }
 }
 
+// LDS-staged form of the same im2col: a block writes I2C_QB output pixels of one output row
+// (n, p, q0 ..): the 3*R input row segments they read are staged in LDS with coalesced loads
+// (zeros outside the image), then each lane writes 16-byte chunks of the Kpad-wide rows from a
+// per-k LDS offset table.  The one-thread-per-chunk gather above issues one scattered 4-byte
+// global load (and the k -> (r, s, c) divisions) per element: 2.4 TB/s of writes (f32), 1.4 (bf16)
+constexpr int I2C_QB = 64, I2C_LDS = 4096, I2C_KMAX = 256;
+static bool im2col_lds_ok(int R, int S, int stride, int Kpad) {
+  const char* e = getenv("DGVCC_IM2COL_LDS");  // =0: the gather kernel (A/B, read per launch)
+  return !(e && e[0] == '0') && 3 * R * ((I2C_QB - 1) * stride + S) <= I2C_LDS && Kpad <= I2C_KMAX;
+}
+template <typename T>
+__global__ __launch_bounds__(256) void im2col_c3_lds_kernel(const float* __restrict__ img, int N, int H, int W, int R,
+                                                            int S, int stride, int pad, int P, int Q, int Kpad,
+                                                            T* __restrict__ out) {
+  __shared__ float seg[I2C_LDS];
+  __shared__ int koff[I2C_KMAX];
+  constexpr int E = 16 / (int)sizeof(T);
+  const int tid = threadIdx.x, qb = (Q + I2C_QB - 1) / I2C_QB;
+  const int b = blockIdx.x, n = b / (P * qb), rem = b - n * P * qb, p = rem / qb, q0 = (rem - p * qb) * I2C_QB;
+  const int Wl = (I2C_QB - 1) * stride + S, RS3 = R * S * 3;
+  const int h0 = p * stride - pad, w0 = q0 * stride - pad;
+  const float* base = img + (long long)n * 3 * H * W;
+  for (int i = tid; i < 3 * R * Wl; i += 256) {
+    const int row = i / Wl, j = i - row * Wl, c = row / R, r = row - c * R;
+    const int h = h0 + r, w = w0 + j;
+    seg[i] = ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) ? base[((long long)c * H + h) * W + w] : 0.f;
+  }
+  for (int k = tid; k < Kpad; k += 256) {
+    int o = -1;
+    if (k < RS3) {
+      const int rs = k / 3, c = k - 3 * rs, r = rs / S, s2 = rs - r * S;
+      o = (c * R + r) * Wl + s2;
+    }
+    koff[k] = o;
+  }
+  __syncthreads();
+  const int nq = min(I2C_QB, Q - q0), nch = Kpad / E;
+  T* orow = out + ((long long)(n * P + p) * Q + q0) * Kpad;
+  for (int i = tid; i < nq * nch; i += 256) {
+    const int qi = i / nch, chk = i - qi * nch;
+    float v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+      const int o = koff[chk * E + e];
+      v[e] = o >= 0 ? seg[o + qi * stride] : 0.f;
+    }
+    stv(orow + (long long)qi * Kpad + chk * E, v);
+  }
+}
+
 __global__ void unpack_c3_ex_kernel(const float* __restrict__ dwcol, int Cout, int R, int S, int Kpad,
                                     float* __restrict__ dw, int acc) {
   const int total = Cout * 3 * R * S;
@@ -5232,7 +5282,18 @@ extern "C" int dg_im2col_c3(int dtype, const float* img, int N, int H, int W, in
   DG_SUPPORTED(Kpad % 8 == 0 && (long long)N * P * Q < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)N * P * Q * (Kpad / (DG_IS16(dtype) ? 8 : 4));
-  if (dtype == DG_BF16)
+  if (im2col_lds_ok(R, S, stride, Kpad) && (dtype == DG_BF16 || dtype == DG_F16 || dtype == DG_F32)) {
+    const dim3 g((unsigned)((long long)N * P * dg_cdiv(Q, I2C_QB)));
+    if (dtype == DG_BF16)
+      hipLaunchKernelGGL(im2col_c3_lds_kernel<bf16>, g, dim3(256), 0, st, img, N, H, W, R, S, stride, pad, P, Q, Kpad,
+                         (bf16*)out);
+    else if (dtype == DG_F16)
+      hipLaunchKernelGGL(im2col_c3_lds_kernel<f16>, g, dim3(256), 0, st, img, N, H, W, R, S, stride, pad, P, Q, Kpad,
+                         (f16*)out);
+    else
+      hipLaunchKernelGGL(im2col_c3_lds_kernel<float>, g, dim3(256), 0, st, img, N, H, W, R, S, stride, pad, P, Q, Kpad,
+                         (float*)out);
+  } else if (dtype == DG_BF16)
     hipLaunchKernelGGL(im2col_c3_ex_kernel<bf16>, dim3(grid_for(total, 256, 1 << 20)), dim3(256), 0, st, img, N, H, W,
                        R, S, stride, pad, P, Q, Kpad, (bf16*)out);
   else if (dtype == DG_F16)

@@ -388,3 +388,20 @@ def test_conv_dgrad_acc_relu(dev, dtype, case):
         assert fused
     assert (d2.buf[ro.buf <= 0] == 0).all()
     assert torch.equal(d1.buf, d2.buf)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(2, 67, 131, 7, 2, 3, 192), (1, 33, 200, 3, 1, 1, 32), (3, 16, 16, 5, 2, 2, 80),
+                                   (1, 9, 260, 7, 2, 3, 152)])
+def test_im2col_lds_matches_gather(dev, dtype, shape, monkeypatch):
+    """The LDS-staged stem im2col (one block per 64 output pixels of a row) writes exactly the
+    one-thread-per-chunk gather kernel's rows: ragged row tails, padding on every edge, zero K tail."""
+    K = _k()
+    N, H, W, R, s, p, kp = shape
+    img = torch.randn(N, 3, H, W, generator=torch.Generator().manual_seed(5)).to(dev)
+    monkeypatch.setenv("DGVCC_IM2COL_LDS", "0")
+    ref = K.im2col_c3_general(img, dtype, R, s, p, kp).clone()
+    monkeypatch.setenv("DGVCC_IM2COL_LDS", "1")
+    got = K.im2col_c3_general(img, dtype, R, s, p, kp)
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got)
