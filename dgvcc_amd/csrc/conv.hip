@@ -58,7 +58,13 @@ struct FwdArgs {
   // the ReLU output, same dtype / rows as y; the accumulated value is zeroed where it is <= 0
   const char* rmask = nullptr;
   long long ldrm = 0;
+  // 16-bit persistent forward: 16-byte epilogue stores (lane pairs exchange halves with
+  // v_permlane16_swap); set by launch_fwd where y's rows are 16-byte aligned (DGVCC_PERS_WST)
+  int wide_st = 0;
 };
+template <typename T> __device__ __forceinline__ unsigned pack2(float lo, float hi);
+template <> __device__ __forceinline__ unsigned pack2<bf16>(float lo, float hi) { return pack_bf2(lo, hi); }
+template <> __device__ __forceinline__ unsigned pack2<f16>(float lo, float hi) { return pack_h2(lo, hi); }
 
 // EPI_ACC_NOTE -- conv epilogues: y += old y (accumulate) runs as a pass of its own ahead of the
 // stores, acc = (acc + bias) + y_old with the loads issued together, and the store loop adds the
@@ -938,7 +944,7 @@ __device__ __forceinline__ bool tapmask_ok(const TapMask<BI>& t, int i, unsigned
 // WIDE (16-bit, BN = 128): 384-pixel tiles with the 8 waves all on pixels, each 128 channels x 48
 // pixels (the 256-channel kernel's per-wave filter reuse; 1.5x the MFMAs per barrier of the 2 x 4
 // layout of 64 x 64 wave tiles), two stages of (16 + 48) KB (DGVCC_PERS_WIDE=0: the 2 x 4 layout).
-template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0, int INC = 1, int WIDE = 0>
+template <int BN, int STG, int EPI = 0, typename T = bf16, int SPL = 0, int INC = 1, int WIDE = 0, int WST = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
   static_assert(!WIDE || (BN == 128 && SPL == 0 && STG == 2), "WIDE: the 16-bit 128-channel kernel");
   constexpr int PB = WIDE ? 384 : PBM;   // pixels per tile
@@ -1213,6 +1219,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
       valid[j] = px < M;
       if (px >= M) continue;
       T* yrow = y + (long long)px * a.ldy;
+      unsigned pk[2];  // wide stores: this lane's packed group i (even) until group i + 1 is ready
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int co = cur.co0 + wco + 16 * i + 4 * fc;
@@ -1238,7 +1245,27 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pers_kernel(FwdArgs a) {
             epi_affine(v, a, co);
           }
         }
-        st4(yrow + co, v);
+        bool stored = false;
+        if constexpr (WST && Is16<T>::value && TI % 2 == 0) {
+          // Lane (fr, fc) holds channels 16i + 4fc .. +3 of pixel fr.  v_permlane16_swap of the
+          // packed groups i (vdst) and i + 1 (src) swaps rows 1 / 3 of vdst with rows 0 / 2 of src,
+          // so fc = 0 / 2 end with channels 16i + 8(fc/2) .. +7 and fc = 1 / 3 with the same of
+          // group i + 1: one 16-byte store per lane per group pair (the lane pairs share fr, so
+          // share px and the bounds check), 16 rows x 64 contiguous bytes per instruction
+          {
+            stored = true;
+            if (i % 2 == 0) {
+              pk[0] = pack2<T>(v[0], v[1]);
+              pk[1] = pack2<T>(v[2], v[3]);
+            } else {
+              const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0], pack2<T>(v[0], v[1]), false, false);
+              const auto r1 = __builtin_amdgcn_permlane16_swap(pk[1], pack2<T>(v[2], v[3]), false, false);
+              *(u4v*)(yrow + cur.co0 + wco + 16 * (i - 1) + 8 * (fc >> 1) + 16 * (fc & 1)) =
+                  u4v{r0[0], r1[0], r0[1], r1[1]};
+            }
+          }
+        }
+        if (!stored) st4(yrow + co, v);
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);
       }
@@ -3053,10 +3080,21 @@ static bool pers16_wide(const FwdArgs& a) {
   return (double)dg_cdiv(tw, G) * 384 * 128 * 1.1 < (double)dg_cdiv(t256, G) * 256 * 256;
 }
 
+// DGVCC_PERS_WST=0: the 8-byte epilogue stores; 1: 16-byte stores on the 1-2-K-step launches only;
+// default 2: on every 16-bit persistent launch with a WST instantiation (256-channel and 384 x 128
+// tiles; bf16 final step +1.9%, 1x1 64 -> 256 convs 1.34x; read per launch: A/B)
+static int pers_wst() {
+  const char* e = getenv("DGVCC_PERS_WST");
+  return e ? e[0] - '0' : 2;
+}
 template <typename T>
 int launch_fwd(const FwdArgs& a0, hipStream_t st) {
   FwdArgs a = a0;
   a.korder = conv_korder();
+  // 16-byte epilogue stores: a template variant (WST = 1) of the persistent kernel, not a run-time
+  // branch -- both store forms in one instantiation pushed the 256-channel kernel past 256 VGPRs
+  a.wide_st = Is16<T>::value && pers_wst() > 0 && a.ldy % 8 == 0 && ((uintptr_t)a.y & 15) == 0 &&
+              (pers_wst() == 2 || a.R * a.S * (a.C / 64) <= 2);
   return launch_fwd_impl<T>(a, st);
 }
 
@@ -3114,19 +3152,22 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 3, T>), dim3(g), dim3(512), 0, st, a);
         } else if (bn == 128 && pers16_wide(a)) {
           const unsigned gw = (unsigned)std::min<long long>((long long)dg_cdiv(M, 384) * (a.Cout / 128), persist_grid());
-          hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1>), dim3(gw), dim3(512), 0, st, a);
+          if (a.wide_st) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1, 1>), dim3(gw), dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1>), dim3(gw), dim3(512), 0, st, a);
         } else {
           if (!pers_inc()) {  // A/B: per-K-step recomputed DMA addressing
             if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
             else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
             else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
-          } else if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
+          } else if (bn == 256 && a.wide_st) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T, 0, 1, 0, 1>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
           else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
         }
       } else if (epi == 0 && pers16_wide(a)) {  // small 256-channel grids on 384 x 128 persistent tiles
         const unsigned gw = (unsigned)std::min<long long>((long long)dg_cdiv(M, 384) * (a.Cout / 128), persist_grid());
-        hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1>), dim3(gw), dim3(512), 0, st, a);
+        if (a.wide_st) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1, 1>), dim3(gw), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 2, 0, T, 0, 1, 1>), dim3(gw), dim3(512), 0, st, a);
       } else if (a.Cout % 256 == 0 && pipe_wide()) PIPE_LAUNCH(256, 2, np * (a.Cout / 256));
       else if (a.Cout % 128 == 0) PIPE_LAUNCH(128, 3, np * (a.Cout / 128));
       else PIPE_LAUNCH(64, 3, np * (a.Cout / 64));

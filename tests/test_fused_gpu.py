@@ -655,3 +655,30 @@ def test_tanh_fwd_bwd(dev):
     torch.tanh(xd).backward(gy.double())
     assert relerr(Y, torch.tanh(x.double())) < 1e-6
     assert relerr(GX, xd.grad) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W,C,Cout,acc,off", [(4, 96, 128, 64, 256, False, 0), (2, 48, 64, 128, 512, True, 0),
+                                                  (2, 24, 32, 64, 256, False, 0), (16, 48, 64, 64, 256, False, 0),
+                                                  (2, 37, 29, 64, 256, True, 0), (4, 96, 128, 64, 256, False, 4)])
+def test_persistent_wide_stores(dev, monkeypatch, dtype, N, H, W, C, Cout, acc, off):
+    """16-byte epilogue stores of the short-K 16-bit persistent forward (lane pairs exchange
+    channel halves with v_permlane16_swap, DGVCC_PERS_WST) against the 8-byte stores:
+    bit-identical outputs, accumulate and ragged pixel tails included; a y slice that is only
+    8-byte aligned (off = 4 channels) takes the 8-byte stores."""
+    K = _k()
+    g = torch.Generator().manual_seed(23)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, dtype)
+    wp = K.pack_weight((torch.randn(Cout, C, 1, 1, generator=g) / C ** 0.5).to(dev), dtype)
+    b = torch.randn(Cout, generator=g).to(dev)
+    base = torch.randn(N, H, W, Cout + 8, generator=g).to(dev, dtype)
+    outs = []
+    for wst in ("0", "1"):
+        monkeypatch.setenv("DGVCC_PERS_WST", wst)
+        yb = base.clone()
+        y = K.Act(yb, off, Cout)
+        K.conv_fwd(K.Act(x), wp, Cout, 1, 0, y, bias=None if acc else b, accumulate=acc)
+        outs.append(yb)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    assert not torch.equal(outs[0], base)
