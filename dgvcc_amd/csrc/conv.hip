@@ -3081,11 +3081,12 @@ static bool pers16_wide(const FwdArgs& a) {
 }
 
 // DGVCC_PERS_WST=0: the 8-byte epilogue stores; 1: 16-byte stores on the 1-2-K-step launches only;
-// default 2: on every 16-bit persistent launch with a WST instantiation (256-channel and 384 x 128
-// tiles; bf16 final step +1.9%, 1x1 64 -> 256 convs 1.34x; read per launch: A/B)
+// 2: every 256-channel / 384 x 128 16-bit persistent launch (bf16 final step +1.9%, 1x1 64 -> 256
+// convs 1.34x); default 3: the 128- / 64-channel 3-stage ones too (SW bf16 step -0.7%); read per
+// launch: A/B
 static int pers_wst() {
   const char* e = getenv("DGVCC_PERS_WST");
-  return e ? e[0] - '0' : 2;
+  return e ? e[0] - '0' : 3;
 }
 template <typename T>
 int launch_fwd(const FwdArgs& a0, hipStream_t st) {
@@ -3094,7 +3095,7 @@ int launch_fwd(const FwdArgs& a0, hipStream_t st) {
   // 16-byte epilogue stores: a template variant (WST = 1) of the persistent kernel, not a run-time
   // branch -- both store forms in one instantiation pushed the 256-channel kernel past 256 VGPRs
   a.wide_st = Is16<T>::value && pers_wst() > 0 && a.ldy % 8 == 0 && ((uintptr_t)a.y & 15) == 0 &&
-              (pers_wst() == 2 || a.R * a.S * (a.C / 64) <= 2);
+              (pers_wst() >= 2 || a.R * a.S * (a.C / 64) <= 2);
   return launch_fwd_impl<T>(a, st);
 }
 
@@ -3161,7 +3162,11 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
             else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, 0, 0>), dim3(g), dim3(512), 0, st, a);
           } else if (bn == 256 && a.wide_st) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T, 0, 1, 0, 1>), dim3(g), dim3(512), 0, st, a);
           else if (bn == 256) hipLaunchKernelGGL((conv_fwd_pers_kernel<256, 2, 0, T>), dim3(g), dim3(512), 0, st, a);
+          else if (bn == 128 && a.wide_st && pers_wst() == 3)
+            hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T, 0, 1, 0, 1>), dim3(g), dim3(512), 0, st, a);
           else if (bn == 128) hipLaunchKernelGGL((conv_fwd_pers_kernel<128, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
+          else if (a.wide_st && pers_wst() == 3)
+            hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T, 0, 1, 0, 1>), dim3(g), dim3(512), 0, st, a);
           else hipLaunchKernelGGL((conv_fwd_pers_kernel<64, 3, 0, T>), dim3(g), dim3(512), 0, st, a);
         }
       } else if (epi == 0 && pers16_wide(a)) {  // small 256-channel grids on 384 x 128 persistent tiles
