@@ -58,7 +58,7 @@ struct FwdArgs {
   // the ReLU output, same dtype / rows as y; the accumulated value is zeroed where it is <= 0
   const char* rmask = nullptr;
   long long ldrm = 0;
-  // 16-bit persistent forward: 16-byte epilogue stores (lane pairs exchange halves with
+  // 16-bit persistent / pipe forward: 16-byte epilogue stores (lane pairs exchange halves with
   // v_permlane16_swap); set by launch_fwd where y's rows are 16-byte aligned (DGVCC_PERS_WST)
   int wide_st = 0;
 };
@@ -885,6 +885,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
     valid[j] = px < M;
     if (px >= M) continue;
     T* yrow = y + (long long)px * a.ldy;
+    unsigned pk[2];
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int co = co0 + wco + 16 * i + 4 * fc;
@@ -893,7 +894,21 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_pipe_kernel(FwdArgs a) {
         const f4v b = bv[i];
         v[0] += b[0]; v[1] += b[1]; v[2] += b[2]; v[3] += b[3];
       }
-      st4(yrow + co, v);
+      bool stored = false;
+      if constexpr (TI % 2 == 0 && EPI == 0) {
+        if (a.wide_st & 2) {  // 16-byte stores as in conv_fwd_pers_kernel's WST epilogue
+          stored = true;
+          if (i % 2 == 0) {
+            pk[0] = pack2<T>(v[0], v[1]);
+            pk[1] = pack2<T>(v[2], v[3]);
+          } else {
+            const auto r0 = __builtin_amdgcn_permlane16_swap(pk[0], pack2<T>(v[0], v[1]), false, false);
+            const auto r1 = __builtin_amdgcn_permlane16_swap(pk[1], pack2<T>(v[2], v[3]), false, false);
+            *(u4v*)(yrow + co0 + wco + 16 * (i - 1) + 8 * (fc >> 1) + 16 * (fc & 1)) = u4v{r0[0], r1[0], r0[1], r1[1]};
+          }
+        }
+      }
+      if (!stored) st4(yrow + co, v);
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[i][j][r] = round_to<T>(v[r]);  // the stored value, for the statistics
     }
@@ -3094,8 +3109,11 @@ int launch_fwd(const FwdArgs& a0, hipStream_t st) {
   a.korder = conv_korder();
   // 16-byte epilogue stores: a template variant (WST = 1) of the persistent kernel, not a run-time
   // branch -- both store forms in one instantiation pushed the 256-channel kernel past 256 VGPRs
+  // (bit 0: the persistent kernels' WST instantiations; bit 1: the pipe kernel's run-time branch,
+  // DGVCC_PIPE_WST=0 off)
   a.wide_st = Is16<T>::value && pers_wst() > 0 && a.ldy % 8 == 0 && ((uintptr_t)a.y & 15) == 0 &&
               (pers_wst() >= 2 || a.R * a.S * (a.C / 64) <= 2);
+  if (a.wide_st && !(getenv("DGVCC_PIPE_WST") && getenv("DGVCC_PIPE_WST")[0] == '0')) a.wide_st |= 2;
   return launch_fwd_impl<T>(a, st);
 }
 
