@@ -277,6 +277,8 @@ def run_leg(args, precision, dev, world, rank):
         for t in model.state_dict().values():
             dist.broadcast(t, 0)
     opt = AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
+    dp = {"overlap": opt.reducer is not None,
+          "bucket_mb": round(opt.reducer.bucket_bytes / (1 << 20), 3) if opt.reducer is not None else None}
     cwd = os.getcwd()
     os.makedirs("/tmp/dgvcc_bench", exist_ok=True)
     os.chdir("/tmp/dgvcc_bench")
@@ -310,6 +312,8 @@ def run_leg(args, precision, dev, world, rank):
     elapsed = time.perf_counter() - t0
     K.set_conv_timer(None)
     res = {"elapsed": elapsed, "last_loss": last, "mode": mode, "model": type(model).__name__}
+    if world > 1:
+        res["allreduce"] = dict(dp, buckets=len(opt.reducer.buckets) if opt.reducer is not None else 1)
     conv_ms, conv_flops, conv_n, conv_bytes = timer.summary(("fwd", "dgrad"))
     wg_ms, wg_flops, wg_n, _ = timer.summary(("wgrad",))
     enc_kinds = ("fwd", "dgrad", "wgrad", "stem", "stem_wgrad")
@@ -502,7 +506,10 @@ def cpu_baseline(args, seconds):
     from oracle import dg_oracle as O
     from dgvcc_amd.models.models import DGModel_base, DGModel_final
     nproc = os.cpu_count() or 1
-    threads = max(1, min(nproc, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
+    phys = _physical_cores()
+    # the host's physical cores; DGVCC_CPU_THREADS overrides
+    threads = int(os.environ.get("DGVCC_CPU_THREADS", "0") or 0) or phys
+    prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     mode = args.mode if args.mode in ("simple", "final") else "simple"
     tmpl = (DGModel_final(pretrained=False) if mode == "final" else DGModel_base(pretrained=False)).state_dict()
@@ -519,12 +526,36 @@ def cpu_baseline(args, seconds):
         if time.perf_counter() - t0 + t_warm / 2 >= seconds or n >= 8:
             break
     dt = time.perf_counter() - t0
+    torch.set_num_threads(prev)
     frames = n * (2 if mode == "final" else 1)
     return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
-            "host_nproc": nproc, "cpu_model": _cpu_model(),
+            "host_nproc": nproc, "host_physical_cores": phys, "cpu_model": _cpu_model(),
             "sample": f"{n} oracle train steps ({mode} mode, batch 1 = {2 if mode == 'final' else 1} frame(s) "
                       f"of {args.height}x{args.width}, fp32, torch CPU {threads} threads) after 1 warm-up step",
             "parity": parity}
+
+
+def _physical_cores() -> int:
+    """Physical cores this process may run on: distinct (package, core) pairs of /proc/cpuinfo
+    among the CPUs of its affinity mask (SMT siblings counted once)."""
+    try:
+        allowed = os.sched_getaffinity(0)
+    except (AttributeError, OSError):
+        allowed = set(range(os.cpu_count() or 1))
+    cores, cpu, pkg = set(), None, "0"
+    try:
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "processor":
+                cpu, pkg = int(v), "0"
+            elif k == "physical id":
+                pkg = v
+            elif k == "core id" and cpu in allowed:
+                cores.add((pkg, v))
+    except OSError:
+        pass
+    return len(cores) or len(allowed) or 1
 
 
 def _cpu_model() -> str:
@@ -614,11 +645,37 @@ def _density_parity_once(sd, batch, loss_ref, outs_ref, mode, grads=False):
                     num += float(d.norm() ** 2)
                     den += float(g_ref[k].double().norm() ** 2)
                 worst = max(err.items(), key=lambda kv: kv[1])
+                # both against the float64 oracle on the same decisions: the fp32 oracle's own spread
+                # beside the HIP step's (tests/test_model_gpu.py test_step_grads_full_frame criterion)
+                sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+                b64 = (img1.double(), img2.double(), (pts, dmaps.double(), bmaps.double()))
+                _, _, g64, _ = O.train_step(sd64, b64, "final", e_mask_in=em, c_pred_in=cp)
+                e64, e32, n64, n32, d64 = {}, {}, 0.0, 0.0, 0.0
+                for k in err:
+                    mine = dict(model.named_parameters())[k].grad.detach().double().cpu()
+                    r = g64[k].double()
+                    e64[k] = float((mine - r).norm() / r.norm())
+                    e32[k] = float((g_ref[k].double() - r).norm() / r.norm())
+                    n64 += float((mine - r).norm() ** 2)
+                    n32 += float((g_ref[k].double() - r).norm() ** 2)
+                    d64 += float(r.norm() ** 2)
+                w64 = max(e64.items(), key=lambda kv: kv[1])
+                g_hip, g_or = (n64 / d64) ** 0.5, (n32 / d64) ** 0.5
+                ok = all(v <= max(2 * e32[k], 1.5e-2) for k, v in e64.items()) and g_hip <= max(2 * g_or, 1.2e-2)
                 res["grad_parity"] = {"worst_param": worst[0], "worst_normwise_rel": worst[1],
                                       "global_normwise_rel": (num / den) ** 0.5, "params": len(err),
+                                      "vs_float64": {"worst_param": w64[0], "worst_normwise_rel": w64[1],
+                                                     "fp32_oracle_there": e32[w64[0]],
+                                                     "fp32_oracle_worst": max(e32.values()),
+                                                     "global_normwise_rel": g_hip,
+                                                     "fp32_oracle_global": g_or,
+                                                     "within_criterion": bool(ok),
+                                                     "criterion": "per param <= max(2 x fp32 oracle, 1.5e-2); "
+                                                                  "global <= max(2 x fp32 oracle, 1.2e-2)"},
                                       "note": "HIP fp32 step backward against the fp32 oracle's step on the HIP "
                                               "decisions; ReLU / max-pool branches are each side's own, so the "
-                                              "residual is their fp32 spread (tests/test_model_gpu.py E2E_GRAD_TOL)"}
+                                              "residual is their fp32 spread (tests/test_model_gpu.py E2E_GRAD_TOL); "
+                                              "vs_float64: both against the float64 oracle on the same decisions"}
         else:
             d = model(img1.to(dev))
             loss = mse_loss(d, dmaps.to(dev), 1000.0)
@@ -705,6 +762,8 @@ def main():
                            "f32 accumulation" if leg == "fp32" else "v_mfma_f32_16x16x4_f32")
     if "params_in_sync" in r:
         out["params_in_sync"] = r["params_in_sync"]
+    if "allreduce" in r:  # the gradient all-reduce: bucketed and overlapped with the backward
+        out["config"]["allreduce"] = r["allreduce"]
     if leg == "fp32" and not args.no_f32_exact:
         re_ = run_leg(args, "fp32_exact", dev, world, rank)
         out["f32_exact"] = {"value": round(re_["frames"] / re_["elapsed"], 3), "unit": "frames/s", "dtype": "fp32",

@@ -59,6 +59,14 @@ def parse_header(path: str = HEADER) -> dict[str, tuple]:
     return protos
 
 
+def header_abi_version(path: str = HEADER) -> int:
+    """DGVCC_ABI_VERSION as include/dgvcc.h declares it."""
+    m = re.search(r"^#define\s+DGVCC_ABI_VERSION\s+(\d+)", open(path).read(), flags=re.M)
+    if m is None:
+        raise DGError(f"{path}: no DGVCC_ABI_VERSION")
+    return int(m.group(1))
+
+
 _lib = None
 _protos = None
 
@@ -75,6 +83,10 @@ def lib():
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args
+        abi = header_abi_version()
+        if l.dg_version() != abi:
+            raise DGError(f"{LIB_PATH} implements ABI {l.dg_version()}, include/dgvcc.h declares {abi}: "
+                          "rebuild with `python -m dgvcc_amd.build`")
         want = source_hash()
         got = library_hash(l)
         if want is not None and got != want:

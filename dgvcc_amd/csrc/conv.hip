@@ -5004,9 +5004,18 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
     a.wsplit = (char*)workspace;
     a.wsplit_bytes = workspace ? ws_bytes : 0;
   }
-  if (part)
-    DG_SUPPORTED(DG_IS16(dtype) ? fwd_has_epi_stats(C, Cout, ldx, R, S)
-                                : (f32_pers_ok(a) || ((rsplit_ok(a) || psplit_ok(a)) && has_split_room(a))));
+  if (part) {
+    if (DG_IS16(dtype)) {
+      DG_SUPPORTED(fwd_has_epi_stats(C, Cout, ldx, R, S));
+    } else if (psplit_ok(a) || (rsplit_ok(a) && rsplit3w_ok(a))) {
+      // dg_conv_stats_rows_ex reports the pre-split kernels' rows (192/256/384- or 512-pixel tiles):
+      // without room for the planes the launch would fall back to the 256-pixel persistent kernel
+      // and write another row count than the caller allocated
+      DG_SUPPORTED(has_split_room(a));
+    } else {
+      DG_SUPPORTED(f32_pers_ok(a) || (rsplit_ok(a) && has_split_room(a)));
+    }
+  }
   {  // the padded 3-tap kernel (faster, no epilogue statistics) serves this shape: the caller
      // runs dg_conv_fwd + the statistics pass instead
     FwdArgs q = a;

@@ -130,6 +130,12 @@ class OverlapReducer:
         """Take the owned parameters' gradients of one layer; return the rest for autograd."""
         if not self.active or self.nfwd == 0:
             return grads
+        # every owned parameter is checked before any is written (ADVICE r4): a late failure must
+        # not leave earlier parameters of this call summed into the buffer or a bucket in flight
+        for p in grads:
+            if p in self.slot and (self.launched[self.bucket_of[p]] or self.count.get(p, 0) >= self.nfwd):
+                raise RuntimeError("OverlapReducer: more FeaturePlan backwards than taped forwards this step "
+                                   "(gradient accumulation is not supported with overlap=True)")
         rest = {}
         for p, g in grads.items():
             sl = self.slot.get(p)
@@ -139,9 +145,6 @@ class OverlapReducer:
             view = self.flat[sl[0]:sl[1]]
             k = self.count.get(p, 0)
             b = self.bucket_of[p]
-            if self.launched[b] or k >= self.nfwd:
-                raise RuntimeError("OverlapReducer: more FeaturePlan backwards than taped forwards this step "
-                                   "(gradient accumulation is not supported with overlap=True)")
             if k == 0:
                 view.copy_(g.reshape(-1))
                 if p.grad is None or p.grad.data_ptr() != view.data_ptr():

@@ -29,10 +29,12 @@ class AdamW(torch.optim.Optimizer):
         defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
         super().__init__(params, defaults)
         self.allreduce = allreduce
-        # overlap (or DGVCC_DP_OVERLAP=1): the FeaturePlan parameters' all-reduce runs in buckets
-        # under the backward (dgvcc_amd.dist.OverlapReducer), from the second step on
+        # overlap (default; DGVCC_DP_OVERLAP=0 or overlap=False: one blocking all-reduce of the flat
+        # buffer after the backward): the FeaturePlan parameters' all-reduce runs in ~bucket_mb
+        # buckets under the backward (dgvcc_amd.dist.OverlapReducer), from the second step on.  A
+        # no-op on one rank.
         if overlap is None:
-            overlap = os.environ.get("DGVCC_DP_OVERLAP", "0") == "1"
+            overlap = os.environ.get("DGVCC_DP_OVERLAP", "1") == "1"
         self.reducer = OverlapReducer(bucket_mb) if (overlap and allreduce) else None
         # fp16 mode: the loss was multiplied by grad_scale before backward (LossScaler); the
         # step unscales the flat gradient and skips the update when it holds inf/NaN

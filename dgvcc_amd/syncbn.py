@@ -15,7 +15,8 @@ The exchange is the one torch's SyncBatchNorm does, in two small collectives per
             coefficients come from the global sums over all ranks' pixels, dgamma / dbeta (and
             the conv bias) from this rank's, which the data-parallel gradient average then
             combines like every other parameter gradient.
-Rows are f32 [3][C] (at most 6 KB per layer), so the collectives are latency, not bandwidth.
+Rows are f32 [3][C] (at most 6 KB per layer; two per rank in the gather, so that the counts stay exact in
+f32 at any batch), so the collectives are latency, not bandwidth.
 """
 from __future__ import annotations
 
@@ -47,26 +48,48 @@ def _all_gather_rows(row: torch.Tensor, pg) -> torch.Tensor:
     w = dist.get_world_size(pg)
     out = [torch.empty_like(row) for _ in range(w)]
     dist.all_gather(out, row.contiguous(), group=pg)
-    return torch.stack(out)  # [world][3][C], rank order
+    return torch.stack(out)  # [world][...], rank order
 
 
-def finalize_rows(bn, row: torch.Tensor, pg) -> torch.Tensor:
-    """Local (n, mean, M2) row -> the global stats [4][C] (mean, invstd, scale, shift)."""
-    rows = _all_gather_rows(row, pg)
+# a rank's (n, mean, M2) row carries its pixel count in f32, exact only below 2^24
+_ROW_EXACT_M = 1 << 24
+
+
+def split_row(row: torch.Tensor, M: int) -> torch.Tensor:
+    """This rank's (n, mean, M2) row [3][C] over M pixels as two rows [2][3][C] whose counts are
+    exact in f32 at any M < 2^36 (no limit at 2^24 pixels per rank).  Below 2^24 the
+    row itself and a zero row (which the Chan merge skips); above, counts M - M % 4096 and
+    M % 4096 with the same mean and M2 shared in proportion, which merge back to (M, mean, M2)."""
+    two = torch.zeros((2,) + tuple(row.shape), dtype=torch.float32, device=row.device)
+    if M < _ROW_EXACT_M:
+        two[0] = row
+        return two
+    lo = M % 4096
+    hi = M - lo
+    for k, n in ((0, hi), (1, lo)):
+        two[k, 0] = float(n)
+        two[k, 1] = row[1]
+        two[k, 2] = (row[2].double() * (n / M)).float()
+    return two
+
+
+def gather_rows(row: torch.Tensor, M: int, pg) -> torch.Tensor:
+    """Every rank's split rows in rank order, [world * 2][3][C] (host logic; the merge is
+    dg_bn_part_finalize's)."""
+    rows = _all_gather_rows(split_row(row, M), pg)
+    return rows.reshape((-1,) + tuple(row.shape))
+
+
+def finalize_rows(bn, row: torch.Tensor, pg, M: int) -> torch.Tensor:
+    """Local (n, mean, M2) row over M pixels -> the global stats [4][C] (mean, invstd, scale, shift)."""
+    rows = gather_rows(row, M, pg)
     C = row.shape[1]
     bn.num_batches_tracked.add_(1)
     return K.bn_part_finalize(rows, rows.shape[0], C, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                               bn.running_var, _momentum(bn), bn.eps)
 
 
-# the (n, mean, M2) rows carry the pixel count in f32: exact below 2^24 pixels per rank
-# (16 frames at 768 x 1024 is 12.6M)
-_ROW_MAX_M = 1 << 24
-
-
 def row_from_z(z: K.Act) -> torch.Tensor:
-    if z.M >= _ROW_MAX_M:
-        raise ValueError(f"SyncBatchNorm: {z.M} pixels per rank exceed the f32-exact row count 2^24")
     row = torch.empty((3, z.C), dtype=torch.float32, device=z.buf.device)
     work = torch.empty(query("dg_bn_workspace", z.M, z.C) // 4 + 1, dtype=torch.float32, device=z.buf.device)
     call("dg_bn_stats_row", z.dt, z.ptr, z.ld, z.M, z.C, ptr(row), ptr(work), stream())
@@ -84,10 +107,8 @@ def fwd_stats(bn, pg, z: K.Act | None = None, part: torch.Tensor | None = None, 
               M: int = 0) -> torch.Tensor:
     """Global batch statistics of a synchronised BN layer from this rank's z or its partial rows
     (M: the pixels those rows cover)."""
-    if part is not None and M >= _ROW_MAX_M:
-        raise ValueError(f"SyncBatchNorm: {M} pixels per rank exceed the f32-exact row count 2^24")
     row = row_from_part(part, nblk, bn.num_features) if part is not None else row_from_z(z)
-    return finalize_rows(bn, row, pg)
+    return finalize_rows(bn, row, pg, M if part is not None else z.M)
 
 
 def _count_row(sums: torch.Tensor, M: int):

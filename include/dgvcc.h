@@ -49,7 +49,7 @@ int dg_set_persist(int mode);
  * drop terms up to ~2^-20 |x*y|, typically ~2^-22, one-sided; see dg_common.h).  Default from DGVCC_F32_MATH (exact | split), else 1. */
 int dg_set_f32_math(int mode);
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 1
+#define DGVCC_ABI_VERSION 2 /* 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes); the f32 workspace holds the pre-split planes */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features

@@ -16,7 +16,7 @@ def test_library_exports_every_header_symbol():
     lib = _capi.lib()
     missing = [n for n in protos if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.dg_version() == 1
+    assert lib.dg_version() == _capi.header_abi_version() == 2
     assert len(protos) >= 30
 
 
@@ -106,6 +106,19 @@ def test_conv_tile_layout_queries(monkeypatch):
     assert rows(1, 16, 384, 512, 128, 128) == 16 * 384 * 512 // 256
     monkeypatch.setenv("DGVCC_PSPLIT_TALL", "2")
     assert rows(0, 16, 48, 64, 512, 512) == 16 * 48 * 64 // 256
+
+
+def test_f32_stats_rows_need_split_room():
+    """with epilogue statistics (part != NULL) on a shape whose rows
+    dg_conv_stats_rows_ex reports for the pre-split kernels, a call without room for the planes
+    is refused (it would fall back to the 256-pixel kernel and write another row count)."""
+    from dgvcc_amd import _capi
+    L = _capi.lib()
+    for (N, H, W, C, Co) in ((16, 48, 64, 512, 512), (4, 64, 512, 64, 64), (16, 192, 256, 256, 256)):
+        ws = L.dg_conv_fwd_workspace(0, N, H, W, C, Co, 3, 3)
+        # x, w, y, part: dummy non-null pointers (the call returns before any launch)
+        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, None, 0, None) == -2
+        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, 8, ws - 256, None) == -2
 
 
 def test_call_raises_on_error():

@@ -254,6 +254,28 @@ def test_step_grads_e2e_256(dev, name, mode):
     assert glob <= max(2 * glob32, E2E_GLOBAL_TOL), (glob, glob32)
 
 
+def test_step_grads_full_frame(dev):
+    """The metric's frame: DGModel_final, final mode, 1 x 3 x 768 x 1024,
+    decisions injected.  The HIP step's gradients against the float64 oracle beside the fp32
+    oracle's own float64 error: per parameter <= max(2 x fp32-oracle error, E2E_GRAD_TOL),
+    globally <= max(2 x fp32-oracle error, E2E_GLOBAL_TOL)."""
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, 16)))
+    mine, g64, g32 = _e2e_grads("DGModel_final", "final", 1, 768, 1024, dev, den_dropout=0.0, cls_dropout=0.0)
+    keys = [k for k in g64 if not _skip_bias(k) and g64[k].norm() > 0]
+    err = {k: ((mine[k] - g64[k]).norm() / g64[k].norm()).item() for k in keys}
+    e32 = {k: ((g32[k].double() - g64[k]).norm() / g64[k].norm()).item() for k in keys}
+    cat = lambda d: torch.cat([d[k].double().reshape(-1) for k in keys])  # noqa: E731
+    ref = cat(g64)
+    glob = ((cat(mine) - ref).norm() / ref.norm()).item()
+    glob32 = ((cat(g32) - ref).norm() / ref.norm()).item()
+    worst = max(err.items(), key=lambda kv: kv[1])
+    print(f"full frame 768x1024: worst {worst} (fp32 oracle there {e32[worst[0]]:.3e}, its worst "
+          f"{max(e32.values()):.3e}), global {glob:.3e} (fp32 oracle {glob32:.3e})")
+    bad = {k: (v, e32[k]) for k, v in err.items() if v > max(2 * e32[k], E2E_GRAD_TOL)}
+    assert not bad, bad
+    assert glob <= max(2 * glob32, E2E_GLOBAL_TOL), (glob, glob32)
+
+
 def _skip_bias(k):
     # conv biases followed by BN: mathematically zero gradient (rounding noise in any implementation)
     return k.endswith(".bias") and (k.startswith("enc") or ".conv." in k) and "cls_head.2" not in k
