@@ -50,9 +50,12 @@ HBM_PEAK_GBPS = 8000.0
 # f32 GEMMs through the 3-way bf16 split issue six bf16 MFMA products per f32 product: their
 # f32-equivalent ceiling is the dense bf16 peak / 6
 F32_SPLIT_PEAK_TFLOPS = BF16_DENSE_PEAK_TFLOPS / 6.0
+# the f16 x3 arithmetic (default): three f16 MFMA products (same rate as bf16) per f32 product
+F32_H16_PEAK_TFLOPS = BF16_DENSE_PEAK_TFLOPS / 3.0
 PEAKS = {"fp32": F32_SPLIT_PEAK_TFLOPS, "fp32_exact": F32_MFMA_PEAK_TFLOPS, "bf16": BF16_DENSE_PEAK_TFLOPS,
          "fp16": BF16_DENSE_PEAK_TFLOPS}
 H0, W0 = 768, 1024
+F32_MATH_MODE = {"split": 1, "exact": 0, "h16": 2}  # dg_set_f32_math
 METRIC = "train-step frames/sec at 768×1024, ShanghaiTech-A; MAE vs reference"
 CONFIG_FILES = {"final": "configs/sta_final.yml", "simple": "configs/stb_reg_base.yml",
                 "base": "configs/ablation (mode base)"}
@@ -84,8 +87,10 @@ def parse():
                     help="secondary workload: ResNet-50 DG counter (IBN-b / SW / ISW) train step")
     ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16", "fp16"])
     ap.add_argument("--no-bf16", action="store_true", help="skip the perf_bf16 leg")
-    ap.add_argument("--f32-math", default="split", choices=["split", "exact"],
-                    help="f32 conv GEMM arithmetic: exact 3-way bf16 split (default) or v_mfma_f32_16x16x4_f32")
+    ap.add_argument("--f32-math", default="h16", choices=["split", "exact", "h16"],
+                    help="f32 conv GEMM arithmetic: h16 (default: two scaled f16 parts per operand, three f16 MFMA "
+                         "products, where the kernel has it; else the split), split (exact 3-way bf16 split, six "
+                         "products) or exact (v_mfma_f32_16x16x4_f32)")
     ap.add_argument("--no-f32-exact", action="store_true", help="skip the f32_exact leg")
     ap.add_argument("--height", type=int, default=H0)
     ap.add_argument("--width", type=int, default=W0)
@@ -248,6 +253,10 @@ FWD_KERNEL_NAMES = {
     "fp32": "conv_fwd_psplit_kernel<256|128> + conv_fwd_rsplit3_kernel + conv_fwd_rsplit_kernel (implicit-GEMM "
             "conv, f32 operands split exactly into 3 bf16 parts, 6 x v_mfma_f32_16x16x32_bf16 per 32-deep block, "
             "f32 accumulation: forward + dgrad launches; peak = dense bf16 / 6)",
+    "fp32_h16": "conv_fwd_psplit_kernel<256|128, HM> + conv_fwd_rsplit3w_kernel<HM> (implicit-GEMM conv, each f32 "
+                "operand scaled by a power of two and cut into two f16 parts, 3 x v_mfma_f32_16x16x32_f16 per "
+                "32-deep block (hi*hi + hi*lo + lo*hi), f32 accumulation: forward + dgrad launches; peak = dense "
+                "f16 / 3)",
     "fp32_exact": "conv_fwd_pers_kernel<float> (implicit-GEMM conv on v_mfma_f32_16x16x4_f32: forward + dgrad "
                   "launches)",
     "bf16": "conv_fwd_pers_kernel + conv_fwd_tap3p_kernel + conv_fwd_pipe_kernel + conv_fwd_tap3_kernel "
@@ -261,7 +270,7 @@ def run_leg(args, precision, dev, world, rank):
     """Build, warm up and time one precision of the workload; returns the measurements.
     precision "fp32_exact" = fp32 with the conv GEMMs on v_mfma_f32_16x16x4_f32."""
     from dgvcc_amd import kernels as K
-    K.call("dg_set_f32_math", 0 if precision == "fp32_exact" else 1)
+    K.call("dg_set_f32_math", 0 if precision == "fp32_exact" else F32_MATH_MODE[args.f32_math])
     precision = "fp32" if precision == "fp32_exact" else precision
     from dgvcc_amd.losses import MSELoss
     from dgvcc_amd.optim import AdamW
@@ -351,7 +360,8 @@ def run_leg(args, precision, dev, world, rank):
 
 def roofline(args, precision, r):
     peak = PEAKS[precision]
-    kname = FWD_KERNEL_NAMES.get(precision, "implicit-GEMM conv forward + dgrad")
+    kname = FWD_KERNEL_NAMES.get("fp32_h16" if precision == "fp32" and args.f32_math == "h16" else precision,
+                                 "implicit-GEMM conv forward + dgrad")
     if args.trunk:  # ResNet-50 trunk: strided/non-"same" convs on conv_gen_kernel, 3x3/1x1 stride 1 as above
         kname = ("conv_gen_kernel (strided / 7x7 stem im2col / parity-class dgrad) + " + kname.split(" (")[0] +
                  " (ResNet-50 trunk convs: forward + dgrad launches)")
@@ -363,6 +373,8 @@ def roofline(args, precision, r):
         ((r["conv_flops"] + r["wg_flops"]) / steps, None)
     step_s = r["elapsed"] / steps
     out = {"bound": "mfma", "kernel": kname,
+           **({"f32_equivalent_frac_of_split6_ceiling": round(achieved / F32_SPLIT_PEAK_TFLOPS, 4)}
+              if precision == "fp32" and args.f32_math == "h16" else {}),
            "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
            "traffic": traffic, "traffic_source": tsrc,
            "algorithmic_bytes_per_launch": round(r["conv_bytes"] / max(r["conv_n"], 1)),
@@ -575,13 +587,14 @@ def density_parity(sd, batch, loss_ref, outs_ref, mode):
     mode: the oracle is re-run on the HIP path's own threshold decisions (e_mask, class maps) and
     the number of decisions that differ is reported; the loss is compared as is."""
     from dgvcc_amd import kernels as K
+    math_mode = int(K.lib_call_status("dg_get_f32_math"))
     try:
         res = _density_parity_once(sd, batch, loss_ref, outs_ref, mode, grads=True)
         K.call("dg_set_f32_math", 0)
         ex = _density_parity_once(sd, batch, loss_ref, outs_ref, mode)
     finally:
-        K.call("dg_set_f32_math", 1)
-    res["f32_math"] = "split"
+        K.call("dg_set_f32_math", math_mode)
+    res["f32_math"] = {1: "split", 2: "h16"}.get(math_mode, str(math_mode))
     res["f32_exact"] = {k: v for k, v in ex.items() if k not in ("precision", "frame", "tolerance_rel", "note")}
     return res
 
@@ -704,6 +717,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.f32_math == "h16":  # the fp32 legs' ceiling is that of the arithmetic they run
+        PEAKS["fp32"] = F32_H16_PEAK_TFLOPS
     if args.global_batch is not None:  # strong scaling: the global batch is fixed, split over the ranks
         if args.global_batch % world:
             raise SystemExit(f"bench.py: --global-batch {args.global_batch} does not split over {world} ranks")
@@ -758,8 +773,12 @@ def main():
         "roofline": roofline(args, leg, r),
     }
     if prec == "fp32":
-        out["f32_math"] = ("exact 3-way bf16 split of both f32 operands, 6 bf16 MFMA products per f32 product, "
-                           "f32 accumulation" if leg == "fp32" else "v_mfma_f32_16x16x4_f32")
+        out["f32_math"] = ("v_mfma_f32_16x16x4_f32" if leg != "fp32" else
+                           "f16 x3: each f32 operand scaled by a power of two into f16 range and cut into two f16 "
+                           "parts by nearest rounding, 3 f16 MFMA products per f32 product (hi*hi + hi*lo + lo*hi), "
+                           "f32 accumulation, exact rescale (DESIGN.md §3.1)" if args.f32_math == "h16" else
+                           "exact 3-way bf16 split of both f32 operands, 6 bf16 MFMA products per f32 product, "
+                           "f32 accumulation")
     if "params_in_sync" in r:
         out["params_in_sync"] = r["params_in_sync"]
     if "allreduce" in r:  # the gradient all-reduce: bucketed and overlapped with the backward
@@ -771,7 +790,7 @@ def main():
                             "note": "same fp32 workload with the conv GEMMs on v_mfma_f32_16x16x4_f32",
                             "last_loss": re_["last_loss"], "roofline": roofline(args, "fp32_exact", re_)}
         K_ = __import__("dgvcc_amd.kernels", fromlist=["call"])
-        K_.call("dg_set_f32_math", 1)
+        K_.call("dg_set_f32_math", F32_MATH_MODE[args.f32_math])
     if prec == "fp32" and not args.no_bf16:
         rb = run_leg(args, "bf16", dev, world, rank)
         out["perf_bf16"] = {"value": round(rb["frames"] / rb["elapsed"], 3), "unit": "frames/s", "dtype": "bf16",
@@ -786,6 +805,7 @@ def main():
         out["bl"] = bl_timing(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.trunk:
         out["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+        __import__("dgvcc_amd.kernels", fromlist=["call"]).call("dg_set_f32_math", F32_MATH_MODE[args.f32_math])
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

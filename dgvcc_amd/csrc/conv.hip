@@ -61,6 +61,8 @@ struct FwdArgs {
   // 16-bit persistent / pipe forward: 16-byte epilogue stores (lane pairs exchange halves with
   // v_permlane16_swap); set by launch_fwd where y's rows are 16-byte aligned (DGVCC_PERS_WST)
   int wide_st = 0;
+  // f32 f16 x3 arithmetic: a device float >= max |x| (NULL: presplit_h runs amax_kernel over x)
+  const float* xamax = nullptr;
 };
 template <typename T> __device__ __forceinline__ unsigned pack2(float lo, float hi);
 template <> __device__ __forceinline__ unsigned pack2<bf16>(float lo, float hi) { return pack_bf2(lo, hi); }
@@ -1353,14 +1355,19 @@ static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA add
 // filter fragment read and every staged filter byte feeds 4 pixel blocks instead of 3.  The two
 // 80-KB stages fill the LDS; the epilogue's statistics scratch and this tile's bias live in the
 // stage the last K-step consumed (free until the next tile's second K-step issues its DMA there).
-template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0>
+// HM = 1: the f16 x3 arithmetic (dg_common.h split2h_8 / mfma_h3): two f16 filter planes
+// (split_weight_h_kernel: per-row scale, 1/(s_row s_x) per output channel after the planes, then
+// s_x), the pixel fragments scaled by s_x and split into two f16 parts, three MFMAs per block.
+template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0, int HM = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   static_assert(!TALL || (BN == 256 && EPI == 0 && STG == 2 && INC), "TALL: 256-channel training forward only");
+  constexpr int NPL = HM ? 2 : 3;  // filter planes
+  constexpr int KB = NPL * 64;     // bytes per (output channel, 32-deep k-block) of the planes
   constexpr int PSB = TALL ? 256 : psplit_psb(BN, WIDE);
   constexpr int NCOG = (BN == 128 && WIDE) ? 1 : 2;  // channel groups of waves
   constexpr int NPXG = 8 / NCOG;                   // pixel groups of waves
   constexpr int AROWB = 64;                        // bytes per A plane row (32 bf16)
-  constexpr int A_BYTES = 3 * BN * AROWB;
+  constexpr int A_BYTES = NPL * BN * AROWB;
   constexpr int AI = A_BYTES / 1024 / 8;           // A DMA instructions per wave per K-step
   constexpr int BI = PSB / 64;                     // B DMA instructions per wave per K-step
   constexpr int TI = BN / NCOG / 16, TJ = PSB / NPXG / 16;  // wave tile: 128 channels x 48 pixels
@@ -1368,10 +1375,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   constexpr int PF = STG - 1;
   constexpr int EPI_B = NPXG * 3 * BN * 4;
   static_assert(AI * 8 * 1024 == A_BYTES, "A tile must split evenly over the 8 waves");
-  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + (TALL ? 0 : EPI_B + PERS_BIAS_MAX * 4)];
-  static_assert(!TALL || EPI_B + BN * 4 <= STAGE, "TALL epilogue scratch must fit in a stage");
+  // non-TALL: epilogue scratch, the bias row and (HM) the per-channel rescale row after the ring
+  __shared__ __attribute__((aligned(1024))) char smem[STG * STAGE + (TALL ? 0 : EPI_B + PERS_BIAS_MAX * 4 * (HM ? 2 : 1))];
+  static_assert(!TALL || EPI_B + (HM ? 2 : 1) * BN * 4 <= STAGE, "TALL epilogue scratch must fit in a stage");
   char* epi_lds = smem + STG * STAGE;
   float* bbuf = (float*)(epi_lds + EPI_B);
+  float* hbuf = bbuf + PERS_BIAS_MAX;  // HM: 2^-(e_row + e_x) by absolute output channel
   constexpr int E3_MAX = (EPI_B + PERS_BIAS_MAX * 4) / 12;
   const bool e3_lds = EPI == 3 && a.Cout <= E3_MAX;
   float* ebias = (float*)epi_lds;
@@ -1394,11 +1403,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   // A source offsets (bytes, K-step 0) of this wave's AI DMA pieces: piece q = plane p, rows rb*16..+15
   // = a lane part (row (lane >> 2) of a 16-row block; the swizzle only sees row & 15) + a
   // wave-uniform part per piece (scalar offset of the DMA), so the pieces cost one VGPR
-  const unsigned alane = (unsigned)((lane >> 2) * KT * 192 + (((lane & 3) ^ psw_a(lane >> 2)) * 16));
+  const unsigned alane = (unsigned)((lane >> 2) * KT * KB + (((lane & 3) ^ psw_a(lane >> 2)) * 16));
+  // HM: the scales after the planes: [Cout] 1/(s_row s_x), then s_x
+  const float* htail = (const float*)(wsp + (long long)a.Cout * KT * KB);
+  const float hsx = HM ? htail[a.Cout] : 1.f;
   auto aoff_s = [&](int q) -> unsigned {
     const int gq = wid * AI + q;
     const int pl = gq / (BN / 16), rb = gq % (BN / 16);
-    return (unsigned)(rb * 16 * KT * 192 + pl * 64);
+    return (unsigned)(rb * 16 * KT * KB + pl * 64);
   };
 
   struct Ctx {
@@ -1424,7 +1436,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     const int phi = min(M, c.px0 + PSB + halo);
     const unsigned win_bytes = (unsigned)(((long long)(phi - plo - 1) * a.ldx + a.C) * 4);
     c.xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long long)plo * a.ldx * 4), 0, win_bytes, 0x00020000);
-    c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(wsp + (long long)c.co0 * KT * 192), 0, (unsigned)(BN * KT * 192),
+    c.wr = __builtin_amdgcn_make_buffer_rsrc((void*)(wsp + (long long)c.co0 * KT * KB), 0, (unsigned)(BN * KT * KB),
                                              0x00020000);
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -1462,7 +1474,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     char* Bs = As + A_BYTES;
 #pragma unroll
     for (int q = 0; q < AI; ++q)
-      lds_dma16s(c.wr, As + (wid * AI + q) * 1024, alane + (unsigned)((rs * CB + icb) * 192), aoff_s(q));
+      lds_dma16s(c.wr, As + (wid * AI + q) * 1024, alane + (unsigned)((rs * CB + icb) * KB), aoff_s(q));
     const unsigned toff = (unsigned)((((ir - a.pad) * a.W + (is - a.pad)) * a.ldx + icb * 32) * 4);
     const unsigned need = tap_need(ir, is);
 #pragma unroll
@@ -1478,7 +1490,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     char* Bs = As + A_BYTES;
 #pragma unroll
     for (int q = 0; q < AI; ++q)
-      lds_dma16s(c.wr, As + (wid * AI + q) * 1024, alane + (unsigned)((rs * CB + cb) * 192), aoff_s(q));
+      lds_dma16s(c.wr, As + (wid * AI + q) * 1024, alane + (unsigned)((rs * CB + cb) * KB), aoff_s(q));
     const int dh = r - a.pad, dw = s2 - a.pad;
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
@@ -1501,6 +1513,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   } else if (a.bias && !TALL) {
     for (int c = tid; c < a.Cout; c += 512) bbuf[c] = a.bias[c];
   }
+  if (HM && !TALL)
+    for (int c = tid; c < a.Cout; c += 512) hbuf[c] = htail[c];
   Ctx cur, nxt;
   setup(lin, cur);
   bool has_next = lin + G < ntile;
@@ -1542,13 +1556,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
         b0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc));
         b1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc + 1));
       }
-      auto aread = [&](int i, s8v (&ah)[3]) __attribute__((always_inline)) {
+      auto aread = [&](int i, s8v (&ah)[NPL]) __attribute__((always_inline)) {
         const int row = wco + 16 * i + fr;
         const int off = row * AROWB + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) ah[pl] = *(const s8v*)(As + pl * BN * AROWB + off);
+        for (int pl = 0; pl < NPL; ++pl) ah[pl] = *(const s8v*)(As + pl * BN * AROWB + off);
       };
-      s8v ah[3];
+      s8v ah[NPL];
       aread(0, ah);
       {
         const int u = t + PF;
@@ -1563,22 +1577,40 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
           else if (has_next) issue(nxt, u - KT, (gs + PF) % STG);
         }
       }
-      s8v bh[TJ][3];
+      s8v bh[TJ][NPL];
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) split3_8(b0[j], b1[j], bh[j][0], bh[j][1], bh[j][2]);
+      for (int j = 0; j < TJ; ++j) {
+        if constexpr (HM) split2h_8(b0[j], b1[j], hsx, bh[j][0], bh[j][1]);
+        else split3_8(b0[j], b1[j], bh[j][0], bh[j][1], bh[j][2]);
+      }
+      if constexpr (HM) __builtin_amdgcn_sched_barrier(0);  // the raw rows die here (else: 59 spilled VGPRs)
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
-        s8v an[3];
+        s8v an[NPL];
         if (i + 1 < TI) aread(i + 1, an);
         __builtin_amdgcn_s_setprio(1);
-        constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+        if constexpr (HM) {
+          constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
 #pragma unroll
-        for (int q = 0; q < 6; ++q)
+          for (int q = 0; q < 3; ++q)
 #pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah[PA[q]]),
+                                                                 __builtin_bit_cast(h8v, bh[j][PB[q]]), acc[i][j], 0, 0, 0);
+        } else {
+          constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
+        }
         __builtin_amdgcn_s_setprio(0);
-        if (i + 1 < TI) { ah[0] = an[0]; ah[1] = an[1]; ah[2] = an[2]; }
+        if (i + 1 < TI) {
+#pragma unroll
+          for (int pl = 0; pl < NPL; ++pl) ah[pl] = an[pl];
+        }
+        if constexpr (HM) __builtin_amdgcn_sched_barrier(0);  // no fragment reads hoisted across blocks
       }
     }
     first_tile = false;
@@ -1587,8 +1619,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       bbuf = (float*)(epi_lds + EPI_B) - cur.co0;  // indexed by absolute channel
       lds_barrier();  // every wave is done reading the stage
       if (a.bias && tid < BN) bbuf[cur.co0 + tid] = a.bias[cur.co0 + tid];
+      hbuf = bbuf + BN;  // absolute channel index, as bbuf
+      if (HM && tid < BN) hbuf[cur.co0 + tid] = htail[cur.co0 + tid];
       lds_barrier();
     }
+    // HM: back from the scaled operands, exact powers of two per output channel, applied where the
+    // epilogue first reads acc (a separate pass over all of acc ahead of the stores spilled 59 VGPRs)
+    auto hscale = [&](int i, int j) __attribute__((always_inline)) {
+      if constexpr (HM) {
+        const f4v sc = *(const f4v*)(hbuf + cur.co0 + wco + 16 * i + 4 * fc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc[r];
+      }
+    };
     float* y = (float*)a.y;
     bool valid[TJ];
     // y += old y ahead of the stores (EPI_ACC_NOTE)
@@ -1601,6 +1644,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
 #pragma unroll
         for (int i = 0; i < TI; ++i) {
           const int co = cur.co0 + wco + 16 * i + 4 * fc;
+          hscale(i, j);
           if (e3_lds) {
             const f4v b = *(const f4v*)(ebias + co);
             for (int r = 0; r < 4; ++r) acc[i][j][r] += b[r];
@@ -1621,6 +1665,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int co = cur.co0 + wco + 16 * i + 4 * fc;
+        if (!a.accumulate) hscale(i, j);
         float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
         if (a.accumulate) {
         } else if (e3_lds) {
@@ -2034,14 +2079,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
 // 64 channels x 64 pixels (twice the per-wave fragment reuse of the 2 x 4 layout): the 514-pixel
 // strip (99 KB of planes) and the three taps' filter planes (36 KB) are single-buffered, both
 // stored between the K-step's two barriers from registers loaded during the previous K-step.
-template <int EPI = 0>
+// HM = 1: the f16 x3 arithmetic (two f16 planes per operand, presplit_h's filter planes and scales).
+template <int EPI = 0, int HM = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int NPL = HM ? 2 : 3, KB = NPL * 64;        // planes; bytes per (co, k-block) of the filter planes
   constexpr int BN = 64, BPX = 512, SR = 520;        // strip rows (514 used)
-  constexpr int B_PL = SR * 64, BUF = 3 * B_PL;      // strip plane / buffer bytes
-  constexpr int A_PL = BN * 64, A_TAP = 3 * A_PL;    // filter plane / tap bytes
+  constexpr int B_PL = SR * 64, BUF = NPL * B_PL;    // strip plane / buffer bytes
+  constexpr int A_PL = BN * 64, A_TAP = NPL * A_PL;  // filter plane / tap bytes
   constexpr int TI = 4, TJ = 4;
   constexpr int NCH = (BPX + 2) * 8, BR = (NCH + 511) / 512;  // 16-B f32 chunks of the strip
-  constexpr int NA = 3 * 3 * BN * 4, AR = (NA + 511) / 512;  // 16-B chunks of the 3 taps' planes
+  constexpr int NA = 3 * NPL * BN * 4, AR = (NA + 511) / 512;  // 16-B chunks of the 3 taps' planes
   __shared__ __attribute__((aligned(16))) char smem[BUF + 3 * A_TAP];
   char* Asm = smem + BUF;
 
@@ -2064,16 +2111,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
                                                                 win_bytes, 0x00020000);
   const int wpx = wid * 64, wco = 0;
   const int fr = lane & 15, fc = lane >> 4;
-  // filter chunk q of a K-step: (tap s, plane, row co, 16-B chunk) = (q / 768, (q / 256) % 3, (q & 255) >> 2, q & 3)
-  const char* wbase = wsp + (long long)co0 * (9 * CB) * 192;
+  // filter chunk q of a K-step: (tap s, plane, row co, 16-B chunk) = (q / (NPL 256), (q / 256) % NPL, (q & 255) >> 2, q & 3)
+  const char* wbase = wsp + (long long)co0 * (9 * CB) * KB;
   int a_src[AR], a_dst[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int q = tid + 512 * i;
-    const int ts = q / 768, pl = (q / 256) % 3, row = (q & 255) >> 2, ch = q & 3;
-    a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * 192 + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*192
+    const int ts = q / (NPL * 256), pl = (q / 256) % NPL, row = (q & 255) >> 2, ch = q & 3;
+    a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * KB + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*KB
     a_dst[i] = ts * A_TAP + pl * A_PL + row * 64 + ((ch ^ psw_a(row)) << 4);
   }
+  // HM: the scales after the planes ([Cout] 2^-(e_row + e_x), then s_x)
+  const float* htail = (const float*)(wsp + (long long)a.Cout * 9 * CB * KB);
+  const float hsx = HM ? htail[a.Cout] : 1.f;
 
   u4v rb[BR], ra[AR];
   auto gload = [&](int t) __attribute__((always_inline)) {
@@ -2087,7 +2137,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
       const long long pin = (long long)tn * HW + (long long)h * a.W + ww - plo;
       rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + cb * 32 + chunk * 4) * 4) : 0xFFFFFFF0u);
     }
-    const long long koff = (long long)(r * 3 * CB + cb) * 192;
+    const long long koff = (long long)(r * 3 * CB + cb) * KB;
 #pragma unroll
     for (int i = 0; i < AR; ++i)
       if (a_src[i] >= 0) ra[i] = *(const u4v*)(wbase + a_src[i] + koff);
@@ -2099,11 +2149,18 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
       const int row = rbase + 64 * i;
       if (row < BPX + 2) {
         const int o = row * 64 + ((((chunk >> 1) ^ psw_a(row))) << 4) + (chunk & 1) * 8;
-        u2v h0, h1, h2;
-        split3_4(rb[i], h0, h1, h2);
-        *(u2v*)(Bs + o) = h0;
-        *(u2v*)(Bs + B_PL + o) = h1;
-        *(u2v*)(Bs + 2 * B_PL + o) = h2;
+        if constexpr (HM) {
+          u2v h0, h1;
+          split2h_4(rb[i], hsx, h0, h1);
+          *(u2v*)(Bs + o) = h0;
+          *(u2v*)(Bs + B_PL + o) = h1;
+        } else {
+          u2v h0, h1, h2;
+          split3_4(rb[i], h0, h1, h2);
+          *(u2v*)(Bs + o) = h0;
+          *(u2v*)(Bs + B_PL + o) = h1;
+          *(u2v*)(Bs + 2 * B_PL + o) = h2;
+        }
       }
     }
   };
@@ -2126,29 +2183,41 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
     const char* Bs = smem;
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      s8v ah[TI][3], bh[TJ][3];
+      s8v ah[TI][NPL], bh[TJ][NPL];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int row = wco + 16 * i + fr;
         const int o = s * A_TAP + row * 64 + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) ah[i][pl] = *(const s8v*)(Asm + pl * A_PL + o);
+        for (int pl = 0; pl < NPL; ++pl) ah[i][pl] = *(const s8v*)(Asm + pl * A_PL + o);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int row = wpx + 16 * j + fr + s;
         const int o = row * 64 + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
+        for (int pl = 0; pl < NPL; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
       }
-      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+      if constexpr (HM) {
+        constexpr int PA3[3] = {1, 0, 0}, PB3[3] = {0, 1, 0};
 #pragma unroll
-      for (int u = 0; u < 6; ++u)
+        for (int u = 0; u < 3; ++u)
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+          for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah[i][PA3[u]]),
+                                                                 __builtin_bit_cast(h8v, bh[j][PB3[u]]), acc[i][j], 0, 0, 0);
+      } else {
+        constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+      }
     }
   }
   __syncthreads();  // smem reuse by the statistics epilogue
@@ -2159,6 +2228,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
 #pragma unroll
   for (int i = 0; i < TI; ++i)
     bv[i] = a.bias ? *(const f4v*)(a.bias + co0 + wco + 16 * i + 4 * fc) : f4v{0.f, 0.f, 0.f, 0.f};
+  if constexpr (HM) {  // back from the scaled operands (exact powers of two per output channel)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const f4v sc = *(const f4v*)(htail + co0 + wco + 16 * i + 4 * fc);
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc[r];
+    }
+  }
   if (a.accumulate || EPI == 3) {  // old y, bias and the eval-BN affine ahead of the stores (EPI_ACC_NOTE)
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
@@ -2221,6 +2300,58 @@ __global__ void split_weight_kernel(const float* __restrict__ w, long long n, un
     d[16] = p1;
     d[32] = p2;
   }
+}
+
+// f16 x3 filter planes (dg_common.h split2h_pair): one block per output row co of the packed
+// f32 filter w[co][K]: the row's largest magnitude sets its power-of-two scale s_row, the parts of
+// w * s_row go to wsp[co][kb][2][32] (f16 hi, lo), and after the Cout * K * 4 bytes of planes the
+// tail [Cout] = 2^-(e_row + e_x) (the epilogue's exact rescale) and [Cout] = s_x = 2^e_x, from the
+// pixel operand's largest magnitude *xamax (amax_kernel).
+__global__ __launch_bounds__(256) void split_weight_h_kernel(const float* __restrict__ w, int K,
+                                                           unsigned short* __restrict__ wsp,
+                                                           const unsigned* __restrict__ xamax, int Cout) {
+  __shared__ float red[4];
+  const int co = blockIdx.x, tid = threadIdx.x;
+  const float* row = w + (long long)co * K;
+  float m = 0.f;
+  for (int e = tid; e < K; e += 256) m = fmaxf(m, fabsf(row[e]));
+  m = wave_max(m);
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int er = h16_exp(m), ex = h16_exp(__uint_as_float(*xamax));
+  const float s = ldexpf(1.f, er);
+  for (int e = 2 * tid; e < K; e += 512) {
+    unsigned ph, pl;
+    split2h_pair(row[e], row[e + 1], s, ph, pl);
+    unsigned* d = (unsigned*)(wsp + (((long long)co * K + e) >> 5) * 64 + (e & 31));
+    d[0] = ph;
+    d[16] = pl;
+  }
+  if (tid == 0) {
+    float* tail = (float*)(wsp + (long long)Cout * K * 2);
+    tail[co] = ldexpf(1.f, -(er + ex));
+    if (co == 0) tail[Cout] = ldexpf(1.f, ex);
+  }
+}
+
+// *out = max |x| over the M x C f32 rows of pixel stride ldx (bit pattern of a non-negative float,
+// so an integer max; *out zeroed by the caller)
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long ldx, long long M, int C,
+                                                   unsigned* __restrict__ out) {
+  __shared__ float red[4];
+  const int cq = C >> 2;
+  const long long total = M * cq;
+  float m = 0.f;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long p = i / cq;
+    const f4v v = *(const f4v*)(x + p * ldx + (i - p * cq) * 4);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
 }
 
 // Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored
@@ -2382,15 +2513,19 @@ static bool f32_pers_shape_ok(const FwdArgs& a, int kmin);
 
 // f32 GEMM arithmetic: 0 = v_mfma_f32_16x16x4_f32, 1 = the exact 3-way bf16 split on
 // v_mfma_f32_16x16x32_bf16 (dg_common.h split3_8; f32-grade).
-// Default: DGVCC_F32_MATH (exact | split), else split; dg_set_f32_math overrides.
+// Default: DGVCC_F32_MATH (exact | split | h16), else h16; dg_set_f32_math overrides.
+// 2 (h16, default since round 5): the split math, with the f16 x3 arithmetic where a kernel has it
+// (dg_common.h: the pre-split forward/dgrad, the 3-tap Cout = 64 forward, the split wgrads)
 static int g_f32_math = -1;
-static bool f32_split() {
+static int f32_math() {
   if (g_f32_math < 0) {
     const char* e = getenv("DGVCC_F32_MATH");
-    g_f32_math = (e && e[0] == 'e') ? 0 : 1;
+    g_f32_math = (e && e[0] == 'e') ? 0 : (e && e[0] == 's') ? 1 : 2;
   }
-  return g_f32_math == 1;
+  return g_f32_math;
 }
+static bool f32_split() { return f32_math() >= 1; }
+static bool f32_h16() { return f32_math() == 2; }
 
 static int persist_grid() {  // one block per CU (the ring takes most of the LDS)
   static int g = -1;
@@ -3026,6 +3161,34 @@ static const unsigned short* presplit(const FwdArgs& a, hipStream_t st) {
                      st, (const float*)a.w, nw, wsp);
   return wsp;
 }
+static int launch_amax(const float* x, long long ldx, long long M, int C, unsigned* out, hipStream_t st) {
+  if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
+  if (M <= 0) return DG_OK;
+  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(M * (C / 4), 256), 2048)), dim3(256), 0,
+                     st, x, ldx, M, C, out);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+// f16 x3 planes + scales (split_weight_h_kernel) in the same workspace (Cout * K * 4 bytes of
+// planes + 2 * Cout + 2 floats of scales, then the pixel operand's amax word): the x amax pass,
+// then the filter split
+static long long presplit_h_bytes(const FwdArgs& a) {
+  return (long long)a.Cout * a.R * a.S * a.C * 4 + (2LL * a.Cout + 4) * 4;
+}
+static const unsigned short* presplit_h(const FwdArgs& a, hipStream_t st) {
+  const long long K = (long long)a.R * a.S * a.C;
+  if (!a.wsplit || a.wsplit_bytes < presplit_h_bytes(a)) return nullptr;
+  unsigned short* wsp = (unsigned short*)a.wsplit;
+  const unsigned* xam = (const unsigned*)a.xamax;
+  if (!xam) {
+    unsigned* slot = (unsigned*)(a.wsplit + a.Cout * K * 4 + (2LL * a.Cout + 2) * 4);
+    if (launch_amax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, slot, st) != DG_OK) return nullptr;
+    xam = slot;
+  }
+  hipLaunchKernelGGL(split_weight_h_kernel, dim3((unsigned)a.Cout), dim3(256), 0, st, (const float*)a.w, (int)K, wsp,
+                     (const unsigned*)xam, a.Cout);
+  return wsp;
+}
 static bool has_split_room(const FwdArgs& a) {
   return a.wsplit && a.wsplit_bytes >= (long long)a.Cout * a.R * a.S * a.C * 6;
 }
@@ -3204,21 +3367,30 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
       FwdArgs q = a;
       q.bpart = nullptr;
       if (!(psplit_ok(q) && psplit_wide() && has_split_room(a))) return DG_ERR_UNSUPPORTED;
-      const unsigned short* wsp = presplit(a, st);
+      const bool h16 = f32_h16();
+      const unsigned short* wsp = h16 ? presplit_h(a, st) : presplit(a, st);
+      if (!wsp) return DG_ERR_HIP;
       const int bn2 = f32_pers_bn(a.Cout);
       const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_psb(bn2)) * (a.Cout / bn2),
                                                         persist_grid());
-      if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 2>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
+      if (h16) {
+        if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 2, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
+        else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 2, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
+      } else if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 2>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
       else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, 2>), dim3(g2), dim3(512), 0, st, a, (const char*)wsp);
       DG_CHECK_LAUNCH();
       return DG_OK;
     }
     if (rsplit_ok(a) && has_split_room(a)) {  // split math, Cout = 64: both operands split once per block
-      const unsigned short* wsp = presplit(a, st);
+      const bool h16 = f32_h16() && rsplit3w_ok(a);  // f16 x3 on the 512-pixel 3-tap form
+      const unsigned short* wsp = h16 ? presplit_h(a, st) : presplit(a, st);
+      if (!wsp) return DG_ERR_HIP;
       const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));
       if (rsplit3w_ok(a)) {
         const dim3 gw((unsigned)((long long)(M / 512) * (a.Cout / 64)));
-        if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3>), gw, dim3(512), 0, st, a, (const char*)wsp);
+        if (h16 && a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3, 1>), gw, dim3(512), 0, st, a, (const char*)wsp);
+        else if (h16) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0, 1>), gw, dim3(512), 0, st, a, (const char*)wsp);
+        else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3>), gw, dim3(512), 0, st, a, (const char*)wsp);
         else hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0>), gw, dim3(512), 0, st, a, (const char*)wsp);
       } else if (rsplit3_ok(a)) {
         if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
@@ -3249,10 +3421,14 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
         } \
       } while (0)
       if (f32_split() && psplit_ok(a) && has_split_room(a)) {
-        const unsigned short* wsp = presplit(a, st);
-        const int bn2 = f32_pers_bn(a.Cout);
-        const bool wide = psplit_wide();
         const bool tall = psplit_tall(a);
+        const bool wide = psplit_wide();
+        const bool inc = psplit_inc();
+        // f16 x3 planes instead (presplit_h) on the default (incremental, wide) forms
+        const bool h16 = f32_h16() && inc && wide;
+        const unsigned short* wsp = h16 ? presplit_h(a, st) : presplit(a, st);
+        if (!wsp) return DG_ERR_HIP;
+        const int bn2 = f32_pers_bn(a.Cout);
         const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_tile_px(a)) * (a.Cout / bn2),
                                                           persist_grid());
         const char* wspc = (const char*)wsp;
@@ -3261,10 +3437,12 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           const char* e = getenv("DGVCC_PSPLIT_ORDER");
           ap.tile_order = (e && e[0] == '1') ? 1 : 0;
         }
-        const bool inc = psplit_inc();
 #define PSPLIT_LAUNCH(EPI_)                                                                                    \
   do {                                                                                                         \
-    if (bn2 == 256) {                                                                                          \
+    if (h16) {                                                                                                 \
+      if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+    } else if (bn2 == 256) {                                                                                   \
       if (inc) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_>), dim3(g2), dim3(512), 0, st, ap, wspc); \
       else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 0>), dim3(g2), dim3(512), 0, st, ap, wspc); \
     } else if (wide) {                                                                                         \
@@ -3273,6 +3451,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
     } else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, EPI_, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);  \
   } while (0)
         if (a.escale) PSPLIT_LAUNCH(3);
+        else if (h16 && tall)
+          hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
         else if (tall) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
         else PSPLIT_LAUNCH(0);
 #undef PSPLIT_LAUNCH
@@ -3310,6 +3490,9 @@ struct WgArgs {
   int whole_x;         // 1: descriptor over the whole x (strided convs)
   int pad_ok = 0;      // 1: the plan may be the padded 9-tap kernel's (dg_conv_wgrad)
   int band = 0;        // > 0: the 9-tap wgrad walks its K-steps in bands of this many image rows
+  // f32 f16 x3 arithmetic: max |x| and max |dy| as float bits (device words)
+  const unsigned* xam = nullptr;
+  const unsigned* dyam = nullptr;
 };
 
 template <typename T> struct WgCfg;
@@ -3537,12 +3720,14 @@ __global__ __launch_bounds__(NT, 2) void conv_wgrad_kernel(WgArgs a) {
 // k = 8g + j -> pixel row 4g + (j & 3) + 16 (j >> 2), both operands), six MFMA products
 // per 16x16x32 block.  The per-wave fragment split (conv_wgrad_kernel SPL = 1) did 4x the
 // split work of this per-block one.
-template <int BCO, int BC, int WCO, int NTH = 512>
+// HM = 1: the f16 x3 arithmetic as conv_wgrad_split3_kernel's.
+template <int BCO, int BC, int WCO, int NTH = 512, int HM = 0>
 __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs a) {
   constexpr int BKP = 32;
   constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
   constexpr int PA = BKP * ROWA, PB = BKP * ROWB;          // bytes per plane
-  constexpr int TILE = 3 * (PA + PB);
+  constexpr int NPL = HM ? 2 : 3;
+  constexpr int TILE = NPL * (PA + PB);
   constexpr int CPRA = BCO / 4, CPRB = BC / 4;             // 16-B f32 chunks per pixel row
   constexpr int AR = BKP * CPRA / NTH, BR = BKP * CPRB / NTH;
   constexpr int WC = NTH / 64 / WCO;
@@ -3568,6 +3753,12 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
   const int kbeg = split * a.pps;
   const int kend = min(M, kbeg + a.pps);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int hedy = 0, hex = 0;
+  if constexpr (HM) {
+    hedy = h16_exp(__uint_as_float(*a.dyam));
+    hex = h16_exp(__uint_as_float(*a.xam));
+  }
+  const float hsdy = ldexpf(1.f, hedy), hsx = ldexpf(1.f, hex);
 
   const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 4);
   __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
@@ -3617,26 +3808,40 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
   };
   auto swrite = [&](int buf) __attribute__((always_inline)) {
     char* As = smem + buf * TILE;
-    char* Bs = As + 3 * PA;
+    char* Bs = As + NPL * PA;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int idx = tid + NTH * i;
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
-      u2v h0, h1, h2;
-      split3_4_rn(ra[i], h0, h1, h2);
-      *(u2v*)(As + o) = h0;
-      *(u2v*)(As + PA + o) = h1;
-      *(u2v*)(As + 2 * PA + o) = h2;
+      if constexpr (HM) {
+        u2v h0, h1;
+        split2h_4(ra[i], hsdy, h0, h1);
+        *(u2v*)(As + o) = h0;
+        *(u2v*)(As + PA + o) = h1;
+      } else {
+        u2v h0, h1, h2;
+        split3_4_rn(ra[i], h0, h1, h2);
+        *(u2v*)(As + o) = h0;
+        *(u2v*)(As + PA + o) = h1;
+        *(u2v*)(As + 2 * PA + o) = h2;
+      }
     }
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int idx = tid + NTH * i;
       const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
-      u2v h0, h1, h2;
-      split3_4_rn(rb[i], h0, h1, h2);
-      *(u2v*)(Bs + o) = h0;
-      *(u2v*)(Bs + PB + o) = h1;
-      *(u2v*)(Bs + 2 * PB + o) = h2;
+      if constexpr (HM) {
+        u2v h0, h1;
+        split2h_4(rb[i], hsx, h0, h1);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + PB + o) = h1;
+      } else {
+        u2v h0, h1, h2;
+        split3_4_rn(rb[i], h0, h1, h2);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + PB + o) = h1;
+        *(u2v*)(Bs + 2 * PB + o) = h2;
+      }
     }
   };
 
@@ -3659,13 +3864,13 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
     const int cur = kt & 1;
     if (kt + 1 < nkt) gload(kbeg + (kt + 1) * BKP);
     const char* As = smem + cur * TILE;
-    const char* Bs = As + 3 * PA;
-    s8v bh[TJ][3];
+    const char* Bs = As + NPL * PA;
+    s8v bh[TJ][NPL];
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int col = (wc + 16 * j + 4 * p4) * 2;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < NPL; ++pl) {
         const char* b = Bs + pl * PB;
         s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r1 * ROWB + col));
         s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r2 * ROWB + col));
@@ -3675,20 +3880,30 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int col = (wco + 16 * i + 4 * p4) * 2;
-      s8v ah[3];
+      s8v ah[NPL];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < NPL; ++pl) {
         const char* b = As + pl * PA;
         s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r1 * ROWA + col));
         s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r2 * ROWA + col));
         ah[pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
       }
-      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+      if constexpr (HM) {
+        constexpr int PA3[3] = {1, 0, 0}, PB3[3] = {0, 1, 0};
 #pragma unroll
-      for (int u = 0; u < 6; ++u)
+        for (int u = 0; u < 3; ++u)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah[PA3[u]]),
+                                                               __builtin_bit_cast(h8v, bh[j][PB3[u]]), acc[i][j], 0, 0, 0);
+      } else {
+        constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+      }
       // the next step's split + LDS stores between the MFMA blocks (the other buffer was last
       // read before the previous barrier), so its VALU/LDS work overlaps this step's MFMAs
       if (NTH == 512 && i == (TI - 1) / 2 && kt + 1 < nkt) swrite(cur ^ 1);
@@ -3699,6 +3914,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 
   const long long ldk = (long long)RS * a.C;
   float* out = a.slab + (long long)split * a.Cout * ldk;
+  const float hinv = ldexpf(1.f, -(hedy + hex));  // 1 unless HM
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
@@ -3707,7 +3923,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         const int co = co0 + wco + 16 * i + 4 * g + rr;
-        out[co * ldk + rs * a.C + c] = acc[i][j][rr];
+        out[co * ldk + rs * a.C + c] = HM ? acc[i][j][rr] * hinv : acc[i][j][rr];
       }
     }
 }
@@ -3725,13 +3941,17 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 // staging the dY rows once and the three X strips of image rows p - 1, p, p + 1 per K-step, instead
 // of three blocks (one per kernel row) each staging and splitting the same dY rows: 33% less split
 // and staging work per MFMA (DGVCC_WGRAD_SPLIT9=0: the 64 x 64 x 3-tap blocks).
-template <int BCO, int BC, int WCO, int NTH, int SWP = 0, int NR = 1>
+// HM = 1: the f16 x3 arithmetic (dg_common.h): dY and X scaled by their tensors' powers of two
+// (a.dyam / a.xam) and split into two f16 planes each, three MFMAs per block, the slab written
+// back at 2^-(e_dy + e_x).
+template <int BCO, int BC, int WCO, int NTH, int SWP = 0, int NR = 1, int HM = 0>
 __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArgs a) {
   static_assert(NR == 1 || NR == 3, "one kernel row per block, or all three");
   constexpr int BKP = 32, XR = BKP + 2;
   constexpr int ROWA = BCO * 2 + 32, ROWB = BC * 2 + 32;  // bytes per bf16 plane row
   constexpr int PA = BKP * ROWA, PB = XR * ROWB;           // bytes per plane
-  constexpr int TILE = 3 * (PA + NR * PB);
+  constexpr int NPL = HM ? 2 : 3;  // planes per operand
+  constexpr int TILE = NPL * (PA + NR * PB);
   constexpr int CPRA = BCO / 4, CPRB = BC / 4;             // 16-B f32 chunks per pixel row
   constexpr int AR = BKP * CPRA / NTH, BR = (NR * XR * CPRB + NTH - 1) / NTH;
   constexpr int WC = NTH / 64 / WCO;
@@ -3754,6 +3974,12 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
   const int kbeg = split * a.pps;
   const int kend = min(M, kbeg + a.pps);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  int hedy = 0, hex = 0;
+  if constexpr (HM) {
+    hedy = h16_exp(__uint_as_float(*a.dyam));
+    hex = h16_exp(__uint_as_float(*a.xam));
+  }
+  const float hsdy = ldexpf(1.f, hedy), hsx = ldexpf(1.f, hex);
 
   const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 4);
   __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
@@ -3794,28 +4020,42 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
   };
   auto swrite = [&](int buf, int part = 3) __attribute__((always_inline)) {
     char* As = smem + buf * TILE;
-    char* Bs = As + 3 * PA;
+    char* Bs = As + NPL * PA;
 #pragma unroll
     for (int i = 0; i < AR * (part & 1); ++i) {
       const int idx = tid + NTH * i;
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
-      u2v h0, h1, h2;
-      split3_4_rn(ra[i], h0, h1, h2);
-      *(u2v*)(As + o) = h0;
-      *(u2v*)(As + PA + o) = h1;
-      *(u2v*)(As + 2 * PA + o) = h2;
+      if constexpr (HM) {
+        u2v h0, h1;
+        split2h_4(ra[i], hsdy, h0, h1);
+        *(u2v*)(As + o) = h0;
+        *(u2v*)(As + PA + o) = h1;
+      } else {
+        u2v h0, h1, h2;
+        split3_4_rn(ra[i], h0, h1, h2);
+        *(u2v*)(As + o) = h0;
+        *(u2v*)(As + PA + o) = h1;
+        *(u2v*)(As + 2 * PA + o) = h2;
+      }
     }
 #pragma unroll
     for (int i = 0; i < BR * ((part >> 1) & 1); ++i) {
       const int idx = tid + NTH * i;
       if (idx < NR * XR * CPRB) {
         const int strip = NR == 3 ? idx / (XR * CPRB) : 0, sidx = idx - strip * (XR * CPRB);
-        const int o = strip * 3 * PB + (sidx / CPRB) * ROWB + (sidx % CPRB) * 8;
-        u2v h0, h1, h2;
-        split3_4_rn(rb[i], h0, h1, h2);
-        *(u2v*)(Bs + o) = h0;
-        *(u2v*)(Bs + PB + o) = h1;
-        *(u2v*)(Bs + 2 * PB + o) = h2;
+        const int o = strip * NPL * PB + (sidx / CPRB) * ROWB + (sidx % CPRB) * 8;
+        if constexpr (HM) {
+          u2v h0, h1;
+          split2h_4(rb[i], hsx, h0, h1);
+          *(u2v*)(Bs + o) = h0;
+          *(u2v*)(Bs + PB + o) = h1;
+        } else {
+          u2v h0, h1, h2;
+          split3_4_rn(rb[i], h0, h1, h2);
+          *(u2v*)(Bs + o) = h0;
+          *(u2v*)(Bs + PB + o) = h1;
+          *(u2v*)(Bs + 2 * PB + o) = h2;
+        }
       }
     }
   };
@@ -3841,13 +4081,13 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
     const int cur = kt & 1;
     if (kt + 1 < nkt) gload(kbeg + (kt + 1) * BKP);
     const char* As = smem + cur * TILE;
-    const char* Bs = As + 3 * PA;
-    s8v ah[TI][3];
+    const char* Bs = As + NPL * PA;
+    s8v ah[TI][NPL];
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int col = (wco + 16 * i + 4 * p4) * 2;
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) {
+      for (int pl = 0; pl < NPL; ++pl) {
         const char* b = As + pl * PA;
         s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r1 * ROWA + col));
         s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + r2 * ROWA + col));
@@ -3857,26 +4097,38 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
 #pragma unroll
     for (int rs = 0; rs < 3 * NR; ++rs) {
       const int s = rs % 3;
-      s8v bh[TJ][3];
+      s8v bh[TJ][NPL];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int col = (wc + 16 * j + 4 * p4) * 2;
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) {
-          const char* b = Bs + (rs / 3) * 3 * PB + pl * PB;
+        for (int pl = 0; pl < NPL; ++pl) {
+          const char* b = Bs + (rs / 3) * NPL * PB + pl * PB;
           s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + (r1 + s) * ROWB + col));
           s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((DG_LDS s4v*)(b + (r2 + s) * ROWB + col));
           bh[j][pl] = s8v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         }
       }
-      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+      if constexpr (HM) {
+        constexpr int PA3[3] = {1, 0, 0}, PB3[3] = {0, 1, 0};
 #pragma unroll
-      for (int u = 0; u < 6; ++u)
+        for (int u = 0; u < 3; ++u)
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+          for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[rs][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[rs][i][j], 0, 0, 0);
+            for (int j = 0; j < TJ; ++j)
+              acc[rs][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                  __builtin_bit_cast(h8v, ah[i][PA3[u]]), __builtin_bit_cast(h8v, bh[j][PB3[u]]), acc[rs][i][j], 0, 0, 0);
+      } else {
+        constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[rs][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[rs][i][j], 0, 0, 0);
+      }
       // one block per CU: the next step's split + LDS stores between the taps' MFMA blocks
       if (NTH == 512 && kt + 1 < nkt) {
         if (SWP == 0 && rs == 1) swrite(cur ^ 1);
@@ -3891,6 +4143,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
 
   const long long ldk = 9ll * a.C;
   float* out = a.slab + (long long)split * a.Cout * ldk;
+  const float hinv = ldexpf(1.f, -(hedy + hex));  // 1 unless HM
 #pragma unroll
   for (int s = 0; s < 3 * NR; ++s)
 #pragma unroll
@@ -3901,7 +4154,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
 #pragma unroll
         for (int rr = 0; rr < 4; ++rr) {
           const int co = co0 + wco + 16 * i + 4 * g + rr;
-          out[co * ldk + (r * 3 + s) * a.C + c] = acc[s][i][j][rr];
+          out[co * ldk + (r * 3 + s) * a.C + c] = HM ? acc[s][i][j][rr] * hinv : acc[s][i][j][rr];
         }
       }
 }
@@ -4595,7 +4848,7 @@ WgPlan wg_plan(int N, int H, int W, int C, int Cout, int R, int S, long long ldx
 }
 
 template <typename T>
-int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
+int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st, unsigned* hslots = nullptr) {
   const int bco = (a.Cout % 128 == 0) ? 128 : 64;
   const int bc = (a.C % 128 == 0) ? 128 : 64;
   const int tiles = (a.Cout / bco) * (a.C / bc) * a.R * a.S;
@@ -4666,7 +4919,22 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
         a.pps = p.pps;
         slab_splits = p.splits;
         const dim3 g3((unsigned)((nr3 ? wgs9_tiles(a.C, a.Cout) : wgs3_tiles(a.C, a.Cout, b3)) * p.splits));
-        if (nr3) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 512, 2, 3>), g3, dim3(512), 0, st, a);
+        const bool h16 = f32_h16() && hslots;
+        if (h16) {  // f16 x3: the operands' largest magnitudes (computed here unless the caller has them)
+          if (!a.xam) {
+            if (launch_amax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, hslots, st) != DG_OK) return DG_ERR_HIP;
+            a.xam = hslots;
+          }
+          if (!a.dyam) {
+            if (launch_amax((const float*)a.dy, a.lddy, M3, a.Cout, hslots + 1, st) != DG_OK) return DG_ERR_HIP;
+            a.dyam = hslots + 1;
+          }
+        }
+        if (h16) {
+          if (nr3) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 512, 2, 3, 1>), g3, dim3(512), 0, st, a);
+          else if (b3 == 64) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 256, 0, 1, 1>), g3, dim3(256), 0, st, a);
+          else hipLaunchKernelGGL((conv_wgrad_split3_kernel<128, 128, 2, 512, 2, 1, 1>), g3, dim3(512), 0, st, a);
+        } else if (nr3) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 512, 2, 3>), g3, dim3(512), 0, st, a);
         else if (b3 == 64) hipLaunchKernelGGL((conv_wgrad_split3_kernel<64, 64, 2, 256>), g3, dim3(256), 0, st, a);
         else {
           // placement of the next step's split + LDS stores among the taps' MFMA blocks: 0 after tap 1,
@@ -4695,7 +4963,22 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st) {
       slab_splits = p.splits;
       const dim3 gs((unsigned)(wgs_tiles(a.C, a.Cout, a.R * a.S) * p.splits));
       const int bco = wgs_bco(a.C, a.Cout), bcw = wgs_bc(a.C, a.Cout);
-      if (bco == 64) hipLaunchKernelGGL((conv_wgrad_split_kernel<64, 64, 2, 256>), gs, dim3(256), 0, st, a);
+      const bool h16 = f32_h16() && hslots;
+      if (h16) {  // f16 x3: the operands' largest magnitudes (computed here unless the caller has them)
+        if (!a.xam) {
+          if (launch_amax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, hslots, st) != DG_OK) return DG_ERR_HIP;
+          a.xam = hslots;
+        }
+        if (!a.dyam) {
+          if (launch_amax((const float*)a.dy, a.lddy, (long long)a.N * a.P * a.Q, a.Cout, hslots + 1, st) != DG_OK)
+            return DG_ERR_HIP;
+          a.dyam = hslots + 1;
+        }
+        if (bco == 64) hipLaunchKernelGGL((conv_wgrad_split_kernel<64, 64, 2, 256, 1>), gs, dim3(256), 0, st, a);
+        else if (bcw == 256) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2, 512, 1>), gs, dim3(512), 0, st, a);
+        else if (bcw == 128) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 128, 2, 512, 1>), gs, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 64, 4, 512, 1>), gs, dim3(512), 0, st, a);
+      } else if (bco == 64) hipLaunchKernelGGL((conv_wgrad_split_kernel<64, 64, 2, 256>), gs, dim3(256), 0, st, a);
       else if (bcw == 256) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2>), gs, dim3(512), 0, st, a);
       else if (bcw == 128) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 128, 2>), gs, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 64, 4>), gs, dim3(512), 0, st, a);
@@ -4905,12 +5188,18 @@ extern "C" int dg_version(void) { return DGVCC_ABI_VERSION; }
 // Test hook: force the persistent pipelined forward on (1) / off (0), or back to the
 // DGVCC_PERSIST environment default (-1).
 extern "C" int dg_set_f32_math(int mode) {
-  DG_REQUIRE(mode == 0 || mode == 1);
+  DG_REQUIRE(mode >= 0 && mode <= 2);
   g_f32_math = mode;
   return DG_OK;
 }
 
-extern "C" int dg_get_f32_math(void) { return f32_split() ? 1 : 0; }
+extern "C" int dg_get_f32_math(void) { return f32_math(); }
+
+extern "C" int dg_amax(int dtype, const void* x, int64_t ldx, int64_t M, int C, float* out, void* stream) {
+  DG_REQUIRE(x && out && M >= 0 && C > 0 && ldx >= C);
+  DG_SUPPORTED(dtype == DG_F32 && C % 4 == 0 && ldx % 4 == 0);
+  return launch_amax((const float*)x, ldx, M, C, (unsigned*)out, (hipStream_t)stream);
+}
 
 extern "C" int dg_set_persist(int mode) {
   DG_REQUIRE(mode >= -1 && mode <= 1);
@@ -4992,7 +5281,8 @@ extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, 
 // a workspace of dg_conv_fwd_workspace bytes lets a small-grid shape split its K loop.
 extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                               int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
-                              int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream) {
+                              int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
+                              void* stream) {
   DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
@@ -5003,6 +5293,7 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   if (dtype == DG_F32) {
     a.wsplit = (char*)workspace;
     a.wsplit_bytes = workspace ? ws_bytes : 0;
+    a.xamax = xamax;
   }
   if (part) {
     if (DG_IS16(dtype)) {
@@ -5043,7 +5334,8 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
 // this workspace: the caller runs the two launches.
 extern "C" int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                                     const void* w, int Cout, const void* relu_out, int64_t ldr, void* y,
-                                    int64_t ldy, void* workspace, int64_t ws_bytes, void* stream) {
+                                    int64_t ldy, void* workspace, int64_t ws_bytes, const float* xamax,
+                                    void* stream) {
   DG_REQUIRE(x && w && y && relu_out && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(Cout % 64 == 0 && (DG_IS16(dtype) ? (C % 64 == 0) : (C % 32 == 0)));
@@ -5055,6 +5347,7 @@ extern "C" int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N
   if (dtype == DG_F32) {
     a.wsplit = (char*)workspace;
     a.wsplit_bytes = workspace ? ws_bytes : 0;
+    a.xamax = xamax;
   }
   if (DG_IS16(dtype) && workspace && fwd_has_epi_stats(C, Cout, ldx, 1, 1)) {
     const long long M = (long long)N * H * W;
@@ -5078,7 +5371,7 @@ extern "C" int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N
 extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                                    int Cout, int R, int S, int pad, const float* bias, const float* scale,
                                    const float* shift, int act, void* y, int64_t ldy, void* workspace,
-                                   int64_t ws_bytes, void* stream) {
+                                   int64_t ws_bytes, const float* xamax, void* stream) {
   DG_REQUIRE(x && w && y && scale && shift && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0 &&
              (act == 0 || act == 1));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
@@ -5093,6 +5386,7 @@ extern "C" int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N,
   if (dtype == DG_F32) {
     a.wsplit = (char*)workspace;
     a.wsplit_bytes = workspace ? ws_bytes : 0;
+    a.xamax = xamax;
   }
   if (DG_IS16(dtype) && workspace && fwd_has_epi_stats(C, Cout, ldx, R, S)) {
     const long long M = (long long)N * H * W;
@@ -5110,7 +5404,7 @@ extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, i
                                  int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
                                  const float* scale, const float* shift, const float* mean, const float* invstd,
                                  int act, const float* drop, int HW, float* bpart, void* workspace, int64_t ws_bytes,
-                                 void* stream) {
+                                 const float* xamax, void* stream) {
   DG_REQUIRE(x && w && y && z && bpart && scale && shift && mean && invstd && N > 0 && H > 0 && W > 0 && C > 0 &&
              Cout > 0 && R > 0 && S > 0 && (act == 0 || act == 1) && (!drop || HW > 0));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
@@ -5129,6 +5423,7 @@ extern "C" int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, i
   if (dtype == DG_F32) {  // conv_fwd_psplit_kernel<.., EPI 2> on the caller's pre-split planes
     a.wsplit = (char*)workspace;
     a.wsplit_bytes = workspace ? ws_bytes : 0;
+    a.xamax = xamax;
     return launch_fwd<float>(a, (hipStream_t)stream);
   }
   return dtype == DG_F16 ? launch_fwd<f16>(a, (hipStream_t)stream) : launch_fwd<bf16>(a, (hipStream_t)stream);
@@ -5192,12 +5487,14 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
     if (wgs9_on(b3) && q9.splits > q.splits) q = q9;
   }
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
-  return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4;
+  // f32: + 256 bytes at the end for the f16 x3 operand maxima the library computes (dg_conv_wgrad)
+  return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4 + (DG_IS16(dtype) ? 0 : 256);
 }
 
 extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,
                              int64_t lddy, int Cout, int R, int S, int pad, float* dw, void* workspace,
-                             int64_t ws_bytes, int accumulate, void* stream) {
+                             int64_t ws_bytes, int accumulate, const float* xamax, const float* dyamax,
+                             void* stream) {
   DG_REQUIRE(x && dy && dw && workspace);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1);
@@ -5213,8 +5510,11 @@ extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H
   WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
            1, H, W, 0};
   a.pad_ok = 1;
+  a.xam = (const unsigned*)xamax;
+  a.dyam = (const unsigned*)dyamax;
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
+  unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - 256) : nullptr;
+  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st, hslots);
 }
 
 extern "C" int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R, int S, int Cpad, int row_len,
@@ -5343,7 +5643,8 @@ extern "C" int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int
   WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
            stride, P, Q, 1};
   hipStream_t st = (hipStream_t)stream;
-  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st);
+  unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - 256) : nullptr;
+  return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st, hslots);
 }
 
 

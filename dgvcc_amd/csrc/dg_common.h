@@ -250,3 +250,79 @@ __device__ __forceinline__ void split3_4t(const u4v& x, u2v& h0, u2v& h1, u2v& h
 }
 __device__ __forceinline__ void split3_4(const u4v& x, u2v& h0, u2v& h1, u2v& h2) { split3_4t<false>(x, h0, h1, h2); }
 __device__ __forceinline__ void split3_4_rn(const u4v& x, u2v& h0, u2v& h1, u2v& h2) { split3_4t<true>(x, h0, h1, h2); }
+
+// ---------------------------------------------------------------------------
+// f32 arithmetic on the f16 matrix cores ("f16 x3", DG_F32 with dg_set_f32_math(2)): each
+// f32 operand, scaled by a power of two s into f16 range (|x*s| < 2^14; s per filter row, per
+// tensor for the pixel operand), is cut into two f16 parts by nearest rounding,
+// x*s = hi + lo + r with |lo| <= 2^-11 |x*s| and |r| <= 2^-23 |x*s|; a product is then
+// hi*hi + hi*lo + lo*hi, three v_mfma_f32_16x16x32_f16 per 16x16x32 block with f32
+// accumulation (f16 products are exact in f32), and the result is scaled back by the exact
+// 1/(s_a*s_b).  Dropped per product: lo*lo (<= 2^-22) and the parts' rounding (<= 2^-22),
+// two-sided.  Values below 2^-3 after scaling get a subnormal lo part: absolute error
+// <= 2^-25 in scaled units, i.e. <= 2^-39 of the operand's largest element.  Three 16-cycle
+// MFMAs per 32-deep block instead of the 3-way bf16 split's six.
+// ---------------------------------------------------------------------------
+typedef _Float16 dg_f16x2 __attribute__((ext_vector_type(2)));
+// power-of-two scale taking |x| <= amax below 2^14 (amax = m 2^e, m in [0.5, 1) -> 2^(14-e))
+__device__ __forceinline__ int h16_exp(float amax) {
+  if (!(amax > 0.f) || !(amax <= 3.4e38f)) return 0;
+  int e;
+  (void)frexpf(amax, &e);
+  return max(-100, min(100, 14 - e));
+}
+// the f16 parts of a pair (lo = a, hi = b in each packed dword) of x * s
+__device__ __forceinline__ void split2h_pair(float a, float b, float s, unsigned& ph, unsigned& pl) {
+  const dg_f32x2 v = dg_f32x2{a, b} * s;
+  const dg_f16x2 h = __builtin_convertvector(v, dg_f16x2);
+  const dg_f32x2 r = v - __builtin_convertvector(h, dg_f32x2);
+  ph = __builtin_bit_cast(unsigned, h);
+  pl = __builtin_bit_cast(unsigned, __builtin_convertvector(r, dg_f16x2));
+}
+// 8 f32 (x0[0..3], x1[0..3]) -> f16 parts hi / lo of x * s, element k of each part = float k
+__device__ __forceinline__ void split2h_8(const u4v& x0, const u4v& x1, float s, s8v& hi, s8v& lo) {
+  u4v ph, pl;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const unsigned a = k < 2 ? x0[2 * k] : x1[2 * k - 4];
+    const unsigned b = k < 2 ? x0[2 * k + 1] : x1[2 * k - 3];
+    unsigned qh, ql;
+    split2h_pair(__uint_as_float(a), __uint_as_float(b), s, qh, ql);
+    ph[k] = qh;
+    pl[k] = ql;
+  }
+  hi = __builtin_bit_cast(s8v, ph);
+  lo = __builtin_bit_cast(s8v, pl);
+}
+// the three products of one block, smallest first
+__device__ __forceinline__ f4v mfma_h3(const s8v& ah, const s8v& al, const s8v& bh, const s8v& bl, f4v c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, al), __builtin_bit_cast(h8v, bh), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah), __builtin_bit_cast(h8v, bl), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah), __builtin_bit_cast(h8v, bh), c, 0, 0, 0);
+  return c;
+}
+// 4 f32 -> the f16 parts of x * s (element k of part p = part p of x[k] * s)
+__device__ __forceinline__ void split2h_4(const u4v& x, float s, u2v& hi, u2v& lo) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    unsigned qh, ql;
+    split2h_pair(__uint_as_float(x[2 * k]), __uint_as_float(x[2 * k + 1]), s, qh, ql);
+    hi[k] = qh;
+    lo[k] = ql;
+  }
+}
+
+// max |v| of the values a block stored, folded into *out (f32 bits of a non-negative float:
+// an unsigned max, *out zeroed before the launch).  Every thread of the block calls it.
+__device__ __forceinline__ void block_amax_commit(float m, float* out) {
+  __shared__ float red[16];
+  m = wave_max(m);
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red[0];
+    for (int i = 1; i < nw; ++i) r = fmaxf(r, red[i]);
+    atomicMax((unsigned*)out, __float_as_uint(r));
+  }
+}

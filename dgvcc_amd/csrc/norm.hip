@@ -146,7 +146,7 @@ template <typename T>
 __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, long long ldz, int M, int C,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
                                                       int act, const float* __restrict__ drop, int HW,
-                                                      T* __restrict__ y, long long ldy) {
+                                                      T* __restrict__ y, long long ldy, float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
@@ -155,6 +155,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
   float sc[V], sf[V];
   ld_chan_row<V>(scale, c0, 1.f, sc);
   ld_chan_row<V>(shift, c0, 0.f, sf);
+  float m = 0.f;  // max |y| (amax: the f16 x3 convs' operand scale)
   for (long long p = gt / tpp; p < M; p += pstride) {
     float v[V];
     ldv(z + p * ldz + c0, v);
@@ -170,7 +171,10 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
       for (int e = 0; e < V; ++e) v[e] *= d[e];
     }
     stv(y + p * ldy + c0, v);
+#pragma unroll
+    for (int e = 0; e < V; ++e) m = fmaxf(m, fabsf(v[e]));
   }
+  if (amax) block_amax_commit(m, amax);
 }
 
 // Per-thread channel-chunk parameters (registers).
@@ -402,7 +406,8 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
                                                    long long ldz, int M, int C, const float* mean, const float* invstd,
                                                    const float* scale, const float* shift, int act, const float* drop,
                                                    int HW, const float* __restrict__ coef, T* __restrict__ dz,
-                                                   long long lddz) {
+                                                   long long lddz, float* __restrict__ amax) {
+  float m = 0.f;  // max |dz| (amax)
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
@@ -455,6 +460,8 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
         f(g1, z1);
         stv(dz + p * lddz + c0, g0);
         stv(dz + q * lddz + c0, g1);
+#pragma unroll
+        for (int e = 0; e < V; ++e) m = fmaxf(m, fmaxf(fabsf(g0[e]), fabsf(g1[e])));
       }
     }
     for (; p < M; p += pstride) {
@@ -464,6 +471,8 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
       bn_mask_t<V, DROP, ACT>(p, c0, C, cp, drop, HW, gv, zv);
       f(gv, zv);
       stv(dz + p * lddz + c0, gv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) m = fmaxf(m, fabsf(gv[e]));
     }
   };
   if constexpr (U == 1) {  // the round-3 loop (runtime dropout / ReLU flags)
@@ -472,6 +481,8 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
       bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
       f(gv, zv);
       stv(dz + p * lddz + c0, gv);
+#pragma unroll
+      for (int e = 0; e < V; ++e) m = fmaxf(m, fabsf(gv[e]));
     }
   } else if (drop) {
     if (act == 1) run(std::true_type{}, std::true_type{});
@@ -480,6 +491,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
     if (act == 1) run(std::false_type{}, std::true_type{});
     else run(std::false_type{}, std::false_type{});
   }
+  if (amax) block_amax_commit(m, amax);
 }
 
 // ---------------------------------------------------------------------------
@@ -522,7 +534,9 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
                                                            long long Mp, int C, const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int act,
                                                            const float* __restrict__ drop, int HW, T* __restrict__ y,
-                                                           long long ldy, T* __restrict__ yp, long long ldyp) {
+                                                           long long ldy, T* __restrict__ yp, long long ldyp,
+                                                           float* __restrict__ amax) {
+  float m = 0.f;  // max |y| over the window values (>= max |yp|: amax of both)
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
@@ -546,6 +560,7 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
         if (act == 1) t = t > 0.f ? t : 0.f;
         if (d) t *= d[e];
         v[k][e] = rnd_t<T>(t);
+        m = fmaxf(m, fabsf(v[k][e]));
       }
       if (y) stv(y + pos[k] * ldy + c0, v[k]);
     }
@@ -554,6 +569,7 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
     for (int e = 0; e < V; ++e) o[e] = v[first_max4(v[0][e], v[1][e], v[2][e], v[3][e])][e];
     stv(yp + pp * ldyp + c0, o);
   }
+  if (amax) block_amax_commit(m, amax);
 }
 
 // The pooled backward keeps 4 pixels x V channels of z and g live per thread: V = 4
@@ -672,8 +688,9 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
                                                         long long Mp, int C, const float* mean, const float* invstd,
                                                         const float* scale, const float* shift, int act,
                                                         const float* drop, int HW, const float* __restrict__ coef,
-                                                        T* __restrict__ dz, long long lddz) {
+                                                        T* __restrict__ dz, long long lddz, float* __restrict__ amax) {
   constexpr int V = POOL_V;
+  float m = 0.f;  // max |dz|
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
@@ -695,10 +712,12 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
       for (int e = 0; e < V; ++e) {
         const float xh = (zv[k][e] - cp.mu[e]) * cp.is[e];
         gv[k][e] = k1[e] * gv[k][e] - k2[e] * xh - k3[e];
+        m = fmaxf(m, fabsf(gv[k][e]));
       }
       stn<V>(dz + pos[k] * lddz + c0, gv[k]);
     }
   }
+  if (amax) block_amax_commit(m, amax);
 }
 
 inline int ew_grid(long long n) {
@@ -732,11 +751,15 @@ int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, 
   return DG_OK;
 }
 
+// amax (may be NULL): max |dz| of the apply pass (dg_common.h block_amax_commit)
+static int zero_amax(float* amax, hipStream_t st) {
+  return amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess ? DG_ERR_HIP : DG_OK;
+}
 template <typename T>
 int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int M, int C, const float* gamma,
                 const float* mean, const float* inv, const float* scale, const float* shift, int act,
                 const float* drop, int HW, void* dz, long long lddz, float* dgamma, float* dbeta, float* dbias,
-                void* ws, hipStream_t st, float* coef_out = nullptr) {
+                void* ws, hipStream_t st, float* coef_out = nullptr, float* amax = nullptr) {
   const int nblk = bn_nblk(M);
   const int ppb = dg_cdiv(M, nblk);
   float* part = (float*)ws;
@@ -748,9 +771,10 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
                      dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
   if (!dz) return DG_OK;  // coefficients only (a fused consumer applies them)
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
   hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<T, 2> : bn_bwd_apply<T, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
-                     mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz);
+                     mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -784,22 +808,23 @@ extern "C" int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int
 }
 
 extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float* scale, const float* shift,
-                           int act, const float* drop, int HW, void* y, int64_t ldy, void* stream) {
+                           int act, const float* drop, int HW, void* y, int64_t ldy, float* amax, void* stream) {
   DG_REQUIRE(z && y && scale && shift && M > 0 && C > 0 && ldz >= C && ldy >= C && (act == 0 || act == 1));
   DG_REQUIRE(!drop || HW > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, ldy));
   hipStream_t st = (hipStream_t)stream;
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
-                       shift, act, drop, HW, (bf16*)y, ldy);
+                       shift, act, drop, HW, (bf16*)y, ldy, amax);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL(bn_apply_kernel<f16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
-                       shift, act, drop, HW, (f16*)y, ldy);
+                       shift, act, drop, HW, (f16*)y, ldy, amax);
   else
     hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
-                       scale, shift, act, drop, HW, (float*)y, ldy);
+                       scale, shift, act, drop, HW, (float*)y, ldy, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -807,7 +832,7 @@ extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, 
 extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
                          const float* gamma, const float* save_mean, const float* save_invstd, const float* scale,
                          const float* shift, int act, const float* drop, int HW, void* dz, int64_t lddz,
-                         float* dgamma, float* dbeta, float* dbias, void* workspace, void* stream) {
+                         float* dgamma, float* dbeta, float* dbias, void* workspace, float* amax, void* stream) {
   DG_REQUIRE(g && z && dz && workspace && M > 0 && C > 0);
   DG_REQUIRE((save_mean && save_invstd && scale && shift) || (!save_mean && !save_invstd));
   DG_REQUIRE(!drop || HW > 0);
@@ -816,10 +841,10 @@ extern "C" int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, i
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16
              ? bn_bwd_impl<bf16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW, dz,
-                                 lddz, dgamma, dbeta, dbias, workspace, st)
+                                 lddz, dgamma, dbeta, dbias, workspace, st, nullptr, amax)
              : dtype == DG_F16 ? bn_bwd_impl<f16>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW, dz,
-                                 lddz, dgamma, dbeta, dbias, workspace, st) : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
-                                  dz, lddz, dgamma, dbeta, dbias, workspace, st);
+                                 lddz, dgamma, dbeta, dbias, workspace, st, nullptr, amax) : bn_bwd_impl<float>(g, ldg, z, ldz, M, C, gamma, save_mean, save_invstd, scale, shift, act, drop, HW,
+                                  dz, lddz, dgamma, dbeta, dbias, workspace, st, nullptr, amax);
 }
 
 // dg_bn_bwd with the partial sums already computed by the producer of g (the dgrad
@@ -828,7 +853,7 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
                                    int64_t ldz, int M, int C, const float* gamma, const float* save_mean,
                                    const float* save_invstd, const float* scale, const float* shift, int act,
                                    const float* drop, int HW, void* dz, int64_t lddz, float* dgamma, float* dbeta,
-                                   float* dbias, float* coef, void* stream) {
+                                   float* dbias, float* coef, float* amax, void* stream) {
   DG_REQUIRE(part && nblk > 0 && g && z && dz && coef && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
   DG_REQUIRE(!drop || HW > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
@@ -837,19 +862,20 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, save_invstd,
                      dgamma, dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   if (dtype == DG_BF16) {
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz, amax);
   } else if (dtype == DG_F16) {
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax);
   } else {
     const long long total = (long long)M * (C / 4);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
-                       (float*)dz, lddz);
+                       (float*)dz, lddz, amax);
   }
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -887,24 +913,25 @@ extern "C" int dg_bn_bwd_coef(int dtype, const void* g, int64_t ldg, const void*
 
 extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, int H, int W, int C,
                                 const float* scale, const float* shift, int act, const float* drop, void* y,
-                                int64_t ldy, void* yp, int64_t ldyp, void* stream) {
+                                int64_t ldy, void* yp, int64_t ldyp, float* amax, void* stream) {
   DG_REQUIRE(z && yp && scale && shift && N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
   DG_REQUIRE(ldz >= C && ldyp >= C && (!y || ldy >= C));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldz) &&
                BN_SHAPE_OK(dtype, C, ldyp) && (!y || BN_SHAPE_OK(dtype, C, ldy)));
   hipStream_t st = (hipStream_t)stream;
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   const long long Mp = (long long)N * (H / 2) * (W / 2);
   const long long total = Mp * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_apply_pool_kernel<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, H, W,
-                       Mp, C, scale, shift, act, drop, H * W, (bf16*)y, ldy, (bf16*)yp, ldyp);
+                       Mp, C, scale, shift, act, drop, H * W, (bf16*)y, ldy, (bf16*)yp, ldyp, amax);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL(bn_apply_pool_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, H, W,
-                       Mp, C, scale, shift, act, drop, H * W, (f16*)y, ldy, (f16*)yp, ldyp);
+                       Mp, C, scale, shift, act, drop, H * W, (f16*)y, ldy, (f16*)yp, ldyp, amax);
   else
     hipLaunchKernelGGL(bn_apply_pool_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, H,
-                       W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp);
+                       W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -914,7 +941,7 @@ static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long
                             long long ldz, int N, int H, int W, int C, const float* gamma, const float* mean,
                             const float* inv, const float* scale, const float* shift, int act, const float* drop,
                             void* dz, long long lddz, float* dgamma, float* dbeta, float* dbias, void* ws,
-                            hipStream_t st) {
+                            hipStream_t st, float* amax = nullptr) {
   const long long M = (long long)N * H * W, Mp = M / 4;
   const int nblk = pool_nblk(Mp);
   const long long ppb = (Mp + nblk - 1) / nblk;
@@ -927,9 +954,10 @@ static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long
                      dgamma, dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
   const long long total = Mp * (C / POOL_V);
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   hipLaunchKernelGGL(bn_pool_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd,
                      ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop, H * W, coef, (T*)dz,
-                     lddz);
+                     lddz, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -938,7 +966,7 @@ extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const voi
                               int64_t ldz, int N, int H, int W, int C, const float* gamma, const float* save_mean,
                               const float* save_invstd, const float* scale, const float* shift, int act,
                               const float* drop, void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
-                              void* workspace, void* stream) {
+                              void* workspace, float* amax, void* stream) {
   DG_REQUIRE(gp && z && dz && workspace && save_mean && save_invstd && scale && shift);
   DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
@@ -948,10 +976,10 @@ extern "C" int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const voi
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16
              ? bn_pool_bwd_impl<bf16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
-                                      shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st)
+                                      shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st, amax)
              : dtype == DG_F16 ? bn_pool_bwd_impl<f16>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
-                                      shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st) : bn_pool_bwd_impl<float>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
-                                       shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st);
+                                      shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st, amax) : bn_pool_bwd_impl<float>(gp, ldgp, gd, ldgd, z, ldz, N, H, W, C, gamma, save_mean, save_invstd, scale,
+                                       shift, act, drop, dz, lddz, dgamma, dbeta, dbias, workspace, st, amax);
 }
 
 // ---------------------------------------------------------------------------
@@ -1065,23 +1093,24 @@ extern "C" int dg_bn_bwd_finalize_sync(const float* sums_local, const float* sum
 extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
                                     const float* save_mean, const float* save_invstd, const float* scale,
                                     const float* shift, int act, const float* drop, int HW, const float* coef,
-                                    void* dz, int64_t lddz, void* stream) {
+                                    void* dz, int64_t lddz, float* amax, void* stream) {
   DG_REQUIRE(g && z && dz && coef && save_mean && save_invstd && scale && shift && M > 0 && C > 0);
   DG_REQUIRE(!drop || HW > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
   hipStream_t st = (hipStream_t)stream;
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz, amax);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax);
   else
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
-                       (float*)dz, lddz);
+                       (float*)dz, lddz, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -1090,7 +1119,7 @@ extern "C" int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp
                                          const void* z, int64_t ldz, int N, int H, int W, int C,
                                          const float* save_mean, const float* save_invstd, const float* scale,
                                          const float* shift, int act, const float* drop, const float* coef, void* dz,
-                                         int64_t lddz, void* stream) {
+                                         int64_t lddz, float* amax, void* stream) {
   DG_REQUIRE(gp && z && dz && coef && save_mean && save_invstd && scale && shift);
   DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && (act == 0 || act == 1));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
@@ -1100,18 +1129,19 @@ extern "C" int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp
   hipStream_t st = (hipStream_t)stream;
   const long long Mp = (long long)N * (H / 2) * (W / 2);
   const long long total = Mp * (C / POOL_V);
+  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_pool_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)gp, ldgp,
                        (const bf16*)gd, ldgd, (const bf16*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift,
-                       act, drop, H * W, coef, (bf16*)dz, lddz);
+                       act, drop, H * W, coef, (bf16*)dz, lddz, amax);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL(bn_pool_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)gp, ldgp,
                        (const f16*)gd, ldgd, (const f16*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift,
-                       act, drop, H * W, coef, (f16*)dz, lddz);
+                       act, drop, H * W, coef, (f16*)dz, lddz, amax);
   else
     hipLaunchKernelGGL(bn_pool_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)gp, ldgp,
                        (const float*)gd, ldgd, (const float*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale,
-                       shift, act, drop, H * W, coef, (float*)dz, lddz);
+                       shift, act, drop, H * W, coef, (float*)dz, lddz, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

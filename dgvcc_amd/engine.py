@@ -465,6 +465,15 @@ def feature_plans_of(params) -> list:
     return [plan for plan in list(_FEATURE_PLANS) if all(p in ps for p in plan.params())]
 
 
+def _cat_act(buf: torch.Tensor, up_src: Act, skip: Act) -> Act:
+    """The decoder concatenation [up2(up_src) | skip] as one Act; its amax (the f32 convs' operand
+    scale) bounds both parts: bilinear upsampling does not exceed its source's max |.|."""
+    a = Act(buf)
+    if up_src.amax is not None and skip.amax is not None:
+        a.amax = torch.maximum(up_src.amax, skip.amax)
+    return a
+
+
 class FeaturePlan:
     """forward_fe of DGModel_base: img [N,3,H,W] f32 -> (y1, y2, y3, x3) NHWC, where the
     reference's y_cat = cat[y1, up2(y2), up4(y3)] (models/models.py:84) is left to the heads'
@@ -545,10 +554,10 @@ class FeaturePlan:
         a13 = nh(H // 16, W // 16, 1024); D[0].forward(x3, a13, training, tape)
         y3 = nh(H // 16, W // 16, 512); D[1].forward(a13, y3, training, tape)
         K.upsample_fwd(y3, 2, K.UP_BILINEAR, Act(dec2in, 0, 512))
-        a15 = nh(H // 8, W // 8, 512); D[2].forward(Act(dec2in), a15, training, tape)
+        a15 = nh(H // 8, W // 8, 512); D[2].forward(_cat_act(dec2in, y3, x2), a15, training, tape)
         y2 = nh(H // 8, W // 8, 256); D[3].forward(a15, y2, training, tape)
         K.upsample_fwd(y2, 2, K.UP_BILINEAR, Act(dec1in, 0, 256))
-        a17 = nh(H // 4, W // 4, 256); D[4].forward(Act(dec1in), a17, training, tape)
+        a17 = nh(H // 4, W // 4, 256); D[4].forward(_cat_act(dec1in, y2, x1), a17, training, tape)
         y1 = nh(H // 4, W // 4, 128); D[5].forward(a17, y1, training, tape)
         if tape is not None:
             tape[self] = dict(dec1in=dec1in, dec2in=dec2in, shape=(N, H, W), dt=dt, inst=inst, x1=x1, x2=x2, x3=x3)

@@ -17,10 +17,13 @@ F32, BF16, F16 = 0, 1, 2
 
 @dataclass
 class Act:
-    """Channel slice [off, off+C) of an NHWC buffer `buf` [N,H,W,Ctot]."""
+    """Channel slice [off, off+C) of an NHWC buffer `buf` [N,H,W,Ctot].  amax: None, or a device
+    f32 [1] >= max |slice| set by the kernel that wrote it (the f32 convs' operand scale, f16 x3
+    arithmetic; None makes the conv take one read pass over the slice for it)."""
     buf: torch.Tensor
     off: int = 0
     C: int | None = None
+    amax: torch.Tensor | None = None
 
     def __post_init__(self):
         if self.buf.dim() != 4:
@@ -106,9 +109,10 @@ def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
     es = x.buf.element_size()
     nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout * (2 if accumulate else 1))  # x, w, y (+y read)
     ws, work = _fwd_workspace(x, Cout, R)
+    y.amax = None  # y is (re)written by a conv: no tracked maximum
     _timed(kind, flops, lambda: call("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
                                      Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate), None,
-                                     ptr(work), ws, stream()), nbytes)
+                                     ptr(work), ws, ptr(x.amax), stream()), nbytes)
 
 
 def conv_fwd_bn_eval(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act, bias, stats, act: int):
@@ -116,9 +120,10 @@ def conv_fwd_bn_eval(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: A
     flops = 2.0 * x.M * x.C * R * R * Cout
     nbytes = x.buf.element_size() * (x.M * x.C + wp.numel() + x.M * Cout)
     ws, work = _fwd_workspace(x, Cout, R)
+    y.amax = None
     _timed("fwd", flops, lambda: call("dg_conv_fwd_bn_eval", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
                                       R, R, pad, ptr(bias), ptr(stats[2]), ptr(stats[3]), act, y.ptr, y.ld,
-                                      ptr(work), ws, stream()), nbytes)
+                                      ptr(work), ws, ptr(x.amax), stream()), nbytes)
 
 
 _FWD_WS: dict = {}
@@ -135,6 +140,13 @@ def _fwd_workspace(x: Act, Cout: int, R: int):
     if ws == 0:
         return 0, None
     return ws, torch.empty(ws, dtype=torch.uint8, device=x.buf.device)
+
+
+def amax(x: Act) -> torch.Tensor:
+    """max |x| over the slice (f32), a device f32 [1] (dg_amax)."""
+    out = torch.empty(1, dtype=torch.float32, device=x.buf.device)
+    call("dg_amax", x.dt, x.ptr, x.ld, x.M, x.C, ptr(out), stream())
+    return out
 
 
 def flip_weight(wp: torch.Tensor, Cout: int, C: int, R: int) -> torch.Tensor:
@@ -155,12 +167,13 @@ def conv_dgrad_acc_relu(dy: Act, wp: torch.Tensor, C: int, dx: Act, relu_out: Ac
     launched) for the shapes that launch does not serve: the caller runs conv_dgrad + relu_bwd."""
     wflip = flip_weight(wp, dy.C, C, 1)
     ws, work = _fwd_workspace(dy, C, 1)
+    dx.amax = None
     flops = 2.0 * dy.M * dy.C * C
     nbytes = dy.buf.element_size() * (dy.M * dy.C + wflip.numel() + 3 * dy.M * C)
     res = []
     _timed("dgrad", flops, lambda: res.append(lib_call_status(
         "dg_conv_fwd_acc_relu", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W, dy.C, ptr(wflip), C, relu_out.ptr,
-        relu_out.ld, dx.ptr, dx.ld, ptr(work), ws, stream())), nbytes)
+        relu_out.ld, dx.ptr, dx.ld, ptr(work), ws, ptr(dy.amax), stream())), nbytes)
     if res[0] == -2:
         return False
     if res[0] != 0:
@@ -191,6 +204,7 @@ def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: A
             else query("dg_conv_stats_rows", dy.N, dy.H, dy.W))
     part = torch.empty((rows, 3, C), dtype=torch.float32, device=dy.buf.device)
     ws, work = _fwd_workspace(dy, C, R)
+    dx.amax = None
     flops = 2.0 * dy.M * dy.C * R * R * C
     nbytes = dy.buf.element_size() * (dy.M * dy.C + wflip.numel() + 2 * dy.M * C)
     res = []
@@ -199,7 +213,7 @@ def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: A
         res.append(lib_call_status("dg_conv_fwd_bnbwd", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W, dy.C, ptr(wflip), C,
                                    R, R, R - 1 - pad, dx.ptr, dx.ld, z.ptr, z.ld, ptr(stats[2]), ptr(stats[3]),
                                    ptr(stats[0]), ptr(stats[1]), act, ptr(drop), z.H * z.W, ptr(part), ptr(work),
-                                   ws, stream()))
+                                   ws, ptr(dy.amax), stream()))
 
     _timed("dgrad", flops, launch, nbytes)
     if res[0] == -2:
@@ -214,9 +228,10 @@ def bn_bwd_from_part(pre, g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamm
     """bn_bwd with the partial sums from conv_dgrad_bnpart."""
     part, rows = pre
     coef = torch.empty((3, z.C), dtype=torch.float32, device=z.buf.device)
+    am = _amax_out(dz)
     call("dg_bn_bwd_from_part", z.dt, ptr(part), rows, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma),
          ptr(stats[0]), ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, dz.ptr, dz.ld,
-         ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), stream())
+         ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), ptr(am), stream())
 
 
 def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=False, k_alg=None):
@@ -226,7 +241,7 @@ def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=F
     nbytes = x.buf.element_size() * (x.M * x.C + dy.M * dy.C) + 4 * dw.numel()
     _timed("wgrad", flops, lambda: call("dg_conv_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
                                         dy.ptr, dy.ld, dy.C, R, R, pad, ptr(dw), ptr(work), ws,
-                                        int(accumulate), stream()), nbytes)
+                                        int(accumulate), ptr(x.amax), ptr(dy.amax), stream()), nbytes)
 
 
 def im2col_c3(img: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
@@ -316,10 +331,12 @@ def conv_fwd_stats(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act
     if _EPI_STATS_OFF:
         return None
     ws, work = _fwd_workspace(x, Cout, R)
+    y.amax = None
 
     def launch():
         res.append(lib_call_status("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
-                                   R, R, pad, ptr(bias), y.ptr, y.ld, 0, ptr(part), ptr(work), ws, stream()))
+                                   R, R, pad, ptr(bias), y.ptr, y.ld, 0, ptr(part), ptr(work), ws, ptr(x.amax),
+                                   stream()))
 
     _timed("fwd", flops, launch, nbytes)
     if res[0] == -2:  # DG_ERR_UNSUPPORTED: nothing was launched
@@ -409,9 +426,22 @@ def bn_eval_stats(gamma, beta, running_mean, running_var, eps):
     return torch.stack([running_mean, invstd, scale, shift])
 
 
+def _amax_out(a: Act | None, *more: Act | None) -> torch.Tensor | None:
+    """A fresh device f32 [1] that an f32 producer fills with max |output|, attached to the Acts
+    it writes (the following f16 x3 convs' operand scale); None for 16-bit outputs."""
+    if a is None or a.buf.dtype != torch.float32:
+        return None
+    t = torch.empty(1, dtype=torch.float32, device=a.buf.device)
+    for o in (a, *more):
+        if o is not None:
+            o.amax = t
+    return t
+
+
 def bn_apply(z: Act, stats, act: int, y: Act, drop: torch.Tensor | None = None):
+    am = _amax_out(y)
     call("dg_bn_apply", z.dt, z.ptr, z.ld, z.M, z.C, ptr(stats[2]), ptr(stats[3]), act, ptr(drop),
-         z.H * z.W, y.ptr, y.ld, stream())
+         z.H * z.W, y.ptr, y.ld, ptr(am), stream())
 
 
 def bn_bwd(g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias=None,
@@ -419,15 +449,17 @@ def bn_bwd(g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias
     ws = query("dg_bn_workspace", z.M, z.C)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
     st = stats if stats is not None else (None, None, None, None)  # None: no normalisation
+    am = _amax_out(dz)
     call("dg_bn_bwd", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma), ptr(st[0]),
          ptr(st[1]), ptr(st[2]), ptr(st[3]), act, ptr(drop), z.H * z.W, dz.ptr, dz.ld,
-         ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), stream())
+         ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), ptr(am), stream())
 
 
 def bn_apply_pool(z: Act, stats, act: int, y: Act | None, yp: Act, drop: torch.Tensor | None = None):
     """y = act(BN(z)) [* drop] (only written when y is given) and yp = maxpool2x2(y)."""
+    am = _amax_out(yp, y)  # max over the un-pooled values bounds both
     call("dg_bn_apply_pool", z.dt, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(stats[2]), ptr(stats[3]), act,
-         ptr(drop), y.ptr if y is not None else None, y.ld if y is not None else 0, yp.ptr, yp.ld, stream())
+         ptr(drop), y.ptr if y is not None else None, y.ld if y is not None else 0, yp.ptr, yp.ld, ptr(am), stream())
 
 
 def bn_bwd_pool(gp: Act, gd: Act | None, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta,
@@ -436,10 +468,11 @@ def bn_bwd_pool(gp: Act, gd: Act | None, z: Act, gamma, stats, act: int, dz: Act
     from z) [+ the direct gradient gd]."""
     ws = query("dg_bn_workspace", z.M, z.C)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
+    am = _amax_out(dz)
     call("dg_bn_bwd_pool", z.dt, gp.ptr, gp.ld, gd.ptr if gd is not None else None,
          gd.ld if gd is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(gamma), ptr(stats[0]),
          ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), dz.ptr, dz.ld, ptr(dgamma),
-         ptr(dbeta), ptr(dbias), ptr(work), stream())
+         ptr(dbeta), ptr(dbias), ptr(work), ptr(am), stream())
 
 
 # ---------------------------------------------------------------- resample -

@@ -157,13 +157,14 @@ def bwd_coef(bn, pg, sums: torch.Tensor, M_local: int, stats, dgamma, dbeta, dbi
 
 
 def bwd_apply(g: K.Act, z: K.Act, stats, act: int, coef, dz: K.Act, drop=None, g_pool: K.Act | None = None):
+    am = K._amax_out(dz)
     if g_pool is not None:
         call("dg_bn_bwd_pool_apply_coef", z.dt, g_pool.ptr, g_pool.ld, g.ptr if g is not None else None,
              g.ld if g is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(stats[0]), ptr(stats[1]),
-             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), ptr(coef), dz.ptr, dz.ld, stream())
+             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), ptr(coef), dz.ptr, dz.ld, ptr(am), stream())
     else:
         call("dg_bn_bwd_apply_coef", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(stats[0]), ptr(stats[1]),
-             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, ptr(coef), dz.ptr, dz.ld, stream())
+             ptr(stats[2]), ptr(stats[3]), act, ptr(drop), z.H * z.W, ptr(coef), dz.ptr, dz.ld, ptr(am), stream())
 
 
 def backward(bn, pg, g: K.Act | None, z: K.Act, stats, act: int, dz: K.Act | None, dgamma, dbeta, dbias=None,

@@ -46,10 +46,16 @@ int dg_set_persist(int mode);
 /* f32 GEMM arithmetic of the DG_F32 convolutions: 0 = v_mfma_f32_16x16x4_f32;
  * 1 = exact 3-way bf16 split of both operands (x = h0 + h1 + h2), six
  * v_mfma_f32_16x16x32_bf16 products per block, f32 accumulation (the truncated parts
- * drop terms up to ~2^-20 |x*y|, typically ~2^-22, one-sided; see dg_common.h).  Default from DGVCC_F32_MATH (exact | split), else 1. */
+ * drop terms up to ~2^-20 |x*y|, typically ~2^-22, one-sided; see dg_common.h).  Default from DGVCC_F32_MATH (exact | split | h16), else 2. */
 int dg_set_f32_math(int mode);
+/* mode 2 (the default since ABI 3; DGVCC_F32_MATH=split selects 1) = 1 with the "f16 x3"
+ * arithmetic where a kernel has it (the pre-split forward/dgrad, the 3-tap Cout = 64 forward,
+ * the split weight gradients):
+ * each f32 operand scaled by a power of two into f16 range and cut into two f16 parts by
+ * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
+ * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 2 /* 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes); the f32 workspace holds the pre-split planes */
+#define DGVCC_ABI_VERSION 3 /* 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -97,7 +103,13 @@ int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, i
  * (bias, accumulate and the statistics partials in the reduce pass). */
 int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                    int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
-                   int accumulate, float* part, void* workspace, int64_t ws_bytes, void* stream);
+                   int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
+                   void* stream);
+/* xamax (f32 entries, f16 x3 arithmetic): NULL, or a device float >= max |x| over the operand
+ * (dg_amax, or the kernel that produced x); NULL makes the library take one read pass over x
+ * for it.  An xamax below the true maximum is undefined behaviour (f16 overflow). */
+/* out[0] (device f32) = max |x| over the M x C f32 rows of pixel stride ldx. */
+int dg_amax(int dtype, const void* x, int64_t ldx, int64_t M, int C, float* out, void* stream);
 /* y = (relu_out > 0) ? conv1x1(x, w) + y : 0: the accumulating dgrad of a bottleneck's conv1 (w
  * flipped, dg_flip_weight) whose input relu_out is the previous block's ReLU output
  * (models/SW/backbones/resnet.py:77 Bottleneck.forward's final relu, autograd's ReLU backward),
@@ -107,7 +119,7 @@ int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, i
  * launch splits over K with this workspace. */
 int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                          int Cout, const void* relu_out, int64_t ldr, void* y, int64_t ldy, void* workspace,
-                         int64_t ws_bytes, void* stream);
+                         int64_t ws_bytes, const float* xamax, void* stream);
 /* Eval-mode Conv + BatchNorm(running stats) [+ ReLU]: y = act((conv(x) + bias) * scale + shift)
  * with scale = gamma/sqrt(running_var+eps), shift = beta - running_mean*scale applied in the conv
  * epilogue (z never stored);
@@ -115,7 +127,7 @@ int dg_conv_fwd_acc_relu(int dtype, const void* x, int64_t ldx, int N, int H, in
 int dg_conv_fwd_bn_eval(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
                         int Cout, int R, int S, int pad, const float* bias, const float* scale,
                         const float* shift, int act, void* y, int64_t ldy, void* workspace, int64_t ws_bytes,
-                        void* stream);
+                        const float* xamax, void* stream);
 /* bf16 forward (used for dgrad: flipped filters) that also emits the BatchNorm-backward
  * partial sums of the layer whose output gradient y is, from the epilogue:
  * bpart[dg_conv_stats_rows][3][Cout] for dg_bn_bwd_from_part (replaces dg_bn_bwd's
@@ -126,7 +138,7 @@ int dg_conv_fwd_bnbwd(int dtype, const void* x, int64_t ldx, int N, int H, int W
                       int Cout, int R, int S, int pad, void* y, int64_t ldy, const void* z, int64_t ldz,
                       const float* scale, const float* shift, const float* mean, const float* invstd,
                       int act, const float* drop, int HW, float* bpart, void* workspace, int64_t ws_bytes,
-                      void* stream);
+                      const float* xamax, void* stream);
 
 /* wflip[C][R][S][Cout] = w[Cout][R-1-r][S-1-s][C] (packed filters of dtype). */
 int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void* wflip, void* stream);
@@ -136,7 +148,9 @@ int dg_flip_weight(int dtype, const void* w, int Cout, int C, int R, int S, void
 int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S);
 int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                   const void* dy, int64_t lddy, int Cout, int R, int S, int pad,
-                  float* dw, void* workspace, int64_t ws_bytes, int accumulate, void* stream);
+                  float* dw, void* workspace, int64_t ws_bytes, int accumulate, const float* xamax,
+                  const float* dyamax, void* stream);
+/* xamax / dyamax: as dg_conv_fwd_ex's xamax, for x and dy (f32, f16 x3 arithmetic). */
 
 /* torch [Cout][C][R][S] f32 -> packed rows out[Cout][row_len] of dtype holding
  * [R][S][Cpad] (zero-padded C, zero tail up to row_len). Cpad=3,row_len=64 gives
@@ -190,7 +204,11 @@ int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C,
  * (Dropout2d mask already scaled by 1/(1-p), models/models.py:55-58). HW = pixels per image. */
 int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float* scale,
                 const float* shift, int act, const float* drop, int HW, void* y, int64_t ldy,
-                void* stream);
+                float* amax, void* stream);
+/* amax (here and on the BN-backward / pooled entries below; may be NULL): a device float that
+ * receives max |output| of the pass (the written activation or dz; the pooled entries: over the
+ * un-pooled values, >= max |yp|) -- the xamax a following f32 conv can take instead of a read
+ * pass of its own. */
 /* Backward: g = dL/dy (pixel stride ldg).  Produces dz (lddz), dgamma, dbeta
  * (written, not accumulated) and dbias_conv (sum dz, may be NULL).
  * save_mean = save_invstd = NULL: no normalisation (a biased conv + activation, e.g. the
@@ -201,7 +219,7 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               const float* gamma, const float* save_mean, const float* save_invstd,
               const float* scale, const float* shift, int act, const float* drop, int HW,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
-              void* workspace, void* stream);
+              void* workspace, float* amax, void* stream);
 /* BN-backward finalize on caller-made partial sums part[nblk][3][C] = (sum g', sum g' xhat,
  * sum xhat): coef[3][C] (dz = k1 g' - k2 xhat - k3) and dgamma/dbeta/dbias (may be NULL). */
 int dg_bn_bwd_finalize_part(const float* part, int nblk, int M, int C, const float* gamma,
@@ -213,7 +231,7 @@ int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const void* g, i
                         int64_t ldz, int M, int C, const float* gamma, const float* save_mean,
                         const float* save_invstd, const float* scale, const float* shift, int act,
                         const float* drop, int HW, void* dz, int64_t lddz, float* dgamma, float* dbeta,
-                        float* dbias, float* coef, void* stream);
+                        float* dbias, float* coef, float* amax, void* stream);
 
 /* BN(+ReLU) fused with the following MaxPool2d(2,2) (vgg16_bn.features[5:7] etc.,
  * models/models.py:35-38).  Apply: y = act(z*scale+shift)*drop (written only when y != NULL,
@@ -223,12 +241,12 @@ int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const void* g, i
  * H, W even; workspace of dg_bn_workspace(N*H*W, C) bytes. */
 int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, int H, int W, int C,
                      const float* scale, const float* shift, int act, const float* drop, void* y,
-                     int64_t ldy, void* yp, int64_t ldyp, void* stream);
+                     int64_t ldy, void* yp, int64_t ldyp, float* amax, void* stream);
 int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
                    const void* z, int64_t ldz, int N, int H, int W, int C, const float* gamma,
                    const float* save_mean, const float* save_invstd, const float* scale,
                    const float* shift, int act, const float* drop, void* dz, int64_t lddz,
-                   float* dgamma, float* dbeta, float* dbias, void* workspace, void* stream);
+                   float* dgamma, float* dbeta, float* dbias, void* workspace, float* amax, void* stream);
 
 /* Coefficients of the BN backward without the dz pass: coef[3][C] = (k1, k2, k3) with
  * dz = k1*act'(g) - k2*xhat - k3 (the bn_bwd_apply arithmetic), plus dgamma/dbeta/dbias.
@@ -279,11 +297,12 @@ int dg_bn_bwd_finalize_sync(const float* sums_local, const float* sums_global, i
 int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz, int M, int C,
                          const float* save_mean, const float* save_invstd, const float* scale,
                          const float* shift, int act, const float* drop, int HW, const float* coef, void* dz,
-                         int64_t lddz, void* stream);
+                         int64_t lddz, float* amax, void* stream);
 int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
                               const void* z, int64_t ldz, int N, int H, int W, int C, const float* save_mean,
                               const float* save_invstd, const float* scale, const float* shift, int act,
-                              const float* drop, const float* coef, void* dz, int64_t lddz, void* stream);
+                              const float* drop, const float* coef, void* dz, int64_t lddz, float* amax,
+                              void* stream);
 
 /* ---- fused first layer (bf16): Conv2d(3,64,3,pad 1) of vgg16_bn.features[0]
  * (models/models.py:35-36) read straight from the NCHW f32 image (no im2col buffer).

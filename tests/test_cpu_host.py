@@ -16,7 +16,7 @@ def test_library_exports_every_header_symbol():
     lib = _capi.lib()
     missing = [n for n in protos if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.dg_version() == _capi.header_abi_version() == 2
+    assert lib.dg_version() == _capi.header_abi_version() == 3
     assert len(protos) >= 30
 
 
@@ -117,14 +117,14 @@ def test_f32_stats_rows_need_split_room():
     for (N, H, W, C, Co) in ((16, 48, 64, 512, 512), (4, 64, 512, 64, 64), (16, 192, 256, 256, 256)):
         ws = L.dg_conv_fwd_workspace(0, N, H, W, C, Co, 3, 3)
         # x, w, y, part: dummy non-null pointers (the call returns before any launch)
-        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, None, 0, None) == -2
-        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, 8, ws - 256, None) == -2
+        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, None, 0, None, None) == -2
+        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, 8, ws - 256, None, None) == -2
 
 
 def test_call_raises_on_error():
     from dgvcc_amd import _capi
     with pytest.raises(_capi.DGError):
-        _capi.call("dg_bn_apply", 0, None, 0, 0, 0, None, None, 0, None, 0, None, 0, None)
+        _capi.call("dg_bn_apply", 0, None, 0, 0, 0, None, None, 0, None, 0, None, 0, None, None)
 
 
 @pytest.mark.parametrize("name", ["DGModel_base", "DGModel_mem", "DGModel_memadd", "DGModel_cls",

@@ -140,6 +140,7 @@ def test_conv_f32_persistent(dev, monkeypatch, case):
     x = K.Act(torch.randn(N, H, W, C, generator=g).to(dev))
     wp = K.pack_weight((torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5).to(dev), torch.float32)
     outs = []
+    prev = K.lib_call_status("dg_get_f32_math")
     K.call("dg_set_f32_math", 0)  # both on v_mfma_f32_16x16x4_f32 (the split math: test_conv_f32_split_math)
     try:
         for flag in ("1", "0"):
@@ -149,7 +150,7 @@ def test_conv_f32_persistent(dev, monkeypatch, case):
             outs.append(y.buf.clone())
         torch.cuda.synchronize()
     finally:
-        K.call("dg_set_f32_math", 1)
+        K.call("dg_set_f32_math", prev)
     assert relerr(outs[0], outs[1]) < 2e-6
 
 
@@ -326,9 +327,10 @@ def test_fused_adamw_matches_torch_with_missing_grads(dev):
 @pytest.mark.parametrize("case", [(1, 256, 288, 64, 256, 3), (1, 256, 288, 128, 128, 3), (1, 256, 288, 64, 64, 3),
                                   (1, 256, 288, 256, 512, 1), (2, 20, 24, 64, 128, 3), (1, 64, 64, 512, 512, 3)])
 def test_conv_f32_split_math(dev, case):
-    """DG_F32 on the bf16 matrix cores (dg_set_f32_math(1): exact 3-way bf16 split, six products)
-    against float64 torch: forward, dgrad and wgrad within 5e-6 relative and no worse than 2x the
-    v_mfma_f32_16x16x4_f32 path's own error on the same launch (f32-grade)."""
+    """DG_F32 on the bf16 matrix cores (dg_set_f32_math(1): exact 3-way bf16 split, six products) and on
+    the f16 ones (2: two scaled f16 parts, three products) against float64 torch: forward, dgrad and
+    wgrad within 5e-6 relative and no worse than 2x the v_mfma_f32_16x16x4_f32 path's own error on
+    the same launch (f32-grade)."""
     K = _k()
     N, H, W, C, Cout, R = case
     pad = R // 2
@@ -344,8 +346,9 @@ def test_conv_f32_split_math(dev, case):
     gyd = K.Act(to_nhwc(gy).to(dev))
     wp = K.pack_weight(w.to(dev), torch.float32)
     errs = {}
+    prev = K.lib_call_status("dg_get_f32_math")
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             K.call("dg_set_f32_math", mode)
             y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
             K.conv_fwd(xd, wp, Cout, R, pad, y)
@@ -356,9 +359,10 @@ def test_conv_f32_split_math(dev, case):
             torch.cuda.synchronize()
             errs[mode] = (relerr(to_nchw(y.buf), yr.detach()), relerr(to_nchw(dx.buf), xr.grad), relerr(dw, wr.grad))
     finally:
-        K.call("dg_set_f32_math", 1)
-    for e0, e1 in zip(errs[0], errs[1]):
-        assert e1 < 5e-6 and e1 < 2 * e0 + 2e-7, errs
+        K.call("dg_set_f32_math", prev)
+    for m in (1, 2):
+        for e0, e1 in zip(errs[0], errs[m]):
+            assert e1 < 5e-6 and e1 < 2 * e0 + 2e-7, errs
 
 
 @pytest.mark.parametrize("case", [(2, 20, 24, 64, 128, 3), (1, 16, 256, 64, 64, 3), (1, 24, 64, 128, 128, 3),
@@ -368,8 +372,35 @@ def test_conv_f32_split_exact_identity(dev, case):
     """The 3-way split is exact (x = h0 + h1 + h2 bit for bit, dg_common.h split3_pair): with an
     identity filter (centre tap) every split-math forward and dgrad path must return its input
     bit-identically, and the weight gradient against a one-hot output gradient must return the
-    input pixel exactly (one nonzero product per output: no rounding anywhere)."""
+    input pixel exactly (one nonzero product per output: no rounding anywhere).  Run on mode 1
+    (the f16 x3 arithmetic of mode 2 keeps 22 bits: test_conv_f32_h16_identity_bound)."""
     K = _k()
+    prev = K.lib_call_status("dg_get_f32_math")
+    K.call("dg_set_f32_math", 1)
+    try:
+        _identity_case(K, dev, case, exact=True)
+    finally:
+        K.call("dg_set_f32_math", prev)
+
+
+@pytest.mark.parametrize("case", [(2, 20, 24, 64, 128, 3), (1, 16, 64, 256, 256, 3), (1, 8, 64, 512, 512, 3),
+                                  (2, 4, 512, 128, 64, 3), (1, 6, 1024, 64, 64, 3), (1, 8, 16, 896, 256, 1)])
+def test_conv_f32_h16_identity_bound(dev, case):
+    """The f16 x3 arithmetic (dg_set_f32_math(2)) on an identity filter: the filter row scales to
+    2^14 exactly, so each output is the input's two f16 parts, x*s = hi + lo + r with
+    |r| <= 2^-23 |x*s| (nearest lo), and elements whose lo part is subnormal lose at most 2^-25 in
+    scaled units (2^-25 / s_x): |y - x| <= 2^-23 |x| + 2^-25 / s_x for forward and dgrad; the
+    one-hot wgrad likewise (dY's part exact, X's within the same bound)."""
+    K = _k()
+    prev = K.lib_call_status("dg_get_f32_math")
+    K.call("dg_set_f32_math", 2)
+    try:
+        _identity_case(K, dev, case, exact=False)
+    finally:
+        K.call("dg_set_f32_math", prev)
+
+
+def _identity_case(K, dev, case, exact):
     N, H, W, C, Cout, R = case
     pad = R // 2
     g = torch.Generator().manual_seed(31)
@@ -390,10 +421,26 @@ def test_conv_f32_split_exact_identity(dev, case):
     dw = torch.empty(Cout, C, R, R, device=dev)
     K.conv_wgrad(xd, K.Act(oh.to(dev)), R, pad, dw)
     torch.cuda.synchronize()
-    assert torch.equal(y.buf.cpu()[..., :n], x[..., :n]), "forward"
-    assert torch.equal(dx.buf.cpu()[..., :n], gy[..., :n]), "dgrad"
     xp = x.view(-1, C)[p]
-    assert torch.equal(dw[:, :, pad, pad].cpu(), xp.view(1, C).expand(Cout, C)), "wgrad"
+    if exact:
+        assert torch.equal(y.buf.cpu()[..., :n], x[..., :n]), "forward"
+        assert torch.equal(dx.buf.cpu()[..., :n], gy[..., :n]), "dgrad"
+        assert torch.equal(dw[:, :, pad, pad].cpu(), xp.view(1, C).expand(Cout, C)), "wgrad"
+        return
+
+    def bound(ref):  # 2^-23 |x| + 2^-25 / s_x with s_x = 2^(14 - e), max |x| = m 2^e
+        e = torch.frexp(ref.abs().max())[1].item()
+        return ref.abs() * 2.0 ** -23 + 2.0 ** (-25 - (14 - e))
+
+    for got, ref, what in ((y.buf.cpu()[..., :n], x[..., :n], "forward"), (dx.buf.cpu()[..., :n], gy[..., :n], "dgrad"),
+                           (dw[:, :, pad, pad].cpu(), xp.view(1, C).expand(Cout, C), "wgrad")):
+        b = bound(x if what != "dgrad" else gy) if what != "wgrad" else bound(x)
+        if what == "wgrad":
+            b = xp.abs() * 2.0 ** -23 + 2.0 ** (-25 - (14 - torch.frexp(x.abs().max())[1].item()))
+            b = b.view(1, C).expand(Cout, C)
+        else:
+            b = b[..., :n]
+        assert bool(((got.double() - ref.double()).abs() <= b.double()).all()), what
 
 
 @pytest.mark.parametrize("case,which", [((1, 32, 64, 512, 512, 3), "fd"),      # K = 4608 fwd + dgrad
@@ -422,8 +469,9 @@ def test_conv_f32_split_same_sign(dev, case, which):
     else:
         ref_dw = torch.nn.grad.conv2d_weight(x.double(), w.shape, gy.double(), padding=pad)
     errs = {}
+    prev = K.lib_call_status("dg_get_f32_math")
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             K.call("dg_set_f32_math", mode)
             if which == "fd":
                 y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
@@ -438,9 +486,10 @@ def test_conv_f32_split_same_sign(dev, case, which):
                 torch.cuda.synchronize()
                 errs[mode] = (relerr(dw, ref_dw),)
     finally:
-        K.call("dg_set_f32_math", 1)
-    for e0, e1 in zip(errs[0], errs[1]):
-        assert e1 < 2 * e0 + 1e-7, errs
+        K.call("dg_set_f32_math", prev)
+    for m in (1, 2):
+        for e0, e1 in zip(errs[0], errs[m]):
+            assert e1 < 2 * e0 + 1e-7, errs
     print("same-sign split errors (exact, split):", errs)
 
 
@@ -624,3 +673,55 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
     for m in ("2", "1"):  # 512-pixel all-pixel-wave form (W % 512 == 0), 256-pixel form
         for e3, e1 in zip(errs[m], errs["0"]):
             assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
+
+
+@pytest.mark.parametrize("xs,ws", [(1e-30, 1.0), (1e-6, 1e-3), (1.0, 1.0), (1e6, 1e3), (1e30, 1e-20)])
+@pytest.mark.parametrize("case", [(1, 64, 96, 256, 256, 3), (1, 32, 512, 64, 64, 3), (1, 48, 64, 128, 128, 3)])
+def test_conv_f32_h16_scales(dev, xs, ws, case):
+    """f16 x3 (dg_set_f32_math(2)) on operands of any magnitude: the power-of-two scales (per filter row,
+    per pixel-operand tensor) bring them into f16 range and back exactly, so forward, dgrad and wgrad
+    stay within 5e-6 (normwise relative) of float64 from 1e-30 to 1e30; one launch also holds a
+    dynamic range of 1e-12 inside one tensor."""
+    K = _k()
+    N, H, W, C, Cout, R = case
+    pad = R // 2
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, C, H, W, generator=g) * xs
+    x[:, : C // 4] *= 1e-12  # a quarter of the channels twelve decades below the rest
+    w = torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5 * ws
+    gy = torch.randn(N, Cout, H, W, generator=g)
+    y64 = F.conv2d(x.double(), w.double(), padding=pad)
+    dx64 = torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double() * xs, padding=pad)
+    dw64 = torch.nn.grad.conv2d_weight(x.double(), w.shape, gy.double(), padding=pad)
+    xd, gyd, gysd = K.Act(to_nhwc(x).to(dev)), K.Act(to_nhwc(gy).to(dev)), K.Act(to_nhwc(gy * xs).to(dev))
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    prev = K.lib_call_status("dg_get_f32_math")
+    K.call("dg_set_f32_math", 2)
+    try:
+        y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+        K.conv_fwd(xd, wp, Cout, R, pad, y)
+        dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.conv_dgrad(gysd, wp, C, R, pad, dx)
+        dw = torch.empty(Cout, C, R, R, device=dev)
+        K.conv_wgrad(xd, gyd, R, pad, dw)
+        torch.cuda.synchronize()
+    finally:
+        K.call("dg_set_f32_math", prev)
+    nrel = lambda a, b: float((a.double().cpu() - b).norm() / b.norm())  # noqa: E731
+    errs = (nrel(to_nchw(y.buf), y64), nrel(to_nchw(dx.buf), dx64), nrel(dw, dw64))
+    assert max(errs) < 5e-6, errs
+    assert all(torch.isfinite(t).all() for t in (y.buf, dx.buf, dw))
+
+
+def test_amax(dev):
+    """dg_amax: max |x| over a channel slice of an NHWC buffer (the f16 x3 operand scale)."""
+    K = _k()
+    g = torch.Generator().manual_seed(9)
+    buf = torch.randn(2, 7, 9, 96, generator=g)
+    buf[1, 3, 4, 70] = -123.5   # outside the slice below: must not count
+    buf[0, 6, 8, 40] = -77.25   # inside
+    a = K.Act(buf.to(dev), off=32, C=32)
+    m = K.amax(a)
+    torch.cuda.synchronize()
+    assert m.item() == 77.25
+    assert K.amax(K.Act(buf.to(dev))).item() == 123.5

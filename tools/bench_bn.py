@@ -44,12 +44,12 @@ for dt in (torch.bfloat16, torch.float32):
         ops = {
             "bn_bwd_apply": (3, lambda: K.call("dg_bn_bwd_apply_coef", dtc, K.ptr(a), C, K.ptr(b), C, M, C,
                                                 K.ptr(st[0]), K.ptr(st[1]), K.ptr(st[2]), K.ptr(st[3]), 1, 0, 0,
-                                                K.ptr(coef), K.ptr(out), C, K.stream())),
+                                                K.ptr(coef), K.ptr(out), C, None, K.stream())),
             "bn_add_apply": (3, lambda: K.call("dg_bn_add_apply", dtc, K.ptr(a), C, M, C, K.ptr(st[2]), K.ptr(st[3]),
                                                 K.ptr(b), C, K.ptr(st[2]), K.ptr(st[3]), 1, K.ptr(out), C,
                                                 K.stream())),
             "bn_apply": (2, lambda: K.call("dg_bn_apply", dtc, K.ptr(a), C, M, C, K.ptr(st[2]), K.ptr(st[3]), 1, 0, 0,
-                                           K.ptr(out), C, K.stream())),
+                                           K.ptr(out), C, None, K.stream())),
         }
         for name, (nstream, fn) in ops.items():
             ms, res = {x: [] for x in arms}, {}
