@@ -63,6 +63,8 @@ struct FwdArgs {
   int wide_st = 0;
   // f32 f16 x3 arithmetic: a device float >= max |x| (NULL: presplit_h runs amax_kernel over x)
   const float* xamax = nullptr;
+  // diagnostic stamp rows (conv_fwd_psplit_kernel STAMP = 1; dg_debug_stamps)
+  unsigned long long* stamps = nullptr;
 };
 template <typename T> __device__ __forceinline__ unsigned pack2(float lo, float hi);
 template <> __device__ __forceinline__ unsigned pack2<bf16>(float lo, float hi) { return pack_bf2(lo, hi); }
@@ -1358,7 +1360,19 @@ static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA add
 // HM = 1: the f16 x3 arithmetic (dg_common.h split2h_8 / mfma_h3): two f16 filter planes
 // (split_weight_h_kernel: per-row scale, 1/(s_row s_x) per output channel after the planes, then
 // s_x), the pixel fragments scaled by s_x and split into two f16 parts, three MFMAs per block.
-template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0, int HM = 0>
+// STAMP = 1: diagnostic build (DGVCC_PSPLIT_STAMP with dg_debug_stamps' buffer): s_memtime stamps around
+// each K-step's phases -- DMA wait, barrier, prologue (fragment reads, next DMA issue, B split), MFMA
+// block -- and the epilogue, summed per wave and stored once at the end (cdna_hip_programming.md §7
+// "In-kernel stamps"; read its shares, not its run time).
+// SCH (HM only): 0 = the next K-step's DMA issued in the prologue (after the first fragment reads), every
+// MFMA block at s_setprio 1; 1 = its AI + BI pieces issued one per MFMA block (i < AI + BI), so the
+// prologue ahead of the first MFMA is reads + split only; 2 = 1 with a static s_setprio 1 for waves
+// 4-7 (the arbitration losers of the 8-wave block) and no per-block priority flips; 3 = SIMD partners
+// out of phase: waves 0-3 issue their DMA in the prologue (as 0) while waves 4-7 run their MFMA block,
+// and waves 4-7 issue theirs after their MFMA block while waves 0-3 run theirs (an LDS-DMA piece costs its
+// wave 100-185 issue cycles, MI355X_MICROARCH.md); 4 = 3 without the per-block s_setprio.
+template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0, int HM = 0, int STAMP = 0,
+          int SCH = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   static_assert(!TALL || (BN == 256 && EPI == 0 && STG == 2 && INC), "TALL: 256-channel training forward only");
   constexpr int NPL = HM ? 2 : 3;  // filter planes
@@ -1483,6 +1497,22 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
                 tapmask_ok<BI>(c.tm, i, need) ? c.bofs + cbytes[i] + (toff + (unsigned)(i * 8 * a.ldx * 4)) : 0xFFFFFFF0u);
     advance();
   };
+  // SCH >= 1: piece p (< AI: filter, else pixels) of the DMA issue_inc makes; the caller advances the
+  // cursor after the last piece
+  auto issue_piece = [&](const Ctx& c, unsigned stage, int pc) __attribute__((always_inline)) {
+    const int is = ko ? d0 : d1, ir = ko ? d1 : d2, icb = ko ? d2 : d0;
+    const int rs = ir * a.S + is;
+    char* As = smem + stage * STAGE;
+    if (pc < AI) {
+      lds_dma16s(c.wr, As + (wid * AI + pc) * 1024, alane + (unsigned)((rs * CB + icb) * KB), aoff_s(pc));
+    } else {
+      const int i = pc - AI;
+      const unsigned toff = (unsigned)((((ir - a.pad) * a.W + (is - a.pad)) * a.ldx + icb * 32) * 4);
+      lds_dma16(c.xr, As + A_BYTES + (wid * BI + i) * 1024,
+                tapmask_ok<BI>(c.tm, i, tap_need(ir, is)) ? c.bofs + cbytes[i] + (toff + (unsigned)(i * 8 * a.ldx * 4))
+                                                          : 0xFFFFFFF0u);
+    }
+  };
   auto issue = [&](const Ctx& c, int kt, int stage) {
     const int rs = a.korder ? kt % RS : kt / CB, cb = a.korder ? kt / RS : kt - rs * CB;
     const int r = rs / a.S, s2 = rs - r * a.S;
@@ -1530,12 +1560,32 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     if (PF > 1) issue(cur, 1, 1);
   }
   bool first_tile = true;
+  unsigned long long st_sum[5] = {0, 0, 0, 0, 0}, st_prev = 0, st_nk = 0, st_tiles = 0;
+  auto stamp = [&]() __attribute__((always_inline)) -> unsigned long long {
+    unsigned long long t = 0;
+    if constexpr (STAMP) {
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return t;
+  };
+  if constexpr (STAMP) st_prev = stamp();
+  if constexpr (SCH == 2) {
+    if (wid >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   while (true) {
     f4v acc[TI][TJ];
 #pragma unroll
     for (int i = 0; i < TI; ++i)
 #pragma unroll
       for (int j = 0; j < TJ; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+    if constexpr (STAMP) {  // epilogue of the previous tile (and the prologue before the first)
+      const unsigned long long s = stamp();
+      st_sum[4] += s - st_prev;
+      st_prev = s;
+      ++st_tiles;
+    }
     for (int t = 0; t < KT; ++t, ++gs) {
       const bool more = t + 1 < KT || has_next;
       if (PF > 1 && more && (t > 0 || first_tile)) {
@@ -1546,8 +1596,18 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      unsigned long long st_a = 0;
+      if constexpr (STAMP) {
+        st_a = stamp();
+        st_sum[0] += st_a - st_prev;
+      }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if constexpr (STAMP) {
+        const unsigned long long s = stamp();
+        st_sum[1] += s - st_a;
+        st_a = s;
+      }
       const char* As = smem + (gs % STG) * STAGE;
       const char* Bs = As + A_BYTES;
       u4v b0[TJ], b1[TJ];
@@ -1564,8 +1624,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       };
       s8v ah[NPL];
       aread(0, ah);
-      {
-        const int u = t + PF;
+      // the next DMA: now (SCH 0), or one piece per MFMA block below (SCH >= 1)
+      const int u_dma = t + PF;
+      const bool dma_cur = u_dma < KT, dma_nxt = !dma_cur && has_next;
+      if constexpr (SCH >= 3) {
+        if (dma_nxt && u_dma == KT) d0 = d1 = d2 = 0;
+        if (wid < 4) {
+          if (dma_cur) issue_inc(cur, (gs + PF) % STG);
+          else if (dma_nxt) issue_inc(nxt, (gs + PF) % STG);
+        }
+      } else if constexpr (SCH >= 1) {
+        if (dma_nxt && u_dma == KT) d0 = d1 = d2 = 0;
+      } else {
+        const int u = u_dma;
         if constexpr (INC) {
           if (u < KT) issue_inc(cur, (gs + PF) % STG);
           else if (has_next) {
@@ -1584,11 +1655,24 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
         else split3_8(b0[j], b1[j], bh[j][0], bh[j][1], bh[j][2]);
       }
       if constexpr (HM) __builtin_amdgcn_sched_barrier(0);  // the raw rows die here (else: 59 spilled VGPRs)
+      if constexpr (STAMP) {
+        const unsigned long long s = stamp();
+        st_sum[2] += s - st_a;
+        st_a = s;
+      }
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         s8v an[NPL];
         if (i + 1 < TI) aread(i + 1, an);
-        __builtin_amdgcn_s_setprio(1);
+        if constexpr (SCH == 1 || SCH == 2) {  // one DMA piece of the next K-step per MFMA block
+          static_assert(SCH == 0 || AI + BI <= TI, "SCH: one piece per MFMA block");
+          if (i < AI + BI) {
+            if (dma_cur) issue_piece(cur, (gs + PF) % STG, i);
+            else if (dma_nxt) issue_piece(nxt, (gs + PF) % STG, i);
+            if (i == AI + BI - 1 && (dma_cur || dma_nxt)) advance();
+          }
+        }
+        if constexpr (SCH != 2 && SCH != 4) __builtin_amdgcn_s_setprio(1);
         if constexpr (HM) {
           constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
 #pragma unroll
@@ -1605,12 +1689,23 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
             for (int j = 0; j < TJ; ++j)
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[PA[q]], bh[j][PB[q]], acc[i][j], 0, 0, 0);
         }
-        __builtin_amdgcn_s_setprio(0);
+        if constexpr (SCH != 2 && SCH != 4) __builtin_amdgcn_s_setprio(0);
         if (i + 1 < TI) {
 #pragma unroll
           for (int pl = 0; pl < NPL; ++pl) ah[pl] = an[pl];
         }
         if constexpr (HM) __builtin_amdgcn_sched_barrier(0);  // no fragment reads hoisted across blocks
+      }
+      if constexpr (SCH >= 3) {  // waves 4-7: the next K-step's DMA after their MFMA block
+        if (wid >= 4) {
+          if (dma_cur) issue_inc(cur, (gs + PF) % STG);
+          else if (dma_nxt) issue_inc(nxt, (gs + PF) % STG);
+        }
+      }
+      if constexpr (STAMP) {
+        st_prev = stamp();
+        st_sum[3] += st_prev - st_a;
+        ++st_nk;
       }
     }
     first_tile = false;
@@ -1704,6 +1799,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     lin += G;
     has_next = lin + G < ntile;
     if (has_next) setup(lin + G, nxt);
+  }
+  if constexpr (STAMP) {  // the last tile's epilogue, then one row of 8 per wave
+    st_sum[4] += stamp() - st_prev;
+    if (lane == 0 && a.stamps) {
+      unsigned long long* o = a.stamps + ((long long)blockIdx.x * 8 + wid) * 8;
+      for (int q = 0; q < 5; ++q) o[q] = st_sum[q];
+      o[5] = st_nk;
+      o[6] = st_tiles;
+      o[7] = (unsigned long long)KT;
+    }
   }
 }
 
@@ -3161,6 +3266,15 @@ static const unsigned short* presplit(const FwdArgs& a, hipStream_t st) {
                      st, (const float*)a.w, nw, wsp);
   return wsp;
 }
+// DGVCC_PSPLIT_SCH=0|1|2 (read per launch: A/B): schedule of the f16 x3 256-pixel pre-split forward
+// (conv_fwd_psplit_kernel SCH)
+static int psplit_sch() {
+  const char* e = getenv("DGVCC_PSPLIT_SCH");
+  return e ? e[0] - '0' : 0;
+}
+// test hook: the diagnostic stamp buffer (dg_debug_stamps)
+static unsigned long long* g_stamps = nullptr;
+static long long g_stamp_bytes = 0;
 static int launch_amax(const float* x, long long ldx, long long M, int C, unsigned* out, hipStream_t st) {
   if (hipMemsetAsync(out, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
   if (M <= 0) return DG_OK;
@@ -3273,10 +3387,11 @@ int launch_fwd(const FwdArgs& a0, hipStream_t st) {
   // 16-byte epilogue stores: a template variant (WST = 1) of the persistent kernel, not a run-time
   // branch -- both store forms in one instantiation pushed the 256-channel kernel past 256 VGPRs
   // (bit 0: the persistent kernels' WST instantiations; bit 1: the pipe kernel's run-time branch,
-  // DGVCC_PIPE_WST=0 off)
+  // opt-in with DGVCC_PIPE_WST=1: bit-identical (test_pipe_wide_stores) but no faster on the bf16 final
+  // step or the SW trunk, same-box A/B in profiles/round5a/pipe_wst/)
   a.wide_st = Is16<T>::value && pers_wst() > 0 && a.ldy % 8 == 0 && ((uintptr_t)a.y & 15) == 0 &&
               (pers_wst() >= 2 || a.R * a.S * (a.C / 64) <= 2);
-  if (a.wide_st && !(getenv("DGVCC_PIPE_WST") && getenv("DGVCC_PIPE_WST")[0] == '0')) a.wide_st |= 2;
+  if (a.wide_st && getenv("DGVCC_PIPE_WST") && getenv("DGVCC_PIPE_WST")[0] == '1') a.wide_st |= 2;
   return launch_fwd_impl<T>(a, st);
 }
 
@@ -3451,8 +3566,23 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
     } else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 3, EPI_, 0>), dim3(g2), dim3(512), 0, st, ap, wspc);  \
   } while (0)
         if (a.escale) PSPLIT_LAUNCH(3);
-        else if (h16 && tall)
-          hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
+        else if (h16 && tall && g_stamps && getenv("DGVCC_PSPLIT_STAMP") &&
+                 (long long)g2 * 8 * 8 * 8 <= g_stamp_bytes) {  // diagnostic stamp build (tools/stamp_psplit.py)
+          ap.stamps = g_stamps;
+          const int sch = psplit_sch();
+          if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 3) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 2>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 1) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
+        } else if (h16 && tall) {
+          const int sch = psplit_sch();
+          if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 3) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 2>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 1) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
+        }
         else if (tall) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
         else PSPLIT_LAUNCH(0);
 #undef PSPLIT_LAUNCH
@@ -5199,6 +5329,13 @@ extern "C" int dg_amax(int dtype, const void* x, int64_t ldx, int64_t M, int C, 
   DG_REQUIRE(x && out && M >= 0 && C > 0 && ldx >= C);
   DG_SUPPORTED(dtype == DG_F32 && C % 4 == 0 && ldx % 4 == 0);
   return launch_amax((const float*)x, ldx, M, C, (unsigned*)out, (hipStream_t)stream);
+}
+
+extern "C" int dg_debug_stamps(void* buf, int64_t bytes) {
+  DG_REQUIRE(bytes >= 0 && (buf || bytes == 0));
+  g_stamps = (unsigned long long*)buf;
+  g_stamp_bytes = bytes;
+  return DG_OK;
 }
 
 extern "C" int dg_set_persist(int mode) {

@@ -41,6 +41,11 @@ int dg_version(void); /* returns DGVCC_ABI_VERSION */
  * returns its length, or -1.  The Python binding refuses a library whose hash differs
  * from the sources beside it. */
 int dg_source_hash(char* out, int cap);
+/* diagnostic hook: with DGVCC_PSPLIT_STAMP set, the f16 x3 256-pixel pre-split forward runs its
+ * stamp build and writes 8 u64 per wave (grid x 8 waves x 8) into buf: cycles in the DMA wait,
+ * barrier, prologue, MFMA block and epilogue, K-steps, tiles, K-steps per tile (tools/stamp_psplit.py).
+ * buf = NULL turns it off. */
+int dg_debug_stamps(void* buf, int64_t bytes);
 /* test hook: 1/0 force the persistent pipelined conv forward on/off, -1 = DGVCC_PERSIST default */
 int dg_set_persist(int mode);
 /* f32 GEMM arithmetic of the DG_F32 convolutions: 0 = v_mfma_f32_16x16x4_f32;

@@ -682,3 +682,40 @@ def test_persistent_wide_stores(dev, monkeypatch, dtype, N, H, W, C, Cout, acc, 
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     assert not torch.equal(outs[0], base)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("N,H,W,C,Cout,R,acc,bias", [(1, 37, 41, 64, 256, 3, False, True), (2, 19, 23, 128, 128, 3, True, False),
+                                                     (1, 33, 29, 64, 256, 1, False, False), (3, 11, 13, 192, 128, 3, False, True)])
+def test_pipe_wide_stores(dev, monkeypatch, dtype, N, H, W, C, Cout, R, acc, bias):
+    """16-byte epilogue stores of the one-tile-per-block pipe kernel (conv_fwd_pipe_kernel, forced by
+    dg_set_persist(0); opt-in with DGVCC_PIPE_WST=1, 8-byte stores otherwise): bit-identical outputs on ragged pixel
+    tails (N*H*W not a multiple of the 256-pixel tile), with and without bias, accumulating or not, both
+    16-bit types, BN = 256 (2 stages) and 128 (3 stages)."""
+    K = _k()
+    g = torch.Generator().manual_seed(29)
+    x = torch.randn(N, H, W, C, generator=g).to(dev, dtype)
+    w = (torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5).to(dev)
+    wp = K.pack_weight(w, dtype)
+    b = torch.randn(Cout, generator=g).to(dev) if bias else None
+    base = torch.randn(N, H, W, Cout, generator=g).to(dev, dtype)
+    assert (N * H * W) % 256 != 0
+    outs = []
+    K.call("dg_set_persist", 0)
+    try:
+        for wst in ("0", "1"):
+            monkeypatch.setenv("DGVCC_PIPE_WST", wst)
+            yb = base.clone()
+            K.conv_fwd(K.Act(x), wp, Cout, R, R // 2, K.Act(yb), bias=b, accumulate=acc)
+            outs.append(yb)
+        torch.cuda.synchronize()
+    finally:
+        K.call("dg_set_persist", -1)
+    assert torch.equal(outs[0], outs[1])
+    assert not torch.equal(outs[0], base)
+    # and against torch on the rounded operands
+    xr = x.float().permute(0, 3, 1, 2)
+    ref = F.conv2d(xr, w.to(dtype).float(), bias=b, padding=R // 2).permute(0, 2, 3, 1)
+    if acc:
+        ref = ref + base.float()
+    assert relerr(outs[1].float(), ref) < 2e-2
