@@ -384,6 +384,8 @@ class CatConvLayer(ConvLayer):
         w = self.conv.weight.detach()
         zs, wps, lo = [], [], 0
         for part in x.parts:
+            if dt == torch.float32 and training and part.amax is None:
+                part.amax = K.amax(part)  # once for the forward and the backward's wgrad (f16 x3 scales)
             build = lambda lo=lo, c=part.C: K.pack_weight(w[:, lo:lo + c].contiguous(), dt)  # noqa: E731
             wp = build() if training else frozen(self, ("cat", dt, lo), (self.conv.weight,), build)
             zk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dt, dev))
@@ -435,6 +437,8 @@ class CatConvLayer(ConvLayer):
         for part, sc in zip(x.parts[1:], CatParts.SCALES[1:]):  # U^T dz at the part's resolution
             gk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dz.buf.dtype, dev))
             K.upsample_bwd(dz, sc, K.UP_BILINEAR, gk)
+            if gk.buf.dtype == torch.float32:
+                gk.amax = K.amax(gk)  # once for the wgrad and the dgrad below
             gzs.append(gk)
         dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
         lo = 0
@@ -839,6 +843,11 @@ class MemRead:
         """g_y = gL . mem^T * scale ; dmem_b[k][slot] = scale * sum_px y[px][k] gL[px][slot]."""
         k, S = self.mem.shape[1], self.mem.shape[2]
         gy = Act(K.nhwc(y.N, y.H, y.W, k, dt, y.buf.device))
+        if dt == torch.float32:  # one operand-max pass each for the two convs below (f16 x3 scales)
+            if gL.amax is None:
+                gL.amax = K.amax(gL)
+            if y.amax is None:
+                y.amax = K.amax(y)
         m_s = K.pack_weight((self.mem.detach()[0] * scale).contiguous().view(k, S, 1, 1), dt)
         K.conv_fwd(gL, m_s, k, 1, 0, gy)
         dmem = torch.empty((k, S, 1, 1), dtype=torch.float32, device=y.buf.device)
