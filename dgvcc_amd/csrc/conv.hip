@@ -5765,7 +5765,8 @@ extern "C" int64_t dg_conv2d_wgrad_workspace(int dtype, int N, int P, int Q, int
 
 extern "C" int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,
                                int64_t lddy, int Cout, int R, int S, int stride, int pad, float* dw, void* workspace,
-                               int64_t ws_bytes, int accumulate, void* stream) {
+                               int64_t ws_bytes, int accumulate, const float* xamax, const float* dyamax,
+                               void* stream) {
   DG_REQUIRE(x && dy && dw && workspace && stride >= 1 && pad >= 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(Cout % 64 == 0 && C % 64 == 0);
@@ -5779,6 +5780,8 @@ extern "C" int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int
   DG_SUPPORTED((long long)p.pps * lddy * 4 < (1ll << 31));
   WgArgs a{(const char*)x, ldx, N, H, W, C, (const char*)dy, lddy, Cout, R, S, pad, (float*)workspace, p.splits, p.pps,
            stride, P, Q, 1};
+  a.xam = (const unsigned*)xamax;
+  a.dyam = (const unsigned*)dyamax;
   hipStream_t st = (hipStream_t)stream;
   unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - 256) : nullptr;
   return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st, hslots);

@@ -35,19 +35,21 @@ inline int ew_unroll() {
   return e && e[0] == '2' ? 2 : 1;
 }
 
-// y = act(z1*s1 + b1 + (s2 ? z2*s2 + b2 : z2))
+// y = act(z1*s1 + b1 + (s2 ? z2*s2 + b2 : z2)); amax (may be NULL): max |y| (the next f16 x3 convs'
+// operand scale, dg_common.h block_amax_commit; zeroed by the launcher)
 template <typename T, int U = 1>
 __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, long long ld1, int M, int C,
                                                     const float* __restrict__ s1, const float* __restrict__ b1,
                                                     const T* __restrict__ z2, long long ld2,
                                                     const float* __restrict__ s2, const float* __restrict__ b2, int act,
-                                                    T* __restrict__ y, long long ldy) {
+                                                    T* __restrict__ y, long long ldy, float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
   const long long pstride = (long long)gridDim.x * NT / tpp;
   float a1[V], c1[V], a2[V], c2[V];
+  float mx = 0.f;
 #pragma unroll
   for (int e = 0; e < V; e += 4) {  // 16-byte parameter loads (c0 % 4 == 0, rows 16-byte aligned)
     ld4(s1 + c0 + e, a1 + e);
@@ -69,10 +71,12 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
       for (int e = 0; e < V; ++e) {
         float t = fmaf(u[e], a1[e], c1[e]) + (s2 ? fmaf(v[e], a2[e], c2[e]) : v[e]);
         if (act == 1) t = t > 0.f ? t : 0.f;
+        mx = fmaxf(mx, fabsf(t));
         u[e] = t;
       }
       stv(y + p * ldy + c0, u);
     }
+    if (amax) block_amax_commit(mx, amax);
     return;
   }
   // two pixels per trip, all four loads ahead of the first use; the second BN and the ReLU as
@@ -84,6 +88,7 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
       for (int e = 0; e < V; ++e) {
         float t = fmaf(u[e], a1[e], c1[e]) + (BN2 ? fmaf(v[e], a2[e], c2[e]) : v[e]);
         if (ACT) t = t > 0.f ? t : 0.f;
+        mx = fmaxf(mx, fabsf(t));
         u[e] = t;
       }
     };
@@ -115,6 +120,7 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
     if (act == 1) run(std::false_type{}, std::true_type{});
     else run(std::false_type{}, std::false_type{});
   }
+  if (amax) block_amax_commit(mx, amax);
 }
 
 // out = g * (y > 0)
@@ -148,12 +154,13 @@ inline int cs_grid(long long total, int tpp) {
   return (g + q - 1) / q * q;
 }
 
-// y = act((x - mu[n,c]) * is[n,c] * gamma[c] + beta[c])
+// y = act((x - mu[n,c]) * is[n,c] * gamma[c] + beta[c]); amax (may be NULL): max |y|, as bn_add_kernel
 template <typename T>
 __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, long long ldx, int N, int HW, int C,
                                                       const float* __restrict__ mu, const float* __restrict__ is,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                      int act, T* __restrict__ y, long long ldy) {
+                                                      int act, T* __restrict__ y, long long ldy,
+                                                      float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const int gt = blockIdx.x * NT + threadIdx.x;
@@ -172,6 +179,7 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
     }
   }
   int cur = -1;
+  float mx = 0.f;
   for (int p = gt / tpp; p < M; p += pstride) {
     const int n = p / HW;
     if (n != cur) {
@@ -186,10 +194,12 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
       float t = (v[e] - m[e]) * s[e];
       if (gamma) t = fmaf(t, ga[e], be[e]);
       if (act == 1) t = t > 0.f ? t : 0.f;
+      mx = fmaxf(mx, fabsf(t));
       v[e] = t;
     }
     stv(y + p * ldy + c0, v);
   }
+  if (amax) block_amax_commit(mx, amax);
 }
 
 // ---------------------------------------------------------------- IN bwd ----
@@ -280,7 +290,8 @@ template <typename T>
 __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ x,
                                                    long long ldx, int N, int HW, int C, const float* __restrict__ mu,
                                                    const float* __restrict__ is, const float* __restrict__ coef,
-                                                   T* __restrict__ dx, long long lddx, int accumulate) {
+                                                   T* __restrict__ dx, long long lddx, int accumulate,
+                                                   float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const int gt = blockIdx.x * NT + threadIdx.x;
@@ -288,6 +299,7 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
   const int pstride = gridDim.x * NT / tpp;
   const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
   float m[V], s[V], k1[V], k2[V], k3[V];
+  float mx = 0.f;  // max |dx| (amax, may be NULL: the following f16 x3 wgrad's operand scale)
   int cur = -1;
   for (int p = gt / tpp; p < M; p += pstride) {
     const int n = p / HW;
@@ -313,9 +325,11 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
       const float xh = (xv[e] - m[e]) * s[e];
       const float d = k1[e] * gv[e] - k2[e] * xh - k3[e];
       o[e] = accumulate ? o[e] + d : d;
+      mx = fmaxf(mx, fabsf(o[e]));
     }
     stv(dx + p * lddx + c0, o);
   }
+  if (amax) block_amax_commit(mx, amax);
 }
 
 }  // namespace
@@ -324,22 +338,23 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
 
 extern "C" int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, int C, const float* scale1,
                                const float* shift1, const void* z2, int64_t ld2, const float* scale2,
-                               const float* shift2, int act, void* y, int64_t ldy, void* stream) {
+                               const float* shift2, int act, void* y, int64_t ldy, float* amax, void* stream) {
   DG_REQUIRE(z1 && z2 && y && scale1 && shift1 && M > 0 && C > 0 && (!scale2 || shift2));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   const int V = DG_IS16(dtype) ? 8 : 4;
   DG_SUPPORTED(VOK(dtype, C, ld1) && VOK(dtype, C, ld2) && VOK(dtype, C, ldy) && NT % (C / V) == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)M * (C / V);
+  if (amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
   if (dtype == DG_BF16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_add_kernel<bf16, 2> : bn_add_kernel<bf16, 1>), dim3(cs_grid_add(total)), dim3(NT), 0, st, (const bf16*)z1, ld1, M, C, scale1,
-                       shift1, (const bf16*)z2, ld2, scale2, shift2, act, (bf16*)y, ldy);
+                       shift1, (const bf16*)z2, ld2, scale2, shift2, act, (bf16*)y, ldy, amax);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_add_kernel<f16, 2> : bn_add_kernel<f16, 1>), dim3(cs_grid_add(total)), dim3(NT), 0, st, (const f16*)z1, ld1, M, C, scale1,
-                       shift1, (const f16*)z2, ld2, scale2, shift2, act, (f16*)y, ldy);
+                       shift1, (const f16*)z2, ld2, scale2, shift2, act, (f16*)y, ldy, amax);
   else
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_add_kernel<float, 2> : bn_add_kernel<float, 1>), dim3(cs_grid_add(total)), dim3(NT), 0, st, (const float*)z1, ld1, M, C,
-                       scale1, shift1, (const float*)z2, ld2, scale2, shift2, act, (float*)y, ldy);
+                       scale1, shift1, (const float*)z2, ld2, scale2, shift2, act, (float*)y, ldy, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -367,7 +382,7 @@ extern "C" int dg_relu_bwd(int dtype, const void* g, int64_t ldg, const void* y,
 
 extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, int HW, int C, const float* mean,
                                  const float* invstd, const float* gamma, const float* beta, int act, void* y,
-                                 int64_t ldy, void* stream) {
+                                 int64_t ldy, float* amax, void* stream) {
   DG_REQUIRE(x && y && mean && invstd && N > 0 && HW > 0 && C > 0 && (!gamma || beta));
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   const int V = DG_IS16(dtype) ? 8 : 4;
@@ -375,15 +390,16 @@ extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, i
   DG_SUPPORTED(VOK(dtype, C, ldx) && VOK(dtype, C, ldy) && total < (1LL << 30));
   hipStream_t st = (hipStream_t)stream;
   const int grid = cs_grid(total, C / V);
+  if (amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(in_apply_kernel<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)x, ldx, N, HW, C,
-                       mean, invstd, gamma, beta, act, (bf16*)y, ldy);
+                       mean, invstd, gamma, beta, act, (bf16*)y, ldy, amax);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL(in_apply_kernel<f16>, dim3(grid), dim3(NT), 0, st, (const f16*)x, ldx, N, HW, C,
-                       mean, invstd, gamma, beta, act, (f16*)y, ldy);
+                       mean, invstd, gamma, beta, act, (f16*)y, ldy, amax);
   else
     hipLaunchKernelGGL(in_apply_kernel<float>, dim3(grid), dim3(NT), 0, st, (const float*)x, ldx, N, HW, C,
-                       mean, invstd, gamma, beta, act, (float*)y, ldy);
+                       mean, invstd, gamma, beta, act, (float*)y, ldy, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -398,7 +414,8 @@ extern "C" int64_t dg_instnorm_bwd_workspace(int N, int HW, int C) {
 // g: upstream gradient already masked by any following ReLU; dgamma/dbeta may be NULL
 extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void* x, int64_t ldx, int N, int HW, int C,
                                const float* mean, const float* invstd, const float* gamma, void* dx, int64_t lddx,
-                               int accumulate, float* dgamma, float* dbeta, void* workspace, void* stream) {
+                               int accumulate, float* dgamma, float* dbeta, void* workspace, float* amax,
+                               void* stream) {
   DG_REQUIRE(g && x && dx && mean && invstd && workspace && N > 0 && HW > 0 && C > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   const int V = DG_IS16(dtype) ? 8 : 4;
@@ -411,6 +428,7 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
   float* coef = part + (long long)N * nb * 2 * C;
   const int grid = cs_grid(total, C / V);
   const dim3 fgrid(dg_cdiv(C, FIN_CH)), fblk(FIN_CH * FIN_KS);
+  if (amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
   if (dtype == DG_BF16) {
     hipLaunchKernelGGL(in_bwd_partial<bf16>, dim3(nb, N), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x, ldx,
                        HW, C, ppb, mean, invstd, part);
@@ -418,7 +436,7 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
     hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
     DG_CHECK_LAUNCH();
     hipLaunchKernelGGL(in_bwd_apply<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x,
-                       ldx, N, HW, C, mean, invstd, coef, (bf16*)dx, lddx, accumulate);
+                       ldx, N, HW, C, mean, invstd, coef, (bf16*)dx, lddx, accumulate, amax);
   } else if (dtype == DG_F16) {
     hipLaunchKernelGGL(in_bwd_partial<f16>, dim3(nb, N), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)x, ldx,
                        HW, C, ppb, mean, invstd, part);
@@ -426,7 +444,7 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
     hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
     DG_CHECK_LAUNCH();
     hipLaunchKernelGGL(in_bwd_apply<f16>, dim3(grid), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)x,
-                       ldx, N, HW, C, mean, invstd, coef, (f16*)dx, lddx, accumulate);
+                       ldx, N, HW, C, mean, invstd, coef, (f16*)dx, lddx, accumulate, amax);
   } else {
     hipLaunchKernelGGL(in_bwd_partial<float>, dim3(nb, N), dim3(NT), 0, st, (const float*)g, ldg, (const float*)x,
                        ldx, HW, C, ppb, mean, invstd, part);
@@ -434,7 +452,7 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
     hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
     DG_CHECK_LAUNCH();
     hipLaunchKernelGGL(in_bwd_apply<float>, dim3(grid), dim3(NT), 0, st, (const float*)g, ldg,
-                       (const float*)x, ldx, N, HW, C, mean, invstd, coef, (float*)dx, lddx, accumulate);
+                       (const float*)x, ldx, N, HW, C, mean, invstd, coef, (float*)dx, lddx, accumulate, amax);
   }
   DG_CHECK_LAUNCH();
   return DG_OK;

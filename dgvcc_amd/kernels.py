@@ -607,7 +607,7 @@ def conv2d_wgrad(x: Act, dy: Act, R: int, stride: int, pad: int, dw: torch.Tenso
     nbytes = x.buf.element_size() * (x.M * x.C + dy.M * dy.C) + 4 * dw.numel()
     _timed("wgrad", flops, lambda: call("dg_conv2d_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
                                         dy.ptr, dy.ld, dy.C, R, R, stride, pad, ptr(dw), ptr(work),
-                                        ws, int(accumulate), stream()), nbytes)
+                                        ws, int(accumulate), ptr(x.amax), ptr(dy.amax), stream()), nbytes)
 
 
 def im2col_c3_general(img: torch.Tensor, dtype: torch.dtype, R: int, stride: int, pad: int,
@@ -640,6 +640,7 @@ def maxpool_k_fwd_idx(x: Act, k: int, stride: int, pad: int, y: Act) -> torch.Te
     idx = torch.empty((y.N, y.H, y.W, x.C), dtype=torch.uint8, device=x.buf.device)
     call("dg_maxpool_fwd_idx", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, k, stride, pad, y.ptr, y.ld,
          ptr(idx), stream())
+    y.amax = x.amax  # a window maximum never exceeds max |x|: x's bound serves the pooled map
     return idx
 
 
@@ -650,9 +651,10 @@ def maxpool_k_bwd_idx(idx: torch.Tensor, gy: Act, k: int, stride: int, pad: int,
 
 def bn_add_apply(z1: Act, st1, z2: Act, st2, act: int, y: Act):
     """y = act(bn1(z1) + (bn2(z2) if st2 is not None else z2)) — Bottleneck join."""
+    am = _amax_out(y)
     call("dg_bn_add_apply", z1.dt, z1.ptr, z1.ld, z1.M, z1.C, ptr(st1[2]), ptr(st1[3]), z2.ptr,
          z2.ld, ptr(st2[2]) if st2 is not None else None, ptr(st2[3]) if st2 is not None else None,
-         act, y.ptr, y.ld, stream())
+         act, y.ptr, y.ld, ptr(am), stream())
 
 
 def relu_bwd(g: Act, y: Act, out: Act):
@@ -670,16 +672,18 @@ def instnorm_stats(x: Act, eps: float = 1e-5) -> torch.Tensor:
 
 
 def instnorm_apply(x: Act, st, gamma, beta, act: int, y: Act):
+    am = _amax_out(y)
     call("dg_instnorm_apply", x.dt, x.ptr, x.ld, x.N, x.H * x.W, x.C, ptr(st[0]), ptr(st[1]),
-         ptr(gamma), ptr(beta), act, y.ptr, y.ld, stream())
+         ptr(gamma), ptr(beta), act, y.ptr, y.ld, ptr(am), stream())
 
 
 def instnorm_bwd(g: Act, x: Act, st, gamma, dx: Act, dgamma=None, dbeta=None, accumulate=False):
     ws = query("dg_instnorm_bwd_workspace", x.N, x.H * x.W, x.C)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
+    am = _amax_out(dx)
     call("dg_instnorm_bwd", x.dt, g.ptr, g.ld, x.ptr, x.ld, x.N, x.H * x.W, x.C, ptr(st[0]),
          ptr(st[1]), ptr(gamma), dx.ptr, dx.ld, int(accumulate), ptr(dgamma), ptr(dbeta),
-         ptr(work), stream())
+         ptr(work), ptr(am), stream())
 
 
 # ---------------------------------------------------------------- whitening -

@@ -360,7 +360,10 @@ class CounterPlan:
         if H % 16 or W % 16:
             raise ValueError(f"input H,W must be multiples of 16 (got {H}x{W})")
         dev = img.device
-        col = Act(K.im2col_c3_general(img.float(), dt, 7, 2, 3, STEM_KPAD))
+        imgf = img.float().contiguous()
+        col = Act(K.im2col_c3_general(imgf, dt, 7, 2, 3, STEM_KPAD))
+        if dt == torch.float32:  # the columns hold image values and zeros: the image's max bounds them
+            col.amax = K.amax(Act(imgf.view(1, 1, N * imgf.shape[1] * H, W)))
         build = lambda: K.pack_weight(self.conv1.weight.detach(), dt, cpad=3, row_len=STEM_KPAD)  # noqa: E731
         wp0 = build() if training else frozen(self, ("stem", dt), (self.conv1.weight,), build)
         P, Q = col.H, col.W
@@ -481,10 +484,21 @@ def gram(w: Act) -> torch.Tensor:
     wgrad GEMM per instance: MFMA, K = H*W)."""
     N, C = w.N, w.C
     fr = torch.empty((N, C, C), dtype=torch.float32, device=w.buf.device)
+    am = _whole_amax(w)
     for n in range(N):
-        wn = Act(w.buf[n:n + 1], w.off, w.C)
+        wn = Act(w.buf[n:n + 1], w.off, w.C, am)
         K.conv_wgrad(wn, wn, 1, 0, fr[n].view(C, C, 1, 1))
     return fr
+
+
+def _whole_amax(w: Act):
+    """f32: max |w| over the whole map (its producer's, else one pass), the f16 x3 operand bound
+    every per-instance launch over w shares; None for 16-bit maps."""
+    if w.buf.dtype != torch.float32:
+        return None
+    if w.amax is None:
+        w.amax = K.amax(w)
+    return w.amax
 
 
 def _iw_grad_hook(w: Act, fr, mask, ns, scale, g_wt):
@@ -495,7 +509,8 @@ def _iw_grad_hook(w: Act, fr, mask, ns, scale, g_wt):
                          grad_coef=g_wt)
         N, C = w.N, w.C
         wp = K.pack_weight(gsym.view(N * C, C, 1, 1), w.buf.dtype)
+        am = _whole_amax(w)
         for n in range(N):
-            K.conv_fwd(Act(w.buf[n:n + 1], w.off, C), wp[n * C:(n + 1) * C], C, 1, 0,
+            K.conv_fwd(Act(w.buf[n:n + 1], w.off, C, am), wp[n * C:(n + 1) * C], C, 1, 0,
                        Act(gt.buf[n:n + 1], gt.off, C), accumulate=True, kind="iw")
     return apply

@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 3 /* 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 4 /* 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -187,7 +187,8 @@ int dg_conv2d_dgrad(int dtype, const void* dy, int64_t lddy, int N, int P, int Q
 int64_t dg_conv2d_wgrad_workspace(int dtype, int N, int P, int Q, int C, int Cout, int R, int S);
 int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C,
                     const void* dy, int64_t lddy, int Cout, int R, int S, int stride, int pad,
-                    float* dw, void* workspace, int64_t ws_bytes, int accumulate, void* stream);
+                    float* dw, void* workspace, int64_t ws_bytes, int accumulate, const float* xamax,
+                    const float* dyamax, void* stream);
 /* Cin=3 stems (7x7/2 of the ResNets): NCHW f32 -> im2col [N*P*Q][Kpad], k=(r*S+s)*3+c */
 int dg_im2col_c3(int dtype, const float* img, int N, int H, int W, int R, int S, int stride,
                  int pad, int Kpad, void* out, void* stream);
@@ -358,7 +359,7 @@ int dg_stem_bwd_coef(const float* img, int N, int H, int W, const void* wpack, c
  * models/SW/backbones/resnet.py:100-118). scale2/shift2 NULL = identity shortcut. */
 int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, int C, const float* scale1,
                     const float* shift1, const void* z2, int64_t ld2, const float* scale2,
-                    const float* shift2, int act, void* y, int64_t ldy, void* stream);
+                    const float* shift2, int act, void* y, int64_t ldy, float* amax, void* stream);
 /* nn.ReLU backward from the saved output: out = g * (y > 0) (out may alias g). */
 int dg_relu_bwd(int dtype, const void* g, int64_t ldg, const void* y, int64_t ldy, int M, int C,
                 void* out, int64_t ldo, void* stream);
@@ -367,14 +368,14 @@ int dg_relu_bwd(int dtype, const void* g, int64_t ldg, const void* y, int64_t ld
  * (IBN-b IN, resnet_ibn.py:77,115,159; ISW InstanceWhitening, instance_whitening.py:5-16). */
 int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, int HW, int C,
                       const float* mean, const float* invstd, const float* gamma,
-                      const float* beta, int act, void* y, int64_t ldy, void* stream);
+                      const float* beta, int act, void* y, int64_t ldy, float* amax, void* stream);
 /* Backward of the above (g already masked by any following ReLU): dx (+)=, dgamma/dbeta
  * written (sum over n), either may be NULL. */
 int64_t dg_instnorm_bwd_workspace(int N, int HW, int C);
 int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void* x, int64_t ldx, int N,
                     int HW, int C, const float* mean, const float* invstd, const float* gamma,
                     void* dx, int64_t lddx, int accumulate, float* dgamma, float* dbeta,
-                    void* workspace, void* stream);
+                    void* workspace, float* amax, void* stream);
 
 /* ---- instance / switchable whitening ------------------------------------------
  * ISW (models/ISW/instance_whitening.py:19-39, models/ISW/__init__.py:93-120):

@@ -173,6 +173,8 @@ def test_bn_add_relu_join(dev, dtype, downsample):
     torch.cuda.synchronize()
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert relerr(y.buf.float(), ref) < tol
+    if dtype == torch.float32:  # the join's max |y| (the next f16 x3 convs' operand bound), exact
+        assert y.amax is not None and y.amax.item() == y.buf.abs().max().item()
     mask = (y.buf.float().cpu() > 0).float()
     assert torch.equal(gout.buf.float().cpu(), gg.to(dtype).float() * mask)
 
@@ -219,6 +221,9 @@ def test_instance_norm(dev, dtype, affine, act, shape):
     if affine:
         assert relerr(dgam, gr.grad) < (2e-5 if dtype == torch.float32 else 1e-2)
         assert relerr(dbet, br.grad) < (2e-5 if dtype == torch.float32 else 1e-2)
+    if dtype == torch.float32:  # max |y| and max |dx| from the apply passes, exact
+        assert y.amax.item() == y.buf.abs().max().item()
+        assert dx.amax.item() == dx.buf.abs().max().item()
 
 
 def _sw_params(C, g):

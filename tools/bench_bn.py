@@ -47,7 +47,7 @@ for dt in (torch.bfloat16, torch.float32):
                                                 K.ptr(coef), K.ptr(out), C, None, K.stream())),
             "bn_add_apply": (3, lambda: K.call("dg_bn_add_apply", dtc, K.ptr(a), C, M, C, K.ptr(st[2]), K.ptr(st[3]),
                                                 K.ptr(b), C, K.ptr(st[2]), K.ptr(st[3]), 1, K.ptr(out), C,
-                                                K.stream())),
+                                                None, K.stream())),
             "bn_apply": (2, lambda: K.call("dg_bn_apply", dtc, K.ptr(a), C, M, C, K.ptr(st[2]), K.ptr(st[3]), 1, 0, 0,
                                            K.ptr(out), C, None, K.stream())),
         }
