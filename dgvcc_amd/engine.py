@@ -69,6 +69,7 @@ def bn_eval_cached(owner, bn: nn.BatchNorm2d) -> torch.Tensor:
 
 def _bn_momentum(bn: nn.BatchNorm2d) -> float:
     if bn.momentum is None:  # cumulative moving average (torch semantics)
+        SB.flush_batches()
         return 1.0 / float(bn.num_batches_tracked.item())
     return float(bn.momentum)
 
@@ -105,6 +106,11 @@ class ConvLayer:
         if self.first:  # im2col filter [Cout][64], k = (r*3+s)*3+c
             return K.pack_weight(w, dt, cpad=self.Cin, row_len=64)
         return K.pack_weight(w, dt)
+
+    def _flip(self, wp):
+        """flip_weight(wp) for the dgrad, once per packed filter (both views of a step)."""
+        return frozen(self, ("flip", wp.dtype, wp.data_ptr()), (self.conv.weight,),
+                      lambda: K.flip_weight(wp, self.Cout, self.Cin, self.R))
 
     def stem_ok(self, dt) -> bool:
         """bf16 first layer with BN + ReLU: fused conv/statistics and BN-backward/wgrad kernels;
@@ -143,7 +149,7 @@ class ConvLayer:
             if pg is not None:
                 stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk, M=z.M)
             elif training:
-                bn.num_batches_tracked.add_(1)
+                SB.bump_batches(bn)
                 stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                            bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
             else:
@@ -161,7 +167,7 @@ class ConvLayer:
                 # backward recomputes z again (27 MACs per output vs 128 B/px per HBM pass)
                 if training:
                     part, nblk = K.stem_stats(x, wp, bias)
-                    bn.num_batches_tracked.add_(1)
+                    SB.bump_batches(bn)
                     stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                                bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
                 else:
@@ -175,7 +181,7 @@ class ConvLayer:
             if pg is not None:
                 stats = SB.fwd_stats(bn, pg, part=part, nblk=nblk, M=z.M)
             elif training:
-                bn.num_batches_tracked.add_(1)
+                SB.bump_batches(bn)
                 stats = K.bn_part_finalize(part, nblk, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                            bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
             else:
@@ -184,7 +190,9 @@ class ConvLayer:
             if tape is not None:
                 tape[self] = (x, z, stats, wp, drop, training)
             return
-        wp = self._pack(dt) if training else frozen(self, ("w", dt), (self.conv.weight,), lambda: self._pack(dt))
+        # packed once per weight version: in training the two views of a step share it (run_plan
+        # starts each autograd forward on a fresh generation)
+        wp = frozen(self, ("w", dt), (self.conv.weight,), lambda: self._pack(dt))
         if (_EVAL_FUSE and not training and bn is not None and pool is None and drop is None
                 and out is not None and not self.first and tape is None):
             # evaluation: BN from the running statistics (+ReLU) in the conv epilogue, no z pass
@@ -203,14 +211,14 @@ class ConvLayer:
         if epi is not None and pg is not None:
             stats = SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1], M=z.M)
         elif epi is not None:
-            bn.num_batches_tracked.add_(1)
+            SB.bump_batches(bn)
             stats = K.bn_part_finalize(epi[0], epi[1], self.Cout, bn.weight.detach(), bn.bias.detach(),
                                        bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
         elif pg is not None:
             stats = SB.fwd_stats(bn, pg, z=z)
         elif bn is not None:
             if training:
-                bn.num_batches_tracked.add_(1)
+                SB.bump_batches(bn)
                 stats = K.bn_fwd_train(z, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                                        bn.running_var, _bn_momentum(bn), bn.eps)
             else:
@@ -299,11 +307,12 @@ class ConvLayer:
                     xn, zn, stn, _, dropn, trn = tape[gx_bn]
                     if trn and not isinstance(xn, torch.Tensor) and zn.C == gx.C:
                         res = K.conv_dgrad_bnpart(dz, wp, self.Cin, self.R, self.pad, gx, zn, stn, gx_bn.act,
-                                                  dropn)
+                                                  dropn, wflip=self._flip(wp))
                         if res is not None:
                             tape[("bnpart", gx_bn)] = res
                 if res is None:
-                    K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, gx, accumulate=accumulate_gx)
+                    K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, gx, accumulate=accumulate_gx,
+                                 wflip=self._flip(wp))
         grads = {self.conv.weight: dw}
         if self.conv.bias is not None:
             grads[self.conv.bias] = dbias if self.bn is not None else dbeta
@@ -406,7 +415,7 @@ class CatConvLayer(ConvLayer):
         elif pg is not None:
             stats = SB.fwd_stats(bn, pg, part=part, nblk=rows, M=z.M)
         elif training:
-            bn.num_batches_tracked.add_(1)
+            SB.bump_batches(bn)
             stats = K.bn_part_finalize(part, rows, self.Cout, bn.weight.detach(), bn.bias.detach(),
                                        bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
         else:
@@ -706,9 +715,14 @@ def run_plan(plan, fwd, inputs, params):
                                         any(isinstance(t, torch.Tensor) and t.requires_grad
                                             for t in inputs))
     if need:
-        return _PlanFn.apply(plan, fwd, len(inputs), *inputs, *params)
-    with torch.no_grad():
-        return fwd(*inputs, tape=None)
+        invalidate_frozen()  # a training forward re-derives packed filters once (both views share them)
+    try:
+        if need:
+            return _PlanFn.apply(plan, fwd, len(inputs), *inputs, *params)
+        with torch.no_grad():
+            return fwd(*inputs, tape=None)
+    finally:
+        SB.flush_batches()  # the BatchNorm batch counts the forward bumped, in one launch
 
 
 # ---------------------------------------------------------------------------

@@ -155,17 +155,20 @@ def flip_weight(wp: torch.Tensor, Cout: int, C: int, R: int) -> torch.Tensor:
     return wflip
 
 
-def conv_dgrad(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, accumulate=False):
-    """dX = conv(dY, flipped W^T): the forward GEMM kernel on the flipped filter."""
-    wflip = flip_weight(wp, dy.C, C, R)
+def conv_dgrad(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, accumulate=False, wflip=None):
+    """dX = conv(dY, flipped W^T): the forward GEMM kernel on the flipped filter (wflip: the caller's
+    flip_weight(wp) when it holds one)."""
+    if wflip is None:
+        wflip = flip_weight(wp, dy.C, C, R)
     conv_fwd(dy, wflip, C, R, R - 1 - pad, dx, accumulate=accumulate, kind="dgrad")
 
 
-def conv_dgrad_acc_relu(dy: Act, wp: torch.Tensor, C: int, dx: Act, relu_out: Act) -> bool:
+def conv_dgrad_acc_relu(dy: Act, wp: torch.Tensor, C: int, dx: Act, relu_out: Act, wflip=None) -> bool:
     """dx = (relu_out > 0) ? dx + dgrad_1x1(dy) : 0 in one launch (the ReLU backward of relu_out
     folded into the accumulating dgrad's epilogue, dg_conv_fwd_acc_relu).  False (nothing
     launched) for the shapes that launch does not serve: the caller runs conv_dgrad + relu_bwd."""
-    wflip = flip_weight(wp, dy.C, C, 1)
+    if wflip is None:
+        wflip = flip_weight(wp, dy.C, C, 1)
     ws, work = _fwd_workspace(dy, C, 1)
     dx.amax = None
     flops = 2.0 * dy.M * dy.C * C
@@ -192,14 +195,15 @@ _BNPART_F32_OFF = __import__("os").environ.get("DGVCC_DGRAD_BNPART_F32", "0") !=
 
 
 def conv_dgrad_bnpart(dy: Act, wp: torch.Tensor, C: int, R: int, pad: int, dx: Act, z: Act, stats,
-                      act: int, drop: torch.Tensor | None = None):
+                      act: int, drop: torch.Tensor | None = None, wflip=None):
     """conv_dgrad (no accumulate) whose epilogue also emits the BatchNorm-backward partial
     sums of the layer whose output gradient dx is (z, stats, act, drop: that layer's);
     returns (part, rows) for bn_bwd_from_part, or None (nothing launched) when the shape is
     not served that way."""
     if stats is None or (dy.dt == 1 and _BNPART_OFF) or (dy.dt == 0 and _BNPART_F32_OFF) or dy.dt == 2:
         return None
-    wflip = flip_weight(wp, dy.C, C, R)
+    if wflip is None:
+        wflip = flip_weight(wp, dy.C, C, R)
     rows = (query("dg_conv_bnpart_rows_ex", 0, dy.N, dy.H, dy.W, dy.C, dy.ld, C, R, R) if dy.dt == 0
             else query("dg_conv_stats_rows", dy.N, dy.H, dy.W))
     part = torch.empty((rows, 3, C), dtype=torch.float32, device=dy.buf.device)

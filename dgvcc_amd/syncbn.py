@@ -38,8 +38,31 @@ def group_of(bn) -> object | None:
     return pg if dist.get_world_size(pg) > 1 else None
 
 
+_BATCHES: dict = {}  # id(num_batches_tracked) -> [tensor, owed count]
+
+
+def bump_batches(bn) -> None:
+    """bn.num_batches_tracked += 1 (nn.BatchNorm2d.forward in training), deferred: flush_batches()
+    adds every owed count in one torch._foreach_add_ launch instead of one launch per layer
+    (a plan forward flushes when it ends; a read of the count flushes first)."""
+    t = bn.num_batches_tracked
+    ent = _BATCHES.get(id(t))
+    if ent is None or ent[0] is not t:
+        _BATCHES[id(t)] = [t, 1]
+    else:
+        ent[1] += 1
+
+
+def flush_batches() -> None:
+    if _BATCHES:
+        ents = list(_BATCHES.values())
+        _BATCHES.clear()
+        torch._foreach_add_([e[0] for e in ents], [e[1] for e in ents])
+
+
 def _momentum(bn) -> float:
     if bn.momentum is None:
+        flush_batches()
         return 1.0 / float(bn.num_batches_tracked.item())
     return float(bn.momentum)
 
@@ -84,7 +107,7 @@ def finalize_rows(bn, row: torch.Tensor, pg, M: int) -> torch.Tensor:
     """Local (n, mean, M2) row over M pixels -> the global stats [4][C] (mean, invstd, scale, shift)."""
     rows = gather_rows(row, M, pg)
     C = row.shape[1]
-    bn.num_batches_tracked.add_(1)
+    bump_batches(bn)
     return K.bn_part_finalize(rows, rows.shape[0], C, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                               bn.running_var, _momentum(bn), bn.eps)
 

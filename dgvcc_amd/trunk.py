@@ -45,8 +45,13 @@ class TConv:
         self.same = self.stride == 1 and 2 * self.pad == self.R - 1
 
     def pack(self, dt, training=True):
-        build = lambda: K.pack_weight(self.conv.weight.detach(), dt)  # noqa: E731
-        return build() if training else frozen(self, ("w", dt), (self.conv.weight,), build)
+        """Packed filter, once per weight version (engine.frozen; run_plan starts each training
+        forward on a fresh generation)."""
+        return frozen(self, ("w", dt), (self.conv.weight,), lambda: K.pack_weight(self.conv.weight.detach(), dt))
+
+    def _flip(self, wp):
+        return frozen(self, ("flip", wp.dtype, wp.data_ptr()), (self.conv.weight,),
+                      lambda: K.flip_weight(wp, self.Cout, self.Cin, self.R))
 
     def out_hw(self, H, W):
         return K.conv_out(H, self.R, self.stride, self.pad), K.conv_out(W, self.R, self.stride, self.pad)
@@ -70,10 +75,11 @@ class TConv:
             return dw
         if relu_out is not None:
             assert accumulate
-            if self.same and self.R == 1 and K.conv_dgrad_acc_relu(dz, wp, self.Cin, dx, relu_out):
+            if self.same and self.R == 1 and K.conv_dgrad_acc_relu(dz, wp, self.Cin, dx, relu_out,
+                                                                   wflip=self._flip(wp)):
                 return dw
         if self.same:
-            K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, dx, accumulate=accumulate)
+            K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, dx, accumulate=accumulate, wflip=self._flip(wp))
         else:
             wt = K.pack_weight_t(wp, self.Cout, self.Cin, self.R, self.R)
             K.conv2d_dgrad(dz, wt, self.R, self.stride, self.pad, dx, accumulate=accumulate)
@@ -90,7 +96,7 @@ def bn_stats(z: Act, bn: nn.BatchNorm2d, training: bool) -> torch.Tensor:
         pg = SB.group_of(bn)
         if pg is not None:
             return SB.fwd_stats(bn, pg, z=z)
-        bn.num_batches_tracked.add_(1)
+        SB.bump_batches(bn)
         return K.bn_fwd_train(z, bn.weight.detach(), bn.bias.detach(), bn.running_mean,
                               bn.running_var, _bn_momentum(bn), bn.eps)
     return bn_eval_cached(bn, bn)
@@ -110,7 +116,7 @@ def conv_bn_stats(tc: "TConv", x: Act, wp, z: Act, bn: nn.BatchNorm2d, training:
             pg = SB.group_of(bn)
             if pg is not None:
                 return SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1], M=z.M)
-            bn.num_batches_tracked.add_(1)
+            SB.bump_batches(bn)
             return K.bn_part_finalize(epi[0], epi[1], tc.Cout, bn.weight.detach(), bn.bias.detach(),
                                       bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
     tc.fwd(x, wp, z)
