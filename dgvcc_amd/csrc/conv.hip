@@ -2456,7 +2456,7 @@ __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, 
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) atomicMax(out, __float_as_uint(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]))));
+  if (threadIdx.x == 0) amax_fold(out, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
 }
 
 // Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored

@@ -728,13 +728,15 @@ inline int ew_grid(long long n) {
 // channel chunk's parameters once, so fewer, longer-lived threads amortise that prologue.
 // DGVCC_EW_GRID (read per launch: tools/bench_bn.py) caps the blocks.
 inline int cs_grid(long long n) {
-  // tools/bench_bn.py (profiles/round4a/bn_grid): 16384 blocks where that leaves every thread >= 2
-  // chunks, else 2048 blocks (each thread then walks several chunks per parameter prologue:
-  // bf16 1024-channel layer3 BN backward 4.2 -> 5.5 TB/s)
+  // tools/bench_bn.py: round 4 (profiles/round4a/bn_grid) took 16384 blocks where that left every
+  // thread >= 2 chunks, else 2048; round 5 (profiles/round5b/bn_grid.txt), with the f32 passes
+  // also folding max |out| for the f16 x3 convs: 1024 blocks (4 per CU) matched or beat both on
+  // the trunk / encoder shapes in f32 and bf16 (bf16 12.6M x 64 BN backward 1.04 -> 0.93 ms,
+  // f32 3.1M x 128 0.99 -> 0.89 ms)
   const char* e = getenv("DGVCC_EW_GRID");
   const long long g = (n + NT - 1) / NT;
   if (e) return (int)std::max<long long>(1, std::min<long long>(g, std::max(64, atoi(e))));
-  return (int)(g >= 2 * 16384 ? 16384 : std::min<long long>(g, 2048));
+  return (int)std::min<long long>(g, 1024);
 }
 
 template <typename T>

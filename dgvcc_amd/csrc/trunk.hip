@@ -19,13 +19,11 @@ inline int ew_grid(long long n) {
 }
 // the channel-stationary residual join: norm.hip's cs_grid (DGVCC_EW_GRID caps the blocks)
 inline int cs_grid_add(long long n) {
-  // tools/bench_bn.py (profiles/round4a/bn_grid): 16384 blocks where that leaves every thread >= 2
-  // chunks, else 2048 blocks (each thread then walks several chunks per parameter prologue:
-  // bf16 1024-channel layer3 BN backward 4.2 -> 5.5 TB/s)
+  // as norm.hip cs_grid (tools/bench_bn.py, profiles/round5b/bn_grid.txt): 1024 blocks
   const char* e = getenv("DGVCC_EW_GRID");
   const long long g = (n + NT - 1) / NT;
   if (e) return (int)std::max<long long>(1, std::min<long long>(g, std::max(64, atoi(e))));
-  return (int)(g >= 2 * 16384 ? 16384 : std::min<long long>(g, 2048));
+  return (int)std::min<long long>(g, 1024);
 }
 
 // DGVCC_EW_UNROLL (read per launch; norm.hip's switch of the same name): 2 two pixels per loop

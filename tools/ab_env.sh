@@ -1,14 +1,11 @@
 #!/bin/bash
-# A/B an environment switch on the headline workload (fp32 final mode), alternating twice in one
-# call.  Usage: PROF_TAG=ab2 VAR=DGVCC_EPI_STATS VALS="1 0" bash tools/ab_env.sh [bench args]
+# Same-box A/B of one environment switch on a bench workload, interleaved rounds.
+# usage: bash tools/ab_env.sh VAR "v0 v1 ..." ROUNDS OUTDIR [bench args...]
 set -u
-cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/${PROF_TAG:-ab}
-mkdir -p $OUT
-A="${*:---no-bf16 --no-cpu-baseline --steps 4 --warmup 2}"
-for i in 1 2; do
-  for v in $VALS; do
-    env $VAR=$v timeout -k 10 300 python3 bench.py $A > $OUT/bench_${v}_$i.json 2> $OUT/bench_${v}_$i.err || { echo "bench failed"; tail -5 $OUT/bench_${v}_$i.err; exit 1; }
-    python3 -c "import json; d=json.load(open('$OUT/bench_${v}_$i.json')); r=d['roofline']; print('$VAR=$v', d['value'], d['ms_per_step'], r['achieved'], r['frac'], r['wgrad_frac'])"
-  done
-done
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+var=$1; vals=$2; rounds=$3; out=$4; shift 4
+mkdir -p "$out"
+for r in $(seq 1 "$rounds"); do for v in $vals; do
+  env "$var=$v" timeout -k 10 200 python -u bench.py --no-cpu-baseline "$@" > "$out/r${r}_$v.json" 2>&1 || exit $?
+  python -c "import json;d=json.loads(open('$out/r${r}_$v.json').read().strip().splitlines()[-1]);print('$var=$v round $r', d['ms_per_step'], 'ms', d['value'], d['unit'])"
+done; done

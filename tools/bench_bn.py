@@ -14,7 +14,7 @@ reps = 10
 dev = "cuda"
 var, arms = (sys.argv[1], sys.argv[2:]) if len(sys.argv) > 2 else ("DGVCC_EW_UNROLL", ["1", "2"])
 # (pixels, channels): ResNet layer1 / layer2 / layer3 at 768x1024 b16, VGG enc1 / enc3
-shapes = [(16 * 192 * 256, 256), (16 * 96 * 128, 512), (16 * 48 * 64, 1024), (16 * 384 * 512, 128),
+shapes = [(16 * 768 * 1024, 64), (16 * 192 * 256, 256), (16 * 96 * 128, 512), (16 * 48 * 64, 1024), (16 * 384 * 512, 128),
           (16 * 192 * 256, 64)]
 
 
@@ -40,6 +40,8 @@ for dt in (torch.bfloat16, torch.float32):
         st = torch.stack([torch.zeros(C, device=dev), torch.rand(C, device=dev) + 0.5,
                           torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1])
         coef = torch.randn(3, C, device=dev) * 0.1
+        am = torch.zeros(1, device=dev)
+        amp = K.ptr(am) if dt == torch.float32 else None  # the f32 passes' max |out| (f16 x3 operand scale)
         dtc = K.DTYPES[dt] if hasattr(K, "DTYPES") else (0 if dt == torch.float32 else 1)
         ops = {
             "bn_bwd_apply": (3, lambda: K.call("dg_bn_bwd_apply_coef", dtc, K.ptr(a), C, K.ptr(b), C, M, C,
@@ -51,6 +53,12 @@ for dt in (torch.bfloat16, torch.float32):
             "bn_apply": (2, lambda: K.call("dg_bn_apply", dtc, K.ptr(a), C, M, C, K.ptr(st[2]), K.ptr(st[3]), 1, 0, 0,
                                            K.ptr(out), C, None, K.stream())),
         }
+        if amp is not None:
+            ops["bn_apply+amax"] = (2, lambda: K.call("dg_bn_apply", dtc, K.ptr(a), C, M, C, K.ptr(st[2]),
+                                                      K.ptr(st[3]), 1, 0, 0, K.ptr(out), C, amp, K.stream()))
+            ops["bn_bwd_apply+amax"] = (3, lambda: K.call("dg_bn_bwd_apply_coef", dtc, K.ptr(a), C, K.ptr(b), C, M, C,
+                                                          K.ptr(st[0]), K.ptr(st[1]), K.ptr(st[2]), K.ptr(st[3]), 1,
+                                                          0, 0, K.ptr(coef), K.ptr(out), C, amp, K.stream()))
         for name, (nstream, fn) in ops.items():
             ms, res = {x: [] for x in arms}, {}
             for rnd in range(3):
