@@ -630,15 +630,19 @@ __global__ __launch_bounds__(NT) void softmax_head_fwd(const T* __restrict__ L1,
 
 // gL_v = P_v (gP_v - <P_v, gP_v>) with gP_v = gpre_v v + (loss term); u/db partials per block:
 // part[blk][0:C] = sum_px sum_v gpre_v P_v, part[blk][C] = sum_px sum_v gpre_v.
+// amax (may be NULL; zeroed by the launcher): [0] max |gL_1|, [1] max |gL_2| (the logits GEMMs'
+// f16 x3 operand scales in the backward, dg_common.h block_amax_commit).
 template <typename T, int EPL, int NV, int LOSS>
 __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1, const T* __restrict__ P2, int M,
                                                        int C, const float* __restrict__ v, int act,
                                                        const float* __restrict__ yh1, const float* __restrict__ yh2,
                                                        const float* __restrict__ gyh1, const float* __restrict__ gyh2,
                                                        const float* __restrict__ coef, T* __restrict__ GL1,
-                                                       T* __restrict__ GL2, float* __restrict__ part) {
+                                                       T* __restrict__ GL2, float* __restrict__ part,
+                                                       float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   __shared__ float sh[4 * EPL * 64 + 4];
+  float mx1 = 0.f, mx2 = 0.f;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float vv[EPL], u[EPL];
   load_vec_as_row<T>(v, lane, vv, EPL);
@@ -695,6 +699,11 @@ __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1,
     }
     if (GL1) store_row(GL1 + r * C, lane, g1, EPL);  // NULL: head gradients only (u, db)
     if (NV == 2 && GL2) store_row(GL2 + r * C, lane, g2, EPL);
+#pragma unroll
+    for (int j = 0; j < EPL; ++j) {
+      mx1 = fmaxf(mx1, fabsf(g1[j]));
+      if (NV == 2) mx2 = fmaxf(mx2, fabsf(g2[j]));
+    }
   }
   // waves' u rows -> LDS at slot order, fixed-order sum over the 4 waves
 #pragma unroll
@@ -706,6 +715,13 @@ __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1,
   if (threadIdx.x == 0) {
     const float* q = sh + 4 * EPL * 64;
     o[C] = ((q[0] + q[1]) + q[2]) + q[3];
+  }
+  if (amax) {  // uniform
+    block_amax_commit(mx1, amax);
+    if (NV == 2) {
+      __syncthreads();  // block_amax_commit's LDS slots are reused
+      block_amax_commit(mx2, amax + 1);
+    }
   }
 }
 
@@ -1070,10 +1086,10 @@ void mh_fwd_c(int C, int grid, hipStream_t st, const void* L1, const void* L2, i
 template <typename T, int NV, int LOSS>
 void mh_bwd_c(int C, int grid, hipStream_t st, const void* P1, const void* P2, int M, const float* v, int act,
               const float* yh1, const float* yh2, const float* g1, const float* g2, const float* coef, void* GL1,
-              void* GL2, float* part) {
+              void* GL2, float* part, float* amax) {
 #define MHB(E)                                                                                                  \
   hipLaunchKernelGGL((softmax_head_bwd<T, E, NV, LOSS>), dim3(grid), dim3(NT), 0, st, (const T*)P1, (const T*)P2, \
-                     M, C, v, act, yh1, yh2, g1, g2, coef, (T*)GL1, (T*)GL2, part)
+                     M, C, v, act, yh1, yh2, g1, g2, coef, (T*)GL1, (T*)GL2, part, amax)
   if (C == 1024) MHB(16);
   else if (C == 512) MHB(8);
   else MHB(32);
@@ -1092,11 +1108,11 @@ void mh_fwd_t(int nv, int loss, int C, int grid, hipStream_t st, const void* L1,
 template <typename T>
 void mh_bwd_t(int nv, int loss, int C, int grid, hipStream_t st, const void* P1, const void* P2, int M,
               const float* v, int act, const float* yh1, const float* yh2, const float* g1, const float* g2,
-              const float* coef, void* GL1, void* GL2, float* part) {
-  if (nv == 1) mh_bwd_c<T, 1, 0>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
-  else if (loss == 0) mh_bwd_c<T, 2, 0>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
-  else if (loss == 1) mh_bwd_c<T, 2, 1>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
-  else mh_bwd_c<T, 2, 2>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part);
+              const float* coef, void* GL1, void* GL2, float* part, float* amax) {
+  if (nv == 1) mh_bwd_c<T, 1, 0>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part, amax);
+  else if (loss == 0) mh_bwd_c<T, 2, 0>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part, amax);
+  else if (loss == 1) mh_bwd_c<T, 2, 1>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part, amax);
+  else mh_bwd_c<T, 2, 2>(C, grid, st, P1, P2, M, v, act, yh1, yh2, g1, g2, coef, GL1, GL2, part, amax);
 }
 
 }  // namespace
@@ -1140,7 +1156,7 @@ extern "C" int dg_softmax_head_fwd(int dtype, int nviews, int loss, const void* 
 extern "C" int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* P1, const void* P2, int M, int C,
                                    const float* v, int act, const float* yh1, const float* yh2, const float* gyh1,
                                    const float* gyh2, const float* coef, void* GL1, void* GL2, void* workspace,
-                                   void* stream) {
+                                   float* amax, void* stream) {
   DG_REQUIRE(P1 && v && yh1 && workspace && M > 0 && (nviews == 1 || nviews == 2) && loss >= 0 && loss <= 2);
   DG_REQUIRE(nviews == 1 ? loss == 0 : (P2 && yh2));
   DG_REQUIRE(nviews == 1 || !GL1 == !GL2);  // logit gradients for every view or none
@@ -1148,12 +1164,13 @@ extern "C" int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* 
   hipStream_t st = (hipStream_t)stream;
   const int grid = mh_grid(M);
   float* part = (float*)workspace;
+  if (amax && hipMemsetAsync(amax, 0, 8, st) != hipSuccess) return DG_ERR_HIP;
   if (dtype == DG_BF16)
-    mh_bwd_t<bf16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part);
+    mh_bwd_t<bf16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part, amax);
   else if (dtype == DG_F16)
-    mh_bwd_t<f16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part);
+    mh_bwd_t<f16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part, amax);
   else if (dtype == DG_F32)
-    mh_bwd_t<float>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part);
+    mh_bwd_t<float>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part, amax);
   else return DG_ERR_INVALID;
   DG_CHECK_LAUNCH();
   return DG_OK;

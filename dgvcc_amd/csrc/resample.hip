@@ -601,73 +601,9 @@ __global__ __launch_bounds__(NT) void upsample_bwd_bl_kernel(const T* __restrict
   }
 }
 
-// C = 1 (the density heads' x4 / x16 upsamplings of a one-channel map): one block per input row
-// (n, ih).  Each output row oh whose taps reach ih is staged in LDS with coalesced loads (gy + gy2),
-// then every thread folds its input columns' windows: acc[iw] += wh(oh) * sum_ow ww(ow, iw) row[ow]
-// (the same taps as upsample_bwd_kernel, summed per output row).  The generic kernel's thread per
-// input pixel walked its (2 scale + 3)^2 window with scattered scalar loads: 0.26 ms for the 16 x
-// 768 x 1024 x16 map of the trunk heads (380 GB/s).
-constexpr int UPC1_COLS = 4;  // input columns per thread: W <= 4 * 256
-template <typename T>
-__global__ __launch_bounds__(256) void upsample_bwd_c1_kernel(const T* __restrict__ gy, long long ldgy,
-                                                             const T* __restrict__ gy2, long long ldgy2, int H,
-                                                             int W, int scale, int mode, T* __restrict__ gx,
-                                                             long long ldgx, int accumulate) {
-  extern __shared__ float urow[];
-  const int Ho = H * scale, Wo = W * scale;
-  const int n = blockIdx.x / H, ih = blockIdx.x - n * H;
-  const int tid = threadIdx.x;
-  float acc[UPC1_COLS];
-#pragma unroll
-  for (int k = 0; k < UPC1_COLS; ++k) acc[k] = 0.f;
-  int hlo, hhi;
-  out_range(ih, H, Ho, scale, mode, hlo, hhi);
-  for (int oh = hlo; oh < hhi; ++oh) {
-    const float wh = tap_weight(src_tap(oh, H, Ho, scale, mode), ih);  // block-uniform
-    if (wh == 0.f) continue;
-    __syncthreads();  // the previous row's readers are done
-    const long long ob = (long long)(n * Ho + oh) * Wo;
-    for (int j = tid; j < Wo; j += 256) {
-      float g = to_f(gy[(ob + j) * ldgy]);
-      if (gy2) g += to_f(gy2[(ob + j) * ldgy2]);
-      urow[j] = g;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < UPC1_COLS; ++k) {
-      const int iw = tid + 256 * k;
-      if (iw >= W) break;
-      int wlo, whi;
-      out_range(iw, W, Wo, scale, mode, wlo, whi);
-      float sw = 0.f;
-      for (int ow = wlo; ow < whi; ++ow) {
-        const float ww = tap_weight(src_tap(ow, W, Wo, scale, mode), iw);
-        if (ww != 0.f) sw = fmaf(ww, urow[ow], sw);
-      }
-      acc[k] = fmaf(wh, sw, acc[k]);
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < UPC1_COLS; ++k) {
-    const int iw = tid + 256 * k;
-    if (iw >= W) break;
-    T* dst = gx + ((long long)(n * H + ih) * W + iw) * ldgx;
-    float v = acc[k];
-    if (accumulate) v += to_f(dst[0]);
-    dst[0] = from_f<T>(v);
-  }
-}
-
 template <typename T>
 int up_bwd(const void* gy, long long ldgy, const void* gy2, long long ldgy2, int N, int H, int W, int C, int scale,
            int mode, void* gx, long long ldgx, int acc, hipStream_t st) {
-  if (C == 1 && W <= UPC1_COLS * 256 && (long long)W * scale <= 16384 && (long long)N * H < (1LL << 31) &&
-      !(getenv("DGVCC_UP_C1") && getenv("DGVCC_UP_C1")[0] == '0')) {  // DGVCC_UP_C1=0: the generic kernel (A/B)
-    hipLaunchKernelGGL((upsample_bwd_c1_kernel<T>), dim3((unsigned)(N * H)), dim3(256), (size_t)W * scale * 4, st,
-                       (const T*)gy, ldgy, (const T*)gy2, ldgy2, H, W, scale, mode, (T*)gx, ldgx, acc);
-    DG_CHECK_LAUNCH();
-    return DG_OK;
-  }
   constexpr int V = 16 / (int)sizeof(T);
   const bool vec = (C % V == 0) && (ldgy % V == 0) && (ldgx % V == 0) && (!gy2 || ldgy2 % V == 0);
   const long long total = (long long)N * H * W * (vec ? C / V : C);

@@ -362,8 +362,8 @@ def as_cat(x):
     """A head plan's concatenation input: a (y1, y2, y3) tuple of NHWC tensors -> CatParts,
     or a materialised NHWC y_cat tensor -> Act."""
     if isinstance(x, (tuple, list)):
-        return CatParts(*(Act(t) for t in x))
-    return Act(x)
+        return CatParts(*(K.import_act(t) for t in x))
+    return K.import_act(x)
 
 
 def cat_empty_like(cat):
@@ -574,7 +574,8 @@ class FeaturePlan:
         y1 = nh(H // 4, W // 4, 128); D[5].forward(a17, y1, training, tape)
         if tape is not None:
             tape[self] = dict(dec1in=dec1in, dec2in=dec2in, shape=(N, H, W), dt=dt, inst=inst, x1=x1, x2=x2, x3=x3)
-        return y1.buf, y2.buf, y3.buf, x3.buf
+        # the plain tensors cross the autograd boundary; their f32 operand maxima go with them
+        return K.export_amax(y1), K.export_amax(y2), K.export_amax(y3), K.export_amax(x3)
 
     @staticmethod
     def _inorm_stage(layer, x, out: Act, pool: Act | None, training, tape):
@@ -947,10 +948,15 @@ class _Heads:
         two = len(Ps) == 2
         work = torch.empty(K.query("dg_mem_head_workspace", M, S) // 4 + 1, dtype=torch.float32, device=dev)
         gLs = [Act(torch.empty_like(P.buf)) for P in Ps] if want_gl else None
+        # f32: max |gL_v| from the same pass, for the logits GEMMs' f16 x3 scales in bwd_logits
+        am = torch.empty(2, dtype=torch.float32, device=dev) if (gLs and P1.buf.dtype == torch.float32) else None
+        if am is not None:
+            for i, gL in enumerate(gLs):
+                gL.amax = am[i:i + 1]
         K.call("dg_softmax_head_bwd", P1.dt, len(Ps), loss, P1.ptr, Ps[1].ptr if two else None, M, S, K.ptr(v),
                self.head_act, K.ptr(yhs[0]), K.ptr(yhs[1]) if two else None, K.ptr(g_hs[0]),
                K.ptr(g_hs[1]) if two else None, K.ptr(coef), gLs[0].ptr if gLs else None,
-               gLs[1].ptr if (gLs and two) else None, K.ptr(work), K.stream())
+               gLs[1].ptr if (gLs and two) else None, K.ptr(work), K.ptr(am), K.stream())
         dmem = None
         if any(g is not None for g in g_hs):
             dmem, gw, gb = self.memr.head_grads(work, M, self.head_w, want_dmem=want_gl)
@@ -963,7 +969,7 @@ class _Heads:
             if training and self.cls_drop_module.p > 0 else None
         a = Act(K.nhwc(N, h, w, self.cls.Cout, x3.dtype, x3.device))
         sub = {} if tape is not None else None
-        self.cls.forward(Act(x3), a, training, sub, drop=drop)
+        self.cls.forward(K.import_act(x3), a, training, sub, drop=drop)
         cb = self.cls_b.detach() if self.cls_b is not None else None
         c = K.head_fwd(a, self.cls_w.detach().reshape(-1), cb, K.ACT_SIGMOID)
         if tape is not None:
@@ -1164,6 +1170,11 @@ class PairPlan(_Heads):
             mask.copy_(em.reshape(-1))
             K.call("dg_emask_bwd", y1.dt, y1.ptr, y2.ptr, N, HW, C, K.ptr(mask), K.ptr(d1), K.ptr(d2), m1.ptr,
                    m2.ptr, C, K.stream())
+        if dt == torch.float32 and y1.amax is not None and y2.amax is not None:
+            # m_v = y_v * e * drop_v with e in {0, 1} and one keep value per mask: fl(max|y_v| * max drop_v)
+            # bounds every fl(|y| * drop) (rounding is monotone), the logits GEMMs' f16 x3 operand scale
+            m1.amax = y1.amax if d1 is None else y1.amax * d1.max()
+            m2.amax = y2.amax if d2 is None else y2.amax * d2.max()
         # memory read, both views, + consistency loss
         memT_s, mem_p, scale = self.memr.packs(dt)
         L1 = self.memr.logits(m1, memT_s, dt)

@@ -6,6 +6,7 @@ becomes "write into a channel slice" with no copy.
 """
 from __future__ import annotations
 
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -140,6 +141,32 @@ def _fwd_workspace(x: Act, Cout: int, R: int):
     if ws == 0:
         return 0, None
     return ws, torch.empty(ws, dtype=torch.uint8, device=x.buf.device)
+
+
+_EXPORTED: dict = {}  # data_ptr -> (weakref to the buffer, its version, shape, amax)
+
+
+def export_amax(a: Act) -> torch.Tensor:
+    """a.buf, with a's operand maximum kept for a consumer that receives the plain tensor (plan
+    outputs cross the autograd boundary as tensors; import_act finds the maximum again)."""
+    if a.amax is not None and a.off == 0 and a.C == a.buf.shape[3]:
+        if len(_EXPORTED) > 64:  # drop the entries whose buffers are gone
+            for k in [k for k, e in _EXPORTED.items() if e[0]() is None]:
+                del _EXPORTED[k]
+        _EXPORTED[a.buf.data_ptr()] = (weakref.ref(a.buf), a.buf._version, tuple(a.buf.shape), a.amax)
+    return a.buf
+
+
+def import_act(t: torch.Tensor) -> Act:
+    """Act(t) with the operand maximum export_amax kept for it: only while the exported buffer is
+    alive (so the address is still its), unmodified (same version) and of the same shape."""
+    a = Act(t)
+    e = _EXPORTED.get(t.data_ptr())
+    if e is not None:
+        src = e[0]()
+        if src is not None and src._version == e[1] and t._version == e[1] and tuple(t.shape) == e[2]:
+            a.amax = e[3]
+    return a
 
 
 def amax(x: Act) -> torch.Tensor:

@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 4 /* 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 5 /* 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -558,7 +558,7 @@ int dg_softmax_head_fwd(int dtype, int nviews, int loss, const void* L1, const v
 int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* P1, const void* P2, int M, int C,
                         const float* v, int act, const float* yh1, const float* yh2, const float* gyh1,
                         const float* gyh2, const float* coef, void* GL1, void* GL2, void* workspace,
-                        void* stream);
+                        float* amax, void* stream);
 int dg_mem_head_grads(void* workspace, int M, int C, const float* mem, const float* w, int k,
                       float* dmem, float* gw, float* gb, void* stream);
 /* loss_err = F.l1_loss(IN(y1), IN(y2)) (models/models2.py:334) from the instance-norm

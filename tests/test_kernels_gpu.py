@@ -241,35 +241,6 @@ def test_upsample(dev, dtype, scale, mode, C):
     assert relerr(to_nchw(gx.buf.float()), xr.grad) < tol
 
 
-@pytest.mark.parametrize("scale,mode,W", [(16, 1, 64), (4, 0, 300), (4, 0, 1024), (2, 2, 7)])
-def test_upsample_bwd_c1_rows(dev, scale, mode, W, monkeypatch):
-    """The one-channel row-staged backward (upsample_bwd_c1_kernel: > 256 input columns, a second
-    gradient, accumulation) against torch's autograd and the generic kernel (DGVCC_UP_C1=0)."""
-    K = _k()
-    N, H = 2, 5
-    g = torch.Generator().manual_seed(8)
-    x = torch.randn(N, 1, H, W, generator=g)
-    gy = torch.randn(N, 1, H * scale, W * scale, generator=g)
-    gy2 = torch.randn(N, 1, H * scale, W * scale, generator=g)
-    old = torch.randn(N, 1, H, W, generator=g)
-    xr = x.clone().requires_grad_(True)
-    if mode == 2:
-        yr = F.interpolate(xr, scale_factor=scale, mode="nearest")
-    else:
-        yr = F.interpolate(xr, scale_factor=scale, mode="bilinear", align_corners=(mode == 1))
-    yr.backward(gy + gy2)
-    outs = []
-    for flag in ("1", "0"):
-        monkeypatch.setenv("DGVCC_UP_C1", flag)
-        gx = K.Act(to_nhwc(old).to(dev))
-        K.upsample_bwd(K.Act(to_nhwc(gy).to(dev)), scale, mode, gx, gy2=K.Act(to_nhwc(gy2).to(dev)), accumulate=True)
-        torch.cuda.synchronize()
-        outs.append(to_nchw(gx.buf).cpu())
-    # f32 sums over up to (2 scale + 3)^2 taps in another order than autograd's: test_upsample's 1e-5
-    assert relerr(outs[0], xr.grad + old) < 1e-5
-    assert relerr(outs[0], outs[1]) < 1e-5
-
-
 @pytest.mark.parametrize("act", [0, 1, 2])
 def test_head(dev, act):
     K = _k()
