@@ -323,6 +323,8 @@ def run_leg(args, precision, dev, world, rank):
     res = {"elapsed": elapsed, "last_loss": last, "mode": mode, "model": type(model).__name__}
     if world > 1:
         res["allreduce"] = dict(dp, buckets=len(opt.reducer.buckets) if opt.reducer is not None else 1)
+    else:  # the setting a --gpus N run of this command uses; one rank all-reduces nothing
+        res["allreduce"] = dict(dp, buckets=None, note="world size 1: no all-reduce runs")
     conv_ms, conv_flops, conv_n, conv_bytes = timer.summary(("fwd", "dgrad"))
     wg_ms, wg_flops, wg_n, _ = timer.summary(("wgrad",))
     enc_kinds = ("fwd", "dgrad", "wgrad", "stem", "stem_wgrad")
