@@ -1370,11 +1370,18 @@ static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA add
 // 4-7 (the arbitration losers of the 8-wave block) and no per-block priority flips; 3 = SIMD partners
 // out of phase: waves 0-3 issue their DMA in the prologue (as 0) while waves 4-7 run their MFMA block,
 // and waves 4-7 issue theirs after their MFMA block while waves 0-3 run theirs (an LDS-DMA piece costs its
-// wave 100-185 issue cycles, MI355X_MICROARCH.md); 4 = 3 without the per-block s_setprio.
+// wave 100-185 issue cycles, MI355X_MICROARCH.md); 4 = 3 without the per-block s_setprio; 5 (TALL, KT >= 2):
+// register staging instead of LDS-DMA -- each K-step's A and B pieces are loaded into registers
+// (buffer_load_dwordx4, the same addresses and out-of-window zero fill) two K-steps ahead and stored
+// to their stage with ds_write_b128 one K-step ahead, after the current stage's fragment reads; the
+// stage is then ordered by lgkmcnt + the barrier instead of vmcnt.  The same LDS image and MFMA
+// order: bit-identical to SCH 0.
 template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0, int HM = 0, int STAMP = 0,
           int SCH = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   static_assert(!TALL || (BN == 256 && EPI == 0 && STG == 2 && INC), "TALL: 256-channel training forward only");
+  static_assert(SCH != 5 || (TALL && HM), "SCH 5: the TALL f16 x3 kernel");
+  constexpr bool RSTG = SCH == 5;
   constexpr int NPL = HM ? 2 : 3;  // filter planes
   constexpr int KB = NPL * 64;     // bytes per (output channel, 32-deep k-block) of the planes
   constexpr int PSB = TALL ? 256 : psplit_psb(BN, WIDE);
@@ -1497,6 +1504,35 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
                 tapmask_ok<BI>(c.tm, i, need) ? c.bofs + cbytes[i] + (toff + (unsigned)(i * 8 * a.ldx * 4)) : 0xFFFFFFF0u);
     advance();
   };
+  // SCH 5: the pieces of issue_inc's K-step into registers (ra: filter, rb: pixels), then stored to a stage
+  u4v ra[RSTG ? AI : 1], rb[RSTG ? BI : 1];
+  auto load_inc = [&](const Ctx& c) __attribute__((always_inline)) {
+    if constexpr (RSTG) {
+      const int is = ko ? d0 : d1, ir = ko ? d1 : d2, icb = ko ? d2 : d0;
+      const int rs = ir * a.S + is;
+#pragma unroll
+      for (int q = 0; q < AI; ++q)
+        ra[q] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                                            c.wr, alane + (unsigned)((rs * CB + icb) * KB), aoff_s(q), 0));
+      const unsigned toff = (unsigned)((((ir - a.pad) * a.W + (is - a.pad)) * a.ldx + icb * 32) * 4);
+      const unsigned need = tap_need(ir, is);
+#pragma unroll
+      for (int i = 0; i < BI; ++i)
+        rb[i] = bload(c.xr, tapmask_ok<BI>(c.tm, i, need) ? c.bofs + cbytes[i] + (toff + (unsigned)(i * 8 * a.ldx * 4))
+                                                           : 0xFFFFFFF0u);
+      advance();
+    }
+  };
+  auto store_stage = [&](unsigned stage) __attribute__((always_inline)) {
+    if constexpr (RSTG) {
+      char* As = smem + stage * STAGE;
+      char* Bs = As + A_BYTES;
+#pragma unroll
+      for (int q = 0; q < AI; ++q) *(u4v*)(As + (wid * AI + q) * 1024 + lane * 16) = ra[q];
+#pragma unroll
+      for (int i = 0; i < BI; ++i) *(u4v*)(Bs + (wid * BI + i) * 1024 + lane * 16) = rb[i];
+    }
+  };
   // SCH >= 1: piece p (< AI: filter, else pixels) of the DMA issue_inc makes; the caller advances the
   // cursor after the last piece
   auto issue_piece = [&](const Ctx& c, unsigned stage, int pc) __attribute__((always_inline)) {
@@ -1552,7 +1588,12 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   const int wpx = (wid % NPXG) * (PSB / NPXG), wco = (wid / NPXG) * (BN / NCOG);
   const int fr = lane & 15, fc = lane >> 4;
   unsigned gs = 0;
-  if constexpr (INC) {
+  if constexpr (RSTG) {  // K-step 0 into stage 0, K-step 1 into registers (KT >= 2, checked by the launcher)
+    load_inc(cur);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_stage(0);
+    load_inc(cur);
+  } else if constexpr (INC) {
     issue_inc(cur, 0);
     if (PF > 1) issue_inc(cur, 1);
   } else {
@@ -1588,7 +1629,8 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     }
     for (int t = 0; t < KT; ++t, ++gs) {
       const bool more = t + 1 < KT || has_next;
-      if (PF > 1 && more && (t > 0 || first_tile)) {
+      if constexpr (RSTG) {  // the stage was written by ds_write: lgkmcnt below + the barrier order it
+      } else if (PF > 1 && more && (t > 0 || first_tile)) {
         if constexpr (AI + BI == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
         else if constexpr (AI + BI == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1627,7 +1669,20 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       // the next DMA: now (SCH 0), or one piece per MFMA block below (SCH >= 1)
       const int u_dma = t + PF;
       const bool dma_cur = u_dma < KT, dma_nxt = !dma_cur && has_next;
-      if constexpr (SCH >= 3) {
+      if constexpr (RSTG) {
+        // K-step u_dma (loaded a K-step ago) into its stage: every wave is past this K-step's barrier,
+        // so done reading that stage (it held K-step t - 1); then K-step t + 2 into the registers
+        if (dma_cur || dma_nxt) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          store_stage((gs + PF) % STG);
+        }
+        const int u2 = t + 2;
+        if (u2 < KT) load_inc(cur);
+        else if (has_next) {
+          if (u2 == KT) d0 = d1 = d2 = 0;
+          load_inc(nxt);
+        }
+      } else if constexpr (SCH >= 3) {
         if (dma_nxt && u_dma == KT) d0 = d1 = d2 = 0;
         if (wid < 4) {
           if (dma_cur) issue_inc(cur, (gs + PF) % STG);
@@ -1696,7 +1751,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
         }
         if constexpr (HM) __builtin_amdgcn_sched_barrier(0);  // no fragment reads hoisted across blocks
       }
-      if constexpr (SCH >= 3) {  // waves 4-7: the next K-step's DMA after their MFMA block
+      if constexpr (SCH == 3 || SCH == 4) {  // waves 4-7: the next K-step's DMA after their MFMA block
         if (wid >= 4) {
           if (dma_cur) issue_inc(cur, (gs + PF) % STG);
           else if (dma_nxt) issue_inc(nxt, (gs + PF) % STG);
@@ -3570,14 +3625,16 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
                  (long long)g2 * 8 * 8 * 8 <= g_stamp_bytes) {  // diagnostic stamp build (tools/stamp_psplit.py)
           ap.stamps = g_stamps;
           const int sch = psplit_sch();
-          if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          if (sch == 5 && a.R * a.S * (a.C / 32) >= 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 5>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 3) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 2>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 1) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
         } else if (h16 && tall) {
           const int sch = psplit_sch();
-          if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          if (sch == 5 && a.R * a.S * (a.C / 32) >= 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 5>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 3) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 2>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 1) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);

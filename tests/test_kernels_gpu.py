@@ -675,6 +675,43 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
             assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
 
 
+@pytest.mark.parametrize("sch", ["1", "3", "5"])
+@pytest.mark.parametrize("N,H,W,C,Cout,R", [(2, 96, 392, 256, 256, 3), (1, 20, 72, 128, 512, 3), (3, 9, 40, 64, 256, 1),
+                                            (1, 33, 47, 512, 256, 3)])
+def test_conv_f32_psplit_schedules(dev, sch, N, H, W, C, Cout, R, monkeypatch):
+    """The f16 x3 256-pixel pre-split forward's schedules (DGVCC_PSPLIT_SCH: 1 DMA pieces spread over the
+    MFMA blocks, 3 SIMD partners out of phase, 5 register staging instead of LDS-DMA) bit-identical to
+    the default (0): several tiles per block (the cross-tile prefetch), ragged pixel tails, bias,
+    epilogue statistics and the dgrad on the same kernel."""
+    K = _k()
+    prev = K.call("dg_get_f32_math")
+    K.call("dg_set_f32_math", 2)
+    try:
+        g = torch.Generator().manual_seed(41)
+        x = K.Act(to_nhwc(torch.relu(torch.randn(N, C, H, W, generator=g))).to(dev))
+        w = (torch.randn(Cout, C, R, R, generator=g) / (R * R * C) ** 0.5).to(dev)
+        bias = (torch.randn(Cout, generator=g) * 0.1).to(dev)
+        gy = K.Act(to_nhwc(torch.randn(N, Cout, H, W, generator=g) * 1e-3).to(dev))
+        wp = K.pack_weight(w, torch.float32)
+        outs = []
+        for v in ("0", sch):
+            monkeypatch.setenv("DGVCC_PSPLIT_SCH", v)
+            y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+            res = K.conv_fwd_stats(x, wp, Cout, R, R // 2, y, bias=bias)
+            if res is None:  # a shape without epilogue statistics: nothing was launched
+                K.conv_fwd(x, wp, Cout, R, R // 2, y, bias=bias)
+            y2 = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+            K.conv_fwd(x, wp, Cout, R, R // 2, y2)
+            dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+            K.conv_dgrad(gy, wp, C, R, R // 2, dx)
+            torch.cuda.synchronize()
+            outs.append([y.buf.clone(), y2.buf.clone(), dx.buf.clone()] + ([res[0].clone()] if res is not None else []))
+        for u, v in zip(*outs):
+            assert torch.equal(u, v)
+    finally:
+        K.call("dg_set_f32_math", prev)
+
+
 @pytest.mark.parametrize("xs,ws", [(1e-30, 1.0), (1e-6, 1e-3), (1.0, 1.0), (1e6, 1e3), (1e30, 1e-20)])
 @pytest.mark.parametrize("case", [(1, 64, 96, 256, 256, 3), (1, 32, 512, 64, 64, 3), (1, 48, 64, 128, 128, 3)])
 def test_conv_f32_h16_scales(dev, xs, ws, case):
