@@ -1375,12 +1375,26 @@ static bool psplit_inc() {  // DGVCC_PSPLIT_INC=0: per-K-step recomputed DMA add
 // (buffer_load_dwordx4, the same addresses and out-of-window zero fill) two K-steps ahead and stored
 // to their stage with ds_write_b128 one K-step ahead, after the current stage's fragment reads; the
 // stage is then ordered by lgkmcnt + the barrier instead of vmcnt.  The same LDS image and MFMA
-// order: bit-identical to SCH 0.
+// order: bit-identical to SCH 0.  6 (TALL, HM): the two channel halves' waves (0-3: channels 0-127, 4-7:
+// 128-255; SIMD partners) one phase apart, two barriers per K-step: in phase 1 of K-step t waves 0-3
+// read and split K-step t's fragments while waves 4-7 run their MFMA block of K-step t - 1; in phase 2
+// every wave issues K-step t + 1's DMA (into the stage K-step t - 1 freed), waves 0-3 run their MFMA
+// block of K-step t and waves 4-7 read and split K-step t's fragments.  Each SIMD then holds one wave
+// in its MFMA block and one in its prologue, where SCH 0 keeps both in the same phase (the stamp build
+// put their prologues at 28% / 66% of the K-step).  A tile ends with a drain phase (waves 4-7's last
+// MFMA block) before the shared epilogue.  The same fragments and MFMA order: bit-identical to SCH 0.
 template <int BN, int STG, int EPI = 0, int WIDE = 1, int INC = 1, int TALL = 0, int HM = 0, int STAMP = 0,
           int SCH = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   static_assert(!TALL || (BN == 256 && EPI == 0 && STG == 2 && INC), "TALL: 256-channel training forward only");
   static_assert(SCH != 5 || (TALL && HM), "SCH 5: the TALL f16 x3 kernel");
+  static_assert(SCH != 6 || (TALL && HM && STG == 2 && !STAMP), "SCH 6: the TALL f16 x3 kernel");
+  static_assert(SCH != 7 || (TALL && HM), "SCH 7: diagnostic timing of the TALL f16 x3 kernel without the split");
+  // SCH 8 (HM): the pixel operand arrives PRE-SPLIT (split_x_h_kernel, once per launch): a.x is the
+  // [M][C/32][hi 32 x f16 | lo 32 x f16] image of x * s_x, the same 128 B per (pixel, 32-channel block)
+  // as the f32 rows, so the DMA is unchanged and the prologue reads the two parts' chunks fc and 4 + fc
+  // instead of splitting (the split was 28% of the kernel: SCH 7).  Bit-identical to SCH 0.
+  static_assert(SCH != 8 || HM, "SCH 8: the f16 x3 kernels");
   constexpr bool RSTG = SCH == 5;
   constexpr int NPL = HM ? 2 : 3;  // filter planes
   constexpr int KB = NPL * 64;     // bytes per (output channel, 32-deep k-block) of the planes
@@ -1627,6 +1641,89 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       st_prev = s;
       ++st_tiles;
     }
+    if constexpr (SCH == 6) {
+      // every wave runs the same K-step code (barrier, prologue, barrier, MFMA block); waves 4-7 pass
+      // one extra barrier at the tile's start and waves 0-3 one at its end, so a wave's k-th barrier
+      // meets its SIMD partner's (k-1)-th: one runs its prologue while the other runs its MFMA block
+      const bool lead = wid < 4;
+      const unsigned gb = gs;  // stage counter of this tile's K-step 0
+      s8v bh6[TJ][NPL], ah6[NPL];
+      auto aread6 = [&](const char* As, int i, s8v (&ah)[NPL]) __attribute__((always_inline)) {
+        const int row = wco + 16 * i + fr;
+        const int off = row * AROWB + ((fc ^ psw_a(row)) << 4);
+#pragma unroll
+        for (int pl = 0; pl < NPL; ++pl) ah[pl] = *(const s8v*)(As + pl * BN * AROWB + off);
+      };
+      // K-step t + 1's DMA (or the next tile's K-step 0) into the stage K-step t - 1 held: issued by
+      // the leaders after their second barrier of K-step t and by the trailers after their first,
+      // which is the same barrier instant; every wave waits for its own pieces one phase later,
+      // ahead of the barrier behind which the leaders read them
+      auto dma6 = [&](int t) __attribute__((always_inline)) {
+        const int u = t + 1;
+        if (u < KT) issue_inc(cur, (gb + u) % STG);
+        else if (has_next) {
+          d0 = d1 = d2 = 0;
+          issue_inc(nxt, (gb + u) % STG);
+        }
+      };
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // K-step 0 (issued before the loop / in the last tile)
+      if (!lead) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      for (int t = 0; t < KT; ++t) {
+        const char* As = smem + ((gb + t) % STG) * STAGE;
+        const char* Bs = As + A_BYTES;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (!lead) dma6(t);
+        {  // prologue: K-step t's pixel fragments read and split, the first filter fragment read
+          u4v b0[TJ], b1[TJ];
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) {
+            b0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc));
+            b1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc + 1));
+          }
+          aread6(As, 0, ah6);
+#pragma unroll
+          for (int j = 0; j < TJ; ++j) split2h_8(b0[j], b1[j], hsx, bh6[j][0], bh6[j][1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (!lead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        if (lead) dma6(t);
+#pragma unroll
+        for (int i = 0; i < TI; ++i) {  // MFMA block of K-step t
+          s8v an[NPL];
+          if (i + 1 < TI) aread6(As, i + 1, an);
+          __builtin_amdgcn_s_setprio(1);
+          constexpr int PA[3] = {1, 0, 0}, PB[3] = {0, 1, 0};
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah6[PA[q]]),
+                                                                 __builtin_bit_cast(h8v, bh6[j][PB[q]]), acc[i][j], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+          if (i + 1 < TI) {
+#pragma unroll
+            for (int pl = 0; pl < NPL; ++pl) ah6[pl] = an[pl];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (lead) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (lead) {  // meets the trailers' second barrier of the last K-step
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      gs = gb + KT;
+    } else
     for (int t = 0; t < KT; ++t, ++gs) {
       const bool more = t + 1 < KT || has_next;
       if constexpr (RSTG) {  // the stage was written by ds_write: lgkmcnt below + the barrier order it
@@ -1654,9 +1751,9 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       const char* Bs = As + A_BYTES;
       u4v b0[TJ], b1[TJ];
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        b0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc));
-        b1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, 2 * fc + 1));
+      for (int j = 0; j < TJ; ++j) {  // SCH 8: the hi / lo chunks of the pre-split rows, else two f32 chunks
+        b0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, SCH == 8 ? fc : 2 * fc));
+        b1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, SCH == 8 ? 4 + fc : 2 * fc + 1));
       }
       auto aread = [&](int i, s8v (&ah)[NPL]) __attribute__((always_inline)) {
         const int row = wco + 16 * i + fr;
@@ -1682,13 +1779,13 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
           if (u2 == KT) d0 = d1 = d2 = 0;
           load_inc(nxt);
         }
-      } else if constexpr (SCH >= 3) {
+      } else if constexpr (SCH == 3 || SCH == 4) {
         if (dma_nxt && u_dma == KT) d0 = d1 = d2 = 0;
         if (wid < 4) {
           if (dma_cur) issue_inc(cur, (gs + PF) % STG);
           else if (dma_nxt) issue_inc(nxt, (gs + PF) % STG);
         }
-      } else if constexpr (SCH >= 1) {
+      } else if constexpr (SCH == 1 || SCH == 2) {
         if (dma_nxt && u_dma == KT) d0 = d1 = d2 = 0;
       } else {
         const int u = u_dma;
@@ -1706,7 +1803,10 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       s8v bh[TJ][NPL];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        if constexpr (HM) split2h_8(b0[j], b1[j], hsx, bh[j][0], bh[j][1]);
+        if constexpr (SCH == 7 || SCH == 8) {  // 8: the parts as stored; 7 (diagnostic): the raw f32 rows
+          bh[j][0] = __builtin_bit_cast(s8v, b0[j]);
+          bh[j][1] = __builtin_bit_cast(s8v, b1[j]);
+        } else if constexpr (HM) split2h_8(b0[j], b1[j], hsx, bh[j][0], bh[j][1]);
         else split3_8(b0[j], b1[j], bh[j][0], bh[j][1], bh[j][2]);
       }
       if constexpr (HM) __builtin_amdgcn_sched_barrier(0);  // the raw rows die here (else: 59 spilled VGPRs)
@@ -2497,6 +2597,29 @@ __global__ __launch_bounds__(256) void split_weight_h_kernel(const float* __rest
 
 // *out = max |x| over the M x C f32 rows of pixel stride ldx (bit pattern of a non-negative float,
 // so an integer max; *out zeroed by the caller)
+// The f16 x3 pixel operand pre-split once per launch (conv_fwd_psplit_kernel SCH 8): out[p][cb] = the two
+// f16 parts of x[p][32 cb .. 32 cb + 31] * s_x (split2h_8, exactly the kernel's own split), hi in bytes
+// 0-63 and lo in 64-127 of the 128-B block; s_x is split_weight_h_kernel's (hsx, after the scales).  One
+// thread per 8 channels.
+__global__ __launch_bounds__(256) void split_x_h_kernel(const float* __restrict__ x, long long ldx, long long M,
+                                                        int C, const float* __restrict__ hsx,
+                                                        unsigned char* __restrict__ out) {
+  const int c8 = C >> 3;
+  const long long total = M * c8;
+  const float s = *hsx;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long p = i / c8;
+    const int q = (int)(i - p * c8);  // 8-channel group: block q >> 2, chunk q & 3
+    const float* src = x + p * ldx + q * 8;
+    const u4v x0 = *(const u4v*)src, x1 = *(const u4v*)(src + 4);
+    s8v hi, lo;
+    split2h_8(x0, x1, s, hi, lo);
+    unsigned char* d = out + (p * (C >> 5) + (q >> 2)) * 128 + (q & 3) * 16;
+    *(s8v*)d = hi;
+    *(s8v*)(d + 64) = lo;
+  }
+}
+
 __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long ldx, long long M, int C,
                                                    unsigned* __restrict__ out) {
   __shared__ float red[4];
@@ -3274,6 +3397,16 @@ static bool psplit_ok(const FwdArgs& a) {
   return (long long)dg_cdiv(M, psplit_tile_px(a)) * (a.Cout / f32_pers_bn(a.Cout)) >= mt;
 }
 
+// DGVCC_PSPLIT_XS=0: the f16 x3 pre-split forward splits its pixel fragments itself (SCH 0) instead of
+// reading them pre-split by split_x_h_kernel (SCH 8); read per launch (A/B)
+static bool psplit_xs() {
+  const char* e = getenv("DGVCC_PSPLIT_XS");
+  return !(e && e[0] == '0');
+}
+// workspace bytes of the pre-split pixel operand (after the filter planes, 256-B aligned)
+static long long xsplit_bytes(const FwdArgs& a) { return (long long)a.N * a.H * a.W * a.C * 4; }
+static long long xsplit_off(long long planes) { return (planes + 255) / 256 * 256; }
+
 // DGVCC_PSPLIT_TALL=0: never the 256-pixel pre-split tiles; 1 (default): where they quantise onto the
 // CUs no worse than the 192-pixel ones; 2: always (256-channel training forwards/dgrads)
 static int psplit_tall_mode() {
@@ -3607,9 +3740,29 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           const char* e = getenv("DGVCC_PSPLIT_ORDER");
           ap.tile_order = (e && e[0] == '1') ? 1 : 0;
         }
+        // f16 x3: the pixel operand split once into the workspace after the filter planes (SCH 8)
+        bool xs = false;
+        if (h16 && psplit_xs() && !a.escale && a.ldx % 4 == 0 && !(g_stamps && getenv("DGVCC_PSPLIT_STAMP"))) {
+          const long long off = xsplit_off(presplit_h_bytes(a));
+          if (a.wsplit_bytes >= off + xsplit_bytes(a)) {
+            const long long KTh = (long long)a.R * a.S * (a.C / 32);
+            const float* hsx = (const float*)((const char*)wsp + (long long)a.Cout * KTh * 128) + a.Cout;
+            unsigned char* xsb = (unsigned char*)a.wsplit + off;
+            const long long n8 = M * (a.C / 8);
+            hipLaunchKernelGGL(split_x_h_kernel, dim3((unsigned)std::min<long long>(dg_cdiv(n8, 256), 16384)), dim3(256),
+                               0, st, (const float*)a.x, a.ldx, M, a.C, hsx, xsb);
+            DG_CHECK_LAUNCH();
+            ap.x = (const char*)xsb;
+            ap.ldx = a.C;
+            xs = true;
+          }
+        }
 #define PSPLIT_LAUNCH(EPI_)                                                                                    \
   do {                                                                                                         \
-    if (h16) {                                                                                                 \
+    if (h16 && xs) {                                                                                           \
+      if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 0, 1, 0, 8>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+      else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 0, 1, 0, 8>), dim3(g2), dim3(512), 0, st, ap, wspc); \
+    } else if (h16) {                                                                                          \
       if (bn2 == 256) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, EPI_, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, ap, wspc); \
       else hipLaunchKernelGGL((conv_fwd_psplit_kernel<128, 2, EPI_, 1, 1, 0, 1>), dim3(g2), dim3(512), 0, st, ap, wspc); \
     } else if (bn2 == 256) {                                                                                   \
@@ -3631,9 +3784,13 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           else if (sch == 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 2>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 1) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 1>), dim3(g2), dim3(512), 0, st, ap, wspc);
+        } else if (h16 && tall && xs) {
+          hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 8>), dim3(g2), dim3(512), 0, st, ap, wspc);
         } else if (h16 && tall) {
           const int sch = psplit_sch();
-          if (sch == 5 && a.R * a.S * (a.C / 32) >= 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 5>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          if (sch == 6) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 6>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 7) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 7>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 5 && a.R * a.S * (a.C / 32) >= 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 5>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 3) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 3>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 2>), dim3(g2), dim3(512), 0, st, ap, wspc);
@@ -5465,7 +5622,14 @@ extern "C" int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, i
 extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
   const long long M = (long long)N * H * W;
-  if (dtype == DG_F32) return ((long long)Cout * R * S * C * 6 + 255) / 256 * 256;  // pre-split filter planes
+  if (dtype == DG_F32) {  // pre-split filter planes (+ the pre-split pixel operand of the f16 x3 pre-split forward)
+    const long long planes = ((long long)Cout * R * S * C * 6 + 255) / 256 * 256;
+    FwdArgs a{nullptr, C, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0, nullptr};
+    // room whatever DGVCC_PSPLIT_XS says (the launch reads the switch; callers cache this size)
+    if (2 * a.pad == R - 1 && 2 * a.pad == S - 1 && psplit_ok(a))
+      return xsplit_off(planes) + xsplit_bytes(a);
+    return planes;
+  }
   if (!DG_IS16(dtype) || !fwd_has_epi_stats(C, Cout, C, R, S)) return 0;
   const int ks = fwd_ksplit(M, Cout, C, R, S);
   return ks > 1 ? (int64_t)ks * M * Cout * 4 : 0;

@@ -116,9 +116,11 @@ def test_f32_stats_rows_need_split_room():
     L = _capi.lib()
     for (N, H, W, C, Co) in ((16, 48, 64, 512, 512), (4, 64, 512, 64, 64), (16, 192, 256, 256, 256)):
         ws = L.dg_conv_fwd_workspace(0, N, H, W, C, Co, 3, 3)
+        planes = (Co * 9 * C * 6 + 255) // 256 * 256  # the filter planes' room (+ the pre-split x after it)
+        assert ws >= planes
         # x, w, y, part: dummy non-null pointers (the call returns before any launch)
         assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, None, 0, None, None) == -2
-        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, 8, ws - 256, None, None) == -2
+        assert L.dg_conv_fwd_ex(0, 8, C, N, H, W, C, 8, Co, 3, 3, 1, None, 8, Co, 0, 8, 8, planes - 256, None, None) == -2
 
 
 def test_call_raises_on_error():

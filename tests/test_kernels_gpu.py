@@ -675,14 +675,15 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
             assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
 
 
-@pytest.mark.parametrize("sch", ["1", "3", "5"])
+@pytest.mark.parametrize("sch", ["1", "3", "5", "6", "xs"])
 @pytest.mark.parametrize("N,H,W,C,Cout,R", [(2, 96, 392, 256, 256, 3), (1, 20, 72, 128, 512, 3), (3, 9, 40, 64, 256, 1),
                                             (1, 33, 47, 512, 256, 3)])
 def test_conv_f32_psplit_schedules(dev, sch, N, H, W, C, Cout, R, monkeypatch):
-    """The f16 x3 256-pixel pre-split forward's schedules (DGVCC_PSPLIT_SCH: 1 DMA pieces spread over the
-    MFMA blocks, 3 SIMD partners out of phase, 5 register staging instead of LDS-DMA) bit-identical to
-    the default (0): several tiles per block (the cross-tile prefetch), ragged pixel tails, bias,
-    epilogue statistics and the dgrad on the same kernel."""
+    """The f16 x3 pre-split forward's schedules (DGVCC_PSPLIT_SCH: 1 DMA pieces spread over the MFMA
+    blocks, 3 SIMD partners out of phase, 5 register staging instead of LDS-DMA, 6 the two channel
+    halves one phase apart; "xs": the pixel operand pre-split by split_x_h_kernel, SCH 8) bit-identical
+    to the in-kernel split (0): several tiles per block (the cross-tile prefetch), ragged pixel tails,
+    bias, epilogue statistics and the dgrad on the same kernel."""
     K = _k()
     prev = K.call("dg_get_f32_math")
     K.call("dg_set_f32_math", 2)
@@ -695,7 +696,11 @@ def test_conv_f32_psplit_schedules(dev, sch, N, H, W, C, Cout, R, monkeypatch):
         wp = K.pack_weight(w, torch.float32)
         outs = []
         for v in ("0", sch):
-            monkeypatch.setenv("DGVCC_PSPLIT_SCH", v)
+            if sch == "xs":  # the pre-split pixel operand (SCH 8, the default) against the in-kernel split
+                monkeypatch.setenv("DGVCC_PSPLIT_XS", "1" if v == "xs" else "0")
+            else:
+                monkeypatch.setenv("DGVCC_PSPLIT_XS", "0")
+                monkeypatch.setenv("DGVCC_PSPLIT_SCH", v)
             y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
             res = K.conv_fwd_stats(x, wp, Cout, R, R // 2, y, bias=bias)
             if res is None:  # a shape without epilogue statistics: nothing was launched

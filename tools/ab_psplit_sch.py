@@ -1,7 +1,7 @@
 """Same-process A/B of the f16 x3 256-pixel pre-split forward's schedules (DGVCC_PSPLIT_SCH, read per
 launch) on the headline's 256-channel layers at batch 16 (forward of 192x256 256->256 and
 96x128 512->512, dgrad of 192x256 512->256): interleaved rounds, best of 3, outputs compared
-bitwise against schedule 0.  usage: python tools/ab_psplit_sch.py [schedules, default 0,5]"""
+bitwise against schedule 0.  usage: python tools/ab_psplit_sch.py [schedules, default 0,5; "xs": the pre-split pixel operand]"""
 import os
 import sys
 
@@ -46,10 +46,16 @@ for (H, W, C, Cout, kind) in [(192, 256, 256, 256, "fwd"), (96, 128, 512, 512, "
     ms, res = {v: [] for v in schs}, {}
     for _ in range(3):
         for v in schs:
-            os.environ["DGVCC_PSPLIT_SCH"] = v
+            if v == "xs":  # the pre-split pixel operand (SCH 8)
+                os.environ["DGVCC_PSPLIT_XS"] = "1"
+                os.environ.pop("DGVCC_PSPLIT_SCH", None)
+            else:
+                os.environ["DGVCC_PSPLIT_XS"] = "0"
+                os.environ["DGVCC_PSPLIT_SCH"] = v
             ms[v].append(timed(fn))
             res[v] = out.buf.clone()
     os.environ.pop("DGVCC_PSPLIT_SCH", None)
+    os.environ.pop("DGVCC_PSPLIT_XS", None)
     line = f"{kind:5s} {B}x{H}x{W} {C}->{Cout}:"
     for v in schs:
         t = min(ms[v])
