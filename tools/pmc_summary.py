@@ -44,15 +44,19 @@ json.dump(out, open(os.path.join(dst, f"pmc_summary{suffix}.json"), "w"), indent
 conv = {k: v for k, v in out.items() if "conv_fwd_" in k and "bn_" not in k.split("(")[0]}
 if conv and key:
     n = sum(v["dispatches"] for v in conv.values())
+    # the f32 pre-split pass (split_x_h_kernel) runs inside the same dg_conv_fwd_ex calls: its bytes are
+    # part of those launches' traffic, its dispatches are not extra launches
+    extra = {k: v for k, v in out.items() if "split_x_h" in k}
     tot = sum((v["fetch_bytes_per_dispatch_corrected"] + v["write_bytes_per_dispatch"]) * v["dispatches"]
-              for v in conv.values())
+              for v in list(conv.values()) + list(extra.values()))
     tdir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "traffic")
     os.makedirs(tdir, exist_ok=True)
-    names = sorted({k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0] for k in conv})
+    names = sorted({k.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
+                    for k in list(conv) + list(extra)})
     json.dump({"workload_key": key, "kernels": names, "dispatches": n, "hbm_bytes_per_launch": tot / n,
                "source": os.path.join(dst, f"pmc_summary{suffix}.json"),
                "note": "FETCH_SIZE x2 (gfx950 wide-read correction) + WRITE_SIZE, KB->bytes, averaged over "
-                       "the conv forward/dgrad dispatches of a rocprofv3 --pmc pass of `bench.py` on this workload"},
+                       "the conv forward/dgrad dispatches (their pre-split passes' bytes included) of a rocprofv3 --pmc pass of `bench.py` on this workload"},
               open(os.path.join(tdir, key + ".json"), "w"), indent=1)
 for k, v in list(out.items())[:12]:
     print(f"{v['fetch_bytes_per_dispatch_corrected']/1e6:10.2f} MB rd {v['write_bytes_per_dispatch']/1e6:10.2f} MB wr  n={v['dispatches']:4d} {k[:80]}")

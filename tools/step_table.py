@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 GROUPS = [  # (group, regex on the short kernel name), first match wins
-    ("conv fwd/dgrad (LDS-DMA pipeline)", r"conv_fwd_(pers|pipe|tap3|psplit|rsplit)"),
+    ("conv fwd/dgrad (LDS-DMA pipeline)", r"conv_fwd_(pers|pipe|tap3|psplit|rsplit)|split_x_h"),
     ("split-weight prep", r"split_weight"),
     ("operand max (f16 x3 scales)", r"amax_kernel"),
     ("conv wgrad", r"conv_wgrad|wgrad_reduce|splitk_reduce"),
