@@ -3397,11 +3397,17 @@ static bool psplit_ok(const FwdArgs& a) {
   return (long long)dg_cdiv(M, psplit_tile_px(a)) * (a.Cout / f32_pers_bn(a.Cout)) >= mt;
 }
 
-// DGVCC_PSPLIT_XS=0: the f16 x3 pre-split forward splits its pixel fragments itself (SCH 0) instead of
-// reading them pre-split by split_x_h_kernel (SCH 8); read per launch (A/B)
-static bool psplit_xs() {
+// The f16 x3 pre-split forward reads its pixel operand pre-split by split_x_h_kernel (SCH 8) when
+// several output-channel tiles share each pixel tile of a 3x3 conv (Cout > the tile's bn): each of those
+// blocks would split the same fragments again, and the pass (8 B per element of HBM traffic) pays for
+// itself; with one channel tile, or a 1x1 conv's short K, the in-kernel split (SCH 0) is faster
+// (profiles/round5e/ab_xs/shapes_*).  DGVCC_PSPLIT_XS=0: never, =2: every eligible launch (A/B); read
+// per launch.
+static bool psplit_xs(const FwdArgs& a, int bn) {
   const char* e = getenv("DGVCC_PSPLIT_XS");
-  return !(e && e[0] == '0');
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '2') return true;
+  return a.Cout > bn && a.R * a.S > 1;
 }
 // workspace bytes of the pre-split pixel operand (after the filter planes, 256-B aligned)
 static long long xsplit_bytes(const FwdArgs& a) { return (long long)a.N * a.H * a.W * a.C * 4; }
@@ -3742,7 +3748,7 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
         }
         // f16 x3: the pixel operand split once into the workspace after the filter planes (SCH 8)
         bool xs = false;
-        if (h16 && psplit_xs() && !a.escale && a.ldx % 4 == 0 && !(g_stamps && getenv("DGVCC_PSPLIT_STAMP"))) {
+        if (h16 && psplit_xs(a, bn2) && !a.escale && a.ldx % 4 == 0 && !(g_stamps && getenv("DGVCC_PSPLIT_STAMP"))) {
           const long long off = xsplit_off(presplit_h_bytes(a));
           if (a.wsplit_bytes >= off + xsplit_bytes(a)) {
             const long long KTh = (long long)a.R * a.S * (a.C / 32);

@@ -696,8 +696,8 @@ def test_conv_f32_psplit_schedules(dev, sch, N, H, W, C, Cout, R, monkeypatch):
         wp = K.pack_weight(w, torch.float32)
         outs = []
         for v in ("0", sch):
-            if sch == "xs":  # the pre-split pixel operand (SCH 8, the default) against the in-kernel split
-                monkeypatch.setenv("DGVCC_PSPLIT_XS", "1" if v == "xs" else "0")
+            if sch == "xs":  # the pre-split pixel operand (SCH 8, forced on every eligible shape) against the in-kernel split
+                monkeypatch.setenv("DGVCC_PSPLIT_XS", "2" if v == "xs" else "0")
             else:
                 monkeypatch.setenv("DGVCC_PSPLIT_XS", "0")
                 monkeypatch.setenv("DGVCC_PSPLIT_SCH", v)

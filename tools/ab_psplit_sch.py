@@ -47,7 +47,7 @@ for (H, W, C, Cout, kind) in [(192, 256, 256, 256, "fwd"), (96, 128, 512, 512, "
     for _ in range(3):
         for v in schs:
             if v == "xs":  # the pre-split pixel operand (SCH 8)
-                os.environ["DGVCC_PSPLIT_XS"] = "1"
+                os.environ["DGVCC_PSPLIT_XS"] = "2"
                 os.environ.pop("DGVCC_PSPLIT_SCH", None)
             else:
                 os.environ["DGVCC_PSPLIT_XS"] = "0"
