@@ -99,9 +99,11 @@ int dg_conv_fwd_stats(int dtype, const void* x, int64_t ldx, int N, int H, int W
 /* Workspace (bytes, 0 = none needed) of dg_conv_fwd_ex / dg_conv_fwd_bn_eval /
  * dg_conv_fwd_bnbwd: 16-bit, the split-K partials of a shape whose tile grid cannot fill the
  * GPU (deep layers at small batch); DG_F32, the pre-split filter planes of the split-math
- * kernels (Cout*R*S*C*6 bytes).  With less (or none, as dg_conv_fwd passes) an f32 launch
- * takes a kernel that splits the filter per wave, and the statistics row counts of
- * dg_conv_stats_rows_ex assume the full workspace. */
+ * kernels (Cout*R*S*C*6 bytes) and, after them (256-B aligned), room for the f16 x3 pixel
+ * operand pre-split once per launch (N*H*W*C*4 bytes; used by 3x3 launches whose Cout spans
+ * several output-channel tiles).  With less (or none, as dg_conv_fwd passes) an f32 launch
+ * splits in-kernel (planes but no pixel room) or takes a kernel that splits the filter per
+ * wave (no planes); the statistics row counts of dg_conv_stats_rows_ex assume the planes. */
 int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S);
 /* dg_conv_fwd + dg_conv_fwd_stats in one entry: part may be NULL; with a workspace of
  * dg_conv_fwd_workspace bytes the K loop is split over blocks and reduced deterministically
