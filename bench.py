@@ -8,9 +8,13 @@ Default workload = the config BASELINE.json's metric is quoted on, configs/sta_f
 MSE count loss x log_para 1000 + 10 BCE class-map loss + 10 JSD-MSE consistency loss,
 fused AdamW), batch 16 per GPU of synthetic 3x768x1024 frames resident in HBM (no dataset
 offline), computed in fp32 like the reference: f32 storage, statistics and accumulation, the conv
-GEMMs on the bf16 matrix cores through an exact 3-way split of each f32 operand (six bf16
-products per f32 product, f32 accumulation: f32-grade; `--f32-math exact`
-runs them on v_mfma_f32_16x16x4_f32 instead, reported beside it as `f32_exact`).  A step is
+GEMMs on the f16 matrix cores as "f16 x3" (default `--f32-math h16`): each f32 operand scaled by a
+power of two (per filter row; per pixel-operand tensor in the forward / dgrad, per channel of both
+operands in the weight gradient) and cut into two f16 parts by nearest rounding, three f16 MFMA
+products per f32 product (hi*hi + hi*lo + lo*hi), f32 accumulation, exact rescale: f32-grade
+(DESIGN.md §3.1).  `--f32-math split` selects the exact 3-way bf16 split (six bf16 products per f32
+product), `--f32-math exact` v_mfma_f32_16x16x4_f32; the exact leg is reported beside the headline
+as `f32_exact`.  A step is
 DGTrainer.train_step: forward + loss + backward + optimizer step + the reference's per-step
 `.item()`; a frame is one 3x768x1024 view through forward and backward (final mode counts
 both views).  The same step in bf16 (bf16 storage/MFMA, f32 accumulation and
@@ -96,6 +100,9 @@ def parse():
     ap.add_argument("--width", type=int, default=W0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the multi-rank plumbing (launcher, gloo ranks, per-rank timing "
+                         "aggregation and the JSON line) with a toy step instead of the GPU workload")
     return ap.parse_args()
 
 
@@ -250,7 +257,7 @@ def measured_traffic(args, precision):
 
 
 FWD_KERNEL_NAMES = {
-    "fp32": "conv_fwd_psplit_kernel<256|128> + conv_fwd_rsplit3_kernel + conv_fwd_rsplit_kernel (implicit-GEMM "
+    "fp32_split": "conv_fwd_psplit_kernel<256|128> + conv_fwd_rsplit3_kernel + conv_fwd_rsplit_kernel (implicit-GEMM "
             "conv, f32 operands split exactly into 3 bf16 parts, 6 x v_mfma_f32_16x16x32_bf16 per 32-deep block, "
             "f32 accumulation: forward + dgrad launches; peak = dense bf16 / 6)",
     "fp32_h16": "conv_fwd_psplit_kernel<256|128, HM> + conv_fwd_rsplit3w_kernel<HM> + split_x_h_kernel (the pixel "
@@ -310,6 +317,7 @@ def run_leg(args, precision, dev, world, rank):
     timer = ConvTimer()
     K.set_conv_timer(timer)
     if world > 1:
+        opt.comm_events = []  # the all-reduce's exposed parts, per step (optim.AdamW)
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -323,9 +331,14 @@ def run_leg(args, precision, dev, world, rank):
     K.set_conv_timer(None)
     res = {"elapsed": elapsed, "last_loss": last, "mode": mode, "model": type(model).__name__}
     if world > 1:
-        res["allreduce"] = dict(dp, buckets=len(opt.reducer.buckets) if opt.reducer is not None else 1)
+        torch.cuda.synchronize()
+        exposed = sum(a.elapsed_time(b) for pair in opt.comm_events for a, b in pair) / args.steps
+        opt.comm_events = None
+        res["allreduce"] = dict(dp, buckets=len(opt.reducer.buckets) if opt.reducer is not None else 1,
+                                **dp_attribution(elapsed, exposed, args.steps, dev))
+        res["elapsed"] = res["allreduce"]["step_ms_max"] * args.steps * 1e-3  # max over ranks
     else:  # the setting a --gpus N run of this command uses; one rank all-reduces nothing
-        res["allreduce"] = dict(dp, buckets=None, note="world size 1: no all-reduce runs")
+        res["allreduce"] = dict(dp, buckets=None, exposed_ms=0.0, note="world size 1: no all-reduce runs")
     conv_ms, conv_flops, conv_n, conv_bytes = timer.summary(("fwd", "dgrad"))
     wg_ms, wg_flops, wg_n, _ = timer.summary(("wgrad",))
     enc_kinds = ("fwd", "dgrad", "wgrad", "stem", "stem_wgrad")
@@ -344,9 +357,6 @@ def run_leg(args, precision, dev, world, rank):
                enc_gemm_ms=enc_gemm_ms, enc_gemm_flops=enc_gemm_flops)
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        res["elapsed"] = t.item()
         # data-parallel sanity check outside the timed region: identical parameters on every rank
         chk = torch.stack([p.detach().double().sum() for p in model.parameters()]).sum().reshape(1)
         hi, lo = chk.clone(), chk.clone()
@@ -361,10 +371,56 @@ def run_leg(args, precision, dev, world, rank):
     return res
 
 
+def dp_attribution(elapsed_s: float, exposed_ms: float, steps: int, device) -> dict:
+    """Per-rank timing of a data-parallel run, gathered from every rank: step time
+    (the timed region / steps) and the gradient all-reduce's exposed time per step (optim.AdamW
+    comm_events: the compute stream's wait for the in-flight buckets + the blocking remainder).  The
+    line's time is the max over ranks; the spread and the exposed share attribute a shortfall."""
+    import torch.distributed as dist
+    t = torch.tensor([elapsed_s / steps * 1e3, exposed_ms], dtype=torch.float64, device=device)
+    rows = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(rows, t)
+    step = [round(float(r[0]), 3) for r in rows]
+    exp = [round(float(r[1]), 3) for r in rows]
+    return {"step_ms_min": min(step), "step_ms_max": max(step), "step_ms_per_rank": step,
+            "exposed_ms": max(exp), "exposed_ms_per_rank": exp,
+            "exposed_note": "ms per step the compute stream waited on the gradient all-reduce (bucket waits + "
+                            "the non-FeaturePlan remainder), HIP events; max over ranks"}
+
+
+def dry_run(args, world, rank):
+    """`--dry-run`: the multi-rank plumbing on CPU (gloo ranks from launch_ranks): a toy step
+    (a matmul) and one blocking all-reduce of a flat 'gradient' per step, timed like run_leg, then
+    dp_attribution and the JSON line.  tests/test_dist_cpu.py runs it at world 8."""
+    import torch.distributed as dist
+    from dgvcc_amd.dist import average_flat_
+    a = torch.randn(256, 256)
+    g = torch.randn(1 << 18)
+    exposed = 0.0
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for _ in range(1 + rank % 2):  # an uneven load: the spread must show it
+            a = torch.tanh(a @ a)
+        t1 = time.perf_counter()
+        average_flat_(g)
+        exposed += (time.perf_counter() - t1) * 1e3
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    att = dp_attribution(elapsed, exposed / args.steps, args.steps, torch.device("cpu"))
+    out = {"metric": METRIC, "value": round(world * args.steps / (att["step_ms_max"] * args.steps * 1e-3), 3),
+           "unit": "toy steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+           "config": {"parallelism": f"dp{world}", "backend": "gloo", "allreduce": att}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def roofline(args, precision, r):
     peak = PEAKS[precision]
-    kname = FWD_KERNEL_NAMES.get("fp32_h16" if precision == "fp32" and args.f32_math == "h16" else precision,
-                                 "implicit-GEMM conv forward + dgrad")
+    kkey = precision
+    if precision == "fp32":
+        kkey = {"h16": "fp32_h16", "split": "fp32_split", "exact": "fp32_exact"}[args.f32_math]
+    kname = FWD_KERNEL_NAMES.get(kkey, "implicit-GEMM conv forward + dgrad")
     if args.trunk:  # ResNet-50 trunk: strided/non-"same" convs on conv_gen_kernel, 3x3/1x1 stride 1 as above
         kname = ("conv_gen_kernel (strided / 7x7 stem im2col / parity-class dgrad) + " + kname.split(" (")[0] +
                  " (ResNet-50 trunk convs: forward + dgrad launches)")
@@ -516,37 +572,55 @@ def bl_timing(args, dev, reps=20):
 
 
 def cpu_baseline(args, seconds):
-    """The oracle's CPU restatement of the same train step (kind 'port'), batch 1, fp32, on
-    this host's cores, plus the full-frame fp32 parity of the HIP path on the warm-up frame."""
+    """The oracle's CPU restatement of the same train step (kind 'port'), batch 1, fp32, on this
+    host's cores, plus the full-frame fp32 parity of the HIP path on the warm-up frame.
+
+    The host's best stated configuration: torch CPU's conv / GEMM threading does
+    not scale across sockets on batch-1 frames, so one step is timed at each thread count of a sweep
+    (16, 32, 64, ..., the physical cores; DGVCC_CPU_THREADS pins one count), and `value` is the mean of
+    >= 2 further timed steps at the fastest count (mean of >= 2 timed steps)."""
     from oracle import dg_oracle as O
     from dgvcc_amd.models.models import DGModel_base, DGModel_final
     nproc = os.cpu_count() or 1
     phys = _physical_cores()
-    # the host's physical cores (VERDICT r4 item 7); DGVCC_CPU_THREADS overrides
-    threads = int(os.environ.get("DGVCC_CPU_THREADS", "0") or 0) or phys
+    pinned = int(os.environ.get("DGVCC_CPU_THREADS", "0") or 0)
+    sweep = [pinned] if pinned else sorted({t for t in (16, 32, 64, 128, 256) if t < phys} | {phys})
     prev = torch.get_num_threads()
-    torch.set_num_threads(threads)
     mode = args.mode if args.mode in ("simple", "final") else "simple"
     tmpl = (DGModel_final(pretrained=False) if mode == "final" else DGModel_base(pretrained=False)).state_dict()
     sd = O.seeded_state_dict(tmpl)
     batch = O.synthetic_batch(1, args.height, args.width, seed=7)
+    torch.set_num_threads(sweep[0])
     t0 = time.perf_counter()
     loss_ref, outs, _, _ = O.train_step(sd, batch, mode)  # warm-up, and the parity reference below
     t_warm = time.perf_counter() - t0
+    torch.set_num_threads(prev)
     parity = density_parity(sd, batch, loss_ref, outs, mode)
+    frames_per_step = 2 if mode == "final" else 1
+    probe = {}
+    for t in sweep:  # one step per thread count (the pool resized before it)
+        torch.set_num_threads(t)
+        t0 = time.perf_counter()
+        O.train_step(sd, batch, mode)
+        probe[t] = time.perf_counter() - t0
+    best = min(probe, key=probe.get)
+    torch.set_num_threads(best)
     n, t0 = 0, time.perf_counter()
     while True:
         O.train_step(sd, batch, mode)
         n += 1
-        if time.perf_counter() - t0 + t_warm / 2 >= seconds or n >= 8:
+        if n >= 2 and (time.perf_counter() - t0 >= seconds / 2 or n >= 8):
             break
     dt = time.perf_counter() - t0
     torch.set_num_threads(prev)
-    frames = n * (2 if mode == "final" else 1)
-    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+    return {"value": n * frames_per_step / dt, "unit": "frames/s", "cores": best, "kind": "port",
+            "threads_sweep": {str(t): round(frames_per_step / v, 4) for t, v in probe.items()},
+            "threads_sweep_unit": "frames/s of one step at each torch CPU thread count",
             "host_nproc": nproc, "host_physical_cores": phys, "cpu_model": _cpu_model(),
-            "sample": f"{n} oracle train steps ({mode} mode, batch 1 = {2 if mode == 'final' else 1} frame(s) "
-                      f"of {args.height}x{args.width}, fp32, torch CPU {threads} threads) after 1 warm-up step",
+            "warmup_step_s": round(t_warm, 2),
+            "sample": f"{n} timed oracle train steps ({mode} mode, batch 1 = {frames_per_step} frame(s) of "
+                      f"{args.height}x{args.width}, fp32, torch CPU {best} threads: the fastest of the sweep) after "
+                      f"1 warm-up step and one step per swept thread count",
             "parity": parity}
 
 
@@ -729,6 +803,13 @@ def main():
     # DGVCC_BENCH_BACKEND=gloo: rehearsal of the multi-rank path with several ranks sharing one
     # GPU (local rank modulo the visible devices); the driver's runs use RCCL ("nccl").
     backend = os.environ.get("DGVCC_BENCH_BACKEND", "nccl")
+    if args.dry_run:  # CPU ranks only: nothing below touches a GPU
+        if world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            dry_run(args, world, rank)
+            dist.destroy_process_group()
+        return
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
     dist_world = 1

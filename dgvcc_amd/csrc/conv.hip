@@ -1415,7 +1415,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   static_assert(!TALL || EPI_B + (HM ? 2 : 1) * BN * 4 <= STAGE, "TALL epilogue scratch must fit in a stage");
   char* epi_lds = smem + STG * STAGE;
   float* bbuf = (float*)(epi_lds + EPI_B);
-  float* hbuf = bbuf + PERS_BIAS_MAX;  // HM: 2^-(e_row + e_x) by absolute output channel
+  float* hbuf = bbuf + PERS_BIAS_MAX;  // HM: the rescale exponents -(e_row + e_x) (int bits) by absolute output channel
   constexpr int E3_MAX = (EPI_B + PERS_BIAS_MAX * 4) / 12;
   const bool e3_lds = EPI == 3 && a.Cout <= E3_MAX;
   float* ebias = (float*)epi_lds;
@@ -1439,7 +1439,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   // = a lane part (row (lane >> 2) of a 16-row block; the swizzle only sees row & 15) + a
   // wave-uniform part per piece (scalar offset of the DMA), so the pieces cost one VGPR
   const unsigned alane = (unsigned)((lane >> 2) * KT * KB + (((lane & 3) ^ psw_a(lane >> 2)) * 16));
-  // HM: the scales after the planes: [Cout] 1/(s_row s_x), then s_x
+  // HM: the scales after the planes: [Cout] the rescale exponents -(e_row + e_x) (int bits), then s_x
   const float* htail = (const float*)(wsp + (long long)a.Cout * KT * KB);
   const float hsx = HM ? htail[a.Cout] : 1.f;
   auto aoff_s = [&](int q) -> unsigned {
@@ -1594,7 +1594,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
     for (int c = tid; c < a.Cout; c += 512) bbuf[c] = a.bias[c];
   }
   if (HM && !TALL)
-    for (int c = tid; c < a.Cout; c += 512) hbuf[c] = htail[c];
+    for (int c = tid; c < a.Cout; c += 512) ((unsigned*)hbuf)[c] = ((const unsigned*)htail)[c];
   Ctx cur, nxt;
   setup(lin, cur);
   bool has_next = lin + G < ntile;
@@ -1870,16 +1870,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       lds_barrier();  // every wave is done reading the stage
       if (a.bias && tid < BN) bbuf[cur.co0 + tid] = a.bias[cur.co0 + tid];
       hbuf = bbuf + BN;  // absolute channel index, as bbuf
-      if (HM && tid < BN) hbuf[cur.co0 + tid] = htail[cur.co0 + tid];
+      if (HM && tid < BN) ((unsigned*)hbuf)[cur.co0 + tid] = ((const unsigned*)htail)[cur.co0 + tid];
       lds_barrier();
     }
     // HM: back from the scaled operands, exact powers of two per output channel, applied where the
     // epilogue first reads acc (a separate pass over all of acc ahead of the stores spilled 59 VGPRs)
     auto hscale = [&](int i, int j) __attribute__((always_inline)) {
-      if constexpr (HM) {
-        const f4v sc = *(const f4v*)(hbuf + cur.co0 + wco + 16 * i + 4 * fc);
+      if constexpr (HM) {  // the tail words hold the exponents (split_weight_h_kernel)
+        const u4v sc = *(const u4v*)(hbuf + cur.co0 + wco + 16 * i + 4 * fc);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc[r];
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], (int)sc[r]);
       }
     };
     float* y = (float*)a.y;
@@ -1974,11 +1974,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
 // Tile 64 channels x 256 pixels, 8 waves of 64 pixels x 32 channels, 32-channel K-steps,
 // double-buffered LDS (2 x 60 KB).  With only two channel fragments per wave, the per-wave
 // pixel split of conv_fwd_pers_kernel<64, .., SPL = 1> cost more VALU than its MFMAs.
-template <int EPI = 0>
+// HM = 1: the f16 x3 arithmetic (two f16 planes per operand: presplit_h's filter planes and scales, the
+// pixel rows scaled by the tensor's power of two), three f16 MFMAs per block.
+template <int EPI = 0, int HM = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, const char* __restrict__ wsp) {
   constexpr int BN = 64, BPX = 256;
+  constexpr int NPL = HM ? 2 : 3, KB = NPL * 64;  // planes; bytes per (co, k-block) of the filter planes
   constexpr int A_PL = BN * 64, B_PL = BPX * 64;  // plane bytes
-  constexpr int BUF = 3 * (A_PL + B_PL);
+  constexpr int BUF = NPL * (A_PL + B_PL);
   constexpr int TI = 2, TJ = 4;
   constexpr int BR = BPX * 8 / 512;               // 16-B f32 chunks of the pixel tile per thread
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF];
@@ -2009,22 +2012,26 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
     pp[i] = (m < M) ? rem / a.W : -100000;
     pq[i] = rem % a.W;
   }
-  // filter-plane chunks: q = tid (all threads) and q = tid + 512 (tid < 256); q -> (plane, row, chunk)
-  const char* wbase = wsp + (long long)co0 * KT * 192;
-  auto wq_off = [&](int q) { return (long long)((q & 255) >> 2) * KT * 192 + (q >> 8) * 64 + (q & 3) * 16; };
+  // filter-plane chunks: q = tid (all threads) and q = tid + 512 (tid < 256, three planes only);
+  // q -> (plane, row, chunk)
+  const char* wbase = wsp + (long long)co0 * KT * KB;
+  auto wq_off = [&](int q) { return (long long)((q & 255) >> 2) * KT * KB + (q >> 8) * 64 + (q & 3) * 16; };
   auto wq_lds = [&](int q) {
     const int row = (q & 255) >> 2;
     return (q >> 8) * A_PL + row * 64 + (((q & 3) ^ psw_a(row)) << 4);
   };
   const long long wo0 = wq_off(tid), wo1 = wq_off(tid + 512);
   const int wl0 = wq_lds(tid), wl1 = wq_lds(tid + 512);
+  // HM: the scales after the planes ([Cout] the rescale exponents -(e_row + e_x) as int bits, then s_x)
+  const float* htail = (const float*)(wsp + (long long)a.Cout * KT * KB);
+  const float hsx = HM ? htail[a.Cout] : 1.f;
 
   u4v ra0, ra1, rb[BR];
   auto gload = [&](int t) __attribute__((always_inline)) {
     const int rs = t / CB, cb = t - rs * CB;
     const int r = rs / a.S, s2 = rs - r * a.S;
-    ra0 = *(const u4v*)(wbase + wo0 + (long long)t * 192);
-    if (tid < 256) ra1 = *(const u4v*)(wbase + wo1 + (long long)t * 192);
+    ra0 = *(const u4v*)(wbase + wo0 + (long long)t * KB);
+    if (!HM && tid < 256) ra1 = *(const u4v*)(wbase + wo1 + (long long)t * KB);
     const int dh = r - a.pad, dw = s2 - a.pad;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
@@ -2037,18 +2044,25 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
   };
   auto swrite = [&](int buf) __attribute__((always_inline)) {
     char* As = smem + buf * BUF;
-    char* Bs = As + 3 * A_PL;
+    char* Bs = As + NPL * A_PL;
     *(u4v*)(As + wl0) = ra0;
-    if (tid < 256) *(u4v*)(As + wl1) = ra1;
+    if (!HM && tid < 256) *(u4v*)(As + wl1) = ra1;
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
       const int row = rbase + 64 * i;
       const int o = row * 64 + ((((chunk >> 1) ^ psw_a(row))) << 4) + (chunk & 1) * 8;
-      u2v h0, h1, h2;
-      split3_4(rb[i], h0, h1, h2);
-      *(u2v*)(Bs + o) = h0;
-      *(u2v*)(Bs + B_PL + o) = h1;
-      *(u2v*)(Bs + 2 * B_PL + o) = h2;
+      if constexpr (HM) {
+        u2v h0, h1;
+        split2h_4(rb[i], hsx, h0, h1);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + B_PL + o) = h1;
+      } else {
+        u2v h0, h1, h2;
+        split3_4(rb[i], h0, h1, h2);
+        *(u2v*)(Bs + o) = h0;
+        *(u2v*)(Bs + B_PL + o) = h1;
+        *(u2v*)(Bs + 2 * B_PL + o) = h2;
+      }
     }
   };
 
@@ -2067,33 +2081,57 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
     const int cur = t & 1;
     if (t + 1 < KT) gload(t + 1);
     const char* As = smem + cur * BUF;
-    const char* Bs = As + 3 * A_PL;
-    s8v bh[TJ][3], ah[TI][3];
+    const char* Bs = As + NPL * A_PL;
+    s8v bh[TJ][NPL], ah[TI][NPL];
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int row = wpx + 16 * j + fr;
       const int o = row * 64 + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
+      for (int pl = 0; pl < NPL; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
     }
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
       const int row = wco + 16 * i + fr;
       const int o = row * 64 + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) ah[i][pl] = *(const s8v*)(As + pl * A_PL + o);
+      for (int pl = 0; pl < NPL; ++pl) ah[i][pl] = *(const s8v*)(As + pl * A_PL + o);
     }
-    constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+    if constexpr (HM) {
+      constexpr int PA3[3] = {1, 0, 0}, PB3[3] = {0, 1, 0};
 #pragma unroll
-    for (int u = 0; u < 6; ++u) {
+      for (int u = 0; u < 3; ++u) {
 #pragma unroll
-      for (int i = 0; i < TI; ++i)
+        for (int i = 0; i < TI; ++i)
 #pragma unroll
-        for (int j = 0; j < TJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
-      if (u == 2 && t + 1 < KT) swrite(cur ^ 1);  // overlapped with the remaining products
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah[i][PA3[u]]),
+                                                               __builtin_bit_cast(h8v, bh[j][PB3[u]]), acc[i][j], 0, 0, 0);
+        if (u == 1 && t + 1 < KT) swrite(cur ^ 1);  // overlapped with the remaining products
+      }
+    } else {
+      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int u = 0; u < 6; ++u) {
+#pragma unroll
+        for (int i = 0; i < TI; ++i)
+#pragma unroll
+          for (int j = 0; j < TJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+        if (u == 2 && t + 1 < KT) swrite(cur ^ 1);  // overlapped with the remaining products
+      }
     }
     __syncthreads();
+  }
+  if constexpr (HM) {  // back from the scaled operands (exact powers of two per output channel)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const u4v sc = *(const u4v*)(htail + co0 + wco + 16 * i + 4 * fc);  // exponents (split_weight_h_kernel)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], (int)sc[r]);
+    }
   }
 
   float* y = (float*)a.y;
@@ -2160,14 +2198,16 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit_kernel(FwdArgs a, cons
 // per wave straight from L2 measured no faster than the per-tap kernel (8 waves x 18 KB per
 // K-step per CU of L2 traffic).  Same tile (256 px x 64 co, 8 waves of 64 px x 32 co) and
 // epilogues as conv_fwd_rsplit_kernel; K order (r, c-block, s) instead of (r, s, c-block).
-template <int EPI = 0>
+// HM = 1: the f16 x3 arithmetic (two f16 planes per operand, presplit_h's filter planes and scales).
+template <int EPI = 0, int HM = 0>
 __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, const char* __restrict__ wsp) {
+  constexpr int NPL = HM ? 2 : 3, KB = NPL * 64;       // planes; bytes per (co, k-block) of the filter planes
   constexpr int BN = 64, BPX = 256, SR = 264;        // strip rows (258 used)
-  constexpr int B_PL = SR * 64, BUF = 3 * B_PL;      // strip plane / buffer bytes
-  constexpr int A_PL = BN * 64, A_TAP = 3 * A_PL;    // filter plane / tap bytes
+  constexpr int B_PL = SR * 64, BUF = NPL * B_PL;    // strip plane / buffer bytes
+  constexpr int A_PL = BN * 64, A_TAP = NPL * A_PL;  // filter plane / tap bytes
   constexpr int TI = 2, TJ = 4;
   constexpr int NCH = (BPX + 2) * 8, BR = (NCH + 511) / 512;  // 16-B f32 chunks of the strip
-  constexpr int NA = 3 * 3 * BN * 4, AR = (NA + 511) / 512;  // 16-B chunks of the 3 taps' planes
+  constexpr int NA = 3 * NPL * BN * 4, AR = (NA + 511) / 512;  // 16-B chunks of the 3 taps' planes
   __shared__ __attribute__((aligned(16))) char smem[2 * BUF + 3 * A_TAP];
   char* Asm = smem + 2 * BUF;
 
@@ -2190,16 +2230,19 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
                                                                 win_bytes, 0x00020000);
   const int wpx = (wid & 3) * 64, wco = (wid >> 2) * 32;
   const int fr = lane & 15, fc = lane >> 4;
-  // filter chunk q of a K-step: (tap s, plane, row co, 16-B chunk) = (q / 768, (q / 256) % 3, (q & 255) >> 2, q & 3)
-  const char* wbase = wsp + (long long)co0 * (9 * CB) * 192;
+  // filter chunk q of a K-step: (tap s, plane, row co, 16-B chunk) = (q / (NPL 256), (q / 256) % NPL, (q & 255) >> 2, q & 3)
+  const char* wbase = wsp + (long long)co0 * (9 * CB) * KB;
   int a_src[AR], a_dst[AR];
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int q = tid + 512 * i;
-    const int ts = q / 768, pl = (q / 256) % 3, row = (q & 255) >> 2, ch = q & 3;
-    a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * 192 + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*192
+    const int ts = q / (NPL * 256), pl = (q / 256) % NPL, row = (q & 255) >> 2, ch = q & 3;
+    a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * KB + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*KB
     a_dst[i] = ts * A_TAP + pl * A_PL + row * 64 + ((ch ^ psw_a(row)) << 4);
   }
+  // HM: the scales after the planes ([Cout] the rescale exponents -(e_row + e_x) as int bits, then s_x)
+  const float* htail = (const float*)(wsp + (long long)a.Cout * 9 * CB * KB);
+  const float hsx = HM ? htail[a.Cout] : 1.f;
 
   u4v rb[BR], ra[AR];
   auto gload = [&](int t) __attribute__((always_inline)) {
@@ -2213,7 +2256,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
       const long long pin = (long long)tn * HW + (long long)h * a.W + ww - plo;
       rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + cb * 32 + chunk * 4) * 4) : 0xFFFFFFF0u);
     }
-    const long long koff = (long long)(r * 3 * CB + cb) * 192;
+    const long long koff = (long long)(r * 3 * CB + cb) * KB;
 #pragma unroll
     for (int i = 0; i < AR; ++i)
       if (a_src[i] >= 0) ra[i] = *(const u4v*)(wbase + a_src[i] + koff);
@@ -2225,11 +2268,18 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
       const int row = rbase + 64 * i;
       if (row < BPX + 2) {
         const int o = row * 64 + ((((chunk >> 1) ^ psw_a(row))) << 4) + (chunk & 1) * 8;
-        u2v h0, h1, h2;
-        split3_4(rb[i], h0, h1, h2);
-        *(u2v*)(Bs + o) = h0;
-        *(u2v*)(Bs + B_PL + o) = h1;
-        *(u2v*)(Bs + 2 * B_PL + o) = h2;
+        if constexpr (HM) {
+          u2v h0, h1;
+          split2h_4(rb[i], hsx, h0, h1);
+          *(u2v*)(Bs + o) = h0;
+          *(u2v*)(Bs + B_PL + o) = h1;
+        } else {
+          u2v h0, h1, h2;
+          split3_4(rb[i], h0, h1, h2);
+          *(u2v*)(Bs + o) = h0;
+          *(u2v*)(Bs + B_PL + o) = h1;
+          *(u2v*)(Bs + 2 * B_PL + o) = h2;
+        }
       }
     }
   };
@@ -2253,33 +2303,55 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3_kernel(FwdArgs a, con
     const char* Bs = smem + cur * BUF;
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      s8v ah[TI][3], bh[TJ][3];
+      s8v ah[TI][NPL], bh[TJ][NPL];
 #pragma unroll
       for (int i = 0; i < TI; ++i) {
         const int row = wco + 16 * i + fr;
         const int o = s * A_TAP + row * 64 + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) ah[i][pl] = *(const s8v*)(Asm + pl * A_PL + o);
+        for (int pl = 0; pl < NPL; ++pl) ah[i][pl] = *(const s8v*)(Asm + pl * A_PL + o);
       }
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int row = wpx + 16 * j + fr + s;
         const int o = row * 64 + ((fc ^ psw_a(row)) << 4);
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
+        for (int pl = 0; pl < NPL; ++pl) bh[j][pl] = *(const s8v*)(Bs + pl * B_PL + o);
       }
-      constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+      if constexpr (HM) {
+        constexpr int PA3[3] = {1, 0, 0}, PB3[3] = {0, 1, 0};
 #pragma unroll
-      for (int u = 0; u < 6; ++u)
+        for (int u = 0; u < 3; ++u)
 #pragma unroll
-        for (int i = 0; i < TI; ++i)
+          for (int i = 0; i < TI; ++i)
 #pragma unroll
-          for (int j = 0; j < TJ; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8v, ah[i][PA3[u]]),
+                                                                 __builtin_bit_cast(h8v, bh[j][PB3[u]]), acc[i][j], 0, 0, 0);
+      } else {
+        constexpr int PA6[6] = {2, 1, 0, 1, 0, 0}, PB6[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int u = 0; u < 6; ++u)
+#pragma unroll
+          for (int i = 0; i < TI; ++i)
+#pragma unroll
+            for (int j = 0; j < TJ; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i][PA6[u]], bh[j][PB6[u]], acc[i][j], 0, 0, 0);
+      }
       if (s == 1 && t + 1 < KT3) swrite(cur ^ 1);  // the other buffer was last read before this step's barriers
     }
   }
   __syncthreads();  // smem reuse by the statistics epilogue
+  if constexpr (HM) {  // back from the scaled operands (exact powers of two per output channel)
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+      const u4v sc = *(const u4v*)(htail + co0 + wco + 16 * i + 4 * fc);  // exponents (split_weight_h_kernel)
+#pragma unroll
+      for (int j = 0; j < TJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], (int)sc[r]);
+    }
+  }
 
   float* y = (float*)a.y;
   bool valid[TJ];
@@ -2381,7 +2453,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
     a_src[i] = q < NA ? (row * (9 * CB) + ts * CB) * KB + pl * 64 + ch * 16 : -1;  // + (r*3*CB + cb)*KB
     a_dst[i] = ts * A_TAP + pl * A_PL + row * 64 + ((ch ^ psw_a(row)) << 4);
   }
-  // HM: the scales after the planes ([Cout] 2^-(e_row + e_x), then s_x)
+  // HM: the scales after the planes ([Cout] the rescale exponents -(e_row + e_x) as int bits, then s_x)
   const float* htail = (const float*)(wsp + (long long)a.Cout * 9 * CB * KB);
   const float hsx = HM ? htail[a.Cout] : 1.f;
 
@@ -2491,11 +2563,11 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_rsplit3w_kernel(FwdArgs a, co
   if constexpr (HM) {  // back from the scaled operands (exact powers of two per output channel)
 #pragma unroll
     for (int i = 0; i < TI; ++i) {
-      const f4v sc = *(const f4v*)(htail + co0 + wco + 16 * i + 4 * fc);
+      const u4v sc = *(const u4v*)(htail + co0 + wco + 16 * i + 4 * fc);  // exponents (split_weight_h_kernel)
 #pragma unroll
       for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] *= sc[r];
+        for (int r = 0; r < 4; ++r) acc[i][j][r] = ldexpf(acc[i][j][r], (int)sc[r]);
     }
   }
   if (a.accumulate || EPI == 3) {  // old y, bias and the eval-BN affine ahead of the stores (EPI_ACC_NOTE)
@@ -2566,7 +2638,9 @@ __global__ void split_weight_kernel(const float* __restrict__ w, long long n, un
 // f32 filter w[co][K]: the row's largest magnitude sets its power-of-two scale s_row, the parts of
 // w * s_row go to wsp[co][kb][2][32] (f16 hi, lo), and after the Cout * K * 4 bytes of planes the
 // tail [Cout] = 2^-(e_row + e_x) (the epilogue's exact rescale) and [Cout] = s_x = 2^e_x, from the
-// pixel operand's largest magnitude *xamax (amax_kernel).
+// pixel operand's largest magnitude *xamax (amax_kernel).  The rescale is stored as the integer exponent
+// -(e_row + e_x) in the float word's bits and applied with ldexp (exact whenever the result is an f32:
+// a factor 2^-(e_row + e_x) itself leaves f32's range once both operands are tiny).
 __global__ __launch_bounds__(256) void split_weight_h_kernel(const float* __restrict__ w, int K,
                                                            unsigned short* __restrict__ wsp,
                                                            const unsigned* __restrict__ xamax, int Cout) {
@@ -2590,7 +2664,7 @@ __global__ __launch_bounds__(256) void split_weight_h_kernel(const float* __rest
   }
   if (tid == 0) {
     float* tail = (float*)(wsp + (long long)Cout * K * 2);
-    tail[co] = ldexpf(1.f, -(er + ex));
+    tail[co] = __int_as_float(-(er + ex));
     if (co == 0) tail[Cout] = ldexpf(1.f, ex);
   }
 }
@@ -2635,6 +2709,27 @@ __global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, 
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
   if (threadIdx.x == 0) amax_fold(out, fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])));
+}
+
+// Operand maxima with channels (dg_amax, and the f16 x3 weight gradients' per-channel scales where no
+// producer supplied them): out[0] = max |x|, out[1 + c] = max over channel c (zeroed before).  A block
+// takes G = min(C/4, 256) 16-byte channel chunks (blockIdx.y picks the group) x 256/G pixel rows, so
+// each thread keeps its 4 channels in registers over a grid-stride pixel loop.
+__global__ __launch_bounds__(256) void camax_kernel(const float* __restrict__ x, long long ldx, long long M, int C,
+                                                    float* __restrict__ out) {
+  const int cq = C >> 2;
+  const int G = min(cq, 256), rows = 256 / G;
+  const int tid = threadIdx.x, ch = blockIdx.y * G + tid % G, r = tid / G;
+  const bool on = r < rows && ch < cq;
+  float m[4] = {0.f, 0.f, 0.f, 0.f};
+  if (on) {
+    for (long long p = (long long)blockIdx.x * rows + r; p < M; p += (long long)gridDim.x * rows) {
+      const f4v v = *(const f4v*)(x + p * ldx + ch * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], fabsf(v[e]));
+    }
+  }
+  block_camax_commit<4>(m, on ? ch * 4 : 0, C, out);
 }
 
 // Split-K finish: y = sum of the ksplit f32 partials (+ bias, + y if accumulate), stored
@@ -3477,6 +3572,17 @@ static int launch_amax(const float* x, long long ldx, long long M, int C, unsign
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
+// out [1 + C]: the tensor's max and each channel's (camax_kernel), ~1024 blocks
+static int launch_camax(const float* x, long long ldx, long long M, int C, unsigned* out, hipStream_t st) {
+  if (C % 4 != 0 || C > DG_CAMAX_C) return DG_ERR_UNSUPPORTED;
+  if (hipMemsetAsync(out, 0, (1 + (size_t)C) * 4, st) != hipSuccess) return DG_ERR_HIP;
+  if (M <= 0) return DG_OK;
+  const int cq = C / 4, G = std::min(cq, 256), rows = 256 / G, gy = dg_cdiv(cq, G);
+  const int gx = (int)std::max(1LL, std::min<long long>(dg_cdiv(M, rows), std::max(1, 1024 / gy)));
+  hipLaunchKernelGGL(camax_kernel, dim3(gx, gy), dim3(256), 0, st, x, ldx, M, C, (float*)out);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
 // f16 x3 planes + scales (split_weight_h_kernel) in the same workspace (Cout * K * 4 bytes of
 // planes + 2 * Cout + 2 floats of scales, then the pixel operand's amax word): the x amax pass,
 // then the filter split
@@ -3691,21 +3797,26 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
       return DG_OK;
     }
     if (rsplit_ok(a) && has_split_room(a)) {  // split math, Cout = 64: both operands split once per block
-      const bool h16 = f32_h16() && rsplit3w_ok(a);  // f16 x3 on the 512-pixel 3-tap form
+      const bool h16 = f32_h16();  // f16 x3 on every Cout = 64 form (512-pixel 3-tap, 256-pixel 3-tap, per tap)
       const unsigned short* wsp = h16 ? presplit_h(a, st) : presplit(a, st);
       if (!wsp) return DG_ERR_HIP;
       const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));
+      const char* ws = (const char*)wsp;
       if (rsplit3w_ok(a)) {
         const dim3 gw((unsigned)((long long)(M / 512) * (a.Cout / 64)));
-        if (h16 && a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3, 1>), gw, dim3(512), 0, st, a, (const char*)wsp);
-        else if (h16) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0, 1>), gw, dim3(512), 0, st, a, (const char*)wsp);
-        else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3>), gw, dim3(512), 0, st, a, (const char*)wsp);
-        else hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0>), gw, dim3(512), 0, st, a, (const char*)wsp);
+        if (h16 && a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3, 1>), gw, dim3(512), 0, st, a, ws);
+        else if (h16) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0, 1>), gw, dim3(512), 0, st, a, ws);
+        else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<3>), gw, dim3(512), 0, st, a, ws);
+        else hipLaunchKernelGGL((conv_fwd_rsplit3w_kernel<0>), gw, dim3(512), 0, st, a, ws);
       } else if (rsplit3_ok(a)) {
-        if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
-        else hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<0>), g, dim3(512), 0, st, a, (const char*)wsp);
-      } else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3>), g, dim3(512), 0, st, a, (const char*)wsp);
-      else hipLaunchKernelGGL((conv_fwd_rsplit_kernel<0>), g, dim3(512), 0, st, a, (const char*)wsp);
+        if (h16 && a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<3, 1>), g, dim3(512), 0, st, a, ws);
+        else if (h16) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<0, 1>), g, dim3(512), 0, st, a, ws);
+        else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<3>), g, dim3(512), 0, st, a, ws);
+        else hipLaunchKernelGGL((conv_fwd_rsplit3_kernel<0>), g, dim3(512), 0, st, a, ws);
+      } else if (h16 && a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3, 1>), g, dim3(512), 0, st, a, ws);
+      else if (h16) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<0, 1>), g, dim3(512), 0, st, a, ws);
+      else if (a.escale) hipLaunchKernelGGL((conv_fwd_rsplit_kernel<3>), g, dim3(512), 0, st, a, ws);
+      else hipLaunchKernelGGL((conv_fwd_rsplit_kernel<0>), g, dim3(512), 0, st, a, ws);
       DG_CHECK_LAUNCH();
       return DG_OK;
     }
@@ -4103,12 +4214,15 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
   const int kbeg = split * a.pps;
   const int kend = min(M, kbeg + a.pps);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int hedy = 0, hex = 0;
+  // HM: per-channel power-of-two scales of this thread's 4 dY and 4 X channels (its 16-byte chunks keep
+  // their channels over every K-step: NTH is a multiple of both chunk counts per row)
+  static_assert(NTH % CPRA == 0 && NTH % CPRB == 0, "a thread's chunks must keep their channels");
+  f4v hsdy = f4v{1.f, 1.f, 1.f, 1.f}, hsx = f4v{1.f, 1.f, 1.f, 1.f};
   if constexpr (HM) {
-    hedy = h16_exp(__uint_as_float(*a.dyam));
-    hex = h16_exp(__uint_as_float(*a.xam));
+    int e4[4];
+    chan_h16_scales(a.dyam, co0 + (tid % CPRA) * 4, e4, hsdy);
+    chan_h16_scales(a.xam, c0 + (tid % CPRB) * 4, e4, hsx);
   }
-  const float hsdy = ldexpf(1.f, hedy), hsx = ldexpf(1.f, hex);
 
   const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 4);
   __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
@@ -4165,7 +4279,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       if constexpr (HM) {
         u2v h0, h1;
-        split2h_4(ra[i], hsdy, h0, h1);
+        split2h_4v(ra[i], hsdy, h0, h1);
         *(u2v*)(As + o) = h0;
         *(u2v*)(As + PA + o) = h1;
       } else {
@@ -4182,7 +4296,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
       const int o = (idx / CPRB) * ROWB + (idx % CPRB) * 8;
       if constexpr (HM) {
         u2v h0, h1;
-        split2h_4(rb[i], hsx, h0, h1);
+        split2h_4v(rb[i], hsx, h0, h1);
         *(u2v*)(Bs + o) = h0;
         *(u2v*)(Bs + PB + o) = h1;
       } else {
@@ -4264,16 +4378,21 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split_kernel(WgArgs
 
   const long long ldk = (long long)RS * a.C;
   float* out = a.slab + (long long)split * a.Cout * ldk;
-  const float hinv = ldexpf(1.f, -(hedy + hex));  // 1 unless HM
+  // HM: back by 2^-(e_dy[co] + e_x[c]), applied to the value (exact unless the result itself leaves
+  // f32's range, as an f32 product would)
+  int ecol[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) ecol[j] = HM ? h16_exp(__uint_as_float(a.xam[1 + c0 + wc + 16 * j + (lane & 15)])) : 0;
 #pragma unroll
   for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      const int c = c0 + wc + 16 * j + (lane & 15);
+    for (int rr = 0; rr < 4; ++rr) {
+      const int co = co0 + wco + 16 * i + 4 * g + rr;
+      const int erow = HM ? h16_exp(__uint_as_float(a.dyam[1 + co])) : 0;
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int co = co0 + wco + 16 * i + 4 * g + rr;
-        out[co * ldk + rs * a.C + c] = HM ? acc[i][j][rr] * hinv : acc[i][j][rr];
+      for (int j = 0; j < TJ; ++j) {
+        const int c = c0 + wc + 16 * j + (lane & 15);
+        out[co * ldk + rs * a.C + c] = HM ? ldexpf(acc[i][j][rr], -(erow + ecol[j])) : acc[i][j][rr];
       }
     }
 }
@@ -4324,12 +4443,15 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
   const int kbeg = split * a.pps;
   const int kend = min(M, kbeg + a.pps);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  int hedy = 0, hex = 0;
+  // HM: per-channel power-of-two scales of this thread's 4 dY and 4 X channels (its 16-byte chunks keep
+  // their channels over every K-step: NTH is a multiple of both chunk counts per row)
+  static_assert(NTH % CPRA == 0 && NTH % CPRB == 0, "a thread's chunks must keep their channels");
+  f4v hsdy = f4v{1.f, 1.f, 1.f, 1.f}, hsx = f4v{1.f, 1.f, 1.f, 1.f};
   if constexpr (HM) {
-    hedy = h16_exp(__uint_as_float(*a.dyam));
-    hex = h16_exp(__uint_as_float(*a.xam));
+    int e4[4];
+    chan_h16_scales(a.dyam, co0 + (tid % CPRA) * 4, e4, hsdy);
+    chan_h16_scales(a.xam, c0 + (tid % CPRB) * 4, e4, hsx);
   }
-  const float hsdy = ldexpf(1.f, hedy), hsx = ldexpf(1.f, hex);
 
   const unsigned dy_bytes = (unsigned)(((long long)(kend - kbeg - 1) * a.lddy + a.Cout) * 4);
   __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
@@ -4377,7 +4499,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
       const int o = (idx / CPRA) * ROWA + (idx % CPRA) * 8;
       if constexpr (HM) {
         u2v h0, h1;
-        split2h_4(ra[i], hsdy, h0, h1);
+        split2h_4v(ra[i], hsdy, h0, h1);
         *(u2v*)(As + o) = h0;
         *(u2v*)(As + PA + o) = h1;
       } else {
@@ -4396,7 +4518,7 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
         const int o = strip * NPL * PB + (sidx / CPRB) * ROWB + (sidx % CPRB) * 8;
         if constexpr (HM) {
           u2v h0, h1;
-          split2h_4(rb[i], hsx, h0, h1);
+          split2h_4v(rb[i], hsx, h0, h1);
           *(u2v*)(Bs + o) = h0;
           *(u2v*)(Bs + PB + o) = h1;
         } else {
@@ -4493,20 +4615,24 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
 
   const long long ldk = 9ll * a.C;
   float* out = a.slab + (long long)split * a.Cout * ldk;
-  const float hinv = ldexpf(1.f, -(hedy + hex));  // 1 unless HM
+  // HM: back by 2^-(e_dy[co] + e_x[c]) on the value (as conv_wgrad_split_kernel)
+  int ecol[TJ];
 #pragma unroll
-  for (int s = 0; s < 3 * NR; ++s)
+  for (int j = 0; j < TJ; ++j) ecol[j] = HM ? h16_exp(__uint_as_float(a.xam[1 + c0 + wc + 16 * j + (lane & 15)])) : 0;
 #pragma unroll
-    for (int i = 0; i < TI; ++i)
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {
-        const int c = c0 + wc + 16 * j + (lane & 15);
+    for (int rr = 0; rr < 4; ++rr) {
+      const int co = co0 + wco + 16 * i + 4 * g + rr;
+      const int erow = HM ? h16_exp(__uint_as_float(a.dyam[1 + co])) : 0;
 #pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          const int co = co0 + wco + 16 * i + 4 * g + rr;
-          out[co * ldk + (r * 3 + s) * a.C + c] = HM ? acc[s][i][j][rr] * hinv : acc[s][i][j][rr];
+      for (int s = 0; s < 3 * NR; ++s)
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int c = c0 + wc + 16 * j + (lane & 15);
+          out[co * ldk + (r * 3 + s) * a.C + c] = HM ? ldexpf(acc[s][i][j][rr], -(erow + ecol[j])) : acc[s][i][j][rr];
         }
-      }
+    }
 }
 
 // Split plan of conv_wgrad_split_kernel: one block per CU (256 slots), 32-pixel K-steps.
@@ -5272,12 +5398,14 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st, unsigned* 
         const bool h16 = f32_h16() && hslots;
         if (h16) {  // f16 x3: the operands' largest magnitudes (computed here unless the caller has them)
           if (!a.xam) {
-            if (launch_amax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, hslots, st) != DG_OK) return DG_ERR_HIP;
+            const int r = launch_camax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, hslots, st);
+            if (r != DG_OK) return r;
             a.xam = hslots;
           }
           if (!a.dyam) {
-            if (launch_amax((const float*)a.dy, a.lddy, M3, a.Cout, hslots + 1, st) != DG_OK) return DG_ERR_HIP;
-            a.dyam = hslots + 1;
+            const int r = launch_camax((const float*)a.dy, a.lddy, M3, a.Cout, hslots + 1 + a.C, st);
+            if (r != DG_OK) return r;
+            a.dyam = hslots + 1 + a.C;
           }
         }
         if (h16) {
@@ -5316,13 +5444,14 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st, unsigned* 
       const bool h16 = f32_h16() && hslots;
       if (h16) {  // f16 x3: the operands' largest magnitudes (computed here unless the caller has them)
         if (!a.xam) {
-          if (launch_amax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, hslots, st) != DG_OK) return DG_ERR_HIP;
+          const int r = launch_camax((const float*)a.x, a.ldx, (long long)a.N * a.H * a.W, a.C, hslots, st);
+          if (r != DG_OK) return r;
           a.xam = hslots;
         }
         if (!a.dyam) {
-          if (launch_amax((const float*)a.dy, a.lddy, (long long)a.N * a.P * a.Q, a.Cout, hslots + 1, st) != DG_OK)
-            return DG_ERR_HIP;
-          a.dyam = hslots + 1;
+          const int r = launch_camax((const float*)a.dy, a.lddy, (long long)a.N * a.P * a.Q, a.Cout, hslots + 1 + a.C, st);
+          if (r != DG_OK) return r;
+          a.dyam = hslots + 1 + a.C;
         }
         if (bco == 64) hipLaunchKernelGGL((conv_wgrad_split_kernel<64, 64, 2, 256, 1>), gs, dim3(256), 0, st, a);
         else if (bcw == 256) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2, 512, 1>), gs, dim3(512), 0, st, a);
@@ -5547,8 +5676,8 @@ extern "C" int dg_get_f32_math(void) { return f32_math(); }
 
 extern "C" int dg_amax(int dtype, const void* x, int64_t ldx, int64_t M, int C, float* out, void* stream) {
   DG_REQUIRE(x && out && M >= 0 && C > 0 && ldx >= C);
-  DG_SUPPORTED(dtype == DG_F32 && C % 4 == 0 && ldx % 4 == 0);
-  return launch_amax((const float*)x, ldx, M, C, (unsigned*)out, (hipStream_t)stream);
+  DG_SUPPORTED(dtype == DG_F32 && C % 4 == 0 && ldx % 4 == 0 && C <= DG_CAMAX_C);
+  return launch_camax((const float*)x, ldx, M, C, (unsigned*)out, (hipStream_t)stream);
 }
 
 extern "C" int dg_debug_stamps(void* buf, int64_t bytes) {
@@ -5631,8 +5760,10 @@ extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, 
   if (dtype == DG_F32) {  // pre-split filter planes (+ the pre-split pixel operand of the f16 x3 pre-split forward)
     const long long planes = ((long long)Cout * R * S * C * 6 + 255) / 256 * 256;
     FwdArgs a{nullptr, C, N, H, W, C, nullptr, Cout, R, S, (R - 1) / 2, nullptr, nullptr, Cout, 0, nullptr};
-    // room whatever DGVCC_PSPLIT_XS says (the launch reads the switch; callers cache this size)
-    if (2 * a.pad == R - 1 && 2 * a.pad == S - 1 && psplit_ok(a))
+    // room only where the launch takes the pre-split operand (psplit_xs with the shape's tile: several
+    // output-channel tiles share a pixel tile of a 3x3 conv; DGVCC_PSPLIT_XS is read here too): a
+    // launch given less room splits in-kernel (bit-identical), so a cached size stays safe
+    if (2 * a.pad == R - 1 && 2 * a.pad == S - 1 && psplit_ok(a) && psplit_xs(a, f32_pers_bn(Cout)))
       return xsplit_off(planes) + xsplit_bytes(a);
     return planes;
   }
@@ -5834,6 +5965,8 @@ extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int
                      stream);
 }
 
+static int64_t wg_amax_bytes(int C, int Cout) { return (int64_t)(2 + C + Cout) * 4 / 256 * 256 + 256; }
+
 extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;
   WgPlan p = DG_IS16(dtype) ? wg_plan<bf16>(N, H, W, C, Cout, R, S, -1, -1, true)
@@ -5851,8 +5984,9 @@ extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C
     if (wgs9_on(b3) && q9.splits > q.splits) q = q9;
   }
   const int kh = (DG_IS16(dtype) && Cout % 128 != 0) ? 2 : 1;  // 9-tap Cout-64 kernel: a slab split per k-half
-  // f32: + 256 bytes at the end for the f16 x3 operand maxima the library computes (dg_conv_wgrad)
-  return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4 + (DG_IS16(dtype) ? 0 : 256);
+  // f32: + the f16 x3 operand maxima the library computes when the caller has none (dg_conv_wgrad):
+  // [1 + C] for x, [1 + Cout] for dy, at the end
+  return (int64_t)std::max(p.splits, q.splits) * kh * Cout * C * R * S * 4 + (DG_IS16(dtype) ? 0 : wg_amax_bytes(C, Cout));
 }
 
 extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* dy,
@@ -5877,7 +6011,7 @@ extern "C" int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H
   a.xam = (const unsigned*)xamax;
   a.dyam = (const unsigned*)dyamax;
   hipStream_t st = (hipStream_t)stream;
-  unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - 256) : nullptr;
+  unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - wg_amax_bytes(C, Cout)) : nullptr;
   return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st, hslots);
 }
 
@@ -6010,7 +6144,7 @@ extern "C" int dg_conv2d_wgrad(int dtype, const void* x, int64_t ldx, int N, int
   a.xam = (const unsigned*)xamax;
   a.dyam = (const unsigned*)dyamax;
   hipStream_t st = (hipStream_t)stream;
-  unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - 256) : nullptr;
+  unsigned* hslots = dtype == DG_F32 ? (unsigned*)((char*)workspace + need - wg_amax_bytes(C, Cout)) : nullptr;
   return dtype == DG_BF16 ? launch_wgrad<bf16>(a, dw, accumulate, st) : dtype == DG_F16 ? launch_wgrad<f16>(a, dw, accumulate, st) : launch_wgrad<float>(a, dw, accumulate, st, hslots);
 }
 

@@ -141,6 +141,15 @@ __device__ __forceinline__ float wave_max(float v) {
 
 static inline int dg_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Zero a producer's operand-maxima buffer before its launch (may be NULL): [1 + C] floats for an f32
+// output (the tensor's word, then one per channel: OutMax), one word for a 16-bit one.
+// DG_ERR_INVALID when an f32 output has more channels than the per-channel fold handles.
+static inline int dg_zero_amax(float* amax, int dtype, int C, hipStream_t st) {
+  if (!amax) return DG_OK;
+  if (dtype == DG_F32 && C > 2048) return DG_ERR_INVALID;  // DG_CAMAX_C
+  return hipMemsetAsync(amax, 0, (dtype == DG_F32 ? 1 + (size_t)C : 1) * 4, st) == hipSuccess ? DG_OK : DG_ERR_HIP;
+}
+
 // ---------------------------------------------------------------------------
 // f32 arithmetic on the bf16 matrix cores ("3-way split", DG_F32 with
 // dg_set_f32_math(1)).  Each f32 x is cut EXACTLY into three bf16 parts, x = h0 + h1 + h2
@@ -311,6 +320,28 @@ __device__ __forceinline__ void split2h_4(const u4v& x, float s, u2v& hi, u2v& l
     lo[k] = ql;
   }
 }
+// the same with one scale per element (per-channel scales: x holds 4 consecutive channels); the
+// packed multiply takes both factors from registers, so the instruction count is split2h_4's
+__device__ __forceinline__ void split2h_4v(const u4v& x, const f4v& s, u2v& hi, u2v& lo) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const dg_f32x2 v = dg_f32x2{__uint_as_float(x[2 * k]), __uint_as_float(x[2 * k + 1])} *
+                       dg_f32x2{s[2 * k], s[2 * k + 1]};
+    const dg_f16x2 h = __builtin_convertvector(v, dg_f16x2);
+    const dg_f32x2 r = v - __builtin_convertvector(h, dg_f32x2);
+    hi[k] = __builtin_bit_cast(unsigned, h);
+    lo[k] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, dg_f16x2));
+  }
+}
+// per-channel f16 x3 scales of 4 consecutive channels c .. c + 3 from an operand-maxima buffer (word 0
+// the tensor's max, word 1 + c channel c's): the exponents, and the factors 2^e
+__device__ __forceinline__ void chan_h16_scales(const unsigned* am, int c, int e[4], f4v& s) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    e[k] = h16_exp(__uint_as_float(am[1 + c + k]));
+    s[k] = ldexpf(1.f, e[k]);
+  }
+}
 
 // Fold a block's max r >= 0 into *out (f32 bits, an unsigned max; zeroed before the launch), skipping
 // the atomic when *out already holds >= r: the word only grows, so a stale read costs at most an
@@ -335,3 +366,49 @@ __device__ __forceinline__ void block_amax_commit(float m, float* out) {
     amax_fold((unsigned*)out, r);
   }
 }
+
+// Operand maxima of an f32 output with channels (the f16 x3 convs' scales): out is
+// [1 + C] floats, out[0] = max |v| over the tensor and out[1 + c] = max |v| over channel c (c local to
+// the slice the kernel wrote; zeroed before the launch).  m[e] is the calling thread's max over the
+// channel c0 + e it stored (channel-stationary passes: every thread keeps its V channels); inactive
+// threads pass zeros.  Channels are reduced in LDS first (one fold per channel per block), C <= DG_CAMAX_C.
+// Every thread of the block calls it.
+constexpr int DG_CAMAX_C = 2048;
+template <int V>
+__device__ __forceinline__ void block_camax_commit(const float (&m)[V], int c0, int C, float* out) {
+  __shared__ unsigned cm[DG_CAMAX_C];
+  for (int c = threadIdx.x; c < C; c += blockDim.x) cm[c] = 0u;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    if (m[e] > 0.f) atomicMax(&cm[c0 + e], __float_as_uint(m[e]));  // non-negative: bit order = value order
+    t = fmaxf(t, m[e]);
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const unsigned v = cm[c];
+    if (v) amax_fold((unsigned*)out + 1 + c, __uint_as_float(v));
+  }
+  block_amax_commit(t, out);
+}
+// A producer's running operand maxima (out_amax_commit's input): per channel for f32 outputs (the only
+// ones an f16 x3 conv reads), one register for 16-bit ones, whose buffer holds the tensor's word alone
+template <typename T, int V>
+struct OutMax {
+  static constexpr int K = sizeof(T) == 4 ? V : 1;
+  float m[K];
+  __device__ __forceinline__ OutMax() {
+#pragma unroll
+    for (int e = 0; e < K; ++e) m[e] = 0.f;
+  }
+  __device__ __forceinline__ void add(int e, float v) {
+    float& r = m[K == 1 ? 0 : e];
+    r = fmaxf(r, fabsf(v));
+  }
+  // every thread of the block calls it
+  __device__ __forceinline__ void commit(int c0, int C, float* out) const {
+    if constexpr (K == 1) block_amax_commit(m[0], out);
+    else block_camax_commit<V>(m, c0, C, out);
+  }
+};

@@ -155,7 +155,7 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
   float sc[V], sf[V];
   ld_chan_row<V>(scale, c0, 1.f, sc);
   ld_chan_row<V>(shift, c0, 0.f, sf);
-  float m = 0.f;  // max |y| (amax: the f16 x3 convs' operand scale)
+  OutMax<T, V> m;  // max |y| per channel (amax: the f16 x3 convs' operand scales)
   for (long long p = gt / tpp; p < M; p += pstride) {
     float v[V];
     ldv(z + p * ldz + c0, v);
@@ -172,9 +172,9 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
     }
     stv(y + p * ldy + c0, v);
 #pragma unroll
-    for (int e = 0; e < V; ++e) m = fmaxf(m, fabsf(v[e]));
+    for (int e = 0; e < V; ++e) m.add(e, v[e]);
   }
-  if (amax) block_amax_commit(m, amax);
+  if (amax) m.commit(c0, C, amax);
 }
 
 // Per-thread channel-chunk parameters (registers).
@@ -407,8 +407,8 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
                                                    const float* scale, const float* shift, int act, const float* drop,
                                                    int HW, const float* __restrict__ coef, T* __restrict__ dz,
                                                    long long lddz, float* __restrict__ amax) {
-  float m = 0.f;  // max |dz| (amax)
   constexpr int V = 16 / (int)sizeof(T);
+  OutMax<T, V> m;  // max |dz| per channel (amax)
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
         stv(dz + p * lddz + c0, g0);
         stv(dz + q * lddz + c0, g1);
 #pragma unroll
-        for (int e = 0; e < V; ++e) m = fmaxf(m, fmaxf(fabsf(g0[e]), fabsf(g1[e])));
+        for (int e = 0; e < V; ++e) { m.add(e, g0[e]); m.add(e, g1[e]); }
       }
     }
     for (; p < M; p += pstride) {
@@ -472,7 +472,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
       f(gv, zv);
       stv(dz + p * lddz + c0, gv);
 #pragma unroll
-      for (int e = 0; e < V; ++e) m = fmaxf(m, fabsf(gv[e]));
+      for (int e = 0; e < V; ++e) m.add(e, gv[e]);
     }
   };
   if constexpr (U == 1) {  // the round-3 loop (runtime dropout / ReLU flags)
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
       f(gv, zv);
       stv(dz + p * lddz + c0, gv);
 #pragma unroll
-      for (int e = 0; e < V; ++e) m = fmaxf(m, fabsf(gv[e]));
+      for (int e = 0; e < V; ++e) m.add(e, gv[e]);
     }
   } else if (drop) {
     if (act == 1) run(std::true_type{}, std::true_type{});
@@ -491,7 +491,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
     if (act == 1) run(std::false_type{}, std::true_type{});
     else run(std::false_type{}, std::false_type{});
   }
-  if (amax) block_amax_commit(m, amax);
+  if (amax) m.commit(c0, C, amax);
 }
 
 // ---------------------------------------------------------------------------
@@ -536,8 +536,8 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
                                                            const float* __restrict__ drop, int HW, T* __restrict__ y,
                                                            long long ldy, T* __restrict__ yp, long long ldyp,
                                                            float* __restrict__ amax) {
-  float m = 0.f;  // max |y| over the window values (>= max |yp|: amax of both)
   constexpr int V = 16 / (int)sizeof(T);
+  OutMax<T, V> m;  // max |y| per channel over the window values (>= max |yp|: amax of both)
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
         if (act == 1) t = t > 0.f ? t : 0.f;
         if (d) t *= d[e];
         v[k][e] = rnd_t<T>(t);
-        m = fmaxf(m, fabsf(v[k][e]));
+        m.add(e, v[k][e]);
       }
       if (y) stv(y + pos[k] * ldy + c0, v[k]);
     }
@@ -569,7 +569,7 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
     for (int e = 0; e < V; ++e) o[e] = v[first_max4(v[0][e], v[1][e], v[2][e], v[3][e])][e];
     stv(yp + pp * ldyp + c0, o);
   }
-  if (amax) block_amax_commit(m, amax);
+  if (amax) m.commit(c0, C, amax);
 }
 
 // The pooled backward keeps 4 pixels x V channels of z and g live per thread: V = 4
@@ -690,7 +690,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
                                                         const float* drop, int HW, const float* __restrict__ coef,
                                                         T* __restrict__ dz, long long lddz, float* __restrict__ amax) {
   constexpr int V = POOL_V;
-  float m = 0.f;  // max |dz|
+  OutMax<T, V> m;  // max |dz| per channel
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
@@ -712,12 +712,12 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
       for (int e = 0; e < V; ++e) {
         const float xh = (zv[k][e] - cp.mu[e]) * cp.is[e];
         gv[k][e] = k1[e] * gv[k][e] - k2[e] * xh - k3[e];
-        m = fmaxf(m, fabsf(gv[k][e]));
+        m.add(e, gv[k][e]);
       }
       stn<V>(dz + pos[k] * lddz + c0, gv[k]);
     }
   }
-  if (amax) block_amax_commit(m, amax);
+  if (amax) m.commit(c0, C, amax);
 }
 
 inline int ew_grid(long long n) {
@@ -753,9 +753,9 @@ int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, 
   return DG_OK;
 }
 
-// amax (may be NULL): max |dz| of the apply pass (dg_common.h block_amax_commit)
-static int zero_amax(float* amax, hipStream_t st) {
-  return amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess ? DG_ERR_HIP : DG_OK;
+// amax (may be NULL): max |out| of the apply pass, per channel for f32 (dg_common.h OutMax)
+static int zero_amax(float* amax, bool f32, int C, hipStream_t st) {
+  return dg_zero_amax(amax, f32 ? DG_F32 : DG_BF16, C, st);
 }
 template <typename T>
 int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int M, int C, const float* gamma,
@@ -773,7 +773,7 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
                      dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
   if (!dz) return DG_OK;  // coefficients only (a fused consumer applies them)
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, sizeof(T) == 4, C, st); if (zr != DG_OK) return zr; }
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
   hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<T, 2> : bn_bwd_apply<T, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
                      mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
@@ -816,7 +816,7 @@ extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, 
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, ldy));
   hipStream_t st = (hipStream_t)stream;
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, dtype == DG_F32, C, st); if (zr != DG_OK) return zr; }
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
@@ -864,7 +864,7 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
   hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, save_invstd,
                      dgamma, dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, dtype == DG_F32, C, st); if (zr != DG_OK) return zr; }
   if (dtype == DG_BF16) {
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
@@ -922,7 +922,7 @@ extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, in
   DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && BN_SHAPE_OK(dtype, C, ldz) &&
                BN_SHAPE_OK(dtype, C, ldyp) && (!y || BN_SHAPE_OK(dtype, C, ldy)));
   hipStream_t st = (hipStream_t)stream;
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, dtype == DG_F32, C, st); if (zr != DG_OK) return zr; }
   const long long Mp = (long long)N * (H / 2) * (W / 2);
   const long long total = Mp * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
@@ -956,7 +956,7 @@ static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long
                      dgamma, dbeta, dbias, coef);
   DG_CHECK_LAUNCH();
   const long long total = Mp * (C / POOL_V);
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, sizeof(T) == 4, C, st); if (zr != DG_OK) return zr; }
   hipLaunchKernelGGL(bn_pool_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd,
                      ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop, H * W, coef, (T*)dz,
                      lddz, amax);
@@ -1101,7 +1101,7 @@ extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(BN_SHAPE_OK(dtype, C, ldg) && BN_SHAPE_OK(dtype, C, ldz) && BN_SHAPE_OK(dtype, C, lddz));
   hipStream_t st = (hipStream_t)stream;
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, dtype == DG_F32, C, st); if (zr != DG_OK) return zr; }
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
@@ -1131,7 +1131,7 @@ extern "C" int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp
   hipStream_t st = (hipStream_t)stream;
   const long long Mp = (long long)N * (H / 2) * (W / 2);
   const long long total = Mp * (C / POOL_V);
-  if (zero_amax(amax, st) != DG_OK) return DG_ERR_HIP;
+  { const int zr = zero_amax(amax, dtype == DG_F32, C, st); if (zr != DG_OK) return zr; }
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(bn_pool_bwd_apply<bf16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const bf16*)gp, ldgp,
                        (const bf16*)gd, ldgd, (const bf16*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift,

@@ -34,7 +34,7 @@ inline int ew_unroll() {
 }
 
 // y = act(z1*s1 + b1 + (s2 ? z2*s2 + b2 : z2)); amax (may be NULL): max |y| (the next f16 x3 convs'
-// operand scale, dg_common.h block_amax_commit; zeroed by the launcher)
+// operand scales: per channel for f32, dg_common.h OutMax; zeroed by the launcher)
 template <typename T, int U = 1>
 __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, long long ld1, int M, int C,
                                                     const float* __restrict__ s1, const float* __restrict__ b1,
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
   const int c0 = (int)(gt % tpp) * V;
   const long long pstride = (long long)gridDim.x * NT / tpp;
   float a1[V], c1[V], a2[V], c2[V];
-  float mx = 0.f;
+  OutMax<T, V> mx;
 #pragma unroll
   for (int e = 0; e < V; e += 4) {  // 16-byte parameter loads (c0 % 4 == 0, rows 16-byte aligned)
     ld4(s1 + c0 + e, a1 + e);
@@ -69,12 +69,12 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
       for (int e = 0; e < V; ++e) {
         float t = fmaf(u[e], a1[e], c1[e]) + (s2 ? fmaf(v[e], a2[e], c2[e]) : v[e]);
         if (act == 1) t = t > 0.f ? t : 0.f;
-        mx = fmaxf(mx, fabsf(t));
+        mx.add(e, t);
         u[e] = t;
       }
       stv(y + p * ldy + c0, u);
     }
-    if (amax) block_amax_commit(mx, amax);
+    if (amax) mx.commit(c0, C, amax);
     return;
   }
   // two pixels per trip, all four loads ahead of the first use; the second BN and the ReLU as
@@ -86,7 +86,7 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
       for (int e = 0; e < V; ++e) {
         float t = fmaf(u[e], a1[e], c1[e]) + (BN2 ? fmaf(v[e], a2[e], c2[e]) : v[e]);
         if (ACT) t = t > 0.f ? t : 0.f;
-        mx = fmaxf(mx, fabsf(t));
+        mx.add(e, t);
         u[e] = t;
       }
     };
@@ -118,7 +118,7 @@ __global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, lo
     if (act == 1) run(std::false_type{}, std::true_type{});
     else run(std::false_type{}, std::false_type{});
   }
-  if (amax) block_amax_commit(mx, amax);
+  if (amax) mx.commit(c0, C, amax);
 }
 
 // out = g * (y > 0)
@@ -177,7 +177,7 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
     }
   }
   int cur = -1;
-  float mx = 0.f;
+  OutMax<T, V> mx;
   for (int p = gt / tpp; p < M; p += pstride) {
     const int n = p / HW;
     if (n != cur) {
@@ -192,12 +192,12 @@ __global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, l
       float t = (v[e] - m[e]) * s[e];
       if (gamma) t = fmaf(t, ga[e], be[e]);
       if (act == 1) t = t > 0.f ? t : 0.f;
-      mx = fmaxf(mx, fabsf(t));
+      mx.add(e, t);
       v[e] = t;
     }
     stv(y + p * ldy + c0, v);
   }
-  if (amax) block_amax_commit(mx, amax);
+  if (amax) mx.commit(c0, C, amax);
 }
 
 // ---------------------------------------------------------------- IN bwd ----
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
   const int pstride = gridDim.x * NT / tpp;
   const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
   float m[V], s[V], k1[V], k2[V], k3[V];
-  float mx = 0.f;  // max |dx| (amax, may be NULL: the following f16 x3 wgrad's operand scale)
+  OutMax<T, V> mx;  // max |dx| per channel (amax, may be NULL: the following f16 x3 wgrad's operand scales)
   int cur = -1;
   for (int p = gt / tpp; p < M; p += pstride) {
     const int n = p / HW;
@@ -323,11 +323,11 @@ __global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long
       const float xh = (xv[e] - m[e]) * s[e];
       const float d = k1[e] * gv[e] - k2[e] * xh - k3[e];
       o[e] = accumulate ? o[e] + d : d;
-      mx = fmaxf(mx, fabsf(o[e]));
+      mx.add(e, o[e]);
     }
     stv(dx + p * lddx + c0, o);
   }
-  if (amax) block_amax_commit(mx, amax);
+  if (amax) mx.commit(c0, C, amax);
 }
 
 }  // namespace
@@ -343,7 +343,7 @@ extern "C" int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, in
   DG_SUPPORTED(VOK(dtype, C, ld1) && VOK(dtype, C, ld2) && VOK(dtype, C, ldy) && NT % (C / V) == 0);
   hipStream_t st = (hipStream_t)stream;
   const long long total = (long long)M * (C / V);
-  if (amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
+  { const int zr = dg_zero_amax(amax, dtype, C, st); if (zr != DG_OK) return zr; }
   if (dtype == DG_BF16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_add_kernel<bf16, 2> : bn_add_kernel<bf16, 1>), dim3(cs_grid_add(total)), dim3(NT), 0, st, (const bf16*)z1, ld1, M, C, scale1,
                        shift1, (const bf16*)z2, ld2, scale2, shift2, act, (bf16*)y, ldy, amax);
@@ -388,7 +388,7 @@ extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, i
   DG_SUPPORTED(VOK(dtype, C, ldx) && VOK(dtype, C, ldy) && total < (1LL << 30));
   hipStream_t st = (hipStream_t)stream;
   const int grid = cs_grid(total, C / V);
-  if (amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
+  { const int zr = dg_zero_amax(amax, dtype, C, st); if (zr != DG_OK) return zr; }
   if (dtype == DG_BF16)
     hipLaunchKernelGGL(in_apply_kernel<bf16>, dim3(grid), dim3(NT), 0, st, (const bf16*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (bf16*)y, ldy, amax);
@@ -426,7 +426,7 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
   float* coef = part + (long long)N * nb * 2 * C;
   const int grid = cs_grid(total, C / V);
   const dim3 fgrid(dg_cdiv(C, FIN_CH)), fblk(FIN_CH * FIN_KS);
-  if (amax && hipMemsetAsync(amax, 0, 4, st) != hipSuccess) return DG_ERR_HIP;
+  { const int zr = dg_zero_amax(amax, dtype, C, st); if (zr != DG_OK) return zr; }
   if (dtype == DG_BF16) {
     hipLaunchKernelGGL(in_bwd_partial<bf16>, dim3(nb, N), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)x, ldx,
                        HW, C, ppb, mean, invstd, part);

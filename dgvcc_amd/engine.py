@@ -109,7 +109,7 @@ class ConvLayer:
 
     def _flip(self, wp):
         """flip_weight(wp) for the dgrad, once per packed filter (both views of a step)."""
-        return frozen(self, ("flip", wp.dtype, wp.data_ptr()), (self.conv.weight,),
+        return frozen(self, ("flip", wp.dtype), (self.conv.weight, wp),
                       lambda: K.flip_weight(wp, self.Cout, self.Cin, self.R))
 
     def stem_ok(self, dt) -> bool:
@@ -483,7 +483,10 @@ def _cat_act(buf: torch.Tensor, up_src: Act, skip: Act) -> Act:
     scale) bounds both parts: bilinear upsampling does not exceed its source's max |.|."""
     a = Act(buf)
     if up_src.amax is not None and skip.amax is not None:
-        a.amax = torch.maximum(up_src.amax, skip.amax)
+        if up_src.amax.numel() == 1 + up_src.C and skip.amax.numel() == 1 + skip.C:  # per channel
+            a.amax = torch.cat([torch.maximum(up_src.amax[:1], skip.amax[:1]), up_src.amax[1:], skip.amax[1:]])
+        else:
+            a.amax = torch.maximum(up_src.amax[:1], skip.amax[:1])
     return a
 
 

@@ -18,9 +18,11 @@ F32, BF16, F16 = 0, 1, 2
 
 @dataclass
 class Act:
-    """Channel slice [off, off+C) of an NHWC buffer `buf` [N,H,W,Ctot].  amax: None, or a device
-    f32 [1] >= max |slice| set by the kernel that wrote it (the f32 convs' operand scale, f16 x3
-    arithmetic; None makes the conv take one read pass over the slice for it)."""
+    """Channel slice [off, off+C) of an NHWC buffer `buf` [N,H,W,Ctot].  amax: None, or the operand
+    maxima the kernel that wrote it produced (the f32 convs' f16 x3 scales): a device f32 [1 + C],
+    [0] >= max |slice| and [1 + c] >= max |channel c| (a [1] tensor carries the tensor's word alone:
+    the forward / dgrad read only that; the weight gradients, which scale per channel, then take a
+    read pass of their own).  None makes the convs take one read pass over the slice."""
     buf: torch.Tensor
     off: int = 0
     C: int | None = None
@@ -86,6 +88,24 @@ def set_scope(scope: str):
     _SCOPE[0] = scope
 
 
+_CHECK_AMAX = __import__("os").environ.get("DGVCC_CHECK_AMAX", "0") == "1"
+
+
+def check_amax(a: Act, what: str = ""):
+    """DGVCC_CHECK_AMAX=1 (debug): the operand maxima attached to an f32 Act must bound the values
+    (each word >= a fresh dg_amax of the slice); a smaller word would overflow the f16 x3 parts."""
+    if a.amax is None or a.buf.dtype != torch.float32:
+        return
+    ref = amax(a)
+    have = a.amax.float()
+    n = min(have.numel(), ref.numel())
+    bad = (have[:n] < ref[:n]).nonzero()
+    if bad.numel():
+        i = int(bad[0, 0])
+        raise DGError(f"operand maxima below the values{' (' + what + ')' if what else ''}: word {i} holds "
+                      f"{have[i].item()!r} < {ref[i].item()!r}")
+
+
 def _timed(kind, flops, fn, nbytes=0.0):
     if _CONV_TIMER is None:
         fn()
@@ -110,6 +130,8 @@ def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
     es = x.buf.element_size()
     nbytes = es * (x.M * x.C + wp.numel() + x.M * Cout * (2 if accumulate else 1))  # x, w, y (+y read)
     ws, work = _fwd_workspace(x, Cout, R)
+    if _CHECK_AMAX:
+        check_amax(x, kind)
     y.amax = None  # y is (re)written by a conv: no tracked maximum
     _timed(kind, flops, lambda: call("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
                                      Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate), None,
@@ -133,8 +155,9 @@ _FWD_WS: dict = {}
 def _fwd_workspace(x: Act, Cout: int, R: int):
     """Split-K partials for small-grid 16-bit forward/dgrad shapes (deep layers at small batch);
     f32: the pre-split filter planes of the split-math kernels (caller-owned, from torch's
-    caching allocator, stream-ordered like every other buffer)."""
-    key = (x.dt, x.N, x.H, x.W, x.C, Cout, R)
+    caching allocator, stream-ordered like every other buffer).  The size depends on
+    DGVCC_PSPLIT_XS (pixel pre-split room), so the switch is part of the cache key."""
+    key = (x.dt, x.N, x.H, x.W, x.C, Cout, R, __import__("os").environ.get("DGVCC_PSPLIT_XS"))
     ws = _FWD_WS.get(key)
     if ws is None:
         ws = _FWD_WS[key] = query("dg_conv_fwd_workspace", x.dt, x.N, x.H, x.W, x.C, Cout, R, R)
@@ -170,8 +193,9 @@ def import_act(t: torch.Tensor) -> Act:
 
 
 def amax(x: Act) -> torch.Tensor:
-    """max |x| over the slice (f32), a device f32 [1] (dg_amax)."""
-    out = torch.empty(1, dtype=torch.float32, device=x.buf.device)
+    """Operand maxima of the slice (f32): a device f32 [1 + C], [0] = max |x|, [1 + c] = max over
+    channel c (dg_amax)."""
+    out = torch.empty(1 + x.C, dtype=torch.float32, device=x.buf.device)
     call("dg_amax", x.dt, x.ptr, x.ld, x.M, x.C, ptr(out), stream())
     return out
 
@@ -265,14 +289,23 @@ def bn_bwd_from_part(pre, g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamm
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), ptr(am), stream())
 
 
+def chan_amax(a: Act):
+    """a.amax when it carries per-channel words ([1 + C]: what the weight gradients' per-channel f16 x3
+    scales need), else None (the library then takes its own per-channel read pass)."""
+    return a.amax if a.amax is not None and a.amax.numel() == 1 + a.C else None
+
+
 def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=False, k_alg=None):
     ws = query("dg_conv_wgrad_workspace", x.dt, x.N, x.H, x.W, x.C, dy.C, R, R)
+    if _CHECK_AMAX:
+        check_amax(x, "wgrad x")
+        check_amax(dy, "wgrad dy")
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=x.buf.device)
     flops = 2.0 * x.M * (k_alg if k_alg else x.C * R * R) * dy.C
     nbytes = x.buf.element_size() * (x.M * x.C + dy.M * dy.C) + 4 * dw.numel()
     _timed("wgrad", flops, lambda: call("dg_conv_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
                                         dy.ptr, dy.ld, dy.C, R, R, pad, ptr(dw), ptr(work), ws,
-                                        int(accumulate), ptr(x.amax), ptr(dy.amax), stream()), nbytes)
+                                        int(accumulate), ptr(chan_amax(x)), ptr(chan_amax(dy)), stream()), nbytes)
 
 
 def im2col_c3(img: torch.Tensor, dtype: torch.dtype) -> torch.Tensor:
@@ -458,11 +491,12 @@ def bn_eval_stats(gamma, beta, running_mean, running_var, eps):
 
 
 def _amax_out(a: Act | None, *more: Act | None) -> torch.Tensor | None:
-    """A fresh device f32 [1] that an f32 producer fills with max |output|, attached to the Acts
-    it writes (the following f16 x3 convs' operand scale); None for 16-bit outputs."""
+    """A fresh device f32 [1 + C] that an f32 producer fills with its output's operand maxima (the
+    tensor's, then each channel's), attached to the Acts it writes (same channels: the following f16
+    x3 convs' scales); None for 16-bit outputs."""
     if a is None or a.buf.dtype != torch.float32:
         return None
-    t = torch.empty(1, dtype=torch.float32, device=a.buf.device)
+    t = torch.empty(1 + a.C, dtype=torch.float32, device=a.buf.device)
     for o in (a, *more):
         if o is not None:
             o.amax = t
@@ -515,6 +549,7 @@ def _expect(y: Act, N, H, W, C, what):
 def maxpool_fwd(x: Act, y: Act):
     _expect(y, x.N, x.H // 2, x.W // 2, x.C, "maxpool_fwd")
     call("dg_maxpool2_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, y.ptr, y.ld, stream())
+    y.amax = x.amax  # a window maximum never exceeds its channel's max |x|
 
 
 def maxpool_bwd(x: Act, gy: Act, gx: Act, accumulate=False):
@@ -522,6 +557,7 @@ def maxpool_bwd(x: Act, gy: Act, gx: Act, accumulate=False):
     _expect(gx, x.N, x.H, x.W, x.C, "maxpool_bwd")
     call("dg_maxpool2_bwd", x.dt, x.ptr, x.ld, gy.ptr, gy.ld, x.N, x.H, x.W, x.C, gx.ptr, gx.ld,
          int(accumulate), stream())
+    gx.amax = None  # rewritten without a tracked maximum
 
 
 UP_BILINEAR, UP_BILINEAR_AC, UP_NEAREST = 0, 1, 2
@@ -530,6 +566,7 @@ UP_BILINEAR, UP_BILINEAR_AC, UP_NEAREST = 0, 1, 2
 def upsample_fwd(x: Act, scale: int, mode: int, y: Act):
     _expect(y, x.N, x.H * scale, x.W * scale, x.C, "upsample_fwd")
     call("dg_upsample_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, scale, mode, y.ptr, y.ld, stream())
+    y.amax = x.amax  # bilinear / nearest values are convex combinations of the source channel's
 
 
 def upsample_bwd(gy: Act, scale: int, mode: int, gx: Act, gy2: Act | None = None, accumulate=False):
@@ -537,6 +574,7 @@ def upsample_bwd(gy: Act, scale: int, mode: int, gx: Act, gy2: Act | None = None
     call("dg_upsample_bwd", gx.dt, gy.ptr, gy.ld, gy2.ptr if gy2 is not None else None,
          gy2.ld if gy2 is not None else 0, gx.N, gx.H, gx.W, gx.C, scale, mode, gx.ptr, gx.ld,
          int(accumulate), stream())
+    gx.amax = None
 
 
 # ---------------------------------------------------------------- head -----
@@ -555,6 +593,8 @@ def head_bwd(x: Act, w, act, y, gy, gx: Act | None, gw, gbias=None, accumulate_g
     call("dg_head_bwd", x.dt, x.ptr, x.ld, x.M, x.C, ptr(w), act, ptr(y), ptr(gy),
          gx.ptr if gx is not None else None, gx.ld if gx is not None else 0, int(accumulate_gx),
          ptr(gw), ptr(gbias), ptr(work), stream())
+    if gx is not None:
+        gx.amax = None
 
 
 # ---------------------------------------------------------------- loss/opt -
@@ -613,6 +653,7 @@ def conv2d_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, stride: int, pad: in
     flops = 2.0 * M * (k_alg if k_alg else x.C * R * R) * Cout
     es = x.buf.element_size()
     nbytes = es * (x.M * x.C + wp.numel() + M * Cout * (2 if accumulate else 1))
+    y.amax = None
     _timed(kind, flops, lambda: call("dg_conv2d_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
                                      Cout, R, R, stride, pad, ptr(bias), y.ptr, y.ld,
                                      int(accumulate), stream()), nbytes)
@@ -625,6 +666,7 @@ def conv2d_dgrad(dy: Act, wt: torch.Tensor, R: int, stride: int, pad: int, dx: A
     flops = 2.0 * dy.M * dx.C * R * R * dy.C
     es = dy.buf.element_size()
     nbytes = es * (dy.M * dy.C + wt.numel() + dx.M * dx.C * (2 if accumulate else 1))
+    dx.amax = None
     _timed("dgrad", flops, lambda: call("dg_conv2d_dgrad", dy.dt, dy.ptr, dy.ld, dy.N, dy.H, dy.W,
                                         dy.C, ptr(wt), dx.C, dx.H, dx.W, R, R, stride, pad, dx.ptr,
                                         dx.ld, int(accumulate), stream()), nbytes)
@@ -638,7 +680,7 @@ def conv2d_wgrad(x: Act, dy: Act, R: int, stride: int, pad: int, dw: torch.Tenso
     nbytes = x.buf.element_size() * (x.M * x.C + dy.M * dy.C) + 4 * dw.numel()
     _timed("wgrad", flops, lambda: call("dg_conv2d_wgrad", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C,
                                         dy.ptr, dy.ld, dy.C, R, R, stride, pad, ptr(dw), ptr(work),
-                                        ws, int(accumulate), ptr(x.amax), ptr(dy.amax), stream()), nbytes)
+                                        ws, int(accumulate), ptr(chan_amax(x)), ptr(chan_amax(dy)), stream()), nbytes)
 
 
 def im2col_c3_general(img: torch.Tensor, dtype: torch.dtype, R: int, stride: int, pad: int,
@@ -659,11 +701,13 @@ def unpack_c3(dwcol: torch.Tensor, dw: torch.Tensor, accumulate=False):
 def maxpool_k_fwd(x: Act, k: int, stride: int, pad: int, y: Act):
     call("dg_maxpool_fwd", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, k, stride, pad, y.ptr, y.ld,
          stream())
+    y.amax = x.amax  # a window maximum never exceeds its channel's max |x|
 
 
 def maxpool_k_bwd(x: Act, gy: Act, k: int, stride: int, pad: int, gx: Act, accumulate=False):
     call("dg_maxpool_bwd", x.dt, x.ptr, x.ld, gy.ptr, gy.ld, x.N, x.H, x.W, x.C, k, stride, pad,
          gx.ptr, gx.ld, int(accumulate), stream())
+    gx.amax = None
 
 
 def maxpool_k_fwd_idx(x: Act, k: int, stride: int, pad: int, y: Act) -> torch.Tensor:
@@ -678,6 +722,7 @@ def maxpool_k_fwd_idx(x: Act, k: int, stride: int, pad: int, y: Act) -> torch.Te
 def maxpool_k_bwd_idx(idx: torch.Tensor, gy: Act, k: int, stride: int, pad: int, gx: Act, accumulate=False):
     call("dg_maxpool_bwd_idx", gx.dt, ptr(idx), gy.ptr, gy.ld, gx.N, gx.H, gx.W, gx.C, k, stride, pad,
          gx.ptr, gx.ld, int(accumulate), stream())
+    gx.amax = None
 
 
 def bn_add_apply(z1: Act, st1, z2: Act, st2, act: int, y: Act):
@@ -690,6 +735,7 @@ def bn_add_apply(z1: Act, st1, z2: Act, st2, act: int, y: Act):
 
 def relu_bwd(g: Act, y: Act, out: Act):
     call("dg_relu_bwd", g.dt, g.ptr, g.ld, y.ptr, y.ld, y.M, y.C, out.ptr, out.ld, stream())
+    out.amax = g.amax  # |g * mask| <= |g| channel by channel
 
 
 def instnorm_stats(x: Act, eps: float = 1e-5) -> torch.Tensor:

@@ -33,9 +33,17 @@ class AdamW(torch.optim.Optimizer):
         # buffer after the backward): the FeaturePlan parameters' all-reduce runs in ~bucket_mb
         # buckets under the backward (dgvcc_amd.dist.OverlapReducer), from the second step on.  A
         # no-op on one rank.
+        # One optimizer step per backward: with the overlap on, a second FeaturePlan backward before
+        # step() (gradient accumulation over micro-batches) raises (dist.OverlapReducer: its buckets
+        # are already in flight); accumulate with overlap=False / DGVCC_DP_OVERLAP=0.
         if overlap is None:
             overlap = os.environ.get("DGVCC_DP_OVERLAP", "1") == "1"
         self.reducer = OverlapReducer(bucket_mb) if (overlap and allreduce) else None
+        # bench.py: a list receives per step and group two (start, end) HIP event pairs on the compute
+        # stream around the gradient all-reduce's exposed parts -- the wait for the in-flight buckets,
+        # and the blocking all-reduce of the remainder (the gather launch between them excluded);
+        # None (default) records nothing
+        self.comm_events = None
         # fp16 mode: the loss was multiplied by grad_scale before backward (LossScaler); the
         # step unscales the flat gradient and skips the update when it holds inf/NaN
         self.grad_scale = None
@@ -137,6 +145,10 @@ class AdamW(torch.optim.Optimizer):
             if all(p.grad is None for p in group["params"]):
                 continue
             self._ensure_flat(group)
+            ev = None
+            if self.comm_events is not None and world() > 1 and group["_g"].is_cuda:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                ev[0].record()
             if self.reducer is not None and self.reducer.flat is not None and self.reducer.flat is not group["_g"]:
                 # the flat buffer was re-created (re-homed parameters): drain the reducer and
                 # re-attach it to the new buffer after this step (its sinks keep pointing at it)
@@ -145,7 +157,11 @@ class AdamW(torch.optim.Optimizer):
                                    and self.reducer.flat is group["_g"]) else None
             if red is not None and not red.finish():  # the FeaturePlan buckets, reduced under the backward
                 red = None
+            if ev is not None:
+                ev[1].record()
             runs = self._gather(group)
+            if ev is not None:
+                ev[2].record()
             g = group["_g"]
             if red is not None:
                 offs, ps = group["_offs"], group["params"]
@@ -161,6 +177,9 @@ class AdamW(torch.optim.Optimizer):
                     i = j
             elif self.allreduce:
                 average_flat_(g)
+            if ev is not None:
+                ev[3].record()
+                self.comm_events.append(((ev[0], ev[1]), (ev[2], ev[3])))
             if self.grad_scale is not None and self.grad_scale != 1.0:
                 flag = group.setdefault("_inf", torch.zeros(1, dtype=torch.int32, device=g.device))
                 call("dg_grad_unscale", ptr(g), g.numel(), 1.0 / float(self.grad_scale), ptr(flag), stream())

@@ -50,7 +50,7 @@ class TConv:
         return frozen(self, ("w", dt), (self.conv.weight,), lambda: K.pack_weight(self.conv.weight.detach(), dt))
 
     def _flip(self, wp):
-        return frozen(self, ("flip", wp.dtype, wp.data_ptr()), (self.conv.weight,),
+        return frozen(self, ("flip", wp.dtype), (self.conv.weight, wp),
                       lambda: K.flip_weight(wp, self.Cout, self.Cin, self.R))
 
     def out_hw(self, H, W):
@@ -368,8 +368,8 @@ class CounterPlan:
         dev = img.device
         imgf = img.float().contiguous()
         col = Act(K.im2col_c3_general(imgf, dt, 7, 2, 3, STEM_KPAD))
-        if dt == torch.float32:  # the columns hold image values and zeros: the image's max bounds them
-            col.amax = K.amax(Act(imgf.view(1, 1, N * imgf.shape[1] * H, W)))
+        if dt == torch.float32:  # the columns hold image values and zeros: the image channels' maxima bound them
+            col.amax = _stem_col_amax(imgf, STEM_KPAD)
         build = lambda: K.pack_weight(self.conv1.weight.detach(), dt, cpad=3, row_len=STEM_KPAD)  # noqa: E731
         wp0 = build() if training else frozen(self, ("stem", dt), (self.conv1.weight,), build)
         P, Q = col.H, col.W
@@ -497,6 +497,16 @@ def gram(w: Act) -> torch.Tensor:
     return fr
 
 
+def _stem_col_amax(imgf: torch.Tensor, kpad: int) -> torch.Tensor:
+    """Operand maxima [1 + kpad] of the stem's im2col columns (dg_im2col_c3: column k < 3RS holds
+    image channel k % 3, the rest zeros) from the image's per-channel maxima."""
+    cm = imgf.abs().amax(dim=(0, 2, 3))  # [3]
+    rs3 = 3 * 7 * 7
+    col = torch.zeros(kpad, dtype=torch.float32, device=imgf.device)
+    col[:rs3] = cm.repeat(rs3 // 3)
+    return torch.cat([cm.max().view(1), col])
+
+
 def _whole_amax(w: Act):
     """f32: max |w| over the whole map (its producer's, else one pass), the f16 x3 operand bound
     every per-instance launch over w shares; None for 16-bit maps."""
@@ -511,6 +521,7 @@ def _iw_grad_hook(w: Act, fr, mask, ns, scale, g_wt):
     """gt += dL_wt/dw: gsym = d loss/d fraw (symmetrised, / (HW-1)), then one 1x1
     conv per instance (w_n @ gsym_n) accumulated into gt."""
     def apply(gt: Act):
+        gt.amax = None  # accumulated into below through per-instance views
         gsym = K.iw_loss(fr, w.H * w.W, mask, ns, scale, None, accumulate=False, want_grad=True,
                          grad_coef=g_wt)
         N, C = w.N, w.C

@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 5 /* 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 6 /* 6: operand maxima with channels ([1 + C] floats for f32 producers and dg_amax; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -112,10 +112,14 @@ int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, i
                    int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                    int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
                    void* stream);
-/* xamax (f32 entries, f16 x3 arithmetic): NULL, or a device float >= max |x| over the operand
- * (dg_amax, or the kernel that produced x); NULL makes the library take one read pass over x
- * for it.  An xamax below the true maximum is undefined behaviour (f16 overflow). */
-/* out[0] (device f32) = max |x| over the M x C f32 rows of pixel stride ldx. */
+/* xamax (f32 entries, f16 x3 arithmetic): NULL, or operand maxima of x (dg_amax, or the kernel that
+ * produced x): word 0 >= max |x| over the operand, and -- for the weight-gradient entries, which
+ * scale per channel -- words 1 .. C >= max |x| over each channel (channel c of the slice x points
+ * at in word 1 + c).  The forward / dgrad entries read word 0 only.  NULL makes the library take
+ * one read pass over x for them.  A maximum below the true one is undefined behaviour (f16
+ * overflow). */
+/* out[0 .. C] (device f32): out[0] = max |x| over the M x C f32 rows of pixel stride ldx, out[1 + c]
+ * = max over channel c (C % 4 == 0, C <= 2048). */
 int dg_amax(int dtype, const void* x, int64_t ldx, int64_t M, int C, float* out, void* stream);
 /* y = (relu_out > 0) ? conv1x1(x, w) + y : 0: the accumulating dgrad of a bottleneck's conv1 (w
  * flipped, dg_flip_weight) whose input relu_out is the previous block's ReLU output
@@ -157,7 +161,10 @@ int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, in
                   const void* dy, int64_t lddy, int Cout, int R, int S, int pad,
                   float* dw, void* workspace, int64_t ws_bytes, int accumulate, const float* xamax,
                   const float* dyamax, void* stream);
-/* xamax / dyamax: as dg_conv_fwd_ex's xamax, for x and dy (f32, f16 x3 arithmetic). */
+/* xamax / dyamax: operand maxima of x and dy with channels ([1 + C] and [1 + Cout] floats, as
+ * dg_amax writes; f32, f16 x3 arithmetic): each channel of x and of dy is scaled by its own power of
+ * two, and each dW element scaled back by 2^-(e_dy[co] + e_x[c]), so a channel far below its
+ * tensor's largest magnitude keeps f32-grade relative precision.  NULL: one read pass each. */
 
 /* torch [Cout][C][R][S] f32 -> packed rows out[Cout][row_len] of dtype holding
  * [R][S][Cpad] (zero-padded C, zero tail up to row_len). Cpad=3,row_len=64 gives
@@ -213,10 +220,11 @@ int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C,
 int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float* scale,
                 const float* shift, int act, const float* drop, int HW, void* y, int64_t ldy,
                 float* amax, void* stream);
-/* amax (here and on the BN-backward / pooled entries below; may be NULL): a device float that
- * receives max |output| of the pass (the written activation or dz; the pooled entries: over the
- * un-pooled values, >= max |yp|) -- the xamax a following f32 conv can take instead of a read
- * pass of its own. */
+/* amax (here and on the BN-backward / pooled / join / InstanceNorm entries below; may be NULL):
+ * the operand maxima of the pass's output (the written activation or dz; the pooled entries: over
+ * the un-pooled values, >= max |yp|) -- the xamax a following f32 conv can take instead of a read
+ * pass of its own.  f32: [1 + C] floats, word 0 the tensor's max and word 1 + c channel c's
+ * (C <= 2048); 16-bit: word 0 only.  Zeroed by the entry before its launch. */
 /* Backward: g = dL/dy (pixel stride ldg).  Produces dz (lddz), dgamma, dbeta
  * (written, not accumulated) and dbias_conv (sum dz, may be NULL).
  * save_mean = save_invstd = NULL: no normalisation (a biased conv + activation, e.g. the

@@ -180,3 +180,28 @@ def test_syncbn_local_without_process_group():
     from dgvcc_amd import syncbn as SB
     assert SB.group_of(torch.nn.SyncBatchNorm(8)) is None  # no process group: a local BatchNorm
     assert SB.group_of(None) is None
+
+
+def test_bench_launcher_dry_run_world8():
+    """bench.py's multi-rank path end to end on CPU: `--gpus 8` without a
+    torchrun environment starts torch.distributed.run (launch_ranks), the 8 ranks join a gloo group,
+    time a toy step with a blocking all-reduce per step, gather the per-rank step times and exposed
+    all-reduce times (bench.dp_attribution), and rank 0 prints one JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "8", "--steps", "3",
+                        "--warmup", "0", "--dry-run"], capture_output=True, text=True, timeout=300, env=env,
+                       cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    att = out["config"]["allreduce"]
+    assert out["n_gpus"] == 8 and out["dry_run"] and out["config"]["parallelism"] == "dp8"
+    assert len(att["step_ms_per_rank"]) == 8 and len(att["exposed_ms_per_rank"]) == 8
+    assert 0 < att["step_ms_min"] <= att["step_ms_max"] and att["exposed_ms"] >= 0
+    assert att["step_ms_max"] == max(att["step_ms_per_rank"])

@@ -673,6 +673,27 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
     for m in ("2", "1"):  # 512-pixel all-pixel-wave form (W % 512 == 0), 256-pixel form
         for e3, e1 in zip(errs[m], errs["0"]):
             assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
+    # every form runs the f16 x3 arithmetic (the per-tap and 256-pixel ones since round 6): each within
+    # 2x the exact v_mfma_f32_16x16x4_f32 path's error on the same launch
+    prev = K.lib_call_status("dg_get_f32_math")
+    K.call("dg_set_f32_math", 0)
+    try:
+        ex = []
+        if Cout == 64:
+            y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+            K.conv_fwd(xd, wp, Cout, 3, 1, y)
+            torch.cuda.synchronize()
+            ex.append(relerr(to_nchw(y.buf), yr.detach()))
+        if C == 64:
+            dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+            K.conv_dgrad(gyd, wp, C, 3, 1, dx)
+            torch.cuda.synchronize()
+            ex.append(relerr(to_nchw(dx.buf), xr.grad))
+    finally:
+        K.call("dg_set_f32_math", prev)
+    for m in ("2", "1", "0"):
+        for e3, e0 in zip(errs[m], ex):
+            assert e3 < 2 * e0 + 2e-7, (m, errs, ex)
 
 
 @pytest.mark.parametrize("sch", ["1", "3", "5", "6", "xs"])
@@ -717,13 +738,15 @@ def test_conv_f32_psplit_schedules(dev, sch, N, H, W, C, Cout, R, monkeypatch):
         K.call("dg_set_f32_math", prev)
 
 
-@pytest.mark.parametrize("xs,ws", [(1e-30, 1.0), (1e-6, 1e-3), (1.0, 1.0), (1e6, 1e3), (1e30, 1e-20)])
+@pytest.mark.parametrize("xs,ws", [(1e-30, 1.0), (1e-6, 1e-3), (1.0, 1.0), (1e6, 1e3), (1e30, 1e-20), (1e-12, 1e-25)])
 @pytest.mark.parametrize("case", [(1, 64, 96, 256, 256, 3), (1, 32, 512, 64, 64, 3), (1, 48, 64, 128, 128, 3)])
 def test_conv_f32_h16_scales(dev, xs, ws, case):
     """f16 x3 (dg_set_f32_math(2)) on operands of any magnitude: the power-of-two scales (per filter row,
     per pixel-operand tensor) bring them into f16 range and back exactly, so forward, dgrad and wgrad
     stay within 5e-6 (normwise relative) of float64 from 1e-30 to 1e30; one launch also holds a
-    dynamic range of 1e-12 inside one tensor."""
+    dynamic range of 1e-12 inside one tensor.  (1e-12, 1e-25): both operands tiny, so the two scales'
+    exponents sum past f32's range (2^-151) while the outputs (~1e-37) are normal f32 values: the
+    rescale is applied as one ldexp of the result, not as a factor that would flush."""
     K = _k()
     N, H, W, C, Cout, R = case
     pad = R // 2
@@ -756,7 +779,8 @@ def test_conv_f32_h16_scales(dev, xs, ws, case):
 
 
 def test_amax(dev):
-    """dg_amax: max |x| over a channel slice of an NHWC buffer (the f16 x3 operand scale)."""
+    """dg_amax: the operand maxima of a channel slice of an NHWC buffer (the f16 x3 scales): [0] the
+    slice's max |x|, [1 + c] channel c's."""
     K = _k()
     g = torch.Generator().manual_seed(9)
     buf = torch.randn(2, 7, 9, 96, generator=g)
@@ -765,5 +789,108 @@ def test_amax(dev):
     a = K.Act(buf.to(dev), off=32, C=32)
     m = K.amax(a)
     torch.cuda.synchronize()
-    assert m.item() == 77.25
-    assert K.amax(K.Act(buf.to(dev))).item() == 123.5
+    assert m.shape == (33,) and m[0].item() == 77.25
+    assert torch.equal(m[1:].cpu(), buf[..., 32:64].abs().amax(dim=(0, 1, 2)))
+    full = K.amax(K.Act(buf.to(dev))).cpu()
+    assert full[0].item() == 123.5 and torch.equal(full[1:], buf.abs().amax(dim=(0, 1, 2)))
+    for C in (4, 12, 896, 2048):  # chunk groups: one partial block, several rows, y-grid groups
+        b = torch.randn(3, 5, 7, C, generator=g) * torch.logspace(-20, 20, C)
+        m = K.amax(K.Act(b.to(dev))).cpu()
+        assert m[0].item() == b.abs().max().item() and torch.equal(m[1:], b.abs().amax(dim=(0, 1, 2))), C
+
+
+# channel magnitudes of the per-channel f16 x3 test: every fifth channel of the operand at full scale,
+# the others 1e-3 .. 1e-12 below it
+CHAN_DECADES = (1.0, 1e-3, 1e-6, 1e-9, 1e-12)
+
+
+def _chan_scaled(n, C, H, W, g):
+    s = torch.tensor([CHAN_DECADES[c % len(CHAN_DECADES)] for c in range(C)], dtype=torch.float64)
+    return (torch.randn(n, C, H, W, generator=g, dtype=torch.float64) * s.view(1, C, 1, 1)).float()
+
+
+def _chan_err(a, ref, dim):
+    """Per-channel relative error along `dim`: max |a - ref| over the channel / max |ref| over it."""
+    d = (a.double().cpu() - ref).abs()
+    other = [i for i in range(ref.dim()) if i != dim]
+    return d.amax(dim=other) / ref.abs().amax(dim=other).clamp_min(1e-300)
+
+
+@pytest.mark.parametrize("case", [(1, 32, 64, 128, 128, 3), (1, 24, 128, 64, 64, 3), (2, 16, 32, 128, 256, 3),
+                                  (1, 16, 64, 256, 128, 1), (1, 20, 36, 64, 128, 3)])
+def test_conv_f32_h16_per_channel(dev, case):
+    """f16 x3 per element: channels of x and dY 1e-3 .. 1e-12 below their tensor's
+    largest magnitude.  The weight gradient scales each channel of x and of dY by its own power of two,
+    so every row (output channel) and column (input channel) of dW keeps f32-grade relative error; the
+    forward and dgrad outputs per channel.  Bound: 2x the exact v_mfma_f32_16x16x4_f32 path's error on
+    the same channel (+1e-7 against two tiny maxima), both against float64.  Shapes: the 3-tap 128 x 128
+    and 64-channel 9-tap weight gradients, the per-tap kernel (1x1, and the 3x3 W % 32 != 0 rows)."""
+    K = _k()
+    N, H, W, C, Cout, R = case
+    pad = R // 2
+    g = torch.Generator().manual_seed(77)
+    x = _chan_scaled(N, C, H, W, g)
+    gy = _chan_scaled(N, Cout, H, W, g)
+    w = torch.randn(Cout, C, R, R, generator=g) / (C * R * R) ** 0.5
+    y64 = F.conv2d(x.double(), w.double(), padding=pad)
+    dx64 = torch.nn.grad.conv2d_input(x.shape, w.double(), gy.double(), padding=pad)
+    dw64 = torch.nn.grad.conv2d_weight(x.double(), w.shape, gy.double(), padding=pad)
+    xd, gyd = K.Act(to_nhwc(x).to(dev)), K.Act(to_nhwc(gy).to(dev))
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    prev = K.lib_call_status("dg_get_f32_math")
+    res = {}
+    try:
+        for m in (2, 0):
+            K.call("dg_set_f32_math", m)
+            y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+            K.conv_fwd(xd, wp, Cout, R, pad, y)
+            dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+            K.conv_dgrad(gyd, wp, C, R, pad, dx)
+            dw = torch.empty(Cout, C, R, R, device=dev)
+            K.conv_wgrad(xd, gyd, R, pad, dw)
+            torch.cuda.synchronize()
+            res[m] = {"fwd": _chan_err(to_nchw(y.buf), y64, 1), "dgrad": _chan_err(to_nchw(dx.buf), dx64, 1),
+                      "wgrad_rows": _chan_err(dw, dw64, 0), "wgrad_cols": _chan_err(dw, dw64, 1)}
+    finally:
+        K.call("dg_set_f32_math", prev)
+    for k in res[2]:
+        h, e = res[2][k], res[0][k]
+        bad = (h > 2 * e + 1e-7).nonzero().flatten().tolist()
+        print(k, f"f16x3 worst {h.max().item():.3e} exact worst {e.max().item():.3e}")
+        assert not bad, (k, [(c, h[c].item(), e[c].item()) for c in bad[:8]])
+    # the small channels are not flushed: every dW column / row carries its own magnitude
+    assert res[2]["wgrad_cols"].max().item() < 1e-5 and res[2]["wgrad_rows"].max().item() < 1e-5
+
+
+def test_producer_channel_maxima(dev):
+    """The f32 producers emit per-channel operand maxima ([1 + C]: bn_apply here, the BN backward
+    below) equal to the written tensor's, and a weight gradient on them is bit-identical to one that
+    takes the library's own read pass (same scales)."""
+    K = _k()
+    g = torch.Generator().manual_seed(12)
+    N, H, W, C = 2, 16, 32, 128
+    z = K.Act(to_nhwc(torch.randn(N, C, H, W, generator=g)).to(dev))
+    scale = torch.tensor([CHAN_DECADES[c % 5] for c in range(C)], dtype=torch.float32, device=dev)
+    shift = torch.randn(C, generator=g).to(dev) * scale
+    stats = torch.stack([torch.zeros_like(scale), torch.ones_like(scale), scale, shift])
+    y = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+    K.bn_apply(z, stats, K.ACT_RELU, y)
+    dy = K.Act(to_nhwc(_chan_scaled(N, 128, H, W, g)).to(dev))
+    torch.cuda.synchronize()
+    ref = y.view().abs().amax(dim=(0, 1, 2))
+    assert y.amax.shape == (1 + C,)
+    assert torch.equal(y.amax[1:], ref) and y.amax[0].item() == ref.max().item()
+    dw1 = torch.empty(128, C, 3, 3, device=dev)
+    dw2 = torch.empty_like(dw1)
+    K.conv_wgrad(y, dy, 3, 1, dw1)
+    K.conv_wgrad(K.Act(y.buf), K.Act(dy.buf), 3, 1, dw2)  # no maxima: the library's pass
+    torch.cuda.synchronize()
+    assert torch.equal(dw1, dw2)
+    # the BN backward's dz maxima
+    gz = K.Act(to_nhwc(torch.randn(N, C, H, W, generator=g)).to(dev))
+    dz = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+    dgam, dbet = (torch.empty(C, device=dev) for _ in range(2))
+    K.bn_bwd(gz, z, torch.ones(C, device=dev), stats, K.ACT_RELU, dz, dgam, dbet)
+    torch.cuda.synchronize()
+    ref = dz.view().abs().amax(dim=(0, 1, 2))
+    assert torch.equal(dz.amax[1:], ref) and dz.amax[0].item() == ref.max().item()

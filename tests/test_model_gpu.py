@@ -274,6 +274,37 @@ def test_step_grads_full_frame(dev):
     bad = {k: (v, e32[k]) for k, v in err.items() if v > max(2 * e32[k], E2E_GRAD_TOL)}
     assert not bad, bad
     assert glob <= max(2 * glob32, E2E_GLOBAL_TOL), (glob, glob32)
+    # the metric's own number: the full-frame density maps of both views
+    # against the oracle on the same decisions, within north_star's 1e-4 relative
+    dm = _full_frame_density_rel(dev)
+    print(f"full frame 768x1024: density map max rel {dm:.3e} (budget 1e-4)")
+    assert dm <= 1e-4, dm
+
+
+def _full_frame_density_rel(dev) -> float:
+    """DGModel_final forward_train at 1 x 3 x 768 x 1024 in fp32 (the f16 x3 default), density maps of
+    both views against the fp32 oracle re-run on the HIP forward's threshold decisions: the largest
+    max |d - r| / max |r| (bench.py density_parity's figure)."""
+    model = _model("DGModel_final", den_dropout=0.0, cls_dropout=0.0)
+    sd0 = O.seeded_state_dict(model.state_dict())
+    model.load_state_dict(sd0)
+    model = model.to(dev).set_precision("fp32").train()
+    img1, img2, (_, _, bmaps) = O.synthetic_batch(1, 768, 1024, seed=2112)
+    plan = model._get_plans()["pair"]
+    plan.capture = {}
+    try:
+        with torch.no_grad():
+            dc1, dc2 = model.forward_train(img1.to(dev), img2.to(dev), bmaps.to(dev))[:2]
+        cap = plan.capture
+    finally:
+        plan.capture = None
+    em = cap["emask"].permute(0, 3, 1, 2).bool().cpu()
+    cp = tuple(c.cpu() for c in cap["c_pred"])
+    with torch.no_grad():
+        r1, r2 = O.final_forward({k: v.clone() for k, v in sd0.items()}, img1, img2, bmaps, e_mask_in=em,
+                                 c_pred_in=cp)[:2]
+    return max(float((d.double().cpu() - r.double()).abs().max() / r.double().abs().max())
+               for d, r in ((dc1, r1), (dc2, r2)))
 
 
 def _skip_bias(k):
