@@ -3797,7 +3797,10 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
       return DG_OK;
     }
     if (rsplit_ok(a) && has_split_room(a)) {  // split math, Cout = 64: both operands split once per block
-      const bool h16 = f32_h16();  // f16 x3 on every Cout = 64 form (512-pixel 3-tap, 256-pixel 3-tap, per tap)
+      // f16 x3 on every Cout = 64 form (512-pixel 3-tap, 256-pixel 3-tap, per tap); DGVCC_RSPLIT_H16=0 keeps
+      // the 256-pixel and per-tap forms on the bf16 x6 split (A/B, read per launch)
+      const char* eh = getenv("DGVCC_RSPLIT_H16");
+      const bool h16 = f32_h16() && (rsplit3w_ok(a) || !(eh && eh[0] == '0'));
       const unsigned short* wsp = h16 ? presplit_h(a, st) : presplit(a, st);
       if (!wsp) return DG_ERR_HIP;
       const dim3 g((unsigned)((long long)dg_cdiv(M, 256) * (a.Cout / 64)));

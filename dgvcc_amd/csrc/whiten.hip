@@ -13,6 +13,7 @@
 // the exact adjoint (Newton iterations recomputed in LDS, no autograd tape).
 #include "dg_common.h"
 #include <algorithm>
+#include <cstdlib>
 
 extern "C" int64_t dg_instnorm_workspace(int N, int HW, int C);
 extern "C" int dg_instnorm_stats(int dtype, const void* x, int64_t ldx, int N, int HW, int C, float eps, float* mean,
@@ -710,6 +711,112 @@ __global__ __launch_bounds__(256) void sw_bwd_apply(const T* __restrict__ gy, lo
   }
 }
 
+// The two per-pixel 16 x 16 whitening products on the matrix cores (round 6; the thread-per-(pixel,
+// group) forms above read their 16 x 16 matrices from LDS once per FMA and ran LDS-bound at 2.4-2.9
+// TB/s).  A wave takes 16 pixels at a time and, for each group g, forms Y_g[16 ch][16 px] = M_g X_g
+// with four v_mfma_f32_16x16x4_f32: MFMA s pairs k-slot q = lane / 16 with channel 4q + s, so lane l
+// loads channels g*16 + 4q .. +3 of pixel l % 16 in one 8-B (16-bit) / 16-B (f32) load, its A
+// operands are row l % 16, columns 4q .. 4q + 3 of M_g (one 16-B LDS read), and its accumulator holds
+// channels 4q .. 4q + 3 of pixel l % 16 (one store).  The accumulator starts at the bias / constant
+// row.  f32 products and accumulation throughout (16-bit operands are exact in f32).
+template <typename T>
+__global__ __launch_bounds__(256) void sw_apply_mfma(const T* __restrict__ x, long long ldx, int HW, int C, int ppb,
+                                                     const float* __restrict__ aff, const float* __restrict__ bias,
+                                                     int act, T* __restrict__ y, long long ldy) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // A[G][256] | b[C]
+  const int n = blockIdx.y, G = C / SWC, tid = threadIdx.x;
+  const f4v* an = (const f4v*)(aff + (long long)n * G * 256);
+  const f4v* bn = (const f4v*)(bias + (long long)n * C);
+  for (int e = tid; e < G * 64; e += 256) ((f4v*)sm)[e] = an[e];
+  for (int e = tid; e < C / 4; e += 256) ((f4v*)(sm + G * 256))[e] = bn[e];
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, pr = lane & 15, q = lane >> 4;
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  for (int pc = p0 + 16 * wave; pc < p1; pc += 64) {
+    const int p = pc + pr;
+    const bool ok = p < p1;
+    const long long pp = (long long)n * HW + (ok ? p : p0);
+    const T* xr = x + pp * ldx + 4 * q;
+    T* yr = y + pp * ldy + 4 * q;
+#pragma unroll 4
+    for (int g = 0; g < G; ++g) {
+      float xv[4];
+      ld4(xr + g * 16, xv);
+      const f4v a = *(const f4v*)(sm + g * 256 + pr * 16 + 4 * q);
+      f4v acc = *(const f4v*)(sm + G * 256 + g * 16 + 4 * q);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], xv[s], acc, 0, 0, 0);
+      float o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (act == 1 && acc[r] < 0.f) ? 0.f : acc[r];
+      if (ok) st4(yr + g * 16, o);
+    }
+  }
+}
+
+// dx_p = K ge_p + L (x_p - mu_n) + c on the matrix cores (as sw_apply_mfma: eight MFMAs per group and
+// 16 pixels, the accumulator starting at c)
+template <typename T>
+__global__ __launch_bounds__(256) void sw_bwd_apply_mfma(const T* __restrict__ gy, long long ldg, const T* __restrict__ y,
+                                                         long long ldy, const T* __restrict__ x, long long ldx, int HW,
+                                                         int C, int ppb, int act, const float* __restrict__ mu,
+                                                         const float* __restrict__ coef, T* __restrict__ dx,
+                                                         long long lddx, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];  // [G][528]: K | L | c, then mu[C]
+  const int n = blockIdx.y, G = C / SWC, tid = threadIdx.x;
+  const f4v* cn = (const f4v*)(coef + (long long)n * G * 528);
+  for (int e = tid; e < G * 132; e += 256) ((f4v*)sm)[e] = cn[e];
+  for (int e = tid; e < C / 4; e += 256) ((f4v*)(sm + G * 528))[e] = ((const f4v*)(mu + (long long)n * C))[e];
+  __syncthreads();
+  const int lane = tid & 63, wave = tid >> 6, pr = lane & 15, q = lane >> 4;
+  const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  for (int pc = p0 + 16 * wave; pc < p1; pc += 64) {
+    const int p = pc + pr;
+    const bool ok = p < p1;
+    const long long pp = (long long)n * HW + (ok ? p : p0);
+#pragma unroll 2
+    for (int g = 0; g < G; ++g) {
+      const int c0 = g * 16 + 4 * q;
+      float ge[4], xv[4];
+      ld4(gy + pp * ldg + c0, ge);
+      ld4(x + pp * ldx + c0, xv);
+      if (act == 1) {
+        float yv[4];
+        ld4(y + pp * ldy + c0, yv);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) ge[s] = yv[s] > 0.f ? ge[s] : 0.f;
+      }
+      const float* Mg = sm + g * 528;
+      const f4v mv = *(const f4v*)(sm + G * 528 + c0);
+      const f4v ka = *(const f4v*)(Mg + pr * 16 + 4 * q);
+      const f4v la = *(const f4v*)(Mg + 256 + pr * 16 + 4 * q);
+      f4v acc = *(const f4v*)(Mg + 512 + 4 * q);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], ge[s], acc, 0, 0, 0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(la[s], xv[s] - mv[s], acc, 0, 0, 0);
+      float o[4] = {acc[0], acc[1], acc[2], acc[3]};
+      if (accumulate) {
+        float od[4];
+        ld4(dx + pp * lddx + c0, od);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] += od[r];
+      }
+      if (ok) st4(dx + pp * lddx + c0, o);
+    }
+  }
+}
+
+// blocks per instance of the MFMA apply passes: ~1024 blocks over the batch, 64 .. 2048 pixels each
+inline int sw_apply_nb(int HW, int N) {
+  return std::max(1, std::min(dg_cdiv(HW, 64), std::max(dg_cdiv(1024, N), dg_cdiv(HW, 2048))));
+}
+// DGVCC_SW_APPLY=0: the thread-per-(pixel, group) apply passes (A/B; read per launch)
+inline bool sw_apply_mfma_on() {
+  const char* e = getenv("DGVCC_SW_APPLY");
+  return !(e && e[0] == '0');
+}
+
 // pixel blocks per instance of the covariance / backward partial passes: enough blocks over the
 // batch to give every CU two (the deep 48x64 layers had 3 per instance, 48 blocks in all: the
 // backward partials ran at 0.3 TB/s), each at least 64 pixels, at most 64 per instance
@@ -850,6 +957,22 @@ extern "C" int dg_sw_fwd_finish(int dtype, const void* x, int64_t ldx, int N, in
   DG_CHECK_LAUNCH();
   const float* aff = save + (int64_t)N * C + (int64_t)N * G * 256 + C + (int64_t)G * 256;
   const float* bias = aff + (int64_t)N * G * 256;
+  if (sw_apply_mfma_on()) {
+    const int mnb = sw_apply_nb(HW, N);
+    const int mppb = dg_cdiv(HW, mnb);
+    const size_t mlds = (size_t)(G * 256 + C) * 4;
+    if (dtype == DG_BF16)
+      hipLaunchKernelGGL(sw_apply_mfma<bf16>, dim3(mnb, N), dim3(256), mlds, st, (const bf16*)x, ldx, HW, C, mppb, aff,
+                         bias, act, (bf16*)y, ldy);
+    else if (dtype == DG_F16)
+      hipLaunchKernelGGL(sw_apply_mfma<f16>, dim3(mnb, N), dim3(256), mlds, st, (const f16*)x, ldx, HW, C, mppb, aff,
+                         bias, act, (f16*)y, ldy);
+    else
+      hipLaunchKernelGGL(sw_apply_mfma<float>, dim3(mnb, N), dim3(256), mlds, st, (const float*)x, ldx, HW, C, mppb,
+                         aff, bias, act, (float*)y, ldy);
+    DG_CHECK_LAUNCH();
+    return DG_OK;
+  }
   const int anb = std::max(1, std::min(256, dg_cdiv(HW, 256)));
   const int appb = dg_cdiv(HW, anb);
   const size_t lds = (size_t)G * 273 * 4;
@@ -934,6 +1057,24 @@ extern "C" int dg_sw_bwd_finish(int dtype, const void* gy, int64_t ldg, const vo
   DG_CHECK_LAUNCH();
   hipLaunchKernelGGL(sw_bwd_weights, dim3(1), dim3(64), 0, st, wpart, G, mean_w, var_w, dmean_w, dvar_w);
   DG_CHECK_LAUNCH();
+  if (sw_apply_mfma_on()) {
+    const int mnb = sw_apply_nb(HW, N);
+    const int mppb = dg_cdiv(HW, mnb);
+    const size_t mlds = (size_t)(G * 528 + C) * 4;
+    if (dtype == DG_BF16)
+      hipLaunchKernelGGL(sw_bwd_apply_mfma<bf16>, dim3(mnb, N), dim3(256), mlds, st, (const bf16*)gy, ldg,
+                         (const bf16*)y, ldy, (const bf16*)x, ldx, HW, C, mppb, act, mu, coef, (bf16*)dx, lddx,
+                         accumulate);
+    else if (dtype == DG_F16)
+      hipLaunchKernelGGL(sw_bwd_apply_mfma<f16>, dim3(mnb, N), dim3(256), mlds, st, (const f16*)gy, ldg, (const f16*)y,
+                         ldy, (const f16*)x, ldx, HW, C, mppb, act, mu, coef, (f16*)dx, lddx, accumulate);
+    else
+      hipLaunchKernelGGL(sw_bwd_apply_mfma<float>, dim3(mnb, N), dim3(256), mlds, st, (const float*)gy, ldg,
+                         (const float*)y, ldy, (const float*)x, ldx, HW, C, mppb, act, mu, coef, (float*)dx, lddx,
+                         accumulate);
+    DG_CHECK_LAUNCH();
+    return DG_OK;
+  }
   const int anb = std::max(1, std::min(256, dg_cdiv(HW, 256)));
   const int appb = dg_cdiv(HW, anb);
   const size_t lds = (size_t)G * 545 * 4;

@@ -173,8 +173,9 @@ def test_bn_add_relu_join(dev, dtype, downsample):
     torch.cuda.synchronize()
     tol = 1e-6 if dtype == torch.float32 else 1e-2
     assert relerr(y.buf.float(), ref) < tol
-    if dtype == torch.float32:  # the join's max |y| (the next f16 x3 convs' operand bound), exact
-        assert y.amax is not None and y.amax.item() == y.buf.abs().max().item()
+    if dtype == torch.float32:  # the join's maxima (the next f16 x3 convs' operand bounds), exact: tensor, channels
+        assert y.amax is not None and y.amax[0].item() == y.buf.abs().max().item()
+        assert torch.equal(y.amax[1:], y.buf.abs().amax(dim=(0, 1, 2)))
     mask = (y.buf.float().cpu() > 0).float()
     assert torch.equal(gout.buf.float().cpu(), gg.to(dtype).float() * mask)
 
@@ -221,9 +222,10 @@ def test_instance_norm(dev, dtype, affine, act, shape):
     if affine:
         assert relerr(dgam, gr.grad) < (2e-5 if dtype == torch.float32 else 1e-2)
         assert relerr(dbet, br.grad) < (2e-5 if dtype == torch.float32 else 1e-2)
-    if dtype == torch.float32:  # max |y| and max |dx| from the apply passes, exact
-        assert y.amax.item() == y.buf.abs().max().item()
-        assert dx.amax.item() == dx.buf.abs().max().item()
+    if dtype == torch.float32:  # max |y| and max |dx| from the apply passes, exact: tensor and channels
+        for t in (y, dx):
+            assert t.amax[0].item() == t.buf.abs().max().item()
+            assert torch.equal(t.amax[1:], t.buf.abs().amax(dim=(0, 1, 2)))
 
 
 def _sw_params(C, g):
@@ -274,6 +276,37 @@ def test_switch_whiten(dev, dtype, shape, act):
         assert relerr(d[k], sd[k].grad) < (1e-3 if f32 else 5e-2), k
     assert relerr(pd["running_mean"], sd["running_mean"]) < (1e-4 if f32 else 1e-2)
     assert relerr(pd["running_cov"], sd["running_cov"]) < (1e-4 if f32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape", [(3, 64, 9, 7), (2, 256, 24, 20), (16, 128, 12, 16)])
+def test_switch_whiten_apply_mfma(dev, dtype, shape, monkeypatch):
+    """The whitening applies on the matrix cores (sw_apply_mfma / sw_bwd_apply_mfma, default) against the
+    thread-per-(pixel, group) FMA forms (DGVCC_SW_APPLY=0): same products, another summation order --
+    f32 within 2e-6 relative, 16-bit within one rounding; ragged pixel tails, ReLU, accumulate."""
+    K = _k()
+    N, C, H, W = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(N, C, H, W, generator=g) * 1.5 + 0.3
+    gy = torch.randn(N, C, H, W, generator=g)
+    p = {k: v.to(dev) for k, v in _sw_params(C, g).items()}
+    dx0 = to_nhwc(torch.randn(N, C, H, W, generator=g)).to(dev, dtype)
+    outs = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("DGVCC_SW_APPLY", mode)
+        pm = {k: v.clone() for k, v in p.items()}
+        xd = K.Act(to_nhwc(x).to(dev, dtype))
+        y = K.Act(K.nhwc(N, H, W, C, dtype, dev))
+        save = K.sw_fwd(xd, pm["sw_mean_weight"], pm["sw_var_weight"], pm["weight"], pm["bias"],
+                        pm["running_mean"], pm["running_cov"], True, 1, y)
+        dx = K.Act(dx0.clone())
+        K.sw_bwd(K.Act(to_nhwc(gy).to(dev, dtype)), y, xd, save, pm["sw_mean_weight"], pm["sw_var_weight"],
+                 pm["weight"], 1, dx, accumulate=True)
+        torch.cuda.synchronize()
+        outs.append((y.buf.float().cpu(), dx.buf.float().cpu()))
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    assert relerr(outs[1][0], outs[0][0]) < tol
+    assert relerr(outs[1][1], outs[0][1]) < tol
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
