@@ -673,8 +673,31 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
     for m in ("2", "1"):  # 512-pixel all-pixel-wave form (W % 512 == 0), 256-pixel form
         for e3, e1 in zip(errs[m], errs["0"]):
             assert e3 < 5e-6 and e3 < 2 * e1 + 2e-7, errs
-    # every form runs the f16 x3 arithmetic (the per-tap and 256-pixel ones since round 6): each within
-    # 2x the exact v_mfma_f32_16x16x4_f32 path's error on the same launch
+    # each form within 2x the exact v_mfma_f32_16x16x4_f32 path's error on the same launch: the 512-pixel
+    # form on f16 x3, the 256-pixel and per-tap ones on bf16 x6 (default) and on f16 x3 (DGVCC_RSPLIT_H16=1)
+    old_h = os.environ.get("DGVCC_RSPLIT_H16")
+    try:
+        os.environ["DGVCC_RSPLIT_H16"] = "1"
+        for m in ("1", "0"):
+            os.environ["DGVCC_RSPLIT3"] = m
+            e = []
+            if Cout == 64:
+                y = K.Act(K.nhwc(N, H, W, Cout, torch.float32, dev))
+                K.conv_fwd(xd, wp, Cout, 3, 1, y)
+                torch.cuda.synchronize()
+                e.append(relerr(to_nchw(y.buf), yr.detach()))
+            if C == 64:
+                dx = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+                K.conv_dgrad(gyd, wp, C, 3, 1, dx)
+                torch.cuda.synchronize()
+                e.append(relerr(to_nchw(dx.buf), xr.grad))
+            errs["h16_" + m] = e
+    finally:
+        for k, v in (("DGVCC_RSPLIT_H16", old_h), ("DGVCC_RSPLIT3", old)):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     prev = K.lib_call_status("dg_get_f32_math")
     K.call("dg_set_f32_math", 0)
     try:
@@ -691,7 +714,7 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
             ex.append(relerr(to_nchw(dx.buf), xr.grad))
     finally:
         K.call("dg_set_f32_math", prev)
-    for m in ("2", "1", "0"):
+    for m in ("2", "1", "0", "h16_1", "h16_0"):
         for e3, e0 in zip(errs[m], ex):
             assert e3 < 2 * e0 + 2e-7, (m, errs, ex)
 
