@@ -3575,7 +3575,7 @@ static int launch_amax(const float* x, long long ldx, long long M, int C, unsign
 // out [1 + C]: the tensor's max and each channel's (camax_kernel), ~1024 blocks
 static int launch_camax(const float* x, long long ldx, long long M, int C, unsigned* out, hipStream_t st) {
   if (C % 4 != 0 || C > DG_CAMAX_C) return DG_ERR_UNSUPPORTED;
-  if (hipMemsetAsync(out, 0, (1 + (size_t)C) * 4, st) != hipSuccess) return DG_ERR_HIP;
+  if (hipMemsetAsync(out, 0, dg_amax_words(C) * 4, st) != hipSuccess) return DG_ERR_HIP;
   if (M <= 0) return DG_OK;
   const int cq = C / 4, G = std::min(cq, 256), rows = 256 / G, gy = dg_cdiv(cq, G);
   const int gx = (int)std::max(1LL, std::min<long long>(dg_cdiv(M, rows), std::max(1, 1024 / gy)));
@@ -4472,23 +4472,38 @@ __global__ __launch_bounds__(NTH, 512 / NTH) void conv_wgrad_split3_kernel(WgArg
   // pixel coordinates of the current K-step's first pixel (uniform over the block)
   int sn = kbeg / HW, sp = (kbeg - sn * HW) / a.W, sq = kbeg - sn * HW - sp * a.W;
   u4v ra[AR], rb[BR];
-  auto gload = [&](int k0) __attribute__((always_inline)) {
+  // per-lane parts of the load offsets, fixed over the K loop: 32-bit byte offsets (the buffer windows
+  // are < 2^31 bytes, checked by the launcher) with the uniform per-K-step part added in the loop, and
+  // an unconditional select for the out-of-image taps (no 64-bit multiplies, no exec-mask branches)
+  unsigned aoff[AR], boff[BR];
+  int brow[BR], bstrip[BR];
+  bool bval[BR];
 #pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const int idx = tid + NTH * i;
-      const int row = idx / CPRA, ch = idx % CPRA;
-      ra[i] = bload(dyr, (unsigned)(((long long)(k0 + row - kbeg) * a.lddy + co0 + ch * 4) * 4));
-    }
+  for (int i = 0; i < AR; ++i) {
+    const int idx = tid + NTH * i;
+    aoff[i] = (unsigned)((idx / CPRA) * a.lddy + co0 + (idx % CPRA) * 4) * 4u;
+  }
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int idx = tid + NTH * i;
+    const int strip = NR == 3 ? idx / (XR * CPRB) : 0, sidx = idx - strip * (XR * CPRB);
+    bstrip[i] = strip;
+    brow[i] = sidx / CPRB;
+    bval[i] = idx < NR * XR * CPRB;
+    boff[i] = (unsigned)(brow[i] * a.ldx + c0 + (sidx % CPRB) * 4) * 4u;
+  }
+  const unsigned ldx4 = (unsigned)a.ldx * 4u, lddy4 = (unsigned)a.lddy * 4u;
+  auto gload = [&](int k0) __attribute__((always_inline)) {
+    const unsigned abase = (unsigned)(k0 - kbeg) * lddy4;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) ra[i] = bload(dyr, abase + aoff[i]);
 #pragma unroll
     for (int i = 0; i < BR; ++i) {
-      const int idx = tid + NTH * i;
-      const int strip = NR == 3 ? idx / (XR * CPRB) : 0, sidx = idx - strip * (XR * CPRB);
-      const int h = sp + (NR == 3 ? strip - 1 : dh);
-      const int row = sidx / CPRB, ch = sidx % CPRB;
-      const int ww = sq - 1 + row;
-      const bool ok = idx < NR * XR * CPRB && (unsigned)h < (unsigned)a.H && (unsigned)ww < (unsigned)a.W;
-      const long long pin = (long long)sn * HW + (long long)h * a.W + ww - xlo;
-      rb[i] = bload(xr, ok ? (unsigned)((pin * a.ldx + c0 + ch * 4) * 4) : 0xFFFFFFF0u);
+      const int h = sp + (NR == 3 ? bstrip[i] - 1 : dh);
+      const bool ok = bval[i] && (unsigned)h < (unsigned)a.H && (unsigned)(sq - 1 + brow[i]) < (unsigned)a.W;
+      // pixel of strip row 0 (column sq - 1) relative to the window start, times the pixel stride
+      const unsigned sbase = (unsigned)(sn * HW + h * a.W + sq - 1 - xlo) * ldx4;
+      rb[i] = bload(xr, ok ? sbase + boff[i] : 0xFFFFFFF0u);
     }
     sq += BKP;
     if (sq >= a.W) {
@@ -5409,9 +5424,10 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st, unsigned* 
             a.xam = hslots;
           }
           if (!a.dyam) {
-            const int r = launch_camax((const float*)a.dy, a.lddy, M3, a.Cout, hslots + 1 + a.C, st);
+            unsigned* dys = hslots + dg_amax_words(a.C);
+            const int r = launch_camax((const float*)a.dy, a.lddy, M3, a.Cout, dys, st);
             if (r != DG_OK) return r;
-            a.dyam = hslots + 1 + a.C;
+            a.dyam = dys;
           }
         }
         if (h16) {
@@ -5455,9 +5471,10 @@ int launch_wgrad(WgArgs a, float* dw, int accumulate, hipStream_t st, unsigned* 
           a.xam = hslots;
         }
         if (!a.dyam) {
-          const int r = launch_camax((const float*)a.dy, a.lddy, (long long)a.N * a.P * a.Q, a.Cout, hslots + 1 + a.C, st);
+          unsigned* dys = hslots + dg_amax_words(a.C);
+          const int r = launch_camax((const float*)a.dy, a.lddy, (long long)a.N * a.P * a.Q, a.Cout, dys, st);
           if (r != DG_OK) return r;
-          a.dyam = hslots + 1 + a.C;
+          a.dyam = dys;
         }
         if (bco == 64) hipLaunchKernelGGL((conv_wgrad_split_kernel<64, 64, 2, 256, 1>), gs, dim3(256), 0, st, a);
         else if (bcw == 256) hipLaunchKernelGGL((conv_wgrad_split_kernel<128, 256, 2, 512, 1>), gs, dim3(512), 0, st, a);
@@ -5971,7 +5988,9 @@ extern "C" int dg_conv_dgrad(int dtype, const void* dy, int64_t lddy, int N, int
                      stream);
 }
 
-static int64_t wg_amax_bytes(int C, int Cout) { return (int64_t)(2 + C + Cout) * 4 / 256 * 256 + 256; }
+static int64_t wg_amax_bytes(int C, int Cout) {
+  return (int64_t)(dg_amax_words(C) + dg_amax_words(Cout)) * 4 / 256 * 256 + 256;
+}
 
 extern "C" int64_t dg_conv_wgrad_workspace(int dtype, int N, int H, int W, int C, int Cout, int R, int S) {
   if (N <= 0 || H <= 0 || W <= 0 || C <= 0 || Cout <= 0 || R <= 0 || S <= 0) return DG_ERR_INVALID;

@@ -141,13 +141,16 @@ __device__ __forceinline__ float wave_max(float v) {
 
 static inline int dg_cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 
-// Zero a producer's operand-maxima buffer before its launch (may be NULL): [1 + C] floats for an f32
-// output (the tensor's word, then one per channel: OutMax), one word for a 16-bit one.
-// DG_ERR_INVALID when an f32 output has more channels than the per-channel fold handles.
+// Words of an f32 output's operand-maxima buffer: 1 + C (the tensor's word, then one per channel:
+// OutMax), rounded up to a multiple of 4 so the zeroing below is one 16-byte-aligned fill (a 4(1 + C)-byte
+// memset ran as two fill dispatches); 16-bit outputs use word 0 alone.
+__host__ __device__ inline size_t dg_amax_words(int C) { return ((size_t)C + 4) & ~(size_t)3; }
+// Zero a producer's operand-maxima buffer before its launch (may be NULL).  DG_ERR_INVALID when an f32
+// output has more channels than the per-channel fold handles.
 static inline int dg_zero_amax(float* amax, int dtype, int C, hipStream_t st) {
   if (!amax) return DG_OK;
   if (dtype == DG_F32 && C > 2048) return DG_ERR_INVALID;  // DG_CAMAX_C
-  return hipMemsetAsync(amax, 0, (dtype == DG_F32 ? 1 + (size_t)C : 1) * 4, st) == hipSuccess ? DG_OK : DG_ERR_HIP;
+  return hipMemsetAsync(amax, 0, (dtype == DG_F32 ? dg_amax_words(C) : 1) * 4, st) == hipSuccess ? DG_OK : DG_ERR_HIP;
 }
 
 // ---------------------------------------------------------------------------
@@ -347,9 +350,12 @@ __device__ __forceinline__ void chan_h16_scales(const unsigned* am, int c, int e
 // the atomic when *out already holds >= r: the word only grows, so a stale read costs at most an
 // atomic that changes nothing.  Thousands of blocks each issuing an atomic on one address serialise
 // (tools/bench_bn.py: 16384 blocks made a 0.07-ms f32 BN apply 0.20 ms).
+// The check is a plain cached load (a relaxed atomic load compiled to a system-coherent one, a memory
+// round trip per word that the per-channel folds paid C / blockDim times per block): a stale value is
+// never larger than the word, so it can only add an atomic that changes nothing.
 __device__ __forceinline__ void amax_fold(unsigned* out, float r) {
   const unsigned v = __float_as_uint(r);
-  if (__atomic_load_n(out, __ATOMIC_RELAXED) < v) atomicMax(out, v);
+  if (*(const unsigned*)out < v) atomicMax(out, v);
 }
 
 // max |v| of the values a block stored, folded into *out (amax_fold).  Every thread of the block

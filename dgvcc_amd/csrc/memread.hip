@@ -630,9 +630,11 @@ __global__ __launch_bounds__(NT) void softmax_head_fwd(const T* __restrict__ L1,
 
 // gL_v = P_v (gP_v - <P_v, gP_v>) with gP_v = gpre_v v + (loss term); u/db partials per block:
 // part[blk][0:C] = sum_px sum_v gpre_v P_v, part[blk][C] = sum_px sum_v gpre_v.
-// amax (may be NULL; zeroed by the launcher): [0] max |gL_1|, [1] max |gL_2| (the logits GEMMs'
-// f16 x3 operand scales in the backward, dg_common.h block_amax_commit).
-template <typename T, int EPL, int NV, int LOSS>
+// amax (may be NULL; zeroed by the launcher): CM = 0: [0] max |gL_1|, [1] max |gL_2|; CM = 1 (f32): per view
+// v, at v * dg_amax_words(C), the operand maxima with channels of gL_v (word 0 the tensor's, 1 + s slot s's:
+// the logits GEMMs' f16 x3 scales in the backward, per channel in their weight gradient), from per-lane
+// running maxima of the lane's slots reduced over the block's waves in LDS.
+template <typename T, int EPL, int NV, int LOSS, int CM = 0>
 __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1, const T* __restrict__ P2, int M,
                                                        int C, const float* __restrict__ v, int act,
                                                        const float* __restrict__ yh1, const float* __restrict__ yh2,
@@ -643,6 +645,9 @@ __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1,
   constexpr int V = 16 / (int)sizeof(T);
   __shared__ float sh[4 * EPL * 64 + 4];
   float mx1 = 0.f, mx2 = 0.f;
+  float cm1[CM ? EPL : 1], cm2[CM ? EPL : 1];  // CM: per-slot running maxima of |gL_v|
+#pragma unroll
+  for (int j = 0; j < (CM ? EPL : 1); ++j) { cm1[j] = 0.f; cm2[j] = 0.f; }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   float vv[EPL], u[EPL];
   load_vec_as_row<T>(v, lane, vv, EPL);
@@ -701,8 +706,13 @@ __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1,
     if (NV == 2 && GL2) store_row(GL2 + r * C, lane, g2, EPL);
 #pragma unroll
     for (int j = 0; j < EPL; ++j) {
-      mx1 = fmaxf(mx1, fabsf(g1[j]));
-      if (NV == 2) mx2 = fmaxf(mx2, fabsf(g2[j]));
+      if constexpr (CM) {
+        cm1[j] = fmaxf(cm1[j], fabsf(g1[j]));
+        if (NV == 2) cm2[j] = fmaxf(cm2[j], fabsf(g2[j]));
+      } else {
+        mx1 = fmaxf(mx1, fabsf(g1[j]));
+        if (NV == 2) mx2 = fmaxf(mx2, fabsf(g2[j]));
+      }
     }
   }
   // waves' u rows -> LDS at slot order, fixed-order sum over the 4 waves
@@ -717,10 +727,30 @@ __global__ __launch_bounds__(NT) void softmax_head_bwd(const T* __restrict__ P1,
     o[C] = ((q[0] + q[1]) + q[2]) + q[3];
   }
   if (amax) {  // uniform
-    block_amax_commit(mx1, amax);
-    if (NV == 2) {
-      __syncthreads();  // block_amax_commit's LDS slots are reused
-      block_amax_commit(mx2, amax + 1);
+    if constexpr (CM) {
+      const int words = (int)dg_amax_words(C);
+#pragma unroll
+      for (int view = 0; view < NV; ++view) {
+        __syncthreads();  // every thread is done reading sh (the u sums, or the previous view)
+#pragma unroll
+        for (int j = 0; j < EPL; ++j)
+          sh[w * EPL * 64 + (j / V) * 64 * V + lane * V + (j % V)] = view == 0 ? cm1[j] : cm2[j];
+        __syncthreads();
+        float bm = 0.f;
+        float* ov = amax + view * words;
+        for (int c = threadIdx.x; c < C; c += NT) {
+          const float m = fmaxf(fmaxf(sh[c], sh[C + c]), fmaxf(sh[2 * C + c], sh[3 * C + c]));
+          bm = fmaxf(bm, m);
+          if (m > 0.f) amax_fold((unsigned*)ov + 1 + c, m);
+        }
+        block_amax_commit(bm, ov);
+      }
+    } else {
+      block_amax_commit(mx1, amax);
+      if (NV == 2) {
+        __syncthreads();  // block_amax_commit's LDS slots are reused
+        block_amax_commit(mx2, amax + 1);
+      }
     }
   }
 }
@@ -1087,12 +1117,20 @@ template <typename T, int NV, int LOSS>
 void mh_bwd_c(int C, int grid, hipStream_t st, const void* P1, const void* P2, int M, const float* v, int act,
               const float* yh1, const float* yh2, const float* g1, const float* g2, const float* coef, void* GL1,
               void* GL2, float* part, float* amax) {
-#define MHB(E)                                                                                                  \
-  hipLaunchKernelGGL((softmax_head_bwd<T, E, NV, LOSS>), dim3(grid), dim3(NT), 0, st, (const T*)P1, (const T*)P2, \
+#define MHB(E, CM_)                                                                                                \
+  hipLaunchKernelGGL((softmax_head_bwd<T, E, NV, LOSS, CM_>), dim3(grid), dim3(NT), 0, st, (const T*)P1, (const T*)P2, \
                      M, C, v, act, yh1, yh2, g1, g2, coef, (T*)GL1, (T*)GL2, part, amax)
-  if (C == 1024) MHB(16);
-  else if (C == 512) MHB(8);
-  else MHB(32);
+  if constexpr (std::is_same<T, float>::value) {  // f32 logit gradients: per-slot operand maxima
+    if (amax) {
+      if (C == 1024) MHB(16, 1);
+      else if (C == 512) MHB(8, 1);
+      else MHB(32, 1);
+      return;
+    }
+  }
+  if (C == 1024) MHB(16, 0);
+  else if (C == 512) MHB(8, 0);
+  else MHB(32, 0);
 #undef MHB
 }
 
@@ -1164,7 +1202,9 @@ extern "C" int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* 
   hipStream_t st = (hipStream_t)stream;
   const int grid = mh_grid(M);
   float* part = (float*)workspace;
-  if (amax && hipMemsetAsync(amax, 0, 8, st) != hipSuccess) return DG_ERR_HIP;
+  // amax: f32, nviews x dg_amax_words(C) floats (per-slot maxima per view); 16-bit, one word per view
+  const size_t am_bytes = dtype == DG_F32 ? (size_t)nviews * dg_amax_words(C) * 4 : 8;
+  if (amax && hipMemsetAsync(amax, 0, am_bytes, st) != hipSuccess) return DG_ERR_HIP;
   if (dtype == DG_BF16)
     mh_bwd_t<bf16>(nviews, loss, C, grid, st, P1, P2, M, v, act, yh1, yh2, gyh1, gyh2, coef, GL1, GL2, part, amax);
   else if (dtype == DG_F16)

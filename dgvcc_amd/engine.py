@@ -483,8 +483,11 @@ def _cat_act(buf: torch.Tensor, up_src: Act, skip: Act) -> Act:
     scale) bounds both parts: bilinear upsampling does not exceed its source's max |.|."""
     a = Act(buf)
     if up_src.amax is not None and skip.amax is not None:
-        if up_src.amax.numel() == 1 + up_src.C and skip.amax.numel() == 1 + skip.C:  # per channel
-            a.amax = torch.cat([torch.maximum(up_src.amax[:1], skip.amax[:1]), up_src.amax[1:], skip.amax[1:]])
+        cu, cs = up_src.C, skip.C
+        if up_src.amax.numel() >= 1 + cu and skip.amax.numel() >= 1 + cs:  # per channel
+            pad = K.amax_words(cu + cs) - (1 + cu + cs)
+            a.amax = torch.cat([torch.maximum(up_src.amax[:1], skip.amax[:1]), up_src.amax[1:1 + cu],
+                                skip.amax[1:1 + cs], up_src.amax.new_zeros(pad)])
         else:
             a.amax = torch.maximum(up_src.amax[:1], skip.amax[:1])
     return a
@@ -951,11 +954,13 @@ class _Heads:
         two = len(Ps) == 2
         work = torch.empty(K.query("dg_mem_head_workspace", M, S) // 4 + 1, dtype=torch.float32, device=dev)
         gLs = [Act(torch.empty_like(P.buf)) for P in Ps] if want_gl else None
-        # f32: max |gL_v| from the same pass, for the logits GEMMs' f16 x3 scales in bwd_logits
-        am = torch.empty(2, dtype=torch.float32, device=dev) if (gLs and P1.buf.dtype == torch.float32) else None
+        # f32: the operand maxima with channels (slots) of gL_v from the same pass, for the logits GEMMs'
+        # f16 x3 scales in bwd_logits (per slot in their weight gradient)
+        nw = K.amax_words(S)
+        am = torch.empty(2 * nw, dtype=torch.float32, device=dev) if (gLs and P1.buf.dtype == torch.float32) else None
         if am is not None:
             for i, gL in enumerate(gLs):
-                gL.amax = am[i:i + 1]
+                gL.amax = am[i * nw:(i + 1) * nw]
         K.call("dg_softmax_head_bwd", P1.dt, len(Ps), loss, P1.ptr, Ps[1].ptr if two else None, M, S, K.ptr(v),
                self.head_act, K.ptr(yhs[0]), K.ptr(yhs[1]) if two else None, K.ptr(g_hs[0]),
                K.ptr(g_hs[1]) if two else None, K.ptr(coef), gLs[0].ptr if gLs else None,

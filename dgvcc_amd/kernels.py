@@ -195,7 +195,7 @@ def import_act(t: torch.Tensor) -> Act:
 def amax(x: Act) -> torch.Tensor:
     """Operand maxima of the slice (f32): a device f32 [1 + C], [0] = max |x|, [1 + c] = max over
     channel c (dg_amax)."""
-    out = torch.empty(1 + x.C, dtype=torch.float32, device=x.buf.device)
+    out = torch.empty(amax_words(x.C), dtype=torch.float32, device=x.buf.device)
     call("dg_amax", x.dt, x.ptr, x.ld, x.M, x.C, ptr(out), stream())
     return out
 
@@ -289,10 +289,16 @@ def bn_bwd_from_part(pre, g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamm
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(coef), ptr(am), stream())
 
 
+def amax_words(C: int) -> int:
+    """Floats of an operand-maxima buffer with channels: 1 + C, rounded up to a multiple of 4 (the
+    library zeroes whole 16-byte words, include/dgvcc.h dg_amax)."""
+    return (C + 4) & ~3
+
+
 def chan_amax(a: Act):
-    """a.amax when it carries per-channel words ([1 + C]: what the weight gradients' per-channel f16 x3
-    scales need), else None (the library then takes its own per-channel read pass)."""
-    return a.amax if a.amax is not None and a.amax.numel() == 1 + a.C else None
+    """a.amax when it carries per-channel words ([1 + C] and up: what the weight gradients' per-channel
+    f16 x3 scales need), else None (the library then takes its own per-channel read pass)."""
+    return a.amax if a.amax is not None and a.amax.numel() >= 1 + a.C else None
 
 
 def conv_wgrad(x: Act, dy: Act, R: int, pad: int, dw: torch.Tensor, accumulate=False, k_alg=None):
@@ -496,7 +502,7 @@ def _amax_out(a: Act | None, *more: Act | None) -> torch.Tensor | None:
     x3 convs' scales); None for 16-bit outputs."""
     if a is None or a.buf.dtype != torch.float32:
         return None
-    t = torch.empty(1 + a.C, dtype=torch.float32, device=a.buf.device)
+    t = torch.empty(amax_words(a.C), dtype=torch.float32, device=a.buf.device)
     for o in (a, *more):
         if o is not None:
             o.amax = t

@@ -498,13 +498,14 @@ def gram(w: Act) -> torch.Tensor:
 
 
 def _stem_col_amax(imgf: torch.Tensor, kpad: int) -> torch.Tensor:
-    """Operand maxima [1 + kpad] of the stem's im2col columns (dg_im2col_c3: column k < 3RS holds
-    image channel k % 3, the rest zeros) from the image's per-channel maxima."""
+    """Operand maxima of the stem's im2col columns (dg_im2col_c3: column k < 3RS holds image channel
+    k % 3, the rest zeros) from the image's per-channel maxima: [kernels.amax_words(kpad)] floats."""
     cm = imgf.abs().amax(dim=(0, 2, 3))  # [3]
     rs3 = 3 * 7 * 7
-    col = torch.zeros(kpad, dtype=torch.float32, device=imgf.device)
-    col[:rs3] = cm.repeat(rs3 // 3)
-    return torch.cat([cm.max().view(1), col])
+    out = torch.zeros(K.amax_words(kpad), dtype=torch.float32, device=imgf.device)
+    out[0] = cm.max()
+    out[1:1 + rs3] = cm.repeat(rs3 // 3)
+    return out
 
 
 def _whole_amax(w: Act):

@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 6 /* 6: operand maxima with channels ([1 + C] floats for f32 producers and dg_amax; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 6 /* 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -119,7 +119,9 @@ int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, i
  * one read pass over x for them.  A maximum below the true one is undefined behaviour (f16
  * overflow). */
 /* out[0 .. C] (device f32): out[0] = max |x| over the M x C f32 rows of pixel stride ldx, out[1 + c]
- * = max over channel c (C % 4 == 0, C <= 2048). */
+ * = max over channel c (C % 4 == 0, C <= 2048).  Every operand-maxima buffer the library writes
+ * (here and the producers' amax) holds 1 + C words rounded up to a multiple of 4: the zeroing
+ * before the pass writes them all. */
 int dg_amax(int dtype, const void* x, int64_t ldx, int64_t M, int C, float* out, void* stream);
 /* y = (relu_out > 0) ? conv1x1(x, w) + y : 0: the accumulating dgrad of a bottleneck's conv1 (w
  * flipped, dg_flip_weight) whose input relu_out is the previous block's ReLU output
@@ -569,6 +571,9 @@ int dg_softmax_head_bwd(int dtype, int nviews, int loss, const void* P1, const v
                         const float* v, int act, const float* yh1, const float* yh2, const float* gyh1,
                         const float* gyh2, const float* coef, void* GL1, void* GL2, void* workspace,
                         float* amax, void* stream);
+/* amax (may be NULL): f32, the logit gradients' operand maxima with channels, view v at
+ * v * words (words = 1 + C rounded up to a multiple of 4; word 0 max |gL_v|, word 1 + s slot s's);
+ * 16-bit, amax[v] = max |gL_v|. */
 int dg_mem_head_grads(void* workspace, int M, int C, const float* mem, const float* w, int k,
                       float* dmem, float* gw, float* gb, void* stream);
 /* loss_err = F.l1_loss(IN(y1), IN(y2)) (models/models2.py:334) from the instance-norm

@@ -812,14 +812,14 @@ def test_amax(dev):
     a = K.Act(buf.to(dev), off=32, C=32)
     m = K.amax(a)
     torch.cuda.synchronize()
-    assert m.shape == (33,) and m[0].item() == 77.25
-    assert torch.equal(m[1:].cpu(), buf[..., 32:64].abs().amax(dim=(0, 1, 2)))
+    assert m.shape == (K.amax_words(32),) and m[0].item() == 77.25  # 1 + C words, a multiple of 4
+    assert torch.equal(m[1:33].cpu(), buf[..., 32:64].abs().amax(dim=(0, 1, 2)))
     full = K.amax(K.Act(buf.to(dev))).cpu()
-    assert full[0].item() == 123.5 and torch.equal(full[1:], buf.abs().amax(dim=(0, 1, 2)))
+    assert full[0].item() == 123.5 and torch.equal(full[1:97], buf.abs().amax(dim=(0, 1, 2)))
     for C in (4, 12, 896, 2048):  # chunk groups: one partial block, several rows, y-grid groups
         b = torch.randn(3, 5, 7, C, generator=g) * torch.logspace(-20, 20, C)
         m = K.amax(K.Act(b.to(dev))).cpu()
-        assert m[0].item() == b.abs().max().item() and torch.equal(m[1:], b.abs().amax(dim=(0, 1, 2))), C
+        assert m[0].item() == b.abs().max().item() and torch.equal(m[1:1 + C], b.abs().amax(dim=(0, 1, 2))), C
 
 
 # channel magnitudes of the per-channel f16 x3 test: every fifth channel of the operand at full scale,
@@ -901,8 +901,8 @@ def test_producer_channel_maxima(dev):
     dy = K.Act(to_nhwc(_chan_scaled(N, 128, H, W, g)).to(dev))
     torch.cuda.synchronize()
     ref = y.view().abs().amax(dim=(0, 1, 2))
-    assert y.amax.shape == (1 + C,)
-    assert torch.equal(y.amax[1:], ref) and y.amax[0].item() == ref.max().item()
+    assert y.amax.shape == (K.amax_words(C),)
+    assert torch.equal(y.amax[1:1 + C], ref) and y.amax[0].item() == ref.max().item()
     dw1 = torch.empty(128, C, 3, 3, device=dev)
     dw2 = torch.empty_like(dw1)
     K.conv_wgrad(y, dy, 3, 1, dw1)
@@ -916,4 +916,4 @@ def test_producer_channel_maxima(dev):
     K.bn_bwd(gz, z, torch.ones(C, device=dev), stats, K.ACT_RELU, dz, dgam, dbet)
     torch.cuda.synchronize()
     ref = dz.view().abs().amax(dim=(0, 1, 2))
-    assert torch.equal(dz.amax[1:], ref) and dz.amax[0].item() == ref.max().item()
+    assert torch.equal(dz.amax[1:1 + C], ref) and dz.amax[0].item() == ref.max().item()

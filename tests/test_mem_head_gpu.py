@@ -91,7 +91,8 @@ def test_softmax_head_kernels_match_reference(dev, nv, loss_kind, C):
     G1, G2 = gd1.reshape(M).to(dev), gd2.reshape(M).to(dev)
     GL1, GL2 = torch.empty_like(P1), torch.empty_like(P2)
     cf = torch.tensor([coef], device=dev)
-    am = torch.full((2,), -1.0, device=dev)
+    nw = K.amax_words(C)  # f32: operand maxima with channels (slots) per view, nw words each
+    am = torch.full((2 * nw,), -1.0, device=dev)
     K.call("dg_softmax_head_bwd", 0, nv, loss_kind, K.ptr(P1), K.ptr(P2) if nv == 2 else None, M, C, K.ptr(v), 1,
            K.ptr(yh1), K.ptr(yh2) if nv == 2 else None, K.ptr(G1), K.ptr(G2) if nv == 2 else None,
            K.ptr(cf) if loss_kind else None, K.ptr(GL1), K.ptr(GL2) if nv == 2 else None, K.ptr(work), K.ptr(am),
@@ -107,10 +108,13 @@ def test_softmax_head_kernels_match_reference(dev, nv, loss_kind, C):
         assert _rel(yh2.view(B, HW), ref["d2"]) < 1e-5
         assert abs(lo.item() - ref["loss"]) <= 1e-5 * abs(ref["loss"])
     assert _rel(back(GL1.cpu()), ref["gl1"]) < 1e-4
-    assert am[0].item() == GL1.abs().max().item()  # max |gL| of the pass (the logits GEMMs' f16 x3 scale)
+    # the pass's operand maxima of gL (the logits GEMMs' f16 x3 scales): tensor word, then one per slot
+    assert am[0].item() == GL1.abs().max().item()
+    assert torch.equal(am[1:1 + C], GL1.abs().amax(dim=0))
     if nv == 2:
         assert _rel(back(GL2.cpu()), ref["gl2"]) < 1e-4
-        assert am[1].item() == GL2.abs().max().item()
+        assert am[nw].item() == GL2.abs().max().item()
+        assert torch.equal(am[nw + 1:nw + 1 + C], GL2.abs().amax(dim=0))
     # dmem here is the readout's share only (the logits' share comes from the logits GEMM)
     assert _rel(dmem, ref["gmem"]) < 1e-5
     assert _rel(gw, ref["gw"]) < 1e-5

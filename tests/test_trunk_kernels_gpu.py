@@ -175,7 +175,7 @@ def test_bn_add_relu_join(dev, dtype, downsample):
     assert relerr(y.buf.float(), ref) < tol
     if dtype == torch.float32:  # the join's maxima (the next f16 x3 convs' operand bounds), exact: tensor, channels
         assert y.amax is not None and y.amax[0].item() == y.buf.abs().max().item()
-        assert torch.equal(y.amax[1:], y.buf.abs().amax(dim=(0, 1, 2)))
+        assert torch.equal(y.amax[1:1 + C], y.buf.abs().amax(dim=(0, 1, 2)))
     mask = (y.buf.float().cpu() > 0).float()
     assert torch.equal(gout.buf.float().cpu(), gg.to(dtype).float() * mask)
 
@@ -225,7 +225,7 @@ def test_instance_norm(dev, dtype, affine, act, shape):
     if dtype == torch.float32:  # max |y| and max |dx| from the apply passes, exact: tensor and channels
         for t in (y, dx):
             assert t.amax[0].item() == t.buf.abs().max().item()
-            assert torch.equal(t.amax[1:], t.buf.abs().amax(dim=(0, 1, 2)))
+            assert torch.equal(t.amax[1:1 + t.C], t.buf.abs().amax(dim=(0, 1, 2)))
 
 
 def _sw_params(C, g):

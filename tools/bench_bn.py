@@ -40,8 +40,8 @@ for dt in (torch.bfloat16, torch.float32):
         st = torch.stack([torch.zeros(C, device=dev), torch.rand(C, device=dev) + 0.5,
                           torch.rand(C, device=dev) + 0.5, torch.randn(C, device=dev) * 0.1])
         coef = torch.randn(3, C, device=dev) * 0.1
-        am = torch.zeros(1, device=dev)
-        amp = K.ptr(am) if dt == torch.float32 else None  # the f32 passes' max |out| (f16 x3 operand scale)
+        am = torch.zeros(K.amax_words(C), device=dev)  # ABI 6: [1 + C] words (rounded up to 4) for f32 outputs
+        amp = K.ptr(am) if dt == torch.float32 else None  # the f32 passes' operand maxima (f16 x3 scales)
         dtc = K.DTYPES[dt] if hasattr(K, "DTYPES") else (0 if dt == torch.float32 else 1)
         ops = {
             "bn_bwd_apply": (3, lambda: K.call("dg_bn_bwd_apply_coef", dtc, K.ptr(a), C, K.ptr(b), C, M, C,
