@@ -841,13 +841,16 @@ def _chan_err(a, ref, dim):
 
 @pytest.mark.parametrize("case", [(1, 32, 64, 128, 128, 3), (1, 24, 128, 64, 64, 3), (2, 16, 32, 128, 256, 3),
                                   (1, 16, 64, 256, 128, 1), (1, 20, 36, 64, 128, 3)])
-def test_conv_f32_h16_per_channel(dev, case):
+def test_conv_f32_h16_per_channel(dev, case, monkeypatch):
     """f16 x3 per element: channels of x and dY 1e-3 .. 1e-12 below their tensor's
     largest magnitude.  The weight gradient scales each channel of x and of dY by its own power of two,
     so every row (output channel) and column (input channel) of dW keeps f32-grade relative error; the
     forward and dgrad outputs per channel.  Bound: 2x the exact v_mfma_f32_16x16x4_f32 path's error on
     the same channel (+1e-7 against two tiny maxima), both against float64.  Shapes: the 3-tap 128 x 128
-    and 64-channel 9-tap weight gradients, the per-tap kernel (1x1, and the 3x3 W % 32 != 0 rows)."""
+    and 64-channel 9-tap weight gradients, the per-tap kernel (1x1, and the 3x3 W % 32 != 0 rows).
+    DGVCC_RSPLIT_H16=1: the Cout = 64 forward / dgrad forms that default to the bf16 x6 split run f16 x3
+    here too, so every launch is the arithmetic under test."""
+    monkeypatch.setenv("DGVCC_RSPLIT_H16", "1")
     K = _k()
     N, H, W, C, Cout, R = case
     pad = R // 2
