@@ -738,30 +738,41 @@ __global__ __launch_bounds__(256) void sw_apply_mfma(const T* __restrict__ x, lo
     const long long pp = (long long)n * HW + (ok ? p : p0);
     const T* xr = x + pp * ldx + 4 * q;
     T* yr = y + pp * ldy + 4 * q;
-#pragma unroll 4
-    for (int g = 0; g < G; ++g) {
-      float xv[4];
-      ld4(xr + g * 16, xv);
-      const f4v a = *(const f4v*)(sm + g * 256 + pr * 16 + 4 * q);
-      f4v acc = *(const f4v*)(sm + G * 256 + g * 16 + 4 * q);
+    // eight groups' loads issued before the first MFMA (one load / wait / MFMA chain / store per
+    // group otherwise); a tail batch re-reads group G - 1 and stores only the groups that exist
+    constexpr int GB = 8;
+    for (int g0 = 0; g0 < G; g0 += GB) {
+      float xv[GB][4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], xv[s], acc, 0, 0, 0);
-      float o[4];
+      for (int j = 0; j < GB; ++j) ld4(xr + min(g0 + j, G - 1) * 16, xv[j]);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (act == 1 && acc[r] < 0.f) ? 0.f : acc[r];
-      if (ok) st4(yr + g * 16, o);
+      for (int j = 0; j < GB; ++j) {
+        const int g = min(g0 + j, G - 1);
+        const f4v a = *(const f4v*)(sm + g * 256 + pr * 16 + 4 * q);
+        f4v acc = *(const f4v*)(sm + G * 256 + g * 16 + 4 * q);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], xv[j][s], acc, 0, 0, 0);
+        float o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (act == 1 && acc[r] < 0.f) ? 0.f : acc[r];
+        if (ok && g0 + j < G) st4(yr + g * 16, o);
+      }
     }
   }
 }
 
 // dx_p = K ge_p + L (x_p - mu_n) + c on the matrix cores (as sw_apply_mfma: eight MFMAs per group and
-// 16 pixels, the accumulator starting at c)
-template <typename T>
+// 16 pixels, the accumulator starting at c).  Groups go four at a time with every load of the four
+// issued before the first MFMA (one group per iteration, each group's loads waited for the previous
+// group's MFMA chain and store: 1.05 ms over the SW step's seven launches, slower than the FMA form);
+// ACT / ACC are template arguments so no branch splits the load batch.  A tail batch (G % 4) re-reads
+// group G - 1 and stores only the groups that exist.
+template <typename T, int ACT, int ACC>
 __global__ __launch_bounds__(256) void sw_bwd_apply_mfma(const T* __restrict__ gy, long long ldg, const T* __restrict__ y,
                                                          long long ldy, const T* __restrict__ x, long long ldx, int HW,
-                                                         int C, int ppb, int act, const float* __restrict__ mu,
+                                                         int C, int ppb, const float* __restrict__ mu,
                                                          const float* __restrict__ coef, T* __restrict__ dx,
-                                                         long long lddx, int accumulate) {
+                                                         long long lddx) {
   extern __shared__ __attribute__((aligned(16))) float sm[];  // [G][528]: K | L | c, then mu[C]
   const int n = blockIdx.y, G = C / SWC, tid = threadIdx.x;
   const f4v* cn = (const f4v*)(coef + (long long)n * G * 528);
@@ -770,41 +781,58 @@ __global__ __launch_bounds__(256) void sw_bwd_apply_mfma(const T* __restrict__ g
   __syncthreads();
   const int lane = tid & 63, wave = tid >> 6, pr = lane & 15, q = lane >> 4;
   const int p0 = blockIdx.x * ppb, p1 = min(HW, p0 + ppb);
+  constexpr int GB = 4;
   for (int pc = p0 + 16 * wave; pc < p1; pc += 64) {
     const int p = pc + pr;
     const bool ok = p < p1;
     const long long pp = (long long)n * HW + (ok ? p : p0);
-#pragma unroll 2
-    for (int g = 0; g < G; ++g) {
-      const int c0 = g * 16 + 4 * q;
-      float ge[4], xv[4];
-      ld4(gy + pp * ldg + c0, ge);
-      ld4(x + pp * ldx + c0, xv);
-      if (act == 1) {
-        float yv[4];
-        ld4(y + pp * ldy + c0, yv);
+    const T* gr = gy + pp * ldg + 4 * q;
+    const T* xr = x + pp * ldx + 4 * q;
+    const T* yr = y + pp * ldy + 4 * q;
+    T* dr = dx + pp * lddx + 4 * q;
+    for (int g0 = 0; g0 < G; g0 += GB) {
+      float ge[GB][4], xv[GB][4], yv[GB][4], od[GB][4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) ge[s] = yv[s] > 0.f ? ge[s] : 0.f;
+      for (int j = 0; j < GB; ++j) {
+        const int c0 = min(g0 + j, G - 1) * 16;
+        ld4(gr + c0, ge[j]);
+        ld4(xr + c0, xv[j]);
+        if (ACT) ld4(yr + c0, yv[j]);
+        if (ACC) ld4(dr + c0, od[j]);
       }
-      const float* Mg = sm + g * 528;
-      const f4v mv = *(const f4v*)(sm + G * 528 + c0);
-      const f4v ka = *(const f4v*)(Mg + pr * 16 + 4 * q);
-      const f4v la = *(const f4v*)(Mg + 256 + pr * 16 + 4 * q);
-      f4v acc = *(const f4v*)(Mg + 512 + 4 * q);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], ge[s], acc, 0, 0, 0);
+      for (int j = 0; j < GB; ++j) {
+        const int g = min(g0 + j, G - 1);
+        const float* Mg = sm + g * 528;
+        const f4v mv = *(const f4v*)(sm + G * 528 + g * 16 + 4 * q);
+        const f4v ka = *(const f4v*)(Mg + pr * 16 + 4 * q);
+        const f4v la = *(const f4v*)(Mg + 256 + pr * 16 + 4 * q);
+        f4v acc = *(const f4v*)(Mg + 512 + 4 * q);
 #pragma unroll
-      for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(la[s], xv[s] - mv[s], acc, 0, 0, 0);
-      float o[4] = {acc[0], acc[1], acc[2], acc[3]};
-      if (accumulate) {
-        float od[4];
-        ld4(dx + pp * lddx + c0, od);
+        for (int s = 0; s < 4; ++s) {
+          const float gs = ACT ? (yv[j][s] > 0.f ? ge[j][s] : 0.f) : ge[j][s];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ka[s], gs, acc, 0, 0, 0);
+        }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] += od[r];
+        for (int s = 0; s < 4; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(la[s], xv[j][s] - mv[s], acc, 0, 0, 0);
+        float o[4] = {acc[0], acc[1], acc[2], acc[3]};
+        if (ACC) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] += od[j][r];
+        }
+        if (ok && g0 + j < G) st4(dr + g * 16, o);
       }
-      if (ok) st4(dx + pp * lddx + c0, o);
     }
   }
+}
+
+template <typename T>
+void launch_sw_bwd_apply_mfma(dim3 grid, size_t lds, hipStream_t st, const T* gy, long long ldg, const T* y,
+                              long long ldy, const T* x, long long ldx, int HW, int C, int ppb, int act,
+                              const float* mu, const float* coef, T* dx, long long lddx, int accumulate) {
+  auto k = act == 1 ? (accumulate ? sw_bwd_apply_mfma<T, 1, 1> : sw_bwd_apply_mfma<T, 1, 0>)
+                    : (accumulate ? sw_bwd_apply_mfma<T, 0, 1> : sw_bwd_apply_mfma<T, 0, 0>);
+  hipLaunchKernelGGL(k, grid, dim3(256), lds, st, gy, ldg, y, ldy, x, ldx, HW, C, ppb, mu, coef, dx, lddx);
 }
 
 // blocks per instance of the MFMA apply passes: ~1024 blocks over the batch, 64 .. 2048 pixels each
@@ -1061,17 +1089,16 @@ extern "C" int dg_sw_bwd_finish(int dtype, const void* gy, int64_t ldg, const vo
     const int mnb = sw_apply_nb(HW, N);
     const int mppb = dg_cdiv(HW, mnb);
     const size_t mlds = (size_t)(G * 528 + C) * 4;
+    const dim3 mg(mnb, N);
     if (dtype == DG_BF16)
-      hipLaunchKernelGGL(sw_bwd_apply_mfma<bf16>, dim3(mnb, N), dim3(256), mlds, st, (const bf16*)gy, ldg,
-                         (const bf16*)y, ldy, (const bf16*)x, ldx, HW, C, mppb, act, mu, coef, (bf16*)dx, lddx,
-                         accumulate);
+      launch_sw_bwd_apply_mfma<bf16>(mg, mlds, st, (const bf16*)gy, ldg, (const bf16*)y, ldy, (const bf16*)x, ldx, HW,
+                                     C, mppb, act, mu, coef, (bf16*)dx, lddx, accumulate);
     else if (dtype == DG_F16)
-      hipLaunchKernelGGL(sw_bwd_apply_mfma<f16>, dim3(mnb, N), dim3(256), mlds, st, (const f16*)gy, ldg, (const f16*)y,
-                         ldy, (const f16*)x, ldx, HW, C, mppb, act, mu, coef, (f16*)dx, lddx, accumulate);
+      launch_sw_bwd_apply_mfma<f16>(mg, mlds, st, (const f16*)gy, ldg, (const f16*)y, ldy, (const f16*)x, ldx, HW, C,
+                                    mppb, act, mu, coef, (f16*)dx, lddx, accumulate);
     else
-      hipLaunchKernelGGL(sw_bwd_apply_mfma<float>, dim3(mnb, N), dim3(256), mlds, st, (const float*)gy, ldg,
-                         (const float*)y, ldy, (const float*)x, ldx, HW, C, mppb, act, mu, coef, (float*)dx, lddx,
-                         accumulate);
+      launch_sw_bwd_apply_mfma<float>(mg, mlds, st, (const float*)gy, ldg, (const float*)y, ldy, (const float*)x, ldx,
+                                      HW, C, mppb, act, mu, coef, (float*)dx, lddx, accumulate);
     DG_CHECK_LAUNCH();
     return DG_OK;
   }
