@@ -4,6 +4,7 @@
 // wider buffer (the decoder's concatenations) is addressed in place.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 #include <type_traits>
 #include "../../include/dgvcc.h"
@@ -398,6 +399,21 @@ __device__ __forceinline__ void block_camax_commit(const float (&m)[V], int c0, 
   }
   block_amax_commit(t, out);
 }
+// Block size of the f32 channel-stationary passes that fold per-channel maxima: 1024 threads, a
+// quarter as many blocks as their 256-thread grids.  Every block folds its C channel words at its
+// end and the blocks of a launch end together, so a launch issues ~blocks x C global atomics there:
+// 1024 x 64 added 20-25 us to a 70-us BN apply on the 786432 x 64 shape, and the pooled and
+// InstanceNorm passes' up-to-8192/16384-block grids paid more (tools/bench_bn.py,
+// profiles/round6d/bn_wide.txt).  DGVCC_EW_NT=256 (read per launch): the 256-thread grids.  The
+// 16-bit passes (one word per block) measured no different in the wide form (profiles/round6d:
+// bf16 step 105.2 vs 105.1 ms) and keep 256 threads.
+constexpr int DG_EW_WIDE = 1024;
+inline bool dg_ew_wide(const float* amax, bool f32) {
+  if (!amax || !f32) return false;
+  const char* e = getenv("DGVCC_EW_NT");
+  return !(e && e[0] == '2');
+}
+
 // A producer's running operand maxima (out_amax_commit's input): per channel for f32 outputs (the only
 // ones an f16 x3 conv reads), one register for 16-bit ones, whose buffer holds the tensor's word alone
 template <typename T, int V>

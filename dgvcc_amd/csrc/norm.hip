@@ -142,23 +142,21 @@ __device__ __forceinline__ void ld_chan_row(const float* r, int c0, float dflt, 
 
 // The grid stride (gridDim*NT) is a multiple of tpp = C/V (a power of two <= NT),
 // so each thread keeps one channel chunk: per-channel parameters live in registers.
-template <typename T>
-__global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, long long ldz, int M, int C,
+template <typename T, int U, int NTB = NT>
+__global__ __launch_bounds__(NTB) void bn_apply_kernel(const T* __restrict__ z, long long ldz, int M, int C,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
                                                       int act, const float* __restrict__ drop, int HW,
                                                       T* __restrict__ y, long long ldy, float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const long long gt = blockIdx.x * (long long)NTB + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
-  const long long pstride = (long long)gridDim.x * NT / tpp;
+  const long long pstride = (long long)gridDim.x * NTB / tpp;
   float sc[V], sf[V];
   ld_chan_row<V>(scale, c0, 1.f, sc);
   ld_chan_row<V>(shift, c0, 0.f, sf);
   OutMax<T, V> m;  // max |y| per channel (amax: the f16 x3 convs' operand scales)
-  for (long long p = gt / tpp; p < M; p += pstride) {
-    float v[V];
-    ldv(z + p * ldz + c0, v);
+  auto apply = [&](long long p, float (&v)[V]) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
       float t = fmaf(v[e], sc[e], sf[e]);
@@ -173,6 +171,22 @@ __global__ __launch_bounds__(NT) void bn_apply_kernel(const T* __restrict__ z, l
     stv(y + p * ldy + c0, v);
 #pragma unroll
     for (int e = 0; e < V; ++e) m.add(e, v[e]);
+  };
+  long long p = gt / tpp;
+  // U pixels per trip, every load issued before the first use (DGVCC_EW_UNROLL)
+  for (; p + (U - 1) * pstride < M; p += U * pstride) {
+    float v[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ldv(z + (p + u * pstride) * ldz + c0, v[u]);
+#pragma unroll
+    for (int u = 0; u < U; ++u) apply(p + u * pstride, v[u]);
+  }
+  if constexpr (U > 1) {
+    for (; p < M; p += pstride) {
+      float v[V];
+      ldv(z + p * ldz + c0, v);
+      apply(p, v);
+    }
   }
   if (amax) m.commit(c0, C, amax);
 }
@@ -235,10 +249,12 @@ __device__ __forceinline__ void bn_bwd_load(const T* g, long long ldg, const T* 
 
 // DGVCC_EW_UNROLL=2: the channel-stationary elementwise passes handle two pixels per loop trip
 // with all four loads issued before the first use; 1 (default): one pixel per trip
-// (tools/bench_bn.py: two per trip is 2-7% slower at 94 VGPRs / 5 waves)
+// (tools/bench_bn.py: two per trip is 2-7% slower at 94 VGPRs / 5 waves).  4 (BN apply only) and 2
+// re-measured on the 1024-block grids in round 6 (profiles/round6d/bn_unroll.txt): still slower on
+// every shape (f32 786432 x 256 BN apply 0.303 / 0.327 / 0.366 ms at 1 / 2 / 4)
 inline int ew_unroll() {  // read per launch: same-process A/B (tools/bench_bn.py)
   const char* e = getenv("DGVCC_EW_UNROLL");
-  return e && e[0] == '2' ? 2 : 1;
+  return e && e[0] == '2' ? 2 : e && e[0] == '4' ? 4 : 1;
 }
 
 template <typename T>
@@ -401,8 +417,8 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_sync(const float* __restri
   coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
 }
 
-template <typename T, int U = 1>
-__global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
+template <typename T, int U = 1, int NTB = NT>
+__global__ __launch_bounds__(NTB, NTB == NT && sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
                                                    long long ldz, int M, int C, const float* mean, const float* invstd,
                                                    const float* scale, const float* shift, int act, const float* drop,
                                                    int HW, const float* __restrict__ coef, T* __restrict__ dz,
@@ -410,9 +426,9 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_
   constexpr int V = 16 / (int)sizeof(T);
   OutMax<T, V> m;  // max |dz| per channel (amax)
   const int tpp = C / V;
-  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const long long gt = blockIdx.x * (long long)NTB + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
-  const long long pstride = (long long)gridDim.x * NT / tpp;
+  const long long pstride = (long long)gridDim.x * NTB / tpp;
   ChanParams<V> cp;
   cp.load(c0, scale, shift, mean, invstd);
   float k1[V], k2[V], k3[V];
@@ -529,8 +545,8 @@ __device__ __forceinline__ int first_max4(float a, float b, float c, float d) {
   return k;
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__ z, long long ldz, int H, int W,
+template <typename T, int NTB = NT>
+__global__ __launch_bounds__(NTB) void bn_apply_pool_kernel(const T* __restrict__ z, long long ldz, int H, int W,
                                                            long long Mp, int C, const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int act,
                                                            const float* __restrict__ drop, int HW, T* __restrict__ y,
@@ -539,9 +555,9 @@ __global__ __launch_bounds__(NT) void bn_apply_pool_kernel(const T* __restrict__
   constexpr int V = 16 / (int)sizeof(T);
   OutMax<T, V> m;  // max |y| per channel over the window values (>= max |yp|: amax of both)
   const int tpp = C / V;
-  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const long long gt = blockIdx.x * (long long)NTB + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
-  const long long pstride = (long long)gridDim.x * NT / tpp;
+  const long long pstride = (long long)gridDim.x * NTB / tpp;
   float sc[V], sf[V];
   ld_chan_row<V>(scale, c0, 1.f, sc);
   ld_chan_row<V>(shift, c0, 0.f, sf);
@@ -681,8 +697,8 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp, long long ldgp,
+template <typename T, int NTB = NT>
+__global__ __launch_bounds__(NTB) void bn_pool_bwd_apply(const T* __restrict__ gp, long long ldgp,
                                                         const T* __restrict__ gd, long long ldgd,
                                                         const T* __restrict__ z, long long ldz, int H, int W,
                                                         long long Mp, int C, const float* mean, const float* invstd,
@@ -692,9 +708,9 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_apply(const T* __restrict__ gp
   constexpr int V = POOL_V;
   OutMax<T, V> m;  // max |dz| per channel
   const int tpp = C / V;
-  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const long long gt = blockIdx.x * (long long)NTB + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
-  const long long pstride = (long long)gridDim.x * NT / tpp;
+  const long long pstride = (long long)gridDim.x * NTB / tpp;
   ChanParams<V> cp;
   cp.load(c0, scale, shift, mean, invstd);
   float k1[V], k2[V], k3[V];
@@ -739,6 +755,12 @@ inline int cs_grid(long long n) {
   return (int)std::min<long long>(g, 1024);
 }
 
+constexpr int EW_WIDE = DG_EW_WIDE;
+inline bool ew_wide(const float* amax, bool f32) { return dg_ew_wide(amax, f32); }
+inline int wide_grid(long long n, int cap) {
+  return (int)std::max<long long>(1, std::min<long long>((n + EW_WIDE - 1) / EW_WIDE, cap));
+}
+
 template <typename T>
 int bn_fwd_impl(const void* z, long long ldz, int M, int C, const float* gamma, const float* beta, float* rm, float* rv,
                 float momentum, float eps, float* smean, float* sinv, float* scale, float* shift, void* ws,
@@ -775,8 +797,12 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
   if (!dz) return DG_OK;  // coefficients only (a fused consumer applies them)
   { const int zr = zero_amax(amax, sizeof(T) == 4, C, st); if (zr != DG_OK) return zr; }
   const long long total = (long long)M * (C / (16 / (int)sizeof(T)));
-  hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<T, 2> : bn_bwd_apply<T, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
-                     mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
+  if (ew_wide(amax, sizeof(T) == 4))
+    hipLaunchKernelGGL((bn_bwd_apply<T, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st, (const T*)g, ldg,
+                       (const T*)z, ldz, M, C, mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
+  else
+    hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<T, 2> : bn_bwd_apply<T, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
+                       mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -819,13 +845,16 @@ extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, 
   { const int zr = zero_amax(amax, dtype == DG_F32, C, st); if (zr != DG_OK) return zr; }
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
-    hipLaunchKernelGGL(bn_apply_kernel<bf16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
+    hipLaunchKernelGGL((ew_unroll() == 4 ? bn_apply_kernel<bf16, 4> : ew_unroll() == 2 ? bn_apply_kernel<bf16, 2> : bn_apply_kernel<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
                        shift, act, drop, HW, (bf16*)y, ldy, amax);
   else if (dtype == DG_F16)
-    hipLaunchKernelGGL(bn_apply_kernel<f16>, dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
+    hipLaunchKernelGGL((ew_unroll() == 4 ? bn_apply_kernel<f16, 4> : ew_unroll() == 2 ? bn_apply_kernel<f16, 2> : bn_apply_kernel<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
                        shift, act, drop, HW, (f16*)y, ldy, amax);
+  else if (ew_wide(amax, true))
+    hipLaunchKernelGGL((bn_apply_kernel<float, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st,
+                       (const float*)z, ldz, M, C, scale, shift, act, drop, HW, (float*)y, ldy, amax);
   else
-    hipLaunchKernelGGL(bn_apply_kernel<float>, dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
+    hipLaunchKernelGGL((ew_unroll() == 4 ? bn_apply_kernel<float, 4> : ew_unroll() == 2 ? bn_apply_kernel<float, 2> : bn_apply_kernel<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
                        scale, shift, act, drop, HW, (float*)y, ldy, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -873,6 +902,11 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax);
+  } else if (ew_wide(amax, true)) {
+    const long long total = (long long)M * (C / 4);
+    hipLaunchKernelGGL((bn_bwd_apply<float, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st,
+                       (const float*)g, ldg, (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act,
+                       drop, HW, coef, (float*)dz, lddz, amax);
   } else {
     const long long total = (long long)M * (C / 4);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
@@ -931,6 +965,10 @@ extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, in
   else if (dtype == DG_F16)
     hipLaunchKernelGGL(bn_apply_pool_kernel<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, H, W,
                        Mp, C, scale, shift, act, drop, H * W, (f16*)y, ldy, (f16*)yp, ldyp, amax);
+  else if (ew_wide(amax, true))
+    hipLaunchKernelGGL((bn_apply_pool_kernel<float, EW_WIDE>), dim3(wide_grid(total, 512)), dim3(EW_WIDE), 0, st,
+                       (const float*)z, ldz, H, W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp,
+                       ldyp, amax);
   else
     hipLaunchKernelGGL(bn_apply_pool_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, H,
                        W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp, amax);
@@ -957,9 +995,14 @@ static int bn_pool_bwd_impl(const void* gp, long long ldgp, const void* gd, long
   DG_CHECK_LAUNCH();
   const long long total = Mp * (C / POOL_V);
   { const int zr = zero_amax(amax, sizeof(T) == 4, C, st); if (zr != DG_OK) return zr; }
-  hipLaunchKernelGGL(bn_pool_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd,
-                     ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop, H * W, coef, (T*)dz,
-                     lddz, amax);
+  if (ew_wide(amax, sizeof(T) == 4))
+    hipLaunchKernelGGL((bn_pool_bwd_apply<T, EW_WIDE>), dim3(wide_grid(total, 512)), dim3(EW_WIDE), 0, st, (const T*)gp,
+                       ldgp, (const T*)gd, ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop,
+                       H * W, coef, (T*)dz, lddz, amax);
+  else
+    hipLaunchKernelGGL(bn_pool_bwd_apply<T>, dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gp, ldgp, (const T*)gd,
+                       ldgd, (const T*)z, ldz, H, W, Mp, C, mean, inv, scale, shift, act, drop, H * W, coef, (T*)dz,
+                       lddz, amax);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -1109,6 +1152,10 @@ extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const
   else if (dtype == DG_F16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
                        ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax);
+  else if (ew_wide(amax, true))
+    hipLaunchKernelGGL((bn_bwd_apply<float, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st,
+                       (const float*)g, ldg, (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act,
+                       drop, HW, coef, (float*)dz, lddz, amax);
   else
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
@@ -1140,6 +1187,10 @@ extern "C" int dg_bn_bwd_pool_apply_coef(int dtype, const void* gp, int64_t ldgp
     hipLaunchKernelGGL(bn_pool_bwd_apply<f16>, dim3(ew_grid(total)), dim3(NT), 0, st, (const f16*)gp, ldgp,
                        (const f16*)gd, ldgd, (const f16*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift,
                        act, drop, H * W, coef, (f16*)dz, lddz, amax);
+  else if (ew_wide(amax, true))
+    hipLaunchKernelGGL((bn_pool_bwd_apply<float, EW_WIDE>), dim3(wide_grid(total, 512)), dim3(EW_WIDE), 0, st,
+                       (const float*)gp, ldgp, (const float*)gd, ldgd, (const float*)z, ldz, H, W, Mp, C, save_mean,
+                       save_invstd, scale, shift, act, drop, H * W, coef, (float*)dz, lddz, amax);
   else
     hipLaunchKernelGGL(bn_pool_bwd_apply<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)gp, ldgp,
                        (const float*)gd, ldgd, (const float*)z, ldz, H, W, Mp, C, save_mean, save_invstd, scale,

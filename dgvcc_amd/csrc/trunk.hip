@@ -35,17 +35,17 @@ inline int ew_unroll() {
 
 // y = act(z1*s1 + b1 + (s2 ? z2*s2 + b2 : z2)); amax (may be NULL): max |y| (the next f16 x3 convs'
 // operand scales: per channel for f32, dg_common.h OutMax; zeroed by the launcher)
-template <typename T, int U = 1>
-__global__ __launch_bounds__(NT) void bn_add_kernel(const T* __restrict__ z1, long long ld1, int M, int C,
+template <typename T, int U = 1, int NTB = NT>
+__global__ __launch_bounds__(NTB) void bn_add_kernel(const T* __restrict__ z1, long long ld1, int M, int C,
                                                     const float* __restrict__ s1, const float* __restrict__ b1,
                                                     const T* __restrict__ z2, long long ld2,
                                                     const float* __restrict__ s2, const float* __restrict__ b2, int act,
                                                     T* __restrict__ y, long long ldy, float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const long long gt = blockIdx.x * (long long)NT + threadIdx.x;
+  const long long gt = blockIdx.x * (long long)NTB + threadIdx.x;
   const int c0 = (int)(gt % tpp) * V;
-  const long long pstride = (long long)gridDim.x * NT / tpp;
+  const long long pstride = (long long)gridDim.x * NTB / tpp;
   float a1[V], c1[V], a2[V], c2[V];
   OutMax<T, V> mx;
 #pragma unroll
@@ -144,26 +144,27 @@ __global__ __launch_bounds__(NT) void relu_bwd_kernel(const T* __restrict__ g, l
 // Grid for the channel-stationary elementwise kernels below: gridDim.x * NT is a multiple of
 // tpp = C/V, so every thread keeps one channel chunk c0 for its whole pixel loop and holds
 // that chunk's per-(n, c) parameters in registers, reloading them only when n changes.
-inline int cs_grid(long long total, int tpp) {
-  int q = tpp, a = NT;  // q = tpp / gcd(tpp, NT)
+inline int cs_grid(long long total, int tpp, int nt = NT) {
+  int q = tpp, a = nt;  // q = tpp / gcd(tpp, nt)
   while (a) { const int t = q % a; q = a; a = t; }
   q = tpp / q;
-  const int g = ew_grid(total);
+  // the 1024-thread form (dg_ew_wide): at most 512 blocks
+  const int g = nt == NT ? ew_grid(total) : (int)std::max<long long>(1, std::min<long long>((total + nt - 1) / nt, 512));
   return (g + q - 1) / q * q;
 }
 
 // y = act((x - mu[n,c]) * is[n,c] * gamma[c] + beta[c]); amax (may be NULL): max |y|, as bn_add_kernel
-template <typename T>
-__global__ __launch_bounds__(NT) void in_apply_kernel(const T* __restrict__ x, long long ldx, int N, int HW, int C,
+template <typename T, int NTB = NT>
+__global__ __launch_bounds__(NTB) void in_apply_kernel(const T* __restrict__ x, long long ldx, int N, int HW, int C,
                                                       const float* __restrict__ mu, const float* __restrict__ is,
                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
                                                       int act, T* __restrict__ y, long long ldy,
                                                       float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const int gt = blockIdx.x * NT + threadIdx.x;
+  const int gt = blockIdx.x * NTB + threadIdx.x;
   const int c0 = (gt % tpp) * V;
-  const int pstride = gridDim.x * NT / tpp;
+  const int pstride = gridDim.x * NTB / tpp;
   const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
   float ga[V], be[V], m[V], s[V];
 #pragma unroll
@@ -284,17 +285,17 @@ __global__ __launch_bounds__(FIN_CH * FIN_KS) void in_bwd_finalize(const float* 
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void in_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ x,
+template <typename T, int NTB = NT>
+__global__ __launch_bounds__(NTB) void in_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ x,
                                                    long long ldx, int N, int HW, int C, const float* __restrict__ mu,
                                                    const float* __restrict__ is, const float* __restrict__ coef,
                                                    T* __restrict__ dx, long long lddx, int accumulate,
                                                    float* __restrict__ amax) {
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
-  const int gt = blockIdx.x * NT + threadIdx.x;
+  const int gt = blockIdx.x * NTB + threadIdx.x;
   const int c0 = (gt % tpp) * V;
-  const int pstride = gridDim.x * NT / tpp;
+  const int pstride = gridDim.x * NTB / tpp;
   const int M = N * HW;  // M * tpp < 2^30 (checked by the ABI)
   float m[V], s[V], k1[V], k2[V], k3[V];
   OutMax<T, V> mx;  // max |dx| per channel (amax, may be NULL: the following f16 x3 wgrad's operand scales)
@@ -350,6 +351,11 @@ extern "C" int dg_bn_add_apply(int dtype, const void* z1, int64_t ld1, int M, in
   else if (dtype == DG_F16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_add_kernel<f16, 2> : bn_add_kernel<f16, 1>), dim3(cs_grid_add(total)), dim3(NT), 0, st, (const f16*)z1, ld1, M, C, scale1,
                        shift1, (const f16*)z2, ld2, scale2, shift2, act, (f16*)y, ldy, amax);
+  else if (dg_ew_wide(amax, true))
+    hipLaunchKernelGGL((bn_add_kernel<float, 1, DG_EW_WIDE>),
+                       dim3(std::max<long long>(1, std::min<long long>((total + DG_EW_WIDE - 1) / DG_EW_WIDE, 256))),
+                       dim3(DG_EW_WIDE), 0, st, (const float*)z1, ld1, M, C, scale1, shift1, (const float*)z2, ld2,
+                       scale2, shift2, act, (float*)y, ldy, amax);
   else
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_add_kernel<float, 2> : bn_add_kernel<float, 1>), dim3(cs_grid_add(total)), dim3(NT), 0, st, (const float*)z1, ld1, M, C,
                        scale1, shift1, (const float*)z2, ld2, scale2, shift2, act, (float*)y, ldy, amax);
@@ -395,6 +401,9 @@ extern "C" int dg_instnorm_apply(int dtype, const void* x, int64_t ldx, int N, i
   else if (dtype == DG_F16)
     hipLaunchKernelGGL(in_apply_kernel<f16>, dim3(grid), dim3(NT), 0, st, (const f16*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (f16*)y, ldy, amax);
+  else if (dg_ew_wide(amax, true))
+    hipLaunchKernelGGL((in_apply_kernel<float, DG_EW_WIDE>), dim3(cs_grid(total, C / V, DG_EW_WIDE)), dim3(DG_EW_WIDE),
+                       0, st, (const float*)x, ldx, N, HW, C, mean, invstd, gamma, beta, act, (float*)y, ldy, amax);
   else
     hipLaunchKernelGGL(in_apply_kernel<float>, dim3(grid), dim3(NT), 0, st, (const float*)x, ldx, N, HW, C,
                        mean, invstd, gamma, beta, act, (float*)y, ldy, amax);
@@ -449,8 +458,13 @@ extern "C" int dg_instnorm_bwd(int dtype, const void* g, int64_t ldg, const void
     DG_CHECK_LAUNCH();
     hipLaunchKernelGGL(in_bwd_finalize, fgrid, fblk, 0, st, part, N, nb, HW, C, invstd, gamma, dgamma, dbeta, coef);
     DG_CHECK_LAUNCH();
-    hipLaunchKernelGGL(in_bwd_apply<float>, dim3(grid), dim3(NT), 0, st, (const float*)g, ldg,
-                       (const float*)x, ldx, N, HW, C, mean, invstd, coef, (float*)dx, lddx, accumulate, amax);
+    if (dg_ew_wide(amax, true))
+      hipLaunchKernelGGL((in_bwd_apply<float, DG_EW_WIDE>), dim3(cs_grid(total, C / V, DG_EW_WIDE)),
+                         dim3(DG_EW_WIDE), 0, st, (const float*)g, ldg, (const float*)x, ldx, N, HW, C, mean, invstd,
+                         coef, (float*)dx, lddx, accumulate, amax);
+    else
+      hipLaunchKernelGGL(in_bwd_apply<float>, dim3(grid), dim3(NT), 0, st, (const float*)g, ldg,
+                         (const float*)x, ldx, N, HW, C, mean, invstd, coef, (float*)dx, lddx, accumulate, amax);
   }
   DG_CHECK_LAUNCH();
   return DG_OK;

@@ -920,3 +920,58 @@ def test_producer_channel_maxima(dev):
     torch.cuda.synchronize()
     ref = dz.view().abs().amax(dim=(0, 1, 2))
     assert torch.equal(dz.amax[1:1 + C], ref) and dz.amax[0].item() == ref.max().item()
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 38, 54, 64), (3, 10, 14, 512)])
+def test_wide_maxima_passes(dev, monkeypatch, N, H, W, C):
+    """The f32 passes that fold per-channel operand maxima run 1024-thread blocks (a quarter of the
+    256-thread grids' atomics, dg_common.h DG_EW_WIDE); DGVCC_EW_NT=256 keeps the 256-thread grids.
+    Both forms write bit-identical outputs and maxima: BN apply / backward, pooled apply / backward,
+    the residual join, InstanceNorm apply / backward (ragged pixel counts, 64 and 512 channels)."""
+    K = _k()
+    g = torch.Generator().manual_seed(21)
+
+    def t(*shape):
+        return to_nhwc(torch.randn(*shape, generator=g) * 2).to(dev)
+
+    z, z2, gz = t(N, C, H, W), t(N, C, H, W), t(N, C, H, W)
+    gp = t(N, C, H // 2, W // 2)
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = torch.randn(C, generator=g).to(dev)
+    zd = K.Act(z)
+    stats = K.bn_fwd_train(zd, gam, bet, torch.zeros(C, device=dev), torch.ones(C, device=dev), 0.1, 1e-5)
+    st2 = torch.randn(4, C, generator=g).to(dev)
+
+    def run():
+        y = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.bn_apply(zd, stats, 1, y)
+        dz = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.bn_bwd(K.Act(gz), zd, gam, stats, 1, dz, torch.empty(C, device=dev), torch.empty(C, device=dev))
+        yq = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        yp = K.Act(K.nhwc(N, H // 2, W // 2, C, torch.float32, dev))
+        K.bn_apply_pool(zd, stats, 1, yq, yp)
+        dzp = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.bn_bwd_pool(K.Act(gp), K.Act(gz), zd, gam, stats, 1, dzp, torch.empty(C, device=dev),
+                      torch.empty(C, device=dev))
+        ya = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.bn_add_apply(zd, st2, K.Act(z2), st2, 1, ya)
+        ist = K.instnorm_stats(zd, 1e-5)
+        yi = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.instnorm_apply(zd, ist, gam, bet, 0, yi)
+        dxi = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        K.instnorm_bwd(K.Act(gz), zd, ist, gam, dxi)
+        outs = []
+        for a in (y, dz, yq, dzp, ya, yi, dxi):
+            outs += [a.buf.clone(), a.amax.clone()]
+        torch.cuda.synchronize()
+        return outs
+
+    wide = run()
+    monkeypatch.setenv("DGVCC_EW_NT", "256")
+    narrow = run()
+    for k, (a, b) in enumerate(zip(wide, narrow)):
+        assert torch.equal(a, b), k
+    # the maxima are the written tensors' own
+    for k in range(0, len(wide), 2):
+        ref = wide[k].reshape(-1, C).abs().amax(dim=0)
+        assert torch.equal(wide[k + 1][1:1 + C], ref) and wide[k + 1][0].item() == ref.max().item(), k
