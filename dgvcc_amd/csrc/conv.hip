@@ -1395,6 +1395,14 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
   // as the f32 rows, so the DMA is unchanged and the prologue reads the two parts' chunks fc and 4 + fc
   // instead of splitting (the split was 28% of the kernel: SCH 7).  Bit-identical to SCH 0.
   static_assert(SCH != 8 || HM, "SCH 8: the f16 x3 kernels");
+  // SCH 9 (TALL, HM): the split once per block instead of once per wave.  The two waves of a pixel group
+  // (its two 128-channel halves) split the same B fragments under SCH 0; here each converts half of the
+  // group's stage rows in place into the SCH 8 image (hi chunks 0-3, lo chunks 4-7 of the 128-B row:
+  // every lane reads its row's two f32 chunks, the four lanes of a row in one instruction, before any
+  // writes) and, after a second barrier, the K-step reads the parts as SCH 8 does.  Half the split VALU
+  // per wave for an LDS round trip of the stage's B bytes and one barrier; bit-identical to SCH 0.
+  static_assert(SCH != 9 || (TALL && HM && !STAMP), "SCH 9: the TALL f16 x3 kernel");
+  constexpr bool PRE = SCH == 8 || SCH == 9;  // the K-step reads the pre-split image
   constexpr bool RSTG = SCH == 5;
   constexpr int NPL = HM ? 2 : 3;  // filter planes
   constexpr int KB = NPL * 64;     // bytes per (output channel, 32-deep k-block) of the planes
@@ -1749,11 +1757,35 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       }
       const char* As = smem + (gs % STG) * STAGE;
       const char* Bs = As + A_BYTES;
+      if constexpr (SCH == 9) {  // this wave's half of its pixel group's rows into the SCH 8 image, in place
+        char* Bw = smem + (gs % STG) * STAGE + A_BYTES;
+        constexpr int ROWS = PSB / NPXG / NCOG;  // 32 rows: 4 lanes (8-channel groups) per row
+        constexpr int NIT = ROWS * 4 / 64;
+        const int r0 = wpx + ROWS * (wid / NPXG) + (lane >> 2), cj = lane & 3;
+        u4v c0[NIT], c1[NIT];
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          c0[k] = *(const u4v*)(Bw + swzb(r0 + 16 * k, 2 * cj));
+          c1[k] = *(const u4v*)(Bw + swzb(r0 + 16 * k, 2 * cj + 1));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < NIT; ++k) {
+          s8v hi, lo;
+          split2h_8(c0[k], c1[k], hsx, hi, lo);
+          *(s8v*)(Bw + swzb(r0 + 16 * k, cj)) = hi;
+          *(s8v*)(Bw + swzb(r0 + 16 * k, 4 + cj)) = lo;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
       u4v b0[TJ], b1[TJ];
 #pragma unroll
-      for (int j = 0; j < TJ; ++j) {  // SCH 8: the hi / lo chunks of the pre-split rows, else two f32 chunks
-        b0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, SCH == 8 ? fc : 2 * fc));
-        b1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, SCH == 8 ? 4 + fc : 2 * fc + 1));
+      for (int j = 0; j < TJ; ++j) {  // SCH 8 / 9: the hi / lo chunks of the pre-split rows, else two f32 chunks
+        b0[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, PRE ? fc : 2 * fc));
+        b1[j] = *(const u4v*)(Bs + swzb(wpx + 16 * j + fr, PRE ? 4 + fc : 2 * fc + 1));
       }
       auto aread = [&](int i, s8v (&ah)[NPL]) __attribute__((always_inline)) {
         const int row = wco + 16 * i + fr;
@@ -1803,7 +1835,7 @@ __global__ __launch_bounds__(512, 1) void conv_fwd_psplit_kernel(FwdArgs a, cons
       s8v bh[TJ][NPL];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        if constexpr (SCH == 7 || SCH == 8) {  // 8: the parts as stored; 7 (diagnostic): the raw f32 rows
+        if constexpr (SCH == 7 || PRE) {  // 8 / 9: the parts as stored; 7 (diagnostic): the raw f32 rows
           bh[j][0] = __builtin_bit_cast(s8v, b0[j]);
           bh[j][1] = __builtin_bit_cast(s8v, b1[j]);
         } else if constexpr (HM) split2h_8(b0[j], b1[j], hsx, bh[j][0], bh[j][1]);
@@ -3555,11 +3587,13 @@ static const unsigned short* presplit(const FwdArgs& a, hipStream_t st) {
                      st, (const float*)a.w, nw, wsp);
   return wsp;
 }
-// DGVCC_PSPLIT_SCH=0|1|2 (read per launch: A/B): schedule of the f16 x3 256-pixel pre-split forward
-// (conv_fwd_psplit_kernel SCH)
+// DGVCC_PSPLIT_SCH=0..9 (read per launch: A/B): schedule of the f16 x3 256-pixel pre-split forward
+// (conv_fwd_psplit_kernel SCH) where the pixel operand is not pre-split by its own pass; default 9 (the
+// split once per block in LDS: 256->256 at 192x256 2.444 -> 2.397 ms, 512->256 dgrad 4.945 -> 4.871,
+// bit-identical; profiles/round6e/ab_sch.txt)
 static int psplit_sch() {
   const char* e = getenv("DGVCC_PSPLIT_SCH");
-  return e ? e[0] - '0' : 0;
+  return e ? e[0] - '0' : 9;
 }
 // test hook: the diagnostic stamp buffer (dg_debug_stamps)
 static unsigned long long* g_stamps = nullptr;
@@ -3911,7 +3945,8 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
           hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 8>), dim3(g2), dim3(512), 0, st, ap, wspc);
         } else if (h16 && tall) {
           const int sch = psplit_sch();
-          if (sch == 6) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 6>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          if (sch == 9) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 9>), dim3(g2), dim3(512), 0, st, ap, wspc);
+          else if (sch == 6) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 6>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 7) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 7>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 5 && a.R * a.S * (a.C / 32) >= 2) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 5>), dim3(g2), dim3(512), 0, st, ap, wspc);
           else if (sch == 4) hipLaunchKernelGGL((conv_fwd_psplit_kernel<256, 2, 0, 1, 1, 1, 1, 0, 4>), dim3(g2), dim3(512), 0, st, ap, wspc);

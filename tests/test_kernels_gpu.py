@@ -719,13 +719,14 @@ def test_conv_f32_rsplit3(dev, N, H, W, C, Cout):
             assert e3 < 2 * e0 + 2e-7, (m, errs, ex)
 
 
-@pytest.mark.parametrize("sch", ["1", "3", "5", "6", "xs"])
+@pytest.mark.parametrize("sch", ["1", "3", "5", "6", "9", "xs"])
 @pytest.mark.parametrize("N,H,W,C,Cout,R", [(2, 96, 392, 256, 256, 3), (1, 20, 72, 128, 512, 3), (3, 9, 40, 64, 256, 1),
                                             (1, 33, 47, 512, 256, 3)])
 def test_conv_f32_psplit_schedules(dev, sch, N, H, W, C, Cout, R, monkeypatch):
     """The f16 x3 pre-split forward's schedules (DGVCC_PSPLIT_SCH: 1 DMA pieces spread over the MFMA
     blocks, 3 SIMD partners out of phase, 5 register staging instead of LDS-DMA, 6 the two channel
-    halves one phase apart; "xs": the pixel operand pre-split by split_x_h_kernel, SCH 8) bit-identical
+    halves one phase apart, 9 the split once per block in LDS; "xs": the pixel operand pre-split by
+    split_x_h_kernel, SCH 8) bit-identical
     to the in-kernel split (0): several tiles per block (the cross-tile prefetch), ragged pixel tails,
     bias, epilogue statistics and the dgrad on the same kernel."""
     K = _k()
