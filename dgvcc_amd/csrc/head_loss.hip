@@ -6,6 +6,7 @@
 //   AdamW               main.py:85-86 (torch.optim.AdamW semantics)
 //   dmap scatter        utils/dmap_gen.py:53-81 (gaussian_filter_density_fixed)
 #include "dg_common.h"
+#include <cmath>
 #include <algorithm>
 
 namespace {
@@ -381,20 +382,36 @@ __device__ __forceinline__ bool dm_point(const float* __restrict__ pts, long lon
 // formed once per block and a tile's point scan overlaps the previous tile's stores (which the block
 // does not wait for); the tile math and the per-pixel summation order are unchanged (bit-identical).
 constexpr int DMAP_PERS_BLOCKS = 1024;
-template <int DFR, int PF, int DFC = 64, int PERS = 0>
+// HOSTW = 1: the normalized 1-D weights formed once on the host by the launcher (the same float64
+// expressions in the same order, glibc's exp as numpy's) and passed by value, so a block only copies
+// them into LDS: no per-block exp / normalization chain and one barrier fewer ahead of the point walk
+struct DmapWeights {
+  double wd[64];
+  float wf[64];
+};
+// PTS = 2: chunks of 512 points, two per thread (both loads issued before the first test; the hits of
+// the first 256 compacted ahead of the second's, so still in point order): one chunk's three barriers
+// for an image of up to 512 points instead of two chunks'
+template <int DFR, int PF, int DFC = 64, int PERS = 0, int HOSTW = 0, int PTS = 1>
 __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __restrict__ pts,
                                                                const int64_t* __restrict__ offsets, int H, int W,
                                                                float sigma, int radius, float* __restrict__ dmap,
-                                                               int nimg = 1) {
+                                                               int nimg, DmapWeights hw) {
+  static_assert(PTS == 1 || !PF, "PTS 2: without the prefetched first chunk");
   __shared__ double ex[64], wd[64];
   __shared__ float wf[64];
-  __shared__ int hr[256], hc[256];
-  __shared__ int wcnt[4];
+  __shared__ int hr[256 * PTS], hc[256 * PTS];
+  __shared__ int wcnt[4 * PTS];
   const int K = 2 * radius + 1;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (tid < K) {
-    const int i = tid - radius;
-    ex[tid] = exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+    if (HOSTW) {
+      wd[tid] = hw.wd[tid];
+      wf[tid] = hw.wf[tid];
+    } else {
+      const int i = tid - radius;
+      ex[tid] = exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+    }
   }
   const int tiles_w = (W + DFC - 1) / DFC;
   const int tiles = ((H + DFR - 1) / DFR) * tiles_w;
@@ -413,7 +430,7 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     fx = pts[2 * (p0 + tid)];
     fy = pts[2 * (p0 + tid) + 1];
   }
-  if (first) {
+  if (!HOSTW && first) {
     __syncthreads();
     if (tid < K) {  // phi / phi.sum(), summed in index order
       double s = 0.0;
@@ -424,7 +441,47 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     first = false;
   }
   float acc[RT][4] = {};
-  for (long long base = p0; base < p1; base += 256) {
+  for (long long base = p0; base < p1; base += 256 * PTS) {
+    int tot4 = 0;
+    if constexpr (PTS > 1) {
+      int rr[PTS], cc[PTS];
+      bool ht[PTS];
+#pragma unroll
+      for (int u = 0; u < PTS; ++u) {
+        const long long q = base + u * 256 + tid;
+        ht[u] = false;
+        rr[u] = cc[u] = 0;
+        if (q < p1 && dm_point(pts, q, H, W, rr[u], cc[u]))
+          ht[u] = rr[u] + radius >= ty0 && rr[u] - radius < ty0 + DFR && cc[u] + radius >= tx0 && cc[u] - radius < tx0 + DFC;
+      }
+      unsigned long long mm[PTS];
+#pragma unroll
+      for (int u = 0; u < PTS; ++u) {
+        mm[u] = __ballot(ht[u]);
+        if (lane == 0) wcnt[u * 4 + wv] = __popcll(mm[u]);
+      }
+      __syncthreads();  // also publishes the weights on the first pass
+      int offu[PTS];
+#pragma unroll
+      for (int u = 0; u < PTS; ++u) {
+        int before = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          before += w < wv ? wcnt[u * 4 + w] : 0;
+          all += wcnt[u * 4 + w];
+        }
+        offu[u] = tot4 + before;
+        tot4 += all;
+      }
+#pragma unroll
+      for (int u = 0; u < PTS; ++u)
+        if (ht[u]) {
+          const int k = offu[u] + __popcll(mm[u] & ((1ull << lane) - 1ull));
+          hr[k] = rr[u];
+          hc[k] = cc[u];
+        }
+      __syncthreads();
+    } else {
     const long long q = base + tid;
     int r = 0, c = 0;
     bool hit = false;
@@ -444,7 +501,7 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
     const unsigned long long m = __ballot(hit);
     if (lane == 0) wcnt[wv] = __popcll(m);
     __syncthreads();  // also publishes the weights on the first pass
-    int off = 0, tot4 = 0;
+    int off = 0;
 #pragma unroll
     for (int w = 0; w < 4; ++w) {
       off += w < wv ? wcnt[w] : 0;
@@ -456,6 +513,7 @@ __global__ __launch_bounds__(256) void dmap_fixed_fused_kernel(const float* __re
       hc[k] = c;
     }
     __syncthreads();
+    }
     for (int j = 0; j < tot4; ++j) {  // the hits in point order
       const int di0 = pr - hr[j] + radius, dj0 = pc - hc[j] + radius;
       if (di0 + (RT - 1) * RPP < 0 || di0 >= K || dj0 + 3 < 0 || dj0 >= K) continue;
@@ -684,6 +742,26 @@ extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, 
   DG_REQUIRE(T < (1ll << 31) && N < 65536);
   const dim3 grid((unsigned)T, (unsigned)N);
   hipStream_t st = (hipStream_t)stream;
+  // the weights on the host (dmap_fixed_fused_kernel HOSTW; DGVCC_DMAP_HOSTW=0: formed per block)
+  DmapWeights hw{};
+  {
+    const int K = 2 * radius + 1;
+    double ex[64], sum = 0.0;
+    for (int t = 0; t < K; ++t) {
+      const int i = t - radius;
+      ex[t] = std::exp(-0.5 / ((double)sigma * sigma) * (double)(i * i));
+    }
+    for (int j = 0; j < K; ++j) sum += ex[j];
+    for (int t = 0; t < K; ++t) {
+      hw.wd[t] = ex[t] / sum;
+      hw.wf[t] = (float)hw.wd[t];
+    }
+  }
+  const char* eh = getenv("DGVCC_DMAP_HOSTW");
+  const bool hostw = !(eh && eh[0] == '0');
+  // DGVCC_DMAP_PTS=1: chunks of 256 points (one per thread) instead of 512 (read per launch: A/B)
+  const char* ec = getenv("DGVCC_DMAP_PTS");
+  const bool pts2 = !(ec && ec[0] == '1');
   // DGVCC_DMAP_PERS=1: the tile-walking grid (measured slower: 22.4 vs 16.5 us on the bench's 16 frames);
   // default one block per (tile, image)
   const char* ep = getenv("DGVCC_DMAP_PERS");
@@ -691,15 +769,17 @@ extern "C" int dg_dmap_fixed_tiled(const float* points, const int64_t* offsets, 
     const long long tot = T * N;
     const unsigned g = (unsigned)std::min<long long>(tot, DMAP_PERS_BLOCKS);
     hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 0, 64, 1>), dim3(g), dim3(256), 0, st, points, offsets, H, W, sigma,
-                       radius, dmap, N);
+                       radius, dmap, N, hw);
     DG_CHECK_LAUNCH();
     return DG_OK;
   }
-  if (wide) hipLaunchKernelGGL((dmap_fixed_fused_kernel<16, 0, 256>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
-  else if (rows == 32 && pf) hipLaunchKernelGGL((dmap_fixed_fused_kernel<32, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
-  else if (rows == 32) hipLaunchKernelGGL((dmap_fixed_fused_kernel<32, 0>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
-  else if (pf) hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
-  else hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 0>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap);
+  if (wide) hipLaunchKernelGGL((dmap_fixed_fused_kernel<16, 0, 256>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
+  else if (rows == 32 && pf) hipLaunchKernelGGL((dmap_fixed_fused_kernel<32, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
+  else if (rows == 32) hipLaunchKernelGGL((dmap_fixed_fused_kernel<32, 0>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
+  else if (pf) hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
+  else if (hostw && pts2) hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 0, 64, 0, 1, 2>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
+  else if (hostw) hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 0, 64, 0, 1>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
+  else hipLaunchKernelGGL((dmap_fixed_fused_kernel<64, 0>), grid, dim3(256), 0, st, points, offsets, H, W, sigma, radius, dmap, 1, hw);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

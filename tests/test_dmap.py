@@ -62,6 +62,29 @@ def test_dmap_fixed_tiled_dense_bit_exact_and_stable(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("sigma_r", [(4.0, 7), (15.0, 4), (2.0, 31)])
+def test_dmap_fixed_host_weights(dev, monkeypatch, sigma_r):
+    """The launcher's host-formed 1-D weights and 512-point chunks (default) give the same map bit
+    for bit as the per-block device weights on 256-point chunks (DGVCC_DMAP_HOSTW=0) and as the
+    256-point chunks alone (DGVCC_DMAP_PTS=1), at the reference's sigma 4 / radius 7 and at other
+    radii (the weights' length 2r + 1 up to the 63 the kernel holds)."""
+    from dgvcc_amd import kernels as K
+    sigma, radius = sigma_r
+    rng = np.random.default_rng(11)
+    H, W = 130, 200
+    n = np.array([0, 1100, 3])
+    pts = torch.from_numpy(rng.uniform([-4, -4], [W + 3, H + 3], (int(n.sum()), 2)).astype(np.float32)).to(dev)
+    offs = torch.tensor([0] + np.cumsum(n).tolist(), dtype=torch.int64, device=dev)
+    a = K.dmap_fixed(pts, offs, 3, H, W, sigma=sigma, radius=radius).cpu()
+    monkeypatch.setenv("DGVCC_DMAP_PTS", "1")
+    c = K.dmap_fixed(pts, offs, 3, H, W, sigma=sigma, radius=radius).cpu()
+    monkeypatch.setenv("DGVCC_DMAP_HOSTW", "0")
+    b = K.dmap_fixed(pts, offs, 3, H, W, sigma=sigma, radius=radius).cpu()
+    assert torch.equal(a, b) and torch.equal(a, c)
+    assert a.abs().sum() > 0
+
+
+@pytest.mark.gpu
 def test_dmap_fixed_tiled_overfull_bin(dev):
     """1500 points inside one 16x16 region plus a sparse background: a tile whose hits span
     several 256-point chunks of the image's point list; still bit-identical to the oracle and
