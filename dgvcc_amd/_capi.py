@@ -36,7 +36,7 @@ def _ctype(tok: str):
         return ctypes.c_void_p
     base = tok.replace("const", "").split()
     base = base[0] if base else ""
-    return {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float,
+    return {"int": ctypes.c_int, "int64_t": ctypes.c_int64, "float": ctypes.c_float, "double": ctypes.c_double,
             "void": None}[base]
 
 

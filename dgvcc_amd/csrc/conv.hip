@@ -63,6 +63,11 @@ struct FwdArgs {
   int wide_st = 0;
   // f32 f16 x3 arithmetic: a device float >= max |x| (NULL: presplit_h runs amax_kernel over x)
   const float* xamax = nullptr;
+  // f32 f16 x3: x's pair image written by its producer (dg_bn_apply_pair, the SCH 8 layout) and the
+  // bound its scale came from; the pre-split forward then reads it (no split_x_h pass, no in-kernel
+  // split) with the bound as its xamax; other kernels use x and xamax
+  const char* xpair = nullptr;
+  const float* xbound = nullptr;
   // diagnostic stamp rows (conv_fwd_psplit_kernel STAMP = 1; dg_debug_stamps)
   unsigned long long* stamps = nullptr;
 };
@@ -3886,7 +3891,11 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
         const bool inc = psplit_inc();
         // f16 x3 planes instead (presplit_h) on the default (incremental, wide) forms
         const bool h16 = f32_h16() && inc && wide;
-        const unsigned short* wsp = h16 ? presplit_h(a, st) : presplit(a, st);
+        // the producer's pair image (the conv's scale from the producer's bound)
+        const bool pair = h16 && a.xpair && a.xbound && !a.escale && !(g_stamps && getenv("DGVCC_PSPLIT_STAMP"));
+        FwdArgs ah = a;
+        if (pair) ah.xamax = a.xbound;
+        const unsigned short* wsp = h16 ? presplit_h(ah, st) : presplit(a, st);
         if (!wsp) return DG_ERR_HIP;
         const int bn2 = f32_pers_bn(a.Cout);
         const unsigned g2 = (unsigned)std::min<long long>((long long)dg_cdiv(M, psplit_tile_px(a)) * (a.Cout / bn2),
@@ -3899,7 +3908,11 @@ int launch_fwd_impl(const FwdArgs& a, hipStream_t st) {
         }
         // f16 x3: the pixel operand split once into the workspace after the filter planes (SCH 8)
         bool xs = false;
-        if (h16 && psplit_xs(a, bn2) && !a.escale && a.ldx % 4 == 0 && !(g_stamps && getenv("DGVCC_PSPLIT_STAMP"))) {
+        if (pair) {
+          ap.x = a.xpair;
+          ap.ldx = a.C;
+          xs = true;
+        } else if (h16 && psplit_xs(a, bn2) && !a.escale && a.ldx % 4 == 0 && !(g_stamps && getenv("DGVCC_PSPLIT_STAMP"))) {
           const long long off = xsplit_off(presplit_h_bytes(a));
           if (a.wsplit_bytes >= off + xsplit_bytes(a)) {
             const long long KTh = (long long)a.R * a.S * (a.C / 32);
@@ -5832,10 +5845,10 @@ extern "C" int64_t dg_conv_fwd_workspace(int dtype, int N, int H, int W, int C, 
 
 // dg_conv_fwd / dg_conv_fwd_stats with a workspace: part may be NULL (no statistics);
 // a workspace of dg_conv_fwd_workspace bytes lets a small-grid shape split its K loop.
-extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
-                              int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
-                              int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
-                              void* stream) {
+static int conv_fwd_ex_impl(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w, int Cout,
+                            int R, int S, int pad, const float* bias, void* y, int64_t ldy, int accumulate,
+                            float* part, void* workspace, int64_t ws_bytes, const float* xamax, const void* xpair,
+                            const float* xbound, void* stream) {
   DG_REQUIRE(x && w && y && N > 0 && H > 0 && W > 0 && C > 0 && Cout > 0 && R > 0 && S > 0);
   DG_REQUIRE(dtype == DG_F32 || DG_IS16(dtype));
   DG_SUPPORTED(2 * pad == R - 1 && 2 * pad == S - 1 && Cout % 64 == 0);
@@ -5847,6 +5860,8 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
     a.wsplit = (char*)workspace;
     a.wsplit_bytes = workspace ? ws_bytes : 0;
     a.xamax = xamax;
+    a.xpair = (const char*)xpair;
+    a.xbound = xbound;
   }
   if (part) {
     if (DG_IS16(dtype)) {
@@ -5877,6 +5892,25 @@ extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int 
   }
   hipStream_t st = (hipStream_t)stream;
   return dtype == DG_BF16 ? launch_fwd<bf16>(a, st) : dtype == DG_F16 ? launch_fwd<f16>(a, st) : launch_fwd<float>(a, st);
+}
+
+extern "C" int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                              int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
+                              int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
+                              void* stream) {
+  return conv_fwd_ex_impl(dtype, x, ldx, N, H, W, C, w, Cout, R, S, pad, bias, y, ldy, accumulate, part, workspace,
+                          ws_bytes, xamax, nullptr, nullptr, stream);
+}
+
+// dg_conv_fwd_ex whose f32 input also comes as its producer's f16 x3 pair image (include/dgvcc.h)
+extern "C" int dg_conv_fwd_pair(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                                int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
+                                int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
+                                const void* xpair, const float* xbound, void* stream) {
+  DG_REQUIRE(dtype == DG_F32 && (xpair == nullptr) == (xbound == nullptr));
+  DG_REQUIRE(!xpair || C % 32 == 0);
+  return conv_fwd_ex_impl(dtype, x, ldx, N, H, W, C, w, Cout, R, S, pad, bias, y, ldy, accumulate, part, workspace,
+                          ws_bytes, xamax, xpair, xbound, stream);
 }
 
 // y = (relu_out > 0) ? conv(x, w) + y : 0 -- the accumulating dgrad of a 1x1 conv whose input is

@@ -142,11 +142,55 @@ __device__ __forceinline__ void ld_chan_row(const float* r, int c0, float dflt, 
 
 // The grid stride (gridDim*NT) is a multiple of tpp = C/V (a power of two <= NT),
 // so each thread keeps one channel chunk: per-channel parameters live in registers.
-template <typename T, int U, int NTB = NT>
+// The f16 x3 pixel operand of the next conv, written by the f32 BN apply itself (dg_bn_apply_pair):
+// the conv_fwd_psplit_kernel SCH 8 image [pixel][C / 32][hi 32 x f16 | lo 32 x f16] of y * 2^e, so the
+// conv neither splits in-kernel nor runs split_x_h_kernel.  The scale must exist before y does, so e
+// comes from a bound instead of max |y|: with the batch statistics over `count` pixels,
+// |z - mean| <= sqrt(count) * sigma <= sqrt(count) / invstd, hence
+//   |y_c| <= |scale_c| sqrt(count) / invstd_c + |shift_c + mean_c scale_c|   (= |gamma| sqrt(n) + |beta|),
+// and ReLU only shrinks it.  2^e from the largest channel bound (h16_exp, as the conv's own scale from
+// max |y|); the looser scale moves the parts' subnormal floor up by the bound's slack (2^7-2^10 here),
+// far under the f32 rounding of the products.  Every block forms the same bound; block 0
+// stores it for the conv (its xamax).
+template <int NTB>
+__device__ __forceinline__ float bn_pair_bound(const float* __restrict__ scale, const float* __restrict__ shift,
+                                               const float* __restrict__ mean, const float* __restrict__ invstd,
+                                               int C, double count) {
+  __shared__ float red[NTB / 64];
+  const float rn = (float)sqrt(count);
+  float b = 0.f;
+  for (int c = threadIdx.x; c < C; c += NTB)
+    b = fmaxf(b, fabsf(scale[c]) * rn / invstd[c] + fabsf(fmaf(mean[c], scale[c], shift[c])));
+  b = wave_max(b);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < NTB / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
+}
+// 4 channels c0 .. c0 + 3 of one pixel row of the pair image
+__device__ __forceinline__ void bn_pair_store(unsigned char* __restrict__ pair, long long p, int C, int c0,
+                                              const float (&v)[4], float s) {
+  unsigned h0, l0, h1, l1;
+  split2h_pair(v[0], v[1], s, h0, l0);
+  split2h_pair(v[2], v[3], s, h1, l1);
+  unsigned char* d = pair + (p * (C >> 5) + (c0 >> 5)) * 128 + (c0 & 31) * 2;
+  *(u2v*)d = u2v{h0, h1};
+  *(u2v*)(d + 64) = u2v{l0, l1};
+}
+
+// PAIR (f32, 1024-thread form): also the f16 x3 pair image of y (bn_pair_bound above)
+template <typename T, int U, int NTB = NT, int PAIR = 0>
 __global__ __launch_bounds__(NTB) void bn_apply_kernel(const T* __restrict__ z, long long ldz, int M, int C,
                                                       const float* __restrict__ scale, const float* __restrict__ shift,
                                                       int act, const float* __restrict__ drop, int HW,
-                                                      T* __restrict__ y, long long ldy, float* __restrict__ amax) {
+                                                      T* __restrict__ y, long long ldy, float* __restrict__ amax,
+                                                      const float* __restrict__ mean = nullptr,
+                                                      const float* __restrict__ invstd = nullptr, double count = 0.0,
+                                                      unsigned char* __restrict__ pair = nullptr,
+                                                      float* __restrict__ pbound = nullptr) {
+  static_assert(!PAIR || (sizeof(T) == 4 && U == 1), "PAIR: the f32 BN apply");
   constexpr int V = 16 / (int)sizeof(T);
   const int tpp = C / V;
   const long long gt = blockIdx.x * (long long)NTB + threadIdx.x;
@@ -156,6 +200,12 @@ __global__ __launch_bounds__(NTB) void bn_apply_kernel(const T* __restrict__ z, 
   ld_chan_row<V>(scale, c0, 1.f, sc);
   ld_chan_row<V>(shift, c0, 0.f, sf);
   OutMax<T, V> m;  // max |y| per channel (amax: the f16 x3 convs' operand scales)
+  float ps = 0.f;
+  if constexpr (PAIR) {
+    const float bnd = bn_pair_bound<NTB>(scale, shift, mean, invstd, C, count);
+    ps = ldexpf(1.f, h16_exp(bnd));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *pbound = bnd;
+  }
   auto apply = [&](long long p, float (&v)[V]) {
 #pragma unroll
     for (int e = 0; e < V; ++e) {
@@ -169,6 +219,7 @@ __global__ __launch_bounds__(NTB) void bn_apply_kernel(const T* __restrict__ z, 
       for (int e = 0; e < V; ++e) v[e] *= d[e];
     }
     stv(y + p * ldy + c0, v);
+    if constexpr (PAIR) bn_pair_store(pair, p, C, c0, v, ps);
 #pragma unroll
     for (int e = 0; e < V; ++e) m.add(e, v[e]);
   };
@@ -545,13 +596,19 @@ __device__ __forceinline__ int first_max4(float a, float b, float c, float d) {
   return k;
 }
 
-template <typename T, int NTB = NT>
+// PAIR (f32, 1024-thread form): also the f16 x3 pair image of the pooled yp (the bound of y bounds it)
+template <typename T, int NTB = NT, int PAIR = 0>
 __global__ __launch_bounds__(NTB) void bn_apply_pool_kernel(const T* __restrict__ z, long long ldz, int H, int W,
                                                            long long Mp, int C, const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int act,
                                                            const float* __restrict__ drop, int HW, T* __restrict__ y,
                                                            long long ldy, T* __restrict__ yp, long long ldyp,
-                                                           float* __restrict__ amax) {
+                                                           float* __restrict__ amax,
+                                                           const float* __restrict__ mean = nullptr,
+                                                           const float* __restrict__ invstd = nullptr,
+                                                           double count = 0.0, unsigned char* __restrict__ pair = nullptr,
+                                                           float* __restrict__ pbound = nullptr) {
+  static_assert(!PAIR || sizeof(T) == 4, "PAIR: the f32 pooled BN apply");
   constexpr int V = 16 / (int)sizeof(T);
   OutMax<T, V> m;  // max |y| per channel over the window values (>= max |yp|: amax of both)
   const int tpp = C / V;
@@ -561,6 +618,12 @@ __global__ __launch_bounds__(NTB) void bn_apply_pool_kernel(const T* __restrict_
   float sc[V], sf[V];
   ld_chan_row<V>(scale, c0, 1.f, sc);
   ld_chan_row<V>(shift, c0, 0.f, sf);
+  float ps = 0.f;
+  if constexpr (PAIR) {
+    const float bnd = bn_pair_bound<NTB>(scale, shift, mean, invstd, C, count);
+    ps = ldexpf(1.f, h16_exp(bnd));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *pbound = bnd;
+  }
   for (long long pp = gt / tpp; pp < Mp; pp += pstride) {
     long long pos[4];
     pool_window(pp, H, W, pos);
@@ -584,6 +647,7 @@ __global__ __launch_bounds__(NTB) void bn_apply_pool_kernel(const T* __restrict_
 #pragma unroll
     for (int e = 0; e < V; ++e) o[e] = v[first_max4(v[0][e], v[1][e], v[2][e], v[3][e])][e];
     stv(yp + pp * ldyp + c0, o);
+    if constexpr (PAIR) bn_pair_store(pair, pp, C, c0, o, ps);
   }
   if (amax) m.commit(c0, C, amax);
 }
@@ -846,16 +910,35 @@ extern "C" int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, 
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL((ew_unroll() == 4 ? bn_apply_kernel<bf16, 4> : ew_unroll() == 2 ? bn_apply_kernel<bf16, 2> : bn_apply_kernel<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)z, ldz, M, C, scale,
-                       shift, act, drop, HW, (bf16*)y, ldy, amax);
+                       shift, act, drop, HW, (bf16*)y, ldy, amax, nullptr, nullptr, 0.0, nullptr, nullptr);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL((ew_unroll() == 4 ? bn_apply_kernel<f16, 4> : ew_unroll() == 2 ? bn_apply_kernel<f16, 2> : bn_apply_kernel<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)z, ldz, M, C, scale,
-                       shift, act, drop, HW, (f16*)y, ldy, amax);
+                       shift, act, drop, HW, (f16*)y, ldy, amax, nullptr, nullptr, 0.0, nullptr, nullptr);
   else if (ew_wide(amax, true))
     hipLaunchKernelGGL((bn_apply_kernel<float, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st,
                        (const float*)z, ldz, M, C, scale, shift, act, drop, HW, (float*)y, ldy, amax);
   else
     hipLaunchKernelGGL((ew_unroll() == 4 ? bn_apply_kernel<float, 4> : ew_unroll() == 2 ? bn_apply_kernel<float, 2> : bn_apply_kernel<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, M, C,
-                       scale, shift, act, drop, HW, (float*)y, ldy, amax);
+                       scale, shift, act, drop, HW, (float*)y, ldy, amax, nullptr, nullptr, 0.0, nullptr, nullptr);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// dg_bn_apply (f32, no dropout) that also writes the f16 x3 pair image of y for the next conv
+// (bn_apply_kernel PAIR; include/dgvcc.h)
+extern "C" int dg_bn_apply_pair(const float* z, int64_t ldz, int M, int C, const float* scale, const float* shift,
+                                const float* mean, const float* invstd, double count, int act, float* y,
+                                int64_t ldy, float* amax, void* pair, float* pbound, void* stream) {
+  DG_REQUIRE(z && y && scale && shift && mean && invstd && pair && pbound && M > 0 && C > 0 && count >= 1.0);
+  DG_REQUIRE(ldz >= C && ldy >= C && (act == 0 || act == 1));
+  DG_SUPPORTED(C % 32 == 0 && C <= 4096 && BN_SHAPE_OK(DG_F32, C, ldz) && BN_SHAPE_OK(DG_F32, C, ldy) &&
+               EW_WIDE % (C / 4) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  { const int zr = zero_amax(amax, true, C, st); if (zr != DG_OK) return zr; }
+  const long long total = (long long)M * (C / 4);
+  hipLaunchKernelGGL((bn_apply_kernel<float, 1, EW_WIDE, 1>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st, z, ldz,
+                     M, C, scale, shift, act, (const float*)nullptr, 1, y, ldy, amax, mean, invstd, count,
+                     (unsigned char*)pair, pbound);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -972,6 +1055,27 @@ extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, in
   else
     hipLaunchKernelGGL(bn_apply_pool_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, H,
                        W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp, amax);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// dg_bn_apply_pool (f32, no dropout) that also writes the f16 x3 pair image of yp (include/dgvcc.h)
+extern "C" int dg_bn_apply_pool_pair(const float* z, int64_t ldz, int N, int H, int W, int C, const float* scale,
+                                     const float* shift, const float* mean, const float* invstd, double count,
+                                     int act, float* y, int64_t ldy, float* yp, int64_t ldyp, float* amax,
+                                     void* pair, float* pbound, void* stream) {
+  DG_REQUIRE(z && yp && scale && shift && mean && invstd && pair && pbound && N > 0 && H > 1 && W > 1 && C > 0);
+  DG_REQUIRE(count >= 1.0 && (act == 0 || act == 1) && ldz >= C && ldyp >= C && (!y || ldy >= C));
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && C % 32 == 0 && C <= 4096 &&
+               BN_SHAPE_OK(DG_F32, C, ldz) && BN_SHAPE_OK(DG_F32, C, ldyp) && (!y || BN_SHAPE_OK(DG_F32, C, ldy)) &&
+               EW_WIDE % (C / 4) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  { const int zr = zero_amax(amax, true, C, st); if (zr != DG_OK) return zr; }
+  const long long Mp = (long long)N * (H / 2) * (W / 2);
+  const long long total = Mp * (C / 4);
+  hipLaunchKernelGGL((bn_apply_pool_kernel<float, EW_WIDE, 1>), dim3(wide_grid(total, 512)), dim3(EW_WIDE), 0, st, z,
+                     ldz, H, W, Mp, C, scale, shift, act, (const float*)nullptr, H * W, y, ldy, yp, ldyp, amax, mean,
+                     invstd, count, (unsigned char*)pair, pbound);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -40,6 +40,9 @@ _STEM_RECOMP = __import__("os").environ.get("DGVCC_STEM_RECOMP", "1") != "0"
 _STEM_F32 = __import__("os").environ.get("DGVCC_STEM_F32", "1") != "0"
 # its backward: dz and the wgrad on f32 MFMA in one pass (dg_stem_bwd_f32); 0 = BN backward + im2col wgrad
 _STEM_BWD_F32 = __import__("os").environ.get("DGVCC_STEM_BWD_F32", "1") != "0"
+# fp32 training: the BN apply of a layer whose output feeds a 3x3 / 1x1 conv forward writes that
+# conv's f16 x3 pair image too (dg_bn_apply_pair; DGVCC_BN_PAIR=0: the conv splits x itself)
+_BN_PAIR = __import__("os").environ.get("DGVCC_BN_PAIR", "1") != "0"
 
 
 def invalidate_frozen():
@@ -92,6 +95,9 @@ class ConvLayer:
         self.R = conv.kernel_size[0]
         self.pad = conv.padding[0]
         self.Cin, self.Cout = conv.in_channels, conv.out_channels
+        # the output (pooled output when pooling) is the input of a conv forward (FeaturePlan sets it):
+        # the fp32 training BN apply then writes that conv's pair image (_BN_PAIR)
+        self.pair_out = False
 
     def params(self):
         ps = [self.conv.weight]
@@ -208,6 +214,7 @@ class ConvLayer:
                 K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
         else:
             K.conv_fwd(x, wp, self.Cout, self.R, self.pad, z, bias=bias)
+        x.pair = None  # consumed (the image is not kept with the tape)
         if epi is not None and pg is not None:
             stats = SB.fwd_stats(bn, pg, part=epi[0], nblk=epi[1], M=z.M)
         elif epi is not None:
@@ -225,15 +232,16 @@ class ConvLayer:
                 stats = bn_eval_cached(self, bn)
         else:
             stats = frozen(self, ("ident", x.buf.device), (), lambda: _ident_stats(self.Cout, x.buf.device))
-        self._apply(z, stats, out, drop, pool)
+        pair = _BN_PAIR and self.pair_out and training and bn is not None and pg is None
+        self._apply(z, stats, out, drop, pool, pair)
         if tape is not None:
             tape[self] = (x, z, stats, wp, drop, training)
 
-    def _apply(self, z: Act, stats, out: Act | None, drop, pool: Act | None):
+    def _apply(self, z: Act, stats, out: Act | None, drop, pool: Act | None, pair: bool = False):
         if pool is not None:
-            K.bn_apply_pool(z, stats, self.act, out, pool, drop)
+            K.bn_apply_pool(z, stats, self.act, out, pool, drop, pair=pair)
         else:
-            K.bn_apply(z, stats, self.act, out, drop)
+            K.bn_apply(z, stats, self.act, out, drop, pair=pair)
 
     def backward(self, tape: dict, g: Act | None, gx: Act | None, accumulate_gx: bool = False,
                  g_pool: Act | None = None, gx_bn: "ConvLayer | None" = None) -> dict:
@@ -517,6 +525,12 @@ class FeaturePlan:
             l.scope = "enc"
         for l in self.dec:
             l.scope = "dec"
+        # outputs read next by a conv forward (the pooled ones for E[1], E[3], E[6], E[9]); not the stem
+        # output (its consumer is the Cout = 64 3-tap kernel), nor y3 / y2 / y1 (upsampled / heads)
+        for i in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12):
+            self.enc[i].pair_out = True
+        for i in (0, 2, 4):
+            self.dec[i].pair_out = True
 
     def params(self):
         return [p for l in self.layers for p in l.params()]

@@ -27,6 +27,10 @@ class Act:
     off: int = 0
     C: int | None = None
     amax: torch.Tensor | None = None
+    # f32: (image, bound) -- the f16 x3 pair image of the slice its producer wrote (bn_apply /
+    # bn_apply_pool with pair=True) and the bound of its scale, for the next conv forward
+    # (dg_conv_fwd_pair); cleared by writers that do not produce it
+    pair: tuple | None = None
 
     def __post_init__(self):
         if self.buf.dim() != 4:
@@ -133,6 +137,13 @@ def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
     if _CHECK_AMAX:
         check_amax(x, kind)
     y.amax = None  # y is (re)written by a conv: no tracked maximum
+    y.pair = None
+    if x.pair is not None and x.dt == 0:
+        xp, xb = x.pair
+        _timed(kind, flops, lambda: call("dg_conv_fwd_pair", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
+                                         Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate), None,
+                                         ptr(work), ws, ptr(x.amax), ptr(xp), ptr(xb), stream()), nbytes)
+        return
     _timed(kind, flops, lambda: call("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp),
                                      Cout, R, R, pad, ptr(bias), y.ptr, y.ld, int(accumulate), None,
                                      ptr(work), ws, ptr(x.amax), stream()), nbytes)
@@ -402,8 +413,15 @@ def conv_fwd_stats(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act
         return None
     ws, work = _fwd_workspace(x, Cout, R)
     y.amax = None
+    y.pair = None
 
     def launch():
+        if x.pair is not None and x.dt == 0:
+            xp, xb = x.pair
+            res.append(lib_call_status("dg_conv_fwd_pair", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
+                                       R, R, pad, ptr(bias), y.ptr, y.ld, 0, ptr(part), ptr(work), ws,
+                                       ptr(x.amax), ptr(xp), ptr(xb), stream()))
+            return
         res.append(lib_call_status("dg_conv_fwd_ex", x.dt, x.ptr, x.ld, x.N, x.H, x.W, x.C, ptr(wp), Cout,
                                    R, R, pad, ptr(bias), y.ptr, y.ld, 0, ptr(part), ptr(work), ws, ptr(x.amax),
                                    stream()))
@@ -509,8 +527,26 @@ def _amax_out(a: Act | None, *more: Act | None) -> torch.Tensor | None:
     return t
 
 
-def bn_apply(z: Act, stats, act: int, y: Act, drop: torch.Tensor | None = None):
+def _pair_bufs(M: int, C: int, dev):
+    return torch.empty(M * C, dtype=torch.float32, device=dev), torch.empty(1, dtype=torch.float32, device=dev)
+
+
+def bn_apply(z: Act, stats, act: int, y: Act, drop: torch.Tensor | None = None, pair: bool = False,
+             count: int | None = None):
+    """pair (f32, train-mode batch statistics over `count` pixels, default z.M; no dropout): also the
+    f16 x3 pair image of y for the next conv forward (dg_bn_apply_pair), attached as y.pair."""
     am = _amax_out(y)
+    y.pair = None
+    if pair and z.dt == 0 and drop is None and z.C % 32 == 0:
+        img, bound = _pair_bufs(z.M, z.C, z.buf.device)
+        st = lib_call_status("dg_bn_apply_pair", z.ptr, z.ld, z.M, z.C, ptr(stats[2]), ptr(stats[3]),
+                             ptr(stats[0]), ptr(stats[1]), float(count or z.M), act, y.ptr, y.ld, ptr(am),
+                             ptr(img), ptr(bound), stream())
+        if st == 0:
+            y.pair = (img, bound)
+            return
+        if st != -2:
+            raise DGError(f"dg_bn_apply_pair failed with status {st}")
     call("dg_bn_apply", z.dt, z.ptr, z.ld, z.M, z.C, ptr(stats[2]), ptr(stats[3]), act, ptr(drop),
          z.H * z.W, y.ptr, y.ld, ptr(am), stream())
 
@@ -526,9 +562,25 @@ def bn_bwd(g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), ptr(am), stream())
 
 
-def bn_apply_pool(z: Act, stats, act: int, y: Act | None, yp: Act, drop: torch.Tensor | None = None):
-    """y = act(BN(z)) [* drop] (only written when y is given) and yp = maxpool2x2(y)."""
+def bn_apply_pool(z: Act, stats, act: int, y: Act | None, yp: Act, drop: torch.Tensor | None = None,
+                  pair: bool = False, count: int | None = None):
+    """y = act(BN(z)) [* drop] (only written when y is given) and yp = maxpool2x2(y).  pair: as
+    bn_apply, the pair image of yp (dg_bn_apply_pool_pair)."""
     am = _amax_out(yp, y)  # max over the un-pooled values bounds both
+    yp.pair = None
+    if y is not None:
+        y.pair = None
+    if pair and z.dt == 0 and drop is None and z.C % 32 == 0:
+        img, bound = _pair_bufs(yp.M, z.C, z.buf.device)
+        st = lib_call_status("dg_bn_apply_pool_pair", z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(stats[2]),
+                             ptr(stats[3]), ptr(stats[0]), ptr(stats[1]), float(count or z.M), act,
+                             y.ptr if y is not None else None, y.ld if y is not None else 0, yp.ptr, yp.ld,
+                             ptr(am), ptr(img), ptr(bound), stream())
+        if st == 0:
+            yp.pair = (img, bound)
+            return
+        if st != -2:
+            raise DGError(f"dg_bn_apply_pool_pair failed with status {st}")
     call("dg_bn_apply_pool", z.dt, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(stats[2]), ptr(stats[3]), act,
          ptr(drop), y.ptr if y is not None else None, y.ld if y is not None else 0, yp.ptr, yp.ld, ptr(am), stream())
 

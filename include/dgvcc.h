@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 6 /* 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 7 /* 7: dg_bn_apply_pair / dg_bn_apply_pool_pair write the f16 x3 pair image of their f32 output and dg_conv_fwd_pair reads it; 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -112,6 +112,15 @@ int dg_conv_fwd_ex(int dtype, const void* x, int64_t ldx, int N, int H, int W, i
                    int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
                    int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
                    void* stream);
+/* dg_conv_fwd_ex (DG_F32) whose input x also comes as xpair, the f16 x3 pair image its producer wrote
+ * (dg_bn_apply_pair / dg_bn_apply_pool_pair), with xbound the producer's *pbound: the f16 x3 pre-split
+ * forward reads the pair (no pass over x to split it, no split in the kernel) with its scale from
+ * xbound; launches on the other kernels read x and xamax as dg_conv_fwd_ex.  xpair = xbound = NULL:
+ * dg_conv_fwd_ex.  Same statistics rows and workspace as dg_conv_fwd_ex. */
+int dg_conv_fwd_pair(int dtype, const void* x, int64_t ldx, int N, int H, int W, int C, const void* w,
+                     int Cout, int R, int S, int pad, const float* bias, void* y, int64_t ldy,
+                     int accumulate, float* part, void* workspace, int64_t ws_bytes, const float* xamax,
+                     const void* xpair, const float* xbound, void* stream);
 /* xamax (f32 entries, f16 x3 arithmetic): NULL, or operand maxima of x (dg_amax, or the kernel that
  * produced x): word 0 >= max |x| over the operand, and -- for the weight-gradient entries, which
  * scale per channel -- words 1 .. C >= max |x| over each channel (channel c of the slice x points
@@ -222,6 +231,16 @@ int dg_bn_fwd_train(int dtype, const void* z, int64_t ldz, int M, int C,
 int dg_bn_apply(int dtype, const void* z, int64_t ldz, int M, int C, const float* scale,
                 const float* shift, int act, const float* drop, int HW, void* y, int64_t ldy,
                 float* amax, void* stream);
+/* dg_bn_apply (f32, train-mode statistics, no dropout) that also writes pair: the f16 x3 image of y
+ * the following conv's pre-split forward reads (dg_conv_fwd_pair), [M][C / 32][32 x f16 hi | 32 x f16
+ * lo] of y * 2^e (the split of y as stored; 4 * M * C bytes, C % 32 == 0), and *pbound, the bound e
+ * came from (>= max |y|): |scale_c| sqrt(count) / invstd_c + |shift_c + mean_c scale_c| maximised over c
+ * (= |gamma_c| sqrt(count) + |beta_c|, since |z - mean| <= sqrt(count) sigma for statistics over count
+ * pixels; mean / invstd the batch statistics y was normalised with).  No read pass over y, but a
+ * scale up to the bound's slack looser than one from max |y|.  y, amax: as dg_bn_apply. */
+int dg_bn_apply_pair(const float* z, int64_t ldz, int M, int C, const float* scale, const float* shift,
+                     const float* mean, const float* invstd, double count, int act, float* y, int64_t ldy,
+                     float* amax, void* pair, float* pbound, void* stream);
 /* amax (here and on the BN-backward / pooled / join / InstanceNorm entries below; may be NULL):
  * the operand maxima of the pass's output (the written activation or dz; the pooled entries: over
  * the un-pooled values, >= max |yp|) -- the xamax a following f32 conv can take instead of a read
@@ -260,6 +279,12 @@ int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const void* g, i
 int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, int H, int W, int C,
                      const float* scale, const float* shift, int act, const float* drop, void* y,
                      int64_t ldy, void* yp, int64_t ldyp, float* amax, void* stream);
+/* dg_bn_apply_pool (f32, train-mode statistics, no dropout) with the pair image of the pooled yp
+ * ([N * H/2 * W/2][C / 32][hi | lo], the bound of the un-pooled y): as dg_bn_apply_pair. */
+int dg_bn_apply_pool_pair(const float* z, int64_t ldz, int N, int H, int W, int C, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, double count, int act,
+                          float* y, int64_t ldy, float* yp, int64_t ldyp, float* amax, void* pair,
+                          float* pbound, void* stream);
 int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const void* gd, int64_t ldgd,
                    const void* z, int64_t ldz, int N, int H, int W, int C, const float* gamma,
                    const float* save_mean, const float* save_invstd, const float* scale,

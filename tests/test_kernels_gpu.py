@@ -976,3 +976,81 @@ def test_wide_maxima_passes(dev, monkeypatch, N, H, W, C):
     for k in range(0, len(wide), 2):
         ref = wide[k].reshape(-1, C).abs().amax(dim=0)
         assert torch.equal(wide[k + 1][1:1 + C], ref) and wide[k + 1][0].item() == ref.max().item(), k
+
+
+def _pair_image_ref(y: torch.Tensor, bound: float) -> torch.Tensor:
+    """The f16 x3 pair image [M][C/32][hi 32 | lo 32] (f16) of y [M][C] * 2^e, e = h16_exp(bound)."""
+    import math
+    e = max(-100, min(100, 14 - math.frexp(bound)[1])) if bound > 0 else 0
+    v = y.float() * (2.0 ** e)
+    hi = v.half()
+    lo = (v - hi.float()).half()
+    M, C = y.shape
+    return torch.cat([hi.view(M, C // 32, 32), lo.view(M, C // 32, 32)], dim=2)
+
+
+@pytest.mark.parametrize("N,H,W,C,Cout,pool", [(2, 128, 128, 128, 256, False), (2, 96, 256, 64, 128, False),
+                                               (2, 64, 128, 256, 512, False), (2, 128, 256, 128, 256, True)])
+def test_bn_pair_image_and_conv(dev, N, H, W, C, Cout, pool):
+    """fp32 training BN apply writing the next conv's f16 x3 pair image (dg_bn_apply_pair /
+    dg_bn_apply_pool_pair): y, yp and the maxima bit-identical to dg_bn_apply(_pool); the bound equals
+    |gamma| sqrt(M) + |beta| in the scale / shift / mean / invstd form and bounds max |y|; the image is
+    the f16 split of y * 2^e (e from the bound) in the pre-split layout.  The conv forward reading it
+    (dg_conv_fwd_pair: the 256-pixel kernel, a single channel tile, 128 channels, and the several-tile
+    form that otherwise runs split_x_h) has per-output-channel error within 2x the exact
+    v_mfma_f32_16x16x4_f32 path's against float64, with its BN statistics rows."""
+    K = _k()
+    g = torch.Generator().manual_seed(31)
+    z = K.Act(to_nhwc(torch.randn(N, C, H, W, generator=g) * 3 + 1).to(dev))
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.3).to(dev)
+    stats = K.bn_fwd_train(z, gam, bet, torch.zeros(C, device=dev), torch.ones(C, device=dev), 0.1, 1e-5)
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    outs = {}
+    for pr in (True, False):
+        y = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        if pool:
+            yp = K.Act(K.nhwc(N, Ho, Wo, C, torch.float32, dev))
+            K.bn_apply_pool(z, stats, K.ACT_RELU, y, yp, pair=pr)
+            outs[pr] = (y, yp)
+        else:
+            K.bn_apply(z, stats, K.ACT_RELU, y, pair=pr)
+            outs[pr] = (y, y)
+    torch.cuda.synchronize()
+    (y1, x1), (y0, x0) = outs[True], outs[False]
+    assert torch.equal(y1.buf, y0.buf) and torch.equal(x1.buf, x0.buf) and torch.equal(x1.amax, x0.amax)
+    assert x1.pair is not None and x0.pair is None
+    img, bound = x1.pair
+    b = bound.item()
+    st = stats.double()
+    ref_b = (st[2].abs() * (z.M ** 0.5) / st[1] + (st[3] + st[0] * st[2]).abs()).max().item()
+    assert abs(b - ref_b) <= 1e-5 * ref_b and b >= x1.buf.abs().max().item()
+    Mx = x1.M
+    ref_img = _pair_image_ref(x1.buf.reshape(Mx, C), b)
+    assert torch.equal(img.view(torch.float16).view(Mx, C // 32, 64), ref_img)
+    # the conv forward on the pair image vs the same conv on x (exact f32 MFMA), against float64
+    w = torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    y64 = F.conv2d(to_nchw(x1.buf).double().cpu(), w.double(), padding=1)
+    prev = K.lib_call_status("dg_get_f32_math")
+    errs = {}
+    try:
+        for m in (2, 0):
+            K.call("dg_set_f32_math", m)
+            src = K.Act(x1.buf)
+            src.amax, src.pair = x1.amax, (x1.pair if m == 2 else None)
+            o = K.Act(K.nhwc(N, Ho, Wo, Cout, torch.float32, dev))
+            res = K.conv_fwd_stats(src, wp, Cout, 3, 1, o)
+            if res is None:
+                K.conv_fwd(src, wp, Cout, 3, 1, o)
+            torch.cuda.synchronize()
+            errs[m] = _chan_err(to_nchw(o.buf), y64, 1)
+            if res is not None:  # the statistics rows merge to the output's own mean
+                part = res[0].double()
+                mean = (part[:, 0] * part[:, 1]).sum(0) / part[:, 0].sum(0)
+                assert torch.allclose(mean.cpu(), o.buf.double().reshape(-1, Cout).mean(0).cpu(), rtol=1e-6, atol=1e-7)
+    finally:
+        K.call("dg_set_f32_math", prev)
+    h, e = errs[2], errs[0]
+    print(f"pair worst {h.max().item():.3e} exact worst {e.max().item():.3e}")
+    assert (h <= 2 * e + 1e-7).all(), (h.max().item(), e.max().item())
