@@ -261,7 +261,8 @@ FWD_KERNEL_NAMES = {
             "conv, f32 operands split exactly into 3 bf16 parts, 6 x v_mfma_f32_16x16x32_bf16 per 32-deep block, "
             "f32 accumulation: forward + dgrad launches; peak = dense bf16 / 6)",
     "fp32_h16": "conv_fwd_psplit_kernel<256|128, HM> + conv_fwd_rsplit3w_kernel<HM> + split_x_h_kernel (the pixel "
-                "operand's hi/lo pre-split pass, timed inside the same launch) (implicit-GEMM conv, each f32 "
+                "operand's hi/lo pre-split pass of the dgrads, timed inside the same launch; the forwards read the "
+                "pair image their BN apply wrote) (implicit-GEMM conv, each f32 "
                 "operand scaled by a power of two and cut into two f16 parts, 3 x v_mfma_f32_16x16x32_f16 per "
                 "32-deep block (hi*hi + hi*lo + lo*hi), f32 accumulation: forward + dgrad launches; peak = dense "
                 "f16 / 3)",
