@@ -308,13 +308,19 @@ inline int ew_unroll() {  // read per launch: same-process A/B (tools/bench_bn.p
   return e && e[0] == '2' ? 2 : e && e[0] == '4' ? 4 : 1;
 }
 
+// gpart (f32, may be NULL): the block's max |g'| per channel, gpart[block][C] (dg_bn_bwd_pair's bound)
 template <typename T>
 __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_partial(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
                                                      long long ldz, int M, int C, int ppb, const float* mean,
                                                      const float* invstd, const float* scale, const float* shift,
-                                                     int act, const float* drop, int HW, float* __restrict__ part) {
+                                                     int act, const float* drop, int HW, float* __restrict__ part,
+                                                     float* __restrict__ gpart = nullptr) {
   constexpr int V = 16 / (int)sizeof(T);
   __shared__ float sh[3][NT * V];
+  __shared__ float shm[sizeof(T) == 4 ? NT * V : 1];
+  float gm[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) gm[e] = 0.f;
   const int tpp = C / V;
   const int rows = NT / tpp;
   const int tid = threadIdx.x;
@@ -360,6 +366,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_partial(con
           sg[e] += gv[e];
           sgx[e] = fmaf(gv[e], xh, sgx[e]);
           sx[e] += xh;
+          gm[e] = fmaxf(gm[e], fabsf(gv[e]));
         }
       }
     }
@@ -368,6 +375,7 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_partial(con
       sh[0][pl * C + c0 + e] = sg[e];
       sh[1][pl * C + c0 + e] = sgx[e];
       sh[2][pl * C + c0 + e] = sx[e];
+      if constexpr (sizeof(T) == 4) shm[pl * C + c0 + e] = gm[e];
     }
   }
   __syncthreads();
@@ -376,16 +384,33 @@ __global__ __launch_bounds__(NT, sizeof(T) == 2 ? 7 : 1) void bn_bwd_partial(con
     for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; d += sh[2][r * C + c]; }
     float* o = part + (long long)blockIdx.x * 3 * C;
     o[c] = a; o[C + c] = b; o[2 * C + c] = d;
+    if constexpr (sizeof(T) == 4) {
+      if (gpart) {
+        float mx = 0.f;
+        for (int r = 0; r < rows; ++r) mx = fmaxf(mx, shm[r * C + c]);
+        gpart[(long long)blockIdx.x * C + c] = mx;
+      }
+    }
   }
 }
 
+// gpart / bpart (may be NULL): the per-block max |g'| rows of bn_bwd_partial -> bpart[blockIdx.x] = the
+// largest over this block's 16 channels of |k1| max |g'| + |k2| sqrt(count) + |k3| >= max |dz| (|xhat| <=
+// sqrt(count) for batch statistics over count pixels): dg_bn_bwd_pair's pair-image scale bound
 __global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ part, int nblk, int M, int C,
                                                       const float* gamma, const float* invstd, float* dgamma,
-                                                      float* dbeta, float* dbias, float* coef) {
+                                                      float* dbeta, float* dbias, float* coef,
+                                                      const float* __restrict__ gpart = nullptr,
+                                                      float* __restrict__ bpart = nullptr, double count = 0.0) {
   __shared__ double sh[3][16][17];
+  __shared__ float shg[16][17];
   const int cl = threadIdx.x & 15, r = threadIdx.x >> 4;
   const int c = blockIdx.x * 16 + cl;
   double a = 0.0, b = 0.0, d = 0.0;
+  float gmx = 0.f;
+  if (gpart && c < C)
+    for (int k = r; k < nblk; k += 16) gmx = fmaxf(gmx, gpart[(long long)k * C + c]);
+  shg[r][cl] = gmx;
   if (c < C) {
     int k = r;
     for (; k + 48 < nblk; k += 64) {
@@ -405,24 +430,36 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ 
   }
   sh[0][r][cl] = a; sh[1][r][cl] = b; sh[2][r][cl] = d;
   __syncthreads();
-  if (r != 0 || c >= C) return;
-  a = 0.0; b = 0.0; d = 0.0;
-  for (int q = 0; q < 16; ++q) { a += sh[0][q][cl]; b += sh[1][q][cl]; d += sh[2][q][cl]; }
-  if (!invstd) {  // no normalisation: dz = act'(z) g ; dbeta = dbias = sum dz
-    if (dgamma) dgamma[c] = 0.f;
-    if (dbeta) dbeta[c] = (float)a;
-    if (dbias) dbias[c] = (float)a;
-    coef[c] = 1.f; coef[C + c] = 0.f; coef[2 * C + c] = 0.f;
-    return;
+  if (r != 0) return;
+  float bnd = 0.f;  // this channel's |dz| bound (bpart)
+  if (c < C) {
+    a = 0.0; b = 0.0; d = 0.0;
+    for (int q = 0; q < 16; ++q) { a += sh[0][q][cl]; b += sh[1][q][cl]; d += sh[2][q][cl]; }
+    float gmax = 0.f;
+    for (int q = 0; q < 16; ++q) gmax = fmaxf(gmax, shg[q][cl]);
+    if (!invstd) {  // no normalisation: dz = act'(z) g ; dbeta = dbias = sum dz
+      if (dgamma) dgamma[c] = 0.f;
+      if (dbeta) dbeta[c] = (float)a;
+      if (dbias) dbias[c] = (float)a;
+      coef[c] = 1.f; coef[C + c] = 0.f; coef[2 * C + c] = 0.f;
+      bnd = gmax;
+    } else {
+      const float gm = gamma ? gamma[c] : 1.f;
+      const float k1 = gm * invstd[c];
+      const float k2 = (float)(k1 * b / M);
+      const float k3 = (float)(k1 * a / M);
+      if (dgamma) dgamma[c] = (float)b;
+      if (dbeta) dbeta[c] = (float)a;
+      if (dbias) dbias[c] = (float)(-(double)k2 * d);
+      coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
+      bnd = fabsf(k1) * gmax + fabsf(k2) * (float)sqrt(count) + fabsf(k3);
+    }
   }
-  const float gm = gamma ? gamma[c] : 1.f;
-  const float k1 = gm * invstd[c];
-  const float k2 = (float)(k1 * b / M);
-  const float k3 = (float)(k1 * a / M);
-  if (dgamma) dgamma[c] = (float)b;
-  if (dbeta) dbeta[c] = (float)a;
-  if (dbias) dbias[c] = (float)(-(double)k2 * d);
-  coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
+  if (bpart) {  // lanes 0-15 of wave 0: the block's largest
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) bnd = fmaxf(bnd, __shfl_xor(bnd, o, 16));
+    if (cl == 0) bpart[blockIdx.x] = bnd;
+  }
 }
 
 // Column sums of part[nblk][3][C] in double -> out[3][C] (a rank's BN-backward sums, fixed order).
@@ -468,12 +505,33 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize_sync(const float* __restri
   coef[c] = k1; coef[C + c] = k2; coef[2 * C + c] = k3;
 }
 
-template <typename T, int U = 1, int NTB = NT>
+// The max over nb bound partials (bn_bwd_finalize bpart), every block alike
+template <int NTB>
+__device__ __forceinline__ float bn_bpart_max(const float* __restrict__ bpart, int nb) {
+  __shared__ float red[NTB / 64];
+  float b = 0.f;
+  for (int i = threadIdx.x; i < nb; i += NTB) b = fmaxf(b, bpart[i]);
+  b = wave_max(b);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = b;
+  __syncthreads();
+  float r = red[0];
+#pragma unroll
+  for (int w = 1; w < NTB / 64; ++w) r = fmaxf(r, red[w]);
+  return r;
+}
+
+// PAIR (f32, 1024-thread form): also the f16 x3 pair image of dz for the dgrad (dg_bn_bwd_pair), its
+// scale from the bound partials (bn_bwd_finalize bpart)
+template <typename T, int U = 1, int NTB = NT, int PAIR = 0>
 __global__ __launch_bounds__(NTB, NTB == NT && sizeof(T) == 2 ? (U == 2 ? 1 : 7) : 1) void bn_bwd_apply(const T* __restrict__ g, long long ldg, const T* __restrict__ z,
                                                    long long ldz, int M, int C, const float* mean, const float* invstd,
                                                    const float* scale, const float* shift, int act, const float* drop,
                                                    int HW, const float* __restrict__ coef, T* __restrict__ dz,
-                                                   long long lddz, float* __restrict__ amax) {
+                                                   long long lddz, float* __restrict__ amax,
+                                                   const float* __restrict__ bpart = nullptr, int nbp = 0,
+                                                   unsigned char* __restrict__ pair = nullptr,
+                                                   float* __restrict__ pbound = nullptr) {
+  static_assert(!PAIR || (sizeof(T) == 4 && U == 1), "PAIR: the f32 BN backward apply");
   constexpr int V = 16 / (int)sizeof(T);
   OutMax<T, V> m;  // max |dz| per channel (amax)
   const int tpp = C / V;
@@ -543,11 +601,18 @@ __global__ __launch_bounds__(NTB, NTB == NT && sizeof(T) == 2 ? (U == 2 ? 1 : 7)
     }
   };
   if constexpr (U == 1) {  // the round-3 loop (runtime dropout / ReLU flags)
+    float ps = 0.f;
+    if constexpr (PAIR) {
+      const float bnd = bn_bpart_max<NTB>(bpart, nbp);
+      ps = ldexpf(1.f, h16_exp(bnd));
+      if (blockIdx.x == 0 && threadIdx.x == 0) *pbound = bnd;
+    }
     for (long long p = gt / tpp; p < M; p += pstride) {
       float gv[V], zv[V];
       bn_bwd_load<T, V>(g, ldg, z, ldz, p, c0, C, cp, act, drop, HW, gv, zv);
       f(gv, zv);
       stv(dz + p * lddz + c0, gv);
+      if constexpr (PAIR) bn_pair_store(pair, p, C, c0, gv, ps);
 #pragma unroll
       for (int e = 0; e < V; ++e) m.add(e, gv[e]);
     }
@@ -709,15 +774,21 @@ __device__ __forceinline__ void bn_pool_bwd_load(const T* gp, long long ldgp, co
   }
 }
 
+// gpart (f32, may be NULL): as bn_bwd_partial
 template <typename T>
 __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ gp, long long ldgp,
                                                           const T* __restrict__ gd, long long ldgd,
                                                           const T* __restrict__ z, long long ldz, int H, int W,
                                                           long long Mp, int C, long long ppb, const float* mean,
                                                           const float* invstd, const float* scale, const float* shift,
-                                                          int act, const float* drop, int HW, float* __restrict__ part) {
+                                                          int act, const float* drop, int HW, float* __restrict__ part,
+                                                          float* __restrict__ gpart = nullptr) {
   constexpr int V = POOL_V;
   __shared__ float sh[3][NT * V];
+  __shared__ float shm[sizeof(T) == 4 ? NT * V : 1];
+  float gm[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) gm[e] = 0.f;
   const int tpp = C / V;
   const int rows = NT / tpp;
   const int tid = threadIdx.x;
@@ -743,6 +814,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
           sg[e] += gv[k][e];
           sgx[e] = fmaf(gv[k][e], xh, sgx[e]);
           sx[e] += xh;
+          if constexpr (sizeof(T) == 4) gm[e] = fmaxf(gm[e], fabsf(gv[k][e]));
         }
     }
 #pragma unroll
@@ -750,6 +822,7 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
       sh[0][pl * C + c0 + e] = sg[e];
       sh[1][pl * C + c0 + e] = sgx[e];
       sh[2][pl * C + c0 + e] = sx[e];
+      if constexpr (sizeof(T) == 4) shm[pl * C + c0 + e] = gm[e];
     }
   }
   __syncthreads();
@@ -758,17 +831,29 @@ __global__ __launch_bounds__(NT) void bn_pool_bwd_partial(const T* __restrict__ 
     for (int r = 0; r < rows; ++r) { a += sh[0][r * C + c]; b += sh[1][r * C + c]; d += sh[2][r * C + c]; }
     float* o = part + (long long)blockIdx.x * 3 * C;
     o[c] = a; o[C + c] = b; o[2 * C + c] = d;
+    if constexpr (sizeof(T) == 4) {
+      if (gpart) {
+        float mx = 0.f;
+        for (int r = 0; r < rows; ++r) mx = fmaxf(mx, shm[r * C + c]);
+        gpart[(long long)blockIdx.x * C + c] = mx;
+      }
+    }
   }
 }
 
-template <typename T, int NTB = NT>
+// PAIR (f32, 1024-thread form): also the pair image of dz (as bn_bwd_apply)
+template <typename T, int NTB = NT, int PAIR = 0>
 __global__ __launch_bounds__(NTB) void bn_pool_bwd_apply(const T* __restrict__ gp, long long ldgp,
                                                         const T* __restrict__ gd, long long ldgd,
                                                         const T* __restrict__ z, long long ldz, int H, int W,
                                                         long long Mp, int C, const float* mean, const float* invstd,
                                                         const float* scale, const float* shift, int act,
                                                         const float* drop, int HW, const float* __restrict__ coef,
-                                                        T* __restrict__ dz, long long lddz, float* __restrict__ amax) {
+                                                        T* __restrict__ dz, long long lddz, float* __restrict__ amax,
+                                                        const float* __restrict__ bpart = nullptr, int nbp = 0,
+                                                        unsigned char* __restrict__ pair = nullptr,
+                                                        float* __restrict__ pbound = nullptr) {
+  static_assert(!PAIR || sizeof(T) == 4, "PAIR: the f32 pooled BN backward apply");
   constexpr int V = POOL_V;
   OutMax<T, V> m;  // max |dz| per channel
   const int tpp = C / V;
@@ -781,6 +866,12 @@ __global__ __launch_bounds__(NTB) void bn_pool_bwd_apply(const T* __restrict__ g
   ld_chan_row<V>(coef, c0, 0.f, k1);
   ld_chan_row<V>(coef + C, c0, 0.f, k2);
   ld_chan_row<V>(coef + 2 * C, c0, 0.f, k3);
+  float ps = 0.f;
+  if constexpr (PAIR) {
+    const float bnd = bn_bpart_max<NTB>(bpart, nbp);
+    ps = ldexpf(1.f, h16_exp(bnd));
+    if (blockIdx.x == 0 && threadIdx.x == 0) *pbound = bnd;
+  }
   for (long long pp = gt / tpp; pp < Mp; pp += pstride) {
     long long pos[4];
     pool_window(pp, H, W, pos);
@@ -795,6 +886,7 @@ __global__ __launch_bounds__(NTB) void bn_pool_bwd_apply(const T* __restrict__ g
         m.add(e, gv[k][e]);
       }
       stn<V>(dz + pos[k] * lddz + c0, gv[k]);
+      if constexpr (PAIR) bn_pair_store(pair, pos[k], C, c0, gv[k], ps);
     }
   }
   if (amax) m.commit(c0, C, amax);
@@ -866,7 +958,7 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
                        (const T*)z, ldz, M, C, mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
   else
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<T, 2> : bn_bwd_apply<T, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const T*)g, ldg, (const T*)z, ldz, M, C,
-                       mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax);
+                       mean, inv, scale, shift, act, drop, HW, coef, (T*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -875,7 +967,9 @@ int bn_bwd_impl(const void* g, long long ldg, const void* z, long long ldz, int 
 
 extern "C" int64_t dg_bn_workspace(int M, int C) {
   if (M <= 0 || C <= 0) return DG_ERR_INVALID;
-  return ((int64_t)std::max(bn_nblk(M), pool_nblk(M / 4)) * 3 + 3) * C * 4;
+  // partials [nblk][3][C], coef [3][C], and for the pair entries the max |g'| rows [nblk][C] and the
+  // bound partials [C / 16]
+  return ((int64_t)std::max(bn_nblk(M), pool_nblk(M / 4)) * 4 + 4) * C * 4 + 1024;
 }
 
 // C/V must divide NT (power of two <= 256): every thread then owns one channel chunk.
@@ -980,11 +1074,11 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
   if (dtype == DG_BF16) {
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz, amax);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   } else if (dtype == DG_F16) {
     const long long total = (long long)M * (C / 8);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   } else if (ew_wide(amax, true)) {
     const long long total = (long long)M * (C / 4);
     hipLaunchKernelGGL((bn_bwd_apply<float, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st,
@@ -994,7 +1088,7 @@ extern "C" int dg_bn_bwd_from_part(int dtype, const float* part, int nblk, const
     const long long total = (long long)M * (C / 4);
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
-                       (float*)dz, lddz, amax);
+                       (float*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   }
   DG_CHECK_LAUNCH();
   return DG_OK;
@@ -1055,6 +1149,75 @@ extern "C" int dg_bn_apply_pool(int dtype, const void* z, int64_t ldz, int N, in
   else
     hipLaunchKernelGGL(bn_apply_pool_kernel<float>, dim3(ew_grid(total)), dim3(NT), 0, st, (const float*)z, ldz, H,
                        W, Mp, C, scale, shift, act, drop, H * W, (float*)y, ldy, (float*)yp, ldyp, amax);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// dg_bn_bwd (f32, train-mode statistics over count pixels, no dropout) that also writes the f16 x3 pair
+// image of dz for the dgrad (include/dgvcc.h): bn_bwd_partial's max |g'| rows -> bn_bwd_finalize's bound
+// partials -> bn_bwd_apply PAIR
+extern "C" int dg_bn_bwd_pair(const float* g, int64_t ldg, const float* z, int64_t ldz, int M, int C,
+                              const float* gamma, const float* save_mean, const float* save_invstd,
+                              const float* scale, const float* shift, int act, double count, float* dz,
+                              int64_t lddz, float* dgamma, float* dbeta, float* dbias, void* workspace, float* amax,
+                              void* pair, float* pbound, void* stream) {
+  DG_REQUIRE(g && z && dz && workspace && save_mean && save_invstd && scale && shift && pair && pbound && M > 0 &&
+             C > 0 && count >= 1.0 && (act == 0 || act == 1));
+  DG_SUPPORTED(C % 32 == 0 && C <= 4096 && EW_WIDE % (C / 4) == 0 && BN_SHAPE_OK(DG_F32, C, ldg) &&
+               BN_SHAPE_OK(DG_F32, C, ldz) && BN_SHAPE_OK(DG_F32, C, lddz));
+  hipStream_t st = (hipStream_t)stream;
+  const int nblk = bn_nblk(M);
+  const int ppb = dg_cdiv(M, nblk);
+  float* part = (float*)workspace;
+  float* coef = part + (long long)nblk * 3 * C;
+  float* gpart = coef + 3 * C;
+  float* bpart = gpart + (long long)nblk * C;
+  hipLaunchKernelGGL(bn_bwd_partial<float>, dim3(nblk), dim3(NT), 0, st, g, ldg, z, ldz, M, C, ppb, save_mean,
+                     save_invstd, scale, shift, act, (const float*)nullptr, 1, part, gpart);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, M, C, gamma, save_invstd,
+                     dgamma, dbeta, dbias, coef, gpart, bpart, count);
+  DG_CHECK_LAUNCH();
+  { const int zr = zero_amax(amax, true, C, st); if (zr != DG_OK) return zr; }
+  const long long total = (long long)M * (C / 4);
+  hipLaunchKernelGGL((bn_bwd_apply<float, 1, EW_WIDE, 1>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st, g, ldg,
+                     z, ldz, M, C, save_mean, save_invstd, scale, shift, act, (const float*)nullptr, 1, coef, dz, lddz,
+                     amax, bpart, dg_cdiv(C, 16), (unsigned char*)pair, pbound);
+  DG_CHECK_LAUNCH();
+  return DG_OK;
+}
+
+// dg_bn_bwd_pool (f32, no dropout) with the pair image of dz (as dg_bn_bwd_pair)
+extern "C" int dg_bn_bwd_pool_pair(const float* gp, int64_t ldgp, const float* gd, int64_t ldgd, const float* z,
+                                   int64_t ldz, int N, int H, int W, int C, const float* gamma, const float* save_mean,
+                                   const float* save_invstd, const float* scale, const float* shift, int act,
+                                   double count, float* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
+                                   void* workspace, float* amax, void* pair, float* pbound, void* stream) {
+  DG_REQUIRE(gp && z && dz && workspace && save_mean && save_invstd && scale && shift && pair && pbound);
+  DG_REQUIRE(N > 0 && H > 1 && W > 1 && C > 0 && count >= 1.0 && (act == 0 || act == 1));
+  DG_SUPPORTED(H % 2 == 0 && W % 2 == 0 && (long long)N * H * W < (1LL << 31) && C % 32 == 0 && C <= 4096 &&
+               EW_WIDE % (C / POOL_V) == 0 && BN_SHAPE_OK(DG_F32, C, ldgp) && BN_SHAPE_OK(DG_F32, C, ldz) &&
+               BN_SHAPE_OK(DG_F32, C, lddz) && (!gd || BN_SHAPE_OK(DG_F32, C, ldgd)) && NT % (C / POOL_V) == 0);
+  hipStream_t st = (hipStream_t)stream;
+  const long long M = (long long)N * H * W, Mp = M / 4;
+  const int nblk = pool_nblk(Mp);
+  const long long ppb = (Mp + nblk - 1) / nblk;
+  float* part = (float*)workspace;
+  float* coef = part + (long long)nblk * 3 * C;
+  float* gpart = coef + 3 * C;
+  float* bpart = gpart + (long long)nblk * C;
+  hipLaunchKernelGGL(bn_pool_bwd_partial<float>, dim3(nblk), dim3(NT), 0, st, gp, ldgp, gd, ldgd, z, ldz, H, W, Mp, C,
+                     ppb, save_mean, save_invstd, scale, shift, act, (const float*)nullptr, H * W, part, gpart);
+  DG_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bn_bwd_finalize, dim3(dg_cdiv(C, 16)), dim3(NT), 0, st, part, nblk, (int)M, C, gamma, save_invstd,
+                     dgamma, dbeta, dbias, coef, gpart, bpart, count);
+  DG_CHECK_LAUNCH();
+  { const int zr = zero_amax(amax, true, C, st); if (zr != DG_OK) return zr; }
+  const long long total = Mp * (C / POOL_V);
+  hipLaunchKernelGGL((bn_pool_bwd_apply<float, EW_WIDE, 1>), dim3(wide_grid(total, 512)), dim3(EW_WIDE), 0, st, gp,
+                     ldgp, gd, ldgd, z, ldz, H, W, Mp, C, save_mean, save_invstd, scale, shift, act,
+                     (const float*)nullptr, H * W, coef, dz, lddz, amax, bpart, dg_cdiv(C, 16), (unsigned char*)pair,
+                     pbound);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }
@@ -1252,10 +1415,10 @@ extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const
   const long long total = (long long)M * (C / (DG_IS16(dtype) ? 8 : 4));
   if (dtype == DG_BF16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<bf16, 2> : bn_bwd_apply<bf16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const bf16*)g, ldg, (const bf16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz, amax);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (bf16*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   else if (dtype == DG_F16)
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<f16, 2> : bn_bwd_apply<f16, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const f16*)g, ldg, (const f16*)z,
-                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax);
+                       ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef, (f16*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   else if (ew_wide(amax, true))
     hipLaunchKernelGGL((bn_bwd_apply<float, 1, EW_WIDE>), dim3(wide_grid(total, 256)), dim3(EW_WIDE), 0, st,
                        (const float*)g, ldg, (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act,
@@ -1263,7 +1426,7 @@ extern "C" int dg_bn_bwd_apply_coef(int dtype, const void* g, int64_t ldg, const
   else
     hipLaunchKernelGGL((ew_unroll() == 2 ? bn_bwd_apply<float, 2> : bn_bwd_apply<float, 1>), dim3(cs_grid(total)), dim3(NT), 0, st, (const float*)g, ldg,
                        (const float*)z, ldz, M, C, save_mean, save_invstd, scale, shift, act, drop, HW, coef,
-                       (float*)dz, lddz, amax);
+                       (float*)dz, lddz, amax, nullptr, 0, nullptr, nullptr);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

@@ -237,6 +237,11 @@ class ConvLayer:
         if tape is not None:
             tape[self] = (x, z, stats, wp, drop, training)
 
+    def _dz_pair(self, gx) -> bool:
+        """fp32 BN backward writes dz's pair image for the dgrad (_BN_PAIR): where a dgrad follows and
+        takes the pre-split forward (its output, this layer's input, has >= 128 channels)."""
+        return _BN_PAIR and gx is not None and not self.first and self.Cin >= 128
+
     def _apply(self, z: Act, stats, out: Act | None, drop, pool: Act | None, pair: bool = False):
         if pool is not None:
             K.bn_apply_pool(z, stats, self.act, out, pool, drop, pair=pair)
@@ -296,12 +301,14 @@ class ConvLayer:
         elif g_pool is not None:
             if self.bn is None:
                 raise RuntimeError("pooled backward needs a BatchNorm layer")
-            K.bn_bwd_pool(g_pool, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
+            # fp32: the dgrad that follows reads dz's pair image (_BN_PAIR)
+            K.bn_bwd_pool(g_pool, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop,
+                          pair=self._dz_pair(gx))
         elif pre is not None:
             K.bn_bwd_from_part(pre, g, z, gamma, stats, self.act, dz, dgamma, dbeta, dbias, drop)
         else:
             K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta,
-                     dbias, drop)
+                     dbias, drop, pair=self._dz_pair(gx) and self.bn is not None)
         dw = torch.empty_like(self.conv.weight, dtype=torch.float32)
         if self.first:
             dwcol = torch.empty((self.Cout, 64, 1, 1), dtype=torch.float32, device=dev)
@@ -321,6 +328,8 @@ class ConvLayer:
                 if res is None:
                     K.conv_dgrad(dz, wp, self.Cin, self.R, self.pad, gx, accumulate=accumulate_gx,
                                  wflip=self._flip(wp))
+        if dz is not None:
+            dz.pair = None
         grads = {self.conv.weight: dw}
         if self.conv.bias is not None:
             grads[self.conv.bias] = dbias if self.bn is not None else dbeta

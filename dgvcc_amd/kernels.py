@@ -552,11 +552,24 @@ def bn_apply(z: Act, stats, act: int, y: Act, drop: torch.Tensor | None = None, 
 
 
 def bn_bwd(g: Act, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta, dbias=None,
-           drop: torch.Tensor | None = None):
+           drop: torch.Tensor | None = None, pair: bool = False, count: int | None = None):
+    """pair (f32, train-mode batch statistics over `count` pixels, default z.M; no dropout): also the
+    f16 x3 pair image of dz for the dgrad (dg_bn_bwd_pair), attached as dz.pair."""
     ws = query("dg_bn_workspace", z.M, z.C)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
     st = stats if stats is not None else (None, None, None, None)  # None: no normalisation
     am = _amax_out(dz)
+    dz.pair = None
+    if pair and stats is not None and z.dt == 0 and drop is None and z.C % 32 == 0:
+        img, bound = _pair_bufs(z.M, z.C, z.buf.device)
+        r = lib_call_status("dg_bn_bwd_pair", g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma), ptr(st[0]),
+                            ptr(st[1]), ptr(st[2]), ptr(st[3]), act, float(count or z.M), dz.ptr, dz.ld,
+                            ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), ptr(am), ptr(img), ptr(bound), stream())
+        if r == 0:
+            dz.pair = (img, bound)
+            return
+        if r != -2:
+            raise DGError(f"dg_bn_bwd_pair failed with status {r}")
     call("dg_bn_bwd", z.dt, g.ptr, g.ld, z.ptr, z.ld, z.M, z.C, ptr(gamma), ptr(st[0]),
          ptr(st[1]), ptr(st[2]), ptr(st[3]), act, ptr(drop), z.H * z.W, dz.ptr, dz.ld,
          ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), ptr(am), stream())
@@ -586,12 +599,25 @@ def bn_apply_pool(z: Act, stats, act: int, y: Act | None, yp: Act, drop: torch.T
 
 
 def bn_bwd_pool(gp: Act, gd: Act | None, z: Act, gamma, stats, act: int, dz: Act, dgamma, dbeta,
-                dbias=None, drop: torch.Tensor | None = None):
+                dbias=None, drop: torch.Tensor | None = None, pair: bool = False, count: int | None = None):
     """BN backward with the upstream gradient = maxpool2x2 backward of gp (argmax recomputed
-    from z) [+ the direct gradient gd]."""
+    from z) [+ the direct gradient gd].  pair: as bn_bwd (dg_bn_bwd_pool_pair)."""
     ws = query("dg_bn_workspace", z.M, z.C)
     work = torch.empty(ws // 4 + 1, dtype=torch.float32, device=z.buf.device)
     am = _amax_out(dz)
+    dz.pair = None
+    if pair and z.dt == 0 and drop is None and z.C % 32 == 0:
+        img, bound = _pair_bufs(z.M, z.C, z.buf.device)
+        r = lib_call_status("dg_bn_bwd_pool_pair", gp.ptr, gp.ld, gd.ptr if gd is not None else None,
+                            gd.ld if gd is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(gamma),
+                            ptr(stats[0]), ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, float(count or z.M),
+                            dz.ptr, dz.ld, ptr(dgamma), ptr(dbeta), ptr(dbias), ptr(work), ptr(am), ptr(img),
+                            ptr(bound), stream())
+        if r == 0:
+            dz.pair = (img, bound)
+            return
+        if r != -2:
+            raise DGError(f"dg_bn_bwd_pool_pair failed with status {r}")
     call("dg_bn_bwd_pool", z.dt, gp.ptr, gp.ld, gd.ptr if gd is not None else None,
          gd.ld if gd is not None else 0, z.ptr, z.ld, z.N, z.H, z.W, z.C, ptr(gamma), ptr(stats[0]),
          ptr(stats[1]), ptr(stats[2]), ptr(stats[3]), act, ptr(drop), dz.ptr, dz.ld, ptr(dgamma),

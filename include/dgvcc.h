@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 7 /* 7: dg_bn_apply_pair / dg_bn_apply_pool_pair write the f16 x3 pair image of their f32 output and dg_conv_fwd_pair reads it; 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 7 /* 7: dg_bn_apply_pair / dg_bn_apply_pool_pair / dg_bn_bwd_pair / dg_bn_bwd_pool_pair write the f16 x3 pair image of their f32 output and dg_conv_fwd_pair reads it (dg_bn_workspace grew for the backward ones); 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -257,6 +257,16 @@ int dg_bn_bwd(int dtype, const void* g, int64_t ldg, const void* z, int64_t ldz,
               const float* scale, const float* shift, int act, const float* drop, int HW,
               void* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
               void* workspace, float* amax, void* stream);
+/* dg_bn_bwd (f32, train-mode statistics over count pixels, no dropout) that also writes pair, the f16
+ * x3 image of dz the dgrad that follows reads (dg_conv_fwd_pair; layout as dg_bn_apply_pair), and
+ * *pbound: the partial pass also keeps max |g'| per channel, and the scale comes from
+ * max_c |k1_c| max |g'_c| + |k2_c| sqrt(count) + |k3_c| >= max |dz| (dz = k1 g' - k2 xhat - k3,
+ * |xhat| <= sqrt(count)).  Workspace: dg_bn_workspace(M, C). */
+int dg_bn_bwd_pair(const float* g, int64_t ldg, const float* z, int64_t ldz, int M, int C,
+                   const float* gamma, const float* save_mean, const float* save_invstd,
+                   const float* scale, const float* shift, int act, double count, float* dz,
+                   int64_t lddz, float* dgamma, float* dbeta, float* dbias, void* workspace,
+                   float* amax, void* pair, float* pbound, void* stream);
 /* BN-backward finalize on caller-made partial sums part[nblk][3][C] = (sum g', sum g' xhat,
  * sum xhat): coef[3][C] (dz = k1 g' - k2 xhat - k3) and dgamma/dbeta/dbias (may be NULL). */
 int dg_bn_bwd_finalize_part(const float* part, int nblk, int M, int C, const float* gamma,
@@ -290,6 +300,12 @@ int dg_bn_bwd_pool(int dtype, const void* gp, int64_t ldgp, const void* gd, int6
                    const float* save_mean, const float* save_invstd, const float* scale,
                    const float* shift, int act, const float* drop, void* dz, int64_t lddz,
                    float* dgamma, float* dbeta, float* dbias, void* workspace, float* amax, void* stream);
+/* dg_bn_bwd_pool (f32, no dropout) with the pair image of dz, as dg_bn_bwd_pair */
+int dg_bn_bwd_pool_pair(const float* gp, int64_t ldgp, const float* gd, int64_t ldgd, const float* z,
+                        int64_t ldz, int N, int H, int W, int C, const float* gamma, const float* save_mean,
+                        const float* save_invstd, const float* scale, const float* shift, int act,
+                        double count, float* dz, int64_t lddz, float* dgamma, float* dbeta, float* dbias,
+                        void* workspace, float* amax, void* pair, float* pbound, void* stream);
 
 /* Coefficients of the BN backward without the dz pass: coef[3][C] = (k1, k2, k3) with
  * dz = k1*act'(g) - k2*xhat - k3 (the bn_bwd_apply arithmetic), plus dgamma/dbeta/dbias.

@@ -1054,3 +1054,60 @@ def test_bn_pair_image_and_conv(dev, N, H, W, C, Cout, pool):
     h, e = errs[2], errs[0]
     print(f"pair worst {h.max().item():.3e} exact worst {e.max().item():.3e}")
     assert (h <= 2 * e + 1e-7).all(), (h.max().item(), e.max().item())
+
+
+@pytest.mark.parametrize("N,H,W,C,Cin,pool", [(2, 128, 128, 256, 256, False), (2, 64, 128, 512, 256, False),
+                                              (2, 128, 256, 128, 256, True)])
+def test_bn_bwd_pair_image_and_dgrad(dev, N, H, W, C, Cin, pool):
+    """fp32 BN backward writing the dgrad's f16 x3 pair image of dz (dg_bn_bwd_pair /
+    dg_bn_bwd_pool_pair): dz, dgamma, dbeta and the maxima bit-identical to dg_bn_bwd(_pool); the bound
+    bounds max |dz| and is max_c |k1| max |g'| + |k2| sqrt(M) + |k3| (k from dgamma / dbeta); the image
+    is the split of dz at the bound's scale; the dgrad reading it has per-channel error within 2x the
+    exact f32 MFMA path's against float64."""
+    K = _k()
+    g = torch.Generator().manual_seed(37)
+    z = K.Act(to_nhwc(torch.randn(N, C, H, W, generator=g) * 2 - 0.5).to(dev))
+    gam = (torch.rand(C, generator=g) + 0.5).to(dev)
+    bet = (torch.randn(C, generator=g) * 0.3).to(dev)
+    stats = K.bn_fwd_train(z, gam, bet, torch.zeros(C, device=dev), torch.ones(C, device=dev), 0.1, 1e-5)
+    Ho, Wo = (H // 2, W // 2) if pool else (H, W)
+    gy = K.Act(to_nhwc(torch.randn(N, C, Ho, Wo, generator=g) * 1e-3).to(dev))
+    outs = {}
+    for pr in (True, False):
+        dz = K.Act(K.nhwc(N, H, W, C, torch.float32, dev))
+        dgam, dbet = torch.empty(C, device=dev), torch.empty(C, device=dev)
+        if pool:
+            K.bn_bwd_pool(gy, None, z, gam, stats, K.ACT_RELU, dz, dgam, dbet, pair=pr)
+        else:
+            K.bn_bwd(gy, z, gam, stats, K.ACT_RELU, dz, dgam, dbet, pair=pr)
+        outs[pr] = (dz, dgam, dbet)
+    torch.cuda.synchronize()
+    (d1, a1, b1), (d0, a0, b0) = outs[True], outs[False]
+    assert torch.equal(d1.buf, d0.buf) and torch.equal(a1, a0) and torch.equal(b1, b0)
+    assert torch.equal(d1.amax, d0.amax) and d1.pair is not None and d0.pair is None
+    img, bound = d1.pair
+    bnd = bound.item()
+    assert bnd >= d1.buf.abs().max().item()
+    ref_img = _pair_image_ref(d1.buf.reshape(d1.M, C), bnd)
+    assert torch.equal(img.view(torch.float16).view(d1.M, C // 32, 64), ref_img)
+    # the dgrad on the pair image vs the exact f32 MFMA path, against float64
+    w = torch.randn(C, Cin, 3, 3, generator=g) / (9 * C) ** 0.5
+    wp = K.pack_weight(w.to(dev), torch.float32)
+    dx64 = torch.nn.grad.conv2d_input((N, Cin, H, W), w.double(), to_nchw(d1.buf).double().cpu(), padding=1)
+    prev = K.lib_call_status("dg_get_f32_math")
+    errs = {}
+    try:
+        for m in (2, 0):
+            K.call("dg_set_f32_math", m)
+            src = K.Act(d1.buf)
+            src.amax, src.pair = d1.amax, (d1.pair if m == 2 else None)
+            dx = K.Act(K.nhwc(N, H, W, Cin, torch.float32, dev))
+            K.conv_dgrad(src, wp, Cin, 3, 1, dx)
+            torch.cuda.synchronize()
+            errs[m] = _chan_err(to_nchw(dx.buf), dx64, 1)
+    finally:
+        K.call("dg_set_f32_math", prev)
+    h, e = errs[2], errs[0]
+    print(f"pair dgrad worst {h.max().item():.3e} exact worst {e.max().item():.3e} bound/max "
+          f"{bnd / d1.buf.abs().max().item():.1f}")
+    assert (h <= 2 * e + 1e-7).all(), (h.max().item(), e.max().item())
