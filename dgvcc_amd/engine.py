@@ -437,7 +437,8 @@ class CatConvLayer(ConvLayer):
                                        bn.running_mean, bn.running_var, _bn_momentum(bn), bn.eps)
         else:
             stats = bn_eval_cached(self, bn)
-        K.bn_apply(z, stats, self.act, out, drop)
+        K.bn_apply(z, stats, self.act, out, drop,
+                   pair=_BN_PAIR and self.pair_out and training and bn is not None and pg is None)
         if tape is not None:
             tape[self] = (x, z, stats, wps, drop, training)
 
@@ -458,7 +459,8 @@ class CatConvLayer(ConvLayer):
         if pg is not None:
             SB.backward(self.bn, pg, g, z, stats, self.act, dz, dgamma, dbeta, dbias, drop=drop)
         else:
-            K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta, dbias, drop)
+            K.bn_bwd(g, z, gamma, stats if self.bn is not None else None, self.act, dz, dgamma, dbeta, dbias, drop,
+                     pair=self._dz_pair(gx) and self.bn is not None)  # read by part 0's dgrad
         gzs = [dz]
         for part, sc in zip(x.parts[1:], CatParts.SCALES[1:]):  # U^T dz at the part's resolution
             gk = Act(K.nhwc(part.N, part.H, part.W, self.Cout, dz.buf.dtype, dev))
@@ -475,6 +477,7 @@ class CatConvLayer(ConvLayer):
             if gx is not None:
                 K.conv_dgrad(gzs[k], wps[k], part.C, 1, 0, gx.parts[k], accumulate=accumulate_gx)
             lo += part.C
+        dz.pair = None
         grads = {self.conv.weight: dw}
         if self.bn is not None:
             grads.update({self.bn.weight: dgamma, self.bn.bias: dbeta})
