@@ -539,7 +539,8 @@ class FeaturePlan:
             l.scope = "dec"
         # outputs read next by a conv forward (the pooled ones for E[1], E[3], E[6], E[9]); not the stem
         # output (its consumer is the Cout = 64 3-tap kernel), nor y3 / y2 / y1 (upsampled / heads)
-        for i in (1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12):
+        # (with inorm the stage outputs E[6], E[9], E[12] go to the InstanceNorm instead)
+        for i in (1, 2, 3, 4, 5, 7, 8, 10, 11) + (() if inorm else (6, 9, 12)):
             self.enc[i].pair_out = True
         for i in (0, 2, 4):
             self.dec[i].pair_out = True
