@@ -408,8 +408,17 @@ __global__ __launch_bounds__(NT) void bn_bwd_finalize(const float* __restrict__ 
   const int c = blockIdx.x * 16 + cl;
   double a = 0.0, b = 0.0, d = 0.0;
   float gmx = 0.f;
-  if (gpart && c < C)
-    for (int k = r; k < nblk; k += 16) gmx = fmaxf(gmx, gpart[(long long)k * C + c]);
+  if (gpart && c < C) {
+    int k = r;
+    for (; k + 48 < nblk; k += 64) {  // four rows in flight (as the sums below)
+      float v4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v4[u] = gpart[(long long)(k + 16 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) gmx = fmaxf(gmx, v4[u]);
+    }
+    for (; k < nblk; k += 16) gmx = fmaxf(gmx, gpart[(long long)k * C + c]);
+  }
   shg[r][cl] = gmx;
   if (c < C) {
     int k = r;
