@@ -343,6 +343,35 @@ __global__ __launch_bounds__(NT) void upsample_fwd_kernel(const T* __restrict__ 
   }
 }
 
+// C = 1 maps (the density heads' x4 / the trunks' x16 upsample): 4 consecutive output columns per
+// thread, one row tap, one 4-element store (the per-element arithmetic of upsample_fwd_kernel, so the
+// values are identical); a channel-per-thread grid spent most of its issue on index math per 4-B store.
+template <typename T>
+__global__ __launch_bounds__(NT) void upsample_fwd_c1_kernel(const T* __restrict__ x, long long ldx, int N, int H,
+                                                             int W, int scale, int mode, T* __restrict__ y) {
+  const int Ho = H * scale, Wo = W * scale, q4 = Wo / 4;
+  const int total = N * Ho * q4;  // < 2^31 (checked by the launcher)
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int qq = i % q4;
+    const int t = i / q4;
+    const int ho = t % Ho, n = t / Ho;
+    const Tap th = src_tap(ho, H, Ho, scale, mode);
+    const float h1l = th.l1, h0l = 1.f - th.l1;
+    const T* r0 = x + ((long long)n * H + th.i0) * W * ldx;
+    const T* r1 = x + ((long long)n * H + th.i1) * W * ldx;
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const Tap tw = src_tap(qq * 4 + e, W, Wo, scale, mode);
+      const float w1l = tw.l1, w0l = 1.f - tw.l1;
+      const float a = to_f(r0[tw.i0 * ldx]), b = to_f(r0[tw.i1 * ldx]);
+      const float c = to_f(r1[tw.i0 * ldx]), d = to_f(r1[tw.i1 * ldx]);
+      o[e] = h0l * (w0l * a + w1l * b) + h1l * (w0l * c + w1l * d);
+    }
+    st4(y + (long long)t * Wo + qq * 4, o);
+  }
+}
+
 // Range of output indices whose taps may touch input index i (superset).
 __device__ __forceinline__ void out_range(int i, int in, int out, int scale, int mode, int& lo, int& hi) {
   if (mode == 1) {
@@ -419,6 +448,69 @@ __global__ __launch_bounds__(NT) void upsample_bwd_kernel(const T* __restrict__ 
     }
     if constexpr (V == 1) dst[0] = from_f<T>(acc[0]);
     else stv(dst, acc);
+  }
+}
+
+// C = 1 bilinear backward (modes 0 / 1), separable: one block per (image, input row ih, tile of TW
+// input columns).  The block first sums each output column of the tile's span over the output rows
+// that touch ih (their weights wh formed once, in LDS), coalesced along the row, then every thread
+// sums its input column's window of those column sums with its ww.  gx = sum_ow ww * (sum_oh wh * g):
+// the same terms as upsample_bwd_kernel's flat sum over (oh, ow) of (wh * ww) * g, grouped by column
+// (rounding differs at the f32 ulp level; ATen's own backward adds them with atomics in no fixed order).
+// The per-pixel form re-derived every (oh, ow) tap of a 36 x 36 window per input pixel for the x16
+// align-corners upsample.  Zero weights are skipped, as there (a NaN/Inf gradient where no tap reads
+// it is not propagated).
+constexpr int UPC1_SPAN = 8192, UPC1_KH = 128;
+template <typename T>
+__global__ __launch_bounds__(NT) void upsample_bwd_c1_kernel(const T* __restrict__ gy, long long ldgy,
+                                                             const T* __restrict__ gy2, long long ldgy2, int N, int H,
+                                                             int W, int scale, int mode, int TW, T* __restrict__ gx,
+                                                             long long ldgx, int accumulate) {
+  __shared__ float wh[UPC1_KH];
+  __shared__ float cs[UPC1_SPAN];
+  const int Ho = H * scale, Wo = W * scale;
+  const int n = blockIdx.y / H, ih = blockIdx.y - n * H;
+  const int iw0 = blockIdx.x * TW, iw1 = min(W, iw0 + TW);
+  int hlo, hhi, wlo, whi, dummy;
+  out_range(ih, H, Ho, scale, mode, hlo, hhi);
+  out_range(iw0, W, Wo, scale, mode, wlo, dummy);
+  out_range(iw1 - 1, W, Wo, scale, mode, dummy, whi);
+  const int KH = min(hhi - hlo, UPC1_KH), span = min(whi - wlo, UPC1_SPAN);  // launcher bounds both
+  for (int k = threadIdx.x; k < KH; k += NT) wh[k] = tap_weight(src_tap(hlo + k, H, Ho, scale, mode), ih);
+  __syncthreads();
+  // out_range is a superset: read only the rows from the first to the last nonzero weight
+  int k0 = KH, k1 = -1;
+  for (int k = 0; k < KH; ++k)
+    if (wh[k] != 0.f) {
+      k0 = min(k0, k);
+      k1 = k;
+    }
+  const long long row0 = (long long)n * Ho + hlo;
+  for (int j = threadIdx.x; j < span; j += NT) {
+    const long long op0 = row0 * Wo + wlo + j;
+    float s = 0.f;
+#pragma unroll 4
+    for (int k = k0; k <= k1; ++k) {
+      const long long op = op0 + (long long)k * Wo;
+      float g = to_f(gy[op * ldgy]);
+      if (gy2) g += to_f(gy2[op * ldgy2]);
+      const float w = wh[k];
+      s = w != 0.f ? fmaf(w, g, s) : s;
+    }
+    cs[j] = s;
+  }
+  __syncthreads();
+  for (int iw = iw0 + threadIdx.x; iw < iw1; iw += NT) {
+    int lo, hi;
+    out_range(iw, W, Wo, scale, mode, lo, hi);
+    float acc = 0.f;
+    for (int ow = lo; ow < hi; ++ow) {
+      const float w = tap_weight(src_tap(ow, W, Wo, scale, mode), iw);
+      acc = w != 0.f ? fmaf(w, cs[ow - wlo], acc) : acc;
+    }
+    T* dst = gx + ((long long)n * H * W + (long long)ih * W + iw) * ldgx;
+    if (accumulate) acc += to_f(dst[0]);
+    dst[0] = from_f<T>(acc);
   }
 }
 
@@ -529,7 +621,10 @@ int up_fwd(const void* x, long long ldx, int N, int H, int W, int C, int scale, 
   constexpr int V = 16 / (int)sizeof(T);
   const bool vec = (C % V == 0) && (ldx % V == 0) && (ldy % V == 0);
   const long long total = (long long)N * H * scale * W * scale * (vec ? C / V : C);
-  if (vec)
+  if (C == 1 && ldy == 1 && (W * scale) % 4 == 0 && total < (1LL << 31) && !getenv("DGVCC_UP_C1_OFF"))
+    hipLaunchKernelGGL(upsample_fwd_c1_kernel<T>, dim3(ew_grid(total / 4)), dim3(NT), 0, st, (const T*)x, ldx, N, H, W,
+                       scale, mode, (T*)y);
+  else if (vec)
     hipLaunchKernelGGL((upsample_fwd_kernel<T, V>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)x, ldx, N, H, W,
                        C, scale, mode, (T*)y, ldy);
   else
@@ -607,7 +702,18 @@ int up_bwd(const void* gy, long long ldgy, const void* gy2, long long ldgy2, int
   constexpr int V = 16 / (int)sizeof(T);
   const bool vec = (C % V == 0) && (ldgy % V == 0) && (ldgx % V == 0) && (!gy2 || ldgy2 % V == 0);
   const long long total = (long long)N * H * W * (vec ? C / V : C);
-  if (vec && mode == 0 && (scale == 2 || scale == 4) && total < (1LL << 31) &&
+  int tw = 0;  // upsample_bwd_c1_kernel's input-column tile: the span and row window fit its LDS
+  if (C == 1 && mode != 2 && (long long)N * H <= 65535 && !getenv("DGVCC_UP_C1_OFF")) {
+    const double rw = mode == 1 ? (W > 1 ? (double)(W * scale - 1) / (W - 1) : (double)W * scale) : scale;
+    const double rh = mode == 1 ? (H > 1 ? (double)(H * scale - 1) / (H - 1) : (double)H * scale) : scale;
+    if (3.0 * rh + 8.0 <= UPC1_KH)
+      for (tw = std::min(W, NT); tw > 0 && (tw + 3.0) * rw + 8.0 > UPC1_SPAN; tw /= 2) {
+      }
+  }
+  if (tw > 0)
+    hipLaunchKernelGGL(upsample_bwd_c1_kernel<T>, dim3(dg_cdiv(W, tw), N * H), dim3(NT), 0, st, (const T*)gy, ldgy,
+                       (const T*)gy2, ldgy2, N, H, W, scale, mode, tw, (T*)gx, ldgx, acc);
+  else if (vec && mode == 0 && (scale == 2 || scale == 4) && total < (1LL << 31) &&
       (long long)N * H * scale * W * scale < (1LL << 31)) {
     if (scale == 2)
       hipLaunchKernelGGL((upsample_bwd_bl_kernel<T, V, 2>), dim3(ew_grid(total)), dim3(NT), 0, st, (const T*)gy, ldgy,

@@ -4,6 +4,7 @@ f32 (parity mode) must agree to ~1e-5 relative (exact-f32 MFMA, different
 summation order); bf16 (perf mode) is compared against the CPU op applied to
 the same bf16-rounded inputs with a bf16-output tolerance.
 """
+import os
 import pytest
 import torch
 import torch.nn.functional as F
@@ -239,6 +240,46 @@ def test_upsample(dev, dtype, scale, mode, C):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert relerr(to_nchw(y.buf.float()), yr.detach()) < tol
     assert relerr(to_nchw(gx.buf.float()), xr.grad) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("scale,mode,N,H,W", [(4, 0, 2, 24, 40), (16, 1, 2, 6, 10), (2, 1, 1, 9, 7), (8, 0, 1, 5, 12),
+                                              (16, 1, 1, 3, 600), (4, 0, 1, 2, 1100)])
+def test_upsample_c1(dev, dtype, scale, mode, N, H, W):
+    """C = 1 maps (upsample_fwd_c1_kernel / upsample_bwd_c1_kernel, the latter in several input-column tiles
+    for W = 600 / 1100): forward and backward (with a second gradient and accumulation) against torch, and
+    against the per-pixel kernels (DGVCC_UP_C1_OFF=1), both within f32 rounding (the compiler contracts the
+    same expression into different FMAs in the two forms)."""
+    K = _k()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(N, 1, H, W, generator=g).to(dtype).float()
+    gy = torch.randn(N, 1, H * scale, W * scale, generator=g).to(dtype).float()
+    gy2 = torch.randn(N, 1, H * scale, W * scale, generator=g).to(dtype).float()
+    g0 = torch.randn(N, 1, H, W, generator=g).to(dtype).float()
+    xr = x.clone().requires_grad_(True)
+    yr = F.interpolate(xr, scale_factor=scale, mode="bilinear", align_corners=(mode == 1))
+    yr.backward(gy + gy2)
+    outs = []
+    for off in (False, True):
+        if off:
+            os.environ["DGVCC_UP_C1_OFF"] = "1"
+        try:
+            xd = K.Act(to_nhwc(x).to(dev, dtype))
+            y = K.Act(K.nhwc(N, H * scale, W * scale, 1, dtype, dev))
+            K.upsample_fwd(xd, scale, mode, y)
+            gx = K.Act(to_nhwc(g0).to(dev, dtype))
+            K.upsample_bwd(K.Act(to_nhwc(gy).to(dev, dtype)), scale, mode, gx,
+                           gy2=K.Act(to_nhwc(gy2).to(dev, dtype)), accumulate=True)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("DGVCC_UP_C1_OFF", None)
+        outs.append((to_nchw(y.buf.float()).cpu(), to_nchw(gx.buf.float()).cpu()))
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert relerr(outs[0][0], yr.detach()) < tol
+    assert relerr(outs[0][1], xr.grad + g0) < tol
+    close = 2e-6 if dtype == torch.float32 else 1e-2
+    assert relerr(outs[0][0], outs[1][0]) < close
+    assert relerr(outs[0][1], outs[1][1]) < close
 
 
 @pytest.mark.parametrize("act", [0, 1, 2])
