@@ -205,15 +205,29 @@ __global__ __launch_bounds__(NT) void adamw_kernel(float* __restrict__ p, const 
   }
 }
 
-__global__ void gather_flat_kernel(const float* const* __restrict__ ptrs, const int64_t* __restrict__ offsets,
-                                   int count, float* __restrict__ flat) {
-  // one block-row per tensor
-  for (int t = blockIdx.y; t < count; t += gridDim.y) {
+// One block per GATHER_CHUNK elements of the flat buffer: the block finds the tensor holding its first
+// element (binary search over the offsets, uniform) and copies the chunk tensor by tensor.  The earlier
+// grid of 64 blocks per tensor left the large tensors (2.4M elements) to 16k threads looping over
+// dependent 4-B copies: 0.13 ms for the ResNet-50 gradients, ~1 TB/s.
+constexpr int GATHER_CHUNK = 4096;
+__global__ __launch_bounds__(NT) void gather_flat_kernel(const float* const* __restrict__ ptrs,
+                                                         const int64_t* __restrict__ offsets, int count,
+                                                         float* __restrict__ flat) {
+  const long long c0 = blockIdx.x * (long long)GATHER_CHUNK;
+  if (c0 >= offsets[count]) return;
+  const long long c1 = min((long long)offsets[count], c0 + GATHER_CHUNK);
+  int lo = 0, hi = count - 1;  // last tensor starting at or before c0
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (offsets[mid] <= c0) lo = mid;
+    else hi = mid - 1;
+  }
+  for (int t = lo; t < count && offsets[t] < c1; ++t) {
+    const long long o = offsets[t];
+    const long long b = max(o, c0), e = min((long long)offsets[t + 1], c1);
     const float* src = ptrs[t];
-    const long long beg = offsets[t], len = offsets[t + 1] - beg;
-    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < len;
-         i += (long long)gridDim.x * blockDim.x)
-      flat[beg + i] = src[i];
+#pragma unroll 4
+    for (long long i = b + threadIdx.x; i < e; i += NT) flat[i] = src[i - o];
   }
 }
 
@@ -688,8 +702,9 @@ extern "C" int dg_adamw_step(float* p, const float* g, float* m, float* v, int64
 extern "C" int dg_gather_flat(const float* const* ptrs, const int64_t* offsets, int count, int64_t total,
                               float* flat, void* stream) {
   DG_REQUIRE(ptrs && offsets && flat && count > 0 && total > 0);
-  hipLaunchKernelGGL(gather_flat_kernel, dim3(64, std::min(count, 1024)), dim3(NT), 0, (hipStream_t)stream, ptrs,
-                     offsets, count, flat);
+  // blocks over the whole buffer (the offsets are device-resident); chunks outside this run exit at once
+  hipLaunchKernelGGL(gather_flat_kernel, dim3((unsigned)dg_cdiv(total, (int64_t)GATHER_CHUNK)), dim3(NT), 0,
+                     (hipStream_t)stream, ptrs, offsets, count, flat);
   DG_CHECK_LAUNCH();
   return DG_OK;
 }

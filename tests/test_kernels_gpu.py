@@ -365,6 +365,31 @@ def test_fused_adamw_matches_torch_with_missing_grads(dev):
     assert torch.equal(ours[2].detach().cpu(), base[2]) and torch.equal(ours[3].detach().cpu(), base[3])
 
 
+def test_gather_flat_chunks(dev):
+    """dg_gather_flat (one block per 4096-element chunk, tensor found by binary search): tensors of 0, 1, odd,
+    chunk-straddling and multi-chunk sizes, gathered as two runs into one flat buffer (the optimizer's dead-
+    parameter gaps stay untouched); bit-exact copies."""
+    K = _k()
+    g = torch.Generator().manual_seed(11)
+    sizes = [5, 0, 4096, 1, 4095, 9000, 3, 0, 70001, 17, 4097, 2]
+    ts = [torch.randn(s, generator=g).to(dev) for s in sizes]
+    offs, o = [], 0
+    for s in sizes:
+        offs.append(o)
+        o += s
+    flat = torch.full((o + 100,), -7.0, device=dev)
+    expect = flat.clone()
+    for run in (range(0, 5), range(6, len(sizes))):  # tensor 5 is a dead parameter: its region stays as it was
+        table = torch.tensor([ts[i].data_ptr() for i in run], dtype=torch.int64, device=dev)
+        last = run[-1]
+        dev_offs = torch.tensor([offs[i] for i in run] + [offs[last] + sizes[last]], dtype=torch.int64, device=dev)
+        K.call("dg_gather_flat", K.ptr(table), K.ptr(dev_offs), len(run), flat.numel(), K.ptr(flat), K.stream())
+        for i in run:
+            expect[offs[i]:offs[i] + sizes[i]] = ts[i]
+    torch.cuda.synchronize()
+    assert torch.equal(flat, expect)
+
+
 @pytest.mark.parametrize("case", [(1, 256, 288, 64, 256, 3), (1, 256, 288, 128, 128, 3), (1, 256, 288, 64, 64, 3),
                                   (1, 256, 288, 256, 512, 1), (2, 20, 24, 64, 128, 3), (1, 64, 64, 512, 512, 3)])
 def test_conv_f32_split_math(dev, case):
