@@ -811,14 +811,26 @@ __global__ __launch_bounds__(SNT) void bn_part_merge(const float* __restrict__ p
   const int r0 = blockIdx.y * PMG, r1 = min(nblk, r0 + PMG);
   float n = 0.f, mean = 0.f, m2 = 0.f;
   if (c < C) {
-    for (int b = r0 + rg; b < r1; b += 4) {
-      const float nb = part[b * row + c];
+    // all of this thread's rows loaded up front (the Chan chain below is serial; loads issued
+    // inside it waited one memory latency per row), merged in row order as before
+    constexpr int RPT = PMG / 4;
+    float nbv[RPT], mbv[RPT], m2v[RPT];
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const int b = r0 + rg + 4 * u;
+      const bool in = b < r1;
+      nbv[u] = in ? part[b * row + c] : 0.f;
+      mbv[u] = in ? part[b * row + C + c] : 0.f;
+      m2v[u] = in ? part[b * row + 2 * C + c] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < RPT; ++u) {
+      const float nb = nbv[u];
       if (nb == 0.f) continue;
-      const float mb = part[b * row + C + c];
       const float nt = n + nb;
-      const float d = mb - mean;
+      const float d = mbv[u] - mean;
       mean += d * (nb / nt);
-      m2 += part[b * row + 2 * C + c] + d * d * (n * nb / nt);
+      m2 += m2v[u] + d * d * (n * nb / nt);
       n = nt;
     }
   }

@@ -259,7 +259,17 @@ __global__ __launch_bounds__(256) void sw_inst_stats(const float* __restrict__ p
   const int g = blockIdx.x, n = blockIdx.y, G = C / SWC, t = threadIdx.x;
   float* cov_in = save + (long long)N * C;
   double s = 0.0;
-  for (int k = 0; k < nb; ++k) s += part[(((long long)n * nb + k) * G + g) * 256 + t];
+  const float* pp = part + ((long long)n * nb * G + g) * 256 + t;
+  const long long ks = (long long)G * 256;
+  int k = 0;
+  for (; k + 8 <= nb; k += 8) {  // 8 loads in flight, added in block order (same sum)
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = pp[(k + u) * ks];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; k < nb; ++k) s += pp[k * ks];
   cov_in[((long long)n * G + g) * 256 + t] = (float)(s / HW);
 }
 
@@ -488,10 +498,28 @@ __global__ __launch_bounds__(256) void sw_bwd_small(const float* __restrict__ pa
   const float ci = cov_in[((long long)n * G + g) * 256 + t];
   // reduce partials of this (n, g)
   float gx = 0.f, sg = 0.f;
-  for (int k = 0; k < nb; ++k) {
-    const float* o = part + (((long long)n * nb + k) * G + g) * 272;
-    gx += o[t];
-    if (t < 16) sg += o[256 + t];
+  {
+    const float* o0 = part + ((long long)n * nb * G + g) * 272;
+    const long long ks = (long long)G * 272;
+    const int ts = t < 16 ? 256 + t : t;  // lanes >= 16: a harmless re-read, not added
+    int k = 0;
+    for (; k + 8 <= nb; k += 8) {  // 8 blocks' loads in flight, added in block order (same sums)
+      float v[8], w[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = o0[(k + u) * ks + t];
+        w[u] = o0[(k + u) * ks + ts];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        gx += v[u];
+        if (t < 16) sg += w[u];
+      }
+    }
+    for (; k < nb; ++k) {
+      gx += o0[k * ks + t];
+      if (t < 16) sg += o0[k * ks + 256 + t];
+    }
   }
   if (t < 16) {
     mv[0][t] = mu_bn[g * 16 + t];
