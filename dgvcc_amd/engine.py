@@ -64,6 +64,24 @@ def frozen(owner, name, srcs, build):
     return ent[1]
 
 
+def frozen_put(owner, name, srcs, value):
+    """Store `value` as frozen(owner, name, srcs, ...)'s memo for the current sources (a tensor built
+    together with another one, e.g. the flipped filter of pack_flip)."""
+    key = (_FROZEN_GEN[0],) + tuple((t.data_ptr(), t._version) for t in srcs)
+    owner.__dict__.setdefault("_frozen", {})[name] = (key, value)
+
+
+# training steps pack each filter and its dgrad flip in one launch (dg_pack_weight_flip); 0: two launches
+_PACK_FLIP = os.environ.get("DGVCC_PACK_FLIP", "1") != "0"
+
+
+def pack_flip(owner, w_param: torch.Tensor, dt) -> torch.Tensor:
+    """Packed filter of w_param; its flip is memoised as owner's ("flip", dt) for the dgrad."""
+    wp, wf = K.pack_weight_flip(w_param.detach(), dt)
+    frozen_put(owner, ("flip", dt), (w_param, wp), wf)
+    return wp
+
+
 def bn_eval_cached(owner, bn: nn.BatchNorm2d) -> torch.Tensor:
     return frozen(owner, "bn_eval", (bn.weight, bn.bias, bn.running_mean, bn.running_var),
                   lambda: K.bn_eval_stats(bn.weight.detach(), bn.bias.detach(), bn.running_mean,
@@ -107,10 +125,12 @@ class ConvLayer:
             ps += [self.bn.weight, self.bn.bias]
         return ps
 
-    def _pack(self, dt):
+    def _pack(self, dt, training=False):
         w = self.conv.weight.detach()
         if self.first:  # im2col filter [Cout][64], k = (r*3+s)*3+c
             return K.pack_weight(w, dt, cpad=self.Cin, row_len=64)
+        if training and _PACK_FLIP:  # the dgrad's flipped filter from the same launch
+            return pack_flip(self, self.conv.weight, dt)
         return K.pack_weight(w, dt)
 
     def _flip(self, wp):
@@ -198,7 +218,7 @@ class ConvLayer:
             return
         # packed once per weight version: in training the two views of a step share it (run_plan
         # starts each autograd forward on a fresh generation)
-        wp = frozen(self, ("w", dt), (self.conv.weight,), lambda: self._pack(dt))
+        wp = frozen(self, ("w", dt), (self.conv.weight,), lambda: self._pack(dt, training))
         if (_EVAL_FUSE and not training and bn is not None and pool is None and drop is None
                 and out is not None and not self.first and tape is None):
             # evaluation: BN from the running statistics (+ReLU) in the conv epilogue, no z pass

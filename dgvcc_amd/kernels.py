@@ -127,6 +127,16 @@ def pack_weight(w: torch.Tensor, dtype: torch.dtype, cpad: int | None = None,
     return out
 
 
+def pack_weight_flip(w: torch.Tensor, dtype: torch.dtype) -> tuple[torch.Tensor, torch.Tensor]:
+    """(pack_weight(w, dtype), flip_weight of it) from one launch (dg_pack_weight_flip)."""
+    Cout, C, R, S = w.shape
+    out = torch.empty((Cout, R * S * C), dtype=dtype, device=w.device)
+    wflip = torch.empty_like(out)
+    call("dg_pack_weight_flip", dtype_code(dtype), ptr(w.contiguous()), Cout, C, R, S, ptr(out), ptr(wflip),
+         stream())
+    return out, wflip
+
+
 def conv_fwd(x: Act, wp: torch.Tensor, Cout: int, R: int, pad: int, y: Act,
              bias: torch.Tensor | None = None, accumulate=False, kind="fwd", k_alg=None):
     """k_alg: algorithmic reduction length when the GEMM K is padded (im2col layer)."""

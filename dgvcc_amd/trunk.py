@@ -23,7 +23,7 @@ import torch.nn as nn
 from . import dist as D
 from . import kernels as K
 from . import syncbn as SB
-from .engine import ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_cached, frozen
+from .engine import _PACK_FLIP, ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_cached, frozen, pack_flip
 from .kernels import Act
 
 STEM_KPAD = 192  # 7*7*3 = 147 taps, padded to a multiple of 64 for the MFMA K loop
@@ -47,6 +47,8 @@ class TConv:
     def pack(self, dt, training=True):
         """Packed filter, once per weight version (engine.frozen; run_plan starts each training
         forward on a fresh generation)."""
+        if training and self.same and _PACK_FLIP:  # the dgrad's flipped filter from the same launch
+            return frozen(self, ("w", dt), (self.conv.weight,), lambda: pack_flip(self, self.conv.weight, dt))
         return frozen(self, ("w", dt), (self.conv.weight,), lambda: K.pack_weight(self.conv.weight.detach(), dt))
 
     def _flip(self, wp):

@@ -60,7 +60,7 @@ int dg_set_f32_math(int mode);
  * nearest rounding, three v_mfma_f32_16x16x32_f16 products per block (hi*hi + hi*lo + lo*hi),
  * f32 accumulation, exact rescale (dropped terms <= ~2^-21 |x*y|, two-sided; dg_common.h). */
 int dg_get_f32_math(void);
-#define DGVCC_ABI_VERSION 7 /* 7: dg_bn_apply_pair / dg_bn_apply_pool_pair / dg_bn_bwd_pair / dg_bn_bwd_pool_pair write the f16 x3 pair image of their f32 output and dg_conv_fwd_pair reads it (dg_bn_workspace grew for the backward ones); 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
+#define DGVCC_ABI_VERSION 8 /* 8: dg_pack_weight_flip; 7: dg_bn_apply_pair / dg_bn_apply_pool_pair / dg_bn_bwd_pair / dg_bn_bwd_pool_pair write the f16 x3 pair image of their f32 output and dg_conv_fwd_pair reads it (dg_bn_workspace grew for the backward ones); 6: operand maxima with channels ([1 + C] floats, rounded up to 4, for f32 producers, dg_amax and the f32 dg_softmax_head_bwd; the f16 x3 weight gradients take per-channel scales from them); 5: amax (max |gL_1|, |gL_2|) on dg_softmax_head_bwd; 4: amax on dg_bn_add_apply / dg_instnorm_apply / dg_instnorm_bwd, operand maxima on dg_conv2d_wgrad; 3: xamax on the f32 conv entries, dg_amax; 2: dg_conv_fwd_bnbwd takes (workspace, ws_bytes) */
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------
  * Replaces nn.Conv2d forward/backward inside vgg16_bn.features
@@ -182,6 +182,11 @@ int dg_conv_wgrad(int dtype, const void* x, int64_t ldx, int N, int H, int W, in
  * the im2col filter of the first layer. */
 int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R, int S, int Cpad,
                    int row_len, void* out, void* stream);
+/* dg_pack_weight's default layout (Cpad = C, row_len = R*S*C) into out and dg_flip_weight of it into
+ * wflip, in one launch (a training step's filter prep: the forward's packed filter and the dgrad's
+ * flipped one); both outputs identical to the two-call sequence.  Cout*C*R*S < 2^31. */
+int dg_pack_weight_flip(int dtype, const float* w, int Cout, int C, int R, int S, void* out, void* wflip,
+                        void* stream);
 
 /* First VGG layer (Cin=3): NCHW f32 image -> im2col rows [N*H*W][64] (27 taps,
  * zero padded to 64) so conv1_1 runs on the same MFMA GEMM (models/models.py:36). */

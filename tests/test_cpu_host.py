@@ -16,7 +16,7 @@ def test_library_exports_every_header_symbol():
     lib = _capi.lib()
     missing = [n for n in protos if not hasattr(lib, n)]
     assert not missing, missing
-    assert lib.dg_version() == _capi.header_abi_version() == 7
+    assert lib.dg_version() == _capi.header_abi_version() == 8
     assert len(protos) >= 30
 
 

@@ -365,6 +365,19 @@ def test_fused_adamw_matches_torch_with_missing_grads(dev):
     assert torch.equal(ours[2].detach().cpu(), base[2]) and torch.equal(ours[3].detach().cpu(), base[3])
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("shape", [(64, 64, 3, 3), (256, 64, 1, 1), (128, 96, 3, 3), (2048, 512, 1, 1)])
+def test_pack_weight_flip(dev, dtype, shape):
+    """dg_pack_weight_flip: both outputs bit-identical to dg_pack_weight + dg_flip_weight."""
+    K = _k()
+    w = torch.randn(shape, generator=torch.Generator().manual_seed(12)).to(dev)
+    wp, wf = K.pack_weight_flip(w, dtype)
+    ref = K.pack_weight(w, dtype)
+    reff = K.flip_weight(ref, shape[0], shape[1], shape[2])
+    torch.cuda.synchronize()
+    assert torch.equal(wp, ref) and torch.equal(wf, reff)
+
+
 def test_gather_flat_chunks(dev):
     """dg_gather_flat (one block per 4096-element chunk, tensor found by binary search): tensors of 0, 1, odd,
     chunk-straddling and multi-chunk sizes, gathered as two runs into one flat buffer (the optimizer's dead-
