@@ -64,22 +64,26 @@ def frozen(owner, name, srcs, build):
     return ent[1]
 
 
-def frozen_put(owner, name, srcs, value):
-    """Store `value` as frozen(owner, name, srcs, ...)'s memo for the current sources (a tensor built
-    together with another one, e.g. the flipped filter of pack_flip)."""
-    key = (_FROZEN_GEN[0],) + tuple((t.data_ptr(), t._version) for t in srcs)
-    owner.__dict__.setdefault("_frozen", {})[name] = (key, value)
-
-
 # training steps pack each filter and its dgrad flip in one launch (dg_pack_weight_flip); 0: two launches
 _PACK_FLIP = os.environ.get("DGVCC_PACK_FLIP", "1") != "0"
 
 
 def pack_flip(owner, w_param: torch.Tensor, dt) -> torch.Tensor:
-    """Packed filter of w_param; its flip is memoised as owner's ("flip", dt) for the dgrad."""
+    """Packed filter of w_param; its flip is kept beside it for the dgrad (flip_of)."""
     wp, wf = K.pack_weight_flip(w_param.detach(), dt)
-    frozen_put(owner, ("flip", dt), (w_param, wp), wf)
+    # the last two (several forwards of one step -- the views -- each pack; the tape holds each one's wp)
+    owner.__dict__["_packflip"] = [(wp, wp._version, wf)] + owner.__dict__.get("_packflip", [])[:1]
     return wp
+
+
+def flip_of(owner, w_param: torch.Tensor, wp: torch.Tensor, cout: int, cin: int, r: int) -> torch.Tensor:
+    """The dgrad's flipped filter of the packed filter wp: the one pack_flip built with wp (a function of
+    wp alone, so no generation check: a later forward's invalidate_frozen() must not discard it while
+    the tape still holds wp), else flip_weight once per packed filter (frozen)."""
+    for pw, ver, wf in owner.__dict__.get("_packflip", ()):
+        if pw is wp and ver == wp._version:
+            return wf
+    return frozen(owner, ("flip", wp.dtype), (w_param, wp), lambda: K.flip_weight(wp, cout, cin, r))
 
 
 def bn_eval_cached(owner, bn: nn.BatchNorm2d) -> torch.Tensor:
@@ -135,8 +139,7 @@ class ConvLayer:
 
     def _flip(self, wp):
         """flip_weight(wp) for the dgrad, once per packed filter (both views of a step)."""
-        return frozen(self, ("flip", wp.dtype), (self.conv.weight, wp),
-                      lambda: K.flip_weight(wp, self.Cout, self.Cin, self.R))
+        return flip_of(self, self.conv.weight, wp, self.Cout, self.Cin, self.R)
 
     def stem_ok(self, dt) -> bool:
         """bf16 first layer with BN + ReLU: fused conv/statistics and BN-backward/wgrad kernels;

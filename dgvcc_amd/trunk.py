@@ -23,7 +23,7 @@ import torch.nn as nn
 from . import dist as D
 from . import kernels as K
 from . import syncbn as SB
-from .engine import _PACK_FLIP, ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_cached, frozen, pack_flip
+from .engine import _PACK_FLIP, ACT_NONE, ACT_RELU, ConvLayer, _acc, _bn_momentum, bn_eval_cached, flip_of, frozen, pack_flip
 from .kernels import Act
 
 STEM_KPAD = 192  # 7*7*3 = 147 taps, padded to a multiple of 64 for the MFMA K loop
@@ -52,8 +52,7 @@ class TConv:
         return frozen(self, ("w", dt), (self.conv.weight,), lambda: K.pack_weight(self.conv.weight.detach(), dt))
 
     def _flip(self, wp):
-        return frozen(self, ("flip", wp.dtype), (self.conv.weight, wp),
-                      lambda: K.flip_weight(wp, self.Cout, self.Cin, self.R))
+        return flip_of(self, self.conv.weight, wp, self.Cout, self.Cin, self.R)
 
     def out_hw(self, H, W):
         return K.conv_out(H, self.R, self.stride, self.pad), K.conv_out(W, self.R, self.stride, self.pad)
