@@ -366,7 +366,8 @@ def test_fused_adamw_matches_torch_with_missing_grads(dev):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
-@pytest.mark.parametrize("shape", [(64, 64, 3, 3), (256, 64, 1, 1), (128, 96, 3, 3), (2048, 512, 1, 1)])
+@pytest.mark.parametrize("shape", [(64, 64, 3, 3), (256, 64, 1, 1), (128, 96, 3, 3), (2048, 512, 1, 1), (1, 70, 3, 3),
+                                   (100, 3, 5, 5)])
 def test_pack_weight_flip(dev, dtype, shape):
     """dg_pack_weight_flip: both outputs bit-identical to dg_pack_weight + dg_flip_weight."""
     K = _k()
