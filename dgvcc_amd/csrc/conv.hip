@@ -5592,30 +5592,19 @@ __global__ void flip_weight_kernel(const T* __restrict__ w, int Cout, int C, int
 
 // pack_weight_kernel's default layout (Cpad = C, row_len = R*S*C) and flip_weight_kernel's wflip of the
 // same stored values in one pass: a training step's per-layer filter prep in one launch instead of two
-// (each ~5 us, almost all launch and ramp: 40-90 of them per step).  One block per (tap, 64 input x 64
-// output channels): the tile is read once into LDS (stored values), then written out twice, both
-// coalesced -- the packed rows with c fastest, the flipped rows with co fastest (a per-element form
-// wrote one of the two at a stride of Cout elements: 17 us per f32 launch against the pack's 8).
+// (each ~5 us, almost all launch and ramp: 40-90 of them per step).  32-bit index math (total < 2^31,
+// checked by the launcher).
 template <typename T>
-__global__ __launch_bounds__(256) void pack_flip_weight_kernel(const float* __restrict__ w, int Cout, int C, int R,
-                                                               int S, T* __restrict__ out, T* __restrict__ wf) {
-  __shared__ float t[64][65];  // [co][c], padded: the co-fastest reads hit distinct banks
-  const int c0 = blockIdx.x * 64, co0 = blockIdx.y * 64, rs = blockIdx.z;
-  const int RS = R * S, r = rs / S, s2 = rs - r * S;
-  const long long RSC = (long long)RS * C;
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int col = e >> 6, cl = e & 63, co = co0 + col, c = c0 + cl;
-    if (co < Cout && c < C) t[col][cl] = to_f(from_f<T>(w[((long long)co * C + c) * RS + rs]));
-  }
-  __syncthreads();
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int col = e >> 6, cl = e & 63, co = co0 + col, c = c0 + cl;
-    if (co < Cout && c < C) out[co * RSC + (long long)rs * C + c] = from_f<T>(t[col][cl]);
-  }
-  const long long frow = (long long)((R - 1 - r) * S + (S - 1 - s2)) * Cout;
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int cl = e >> 6, col = e & 63, co = co0 + col, c = c0 + cl;
-    if (co < Cout && c < C) wf[(long long)c * RS * Cout + frow + co] = from_f<T>(t[col][cl]);
+__global__ void pack_flip_weight_kernel(const float* __restrict__ w, int Cout, int C, int R, int S,
+                                        T* __restrict__ out, T* __restrict__ wf) {
+  const int RSC = R * S * C, total = Cout * RSC;
+  for (int o = blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gridDim.x * blockDim.x) {
+    const int co = o / RSC, k = o - co * RSC;
+    const int rs = k / C, c = k - rs * C;
+    const int r = rs / S, s2 = rs - r * S;
+    const T v = from_f<T>(w[((co * C + c) * R + r) * S + s2]);
+    out[o] = v;
+    wf[((c * R + (R - 1 - r)) * S + (S - 1 - s2)) * Cout + co] = v;
   }
 }
 
@@ -6161,18 +6150,18 @@ extern "C" int dg_pack_weight(int dtype, const float* w, int Cout, int C, int R,
 extern "C" int dg_pack_weight_flip(int dtype, const float* w, int Cout, int C, int R, int S, void* out, void* wflip,
                                    void* stream) {
   DG_REQUIRE(w && out && wflip && Cout > 0 && C > 0 && R > 0 && S > 0);
-  DG_SUPPORTED((long long)Cout * C * R * S < (1LL << 31) && R * S <= 65535 && Cout <= 64 * 65535);
+  DG_SUPPORTED((long long)Cout * C * R * S < (1LL << 31));
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid(dg_cdiv(C, 64), dg_cdiv(Cout, 64), R * S);
+  const long long total = (long long)Cout * C * R * S;
   if (dtype == DG_BF16)
-    hipLaunchKernelGGL(pack_flip_weight_kernel<bf16>, grid, dim3(256), 0, st, w, Cout, C, R, S, (bf16*)out,
-                       (bf16*)wflip);
+    hipLaunchKernelGGL(pack_flip_weight_kernel<bf16>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S,
+                       (bf16*)out, (bf16*)wflip);
   else if (dtype == DG_F16)
-    hipLaunchKernelGGL(pack_flip_weight_kernel<f16>, grid, dim3(256), 0, st, w, Cout, C, R, S, (f16*)out,
-                       (f16*)wflip);
+    hipLaunchKernelGGL(pack_flip_weight_kernel<f16>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S,
+                       (f16*)out, (f16*)wflip);
   else if (dtype == DG_F32)
-    hipLaunchKernelGGL(pack_flip_weight_kernel<float>, grid, dim3(256), 0, st, w, Cout, C, R, S, (float*)out,
-                       (float*)wflip);
+    hipLaunchKernelGGL(pack_flip_weight_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, w, Cout, C, R, S,
+                       (float*)out, (float*)wflip);
   else
     return DG_ERR_INVALID;
   DG_CHECK_LAUNCH();
